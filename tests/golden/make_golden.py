@@ -1,0 +1,292 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by running the REAL reference (hilbert_quantization v1.3.0) on seeded
+inputs.  Build-container only: it needs /root/reference, which never travels to the GPU box; the
+resulting *.npz files are committed and are pure data (no pickles: np.load(allow_pickle=False)).
+
+    python tests/golden/make_golden.py [--ref /root/reference]
+
+The reference imports cv2 at package import time (core/video_storage.py:19) although none of the
+hot-path modules use it, so a do-nothing `cv2` module is placed on sys.path from a temp dir.
+"""
+import argparse
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _import_reference(ref_root):
+    stub_dir = tempfile.mkdtemp(prefix="hq_cv2stub_")
+    with open(os.path.join(stub_dir, "cv2.py"), "w") as f:
+        f.write("# inert stub: the hot-path modules never call cv2\n")
+    sys.path[:0] = [stub_dir, ref_root]
+    sys.dont_write_bytecode = True
+    import logging
+    logging.disable(logging.CRITICAL)
+    import hilbert_quantization  # noqa: F401
+    return hilbert_quantization
+
+
+def mapper_fixtures(hq):
+    from hilbert_quantization.core.hilbert_mapper import HilbertCurveMapper
+    from hilbert_quantization.rag.embedding_generation.hilbert_mapper import HilbertCurveMapperImpl
+    m = HilbertCurveMapper()
+    rm = HilbertCurveMapperImpl(None)
+    out = {}
+    for n in [1, 2, 4, 8, 16, 32, 64, 128]:
+        out[f"coords_n{n}"] = np.array(m.generate_hilbert_coordinates(n), dtype=np.int16).reshape(-1, 2)
+    for n in [1, 2, 4, 8, 16, 32, 64]:
+        t = np.zeros((n, n), dtype=np.int32)
+        for y in range(n):
+            for x in range(n):
+                t[y, x] = m._xy_to_hilbert_index(x, y, n)
+        out[f"xy2d_n{n}"] = t
+    rng = np.random.default_rng(1234)
+    cases = [(5, 4, np.float32), (16, 4, np.float64), (100, 16, np.float32), (1024, 32, np.float32),
+             (1536, 64, np.float32), (700, 32, np.int32), (256, 16, np.float16), (4096, 64, np.float64)]
+    for k, (d, n, dt) in enumerate(cases):
+        if np.issubdtype(dt, np.integer):
+            p = rng.integers(-1000, 1000, size=d).astype(dt)
+        else:
+            p = rng.standard_normal(d).astype(dt)
+        img = m.map_to_2d(p, (n, n))
+        out[f"map_in_{k}"] = p
+        out[f"map_out_{k}"] = img
+        out[f"unmap_out_{k}"] = m.map_from_2d(img)
+        out[f"rag_map_out_{k}"] = rm.map_to_2d(p, (n, n))
+        out[f"rag_unmap_out_{k}"] = rm.map_from_2d(img)
+    return out
+
+
+def index_fixtures(hq):
+    from hilbert_quantization.core.hilbert_mapper import HilbertCurveMapper
+    from hilbert_quantization.core.streaming_index_builder import StreamingHilbertIndexGenerator
+    from hilbert_quantization.core.index_generator import HierarchicalIndexGeneratorImpl
+    from hilbert_quantization.rag.embedding_generation.hierarchical_index_generator import (
+        HierarchicalIndexGenerator as RagGen)
+    m = HilbertCurveMapper()
+    sg = StreamingHilbertIndexGenerator()
+    tg = HierarchicalIndexGeneratorImpl()
+    rg = RagGen()
+    rng = np.random.default_rng(99)
+    out = {}
+    k = 0
+    for (n, L, d) in [(2, 2, 4), (4, 4, 16), (8, 8, 64), (16, 16, 200), (32, 32, 1024), (64, 64, 1536),
+                      (32, 20, 1000), (64, 100, 4096), (16, 7, 256), (128, 128, 10000)]:
+        p = rng.standard_normal(d).astype(np.float32)
+        img = m.map_to_2d(p, (n, n))
+        out[f"stream_img_{k}"] = img
+        out[f"stream_L_{k}"] = np.int64(L)
+        out[f"stream_idx_{k}"] = sg.generate_optimized_indices(img, L)
+        k += 1
+    k = 0
+    for (n, L, d) in [(8, 8, 64), (16, 16, 256), (32, 32, 1024), (64, 64, 1536), (32, 32, 512), (16, 40, 200),
+                      (64, 32, 3000)]:
+        p = (rng.standard_normal(d) * 3 + 0.5).astype(np.float32)
+        img = m.map_to_2d(p, (n, n))
+        out[f"trad_img_{k}"] = img
+        out[f"trad_L_{k}"] = np.int64(L)
+        out[f"trad_idx_{k}"] = tg.generate_optimized_indices(img, L)
+        k += 1
+    out["trad_alloc_32"] = np.array(tg.calculate_level_allocation(32), dtype=np.int64)
+    out["trad_alloc_64"] = np.array(tg.calculate_level_allocation(64), dtype=np.int64)
+    k = 0
+    for (n, d, dt) in [(16, 256, np.float32), (32, 1024, np.float32), (64, 4096, np.float32),
+                       (32, 768, np.float64), (8, 64, np.float32)]:
+        p = rng.standard_normal(d).astype(dt)
+        img = m.map_to_2d(p, (n, n))
+        out[f"rag_img_{k}"] = img
+        out[f"rag_rows_{k}"] = rg.generate_multi_level_indices(img)
+        k += 1
+    return out
+
+
+def quant_fixtures(hq):
+    """cfg2 slice: pad -> map -> streaming index (L = n) -> embed -> uint8 normalise, exactly the
+    component sequence of QuantizationPipeline.quantize_model (core/pipeline.py:97-146)."""
+    from hilbert_quantization.core.pipeline import QuantizationPipeline
+    from hilbert_quantization.core.compressor import MPEGAICompressorImpl
+    from hilbert_quantization.core.dimension_calculator import PowerOf4DimensionCalculator
+    pipe = QuantizationPipeline(dimension_calculator=PowerOf4DimensionCalculator(min_efficiency_ratio=0.2))
+    out = {}
+    rng = np.random.default_rng(7)
+    for tag, d, N in [("d1536", 1536, 6), ("d1024", 1024, 6), ("d300", 300, 4), ("d4096", 4096, 2)]:
+        P = rng.standard_normal((N, d)).astype(np.float32)
+        frames, idxs, mins, maxs, enhs = [], [], [], [], []
+        for i in range(N):
+            p = P[i]
+            dims = pipe.dimension_calculator.calculate_optimal_dimensions(len(p))
+            pc = pipe.dimension_calculator.calculate_padding_strategy(len(p), dims)
+            pp = pipe._pad_parameters(p, dims, pc)
+            img = pipe.hilbert_mapper.map_to_2d(pp, dims)
+            idx = pipe.index_generator.generate_optimized_indices(img, dims[0])
+            enh = pipe.index_generator.embed_indices_in_image(img, idx)
+            comp = MPEGAICompressorImpl()
+            u8 = comp._normalize_for_compression(enh)
+            frames.append(u8)
+            idxs.append(idx)
+            mins.append(comp._norm_min)
+            maxs.append(comp._norm_max)
+            enhs.append(enh)
+        out[f"{tag}_params"] = P
+        out[f"{tag}_frames"] = np.stack(frames)
+        out[f"{tag}_idx"] = np.stack(idxs)
+        out[f"{tag}_min"] = np.array(mins, dtype=np.float32)
+        out[f"{tag}_max"] = np.array(maxs, dtype=np.float32)
+        comp = MPEGAICompressorImpl()
+        comp._normalize_for_compression(enhs[0])
+        out[f"{tag}_denorm0"] = comp._denormalize_from_compression(frames[0])
+    comp = MPEGAICompressorImpl()
+    out["const_frame"] = comp._normalize_for_compression(np.full((5, 4), 2.5, dtype=np.float32))
+    # dimension table (core/dimension_calculator.py:36-61, tests/test_dimension_calculator.py:224-238)
+    dc = PowerOf4DimensionCalculator()
+    sizes = np.array([1, 3, 4, 5, 16, 17, 64, 100, 256, 384, 768, 1024, 1536, 3000, 4096, 10000, 16384,
+                      16385, 70000], dtype=np.int64)
+    out["dim_sizes"] = sizes
+    out["dim_n"] = np.array([dc.calculate_optimal_dimensions(int(s))[0] for s in sizes], dtype=np.int64)
+    errs = []
+    for s in sizes:
+        n = dc.calculate_optimal_dimensions(int(s))
+        try:
+            dc.calculate_padding_strategy(int(s), n)
+            errs.append("")
+        except ValueError as e:
+            errs.append(str(e))
+    out["dim_err"] = np.array(errs)
+    return out
+
+
+def search_fixtures(hq):
+    from hilbert_quantization.core.hilbert_mapper import HilbertCurveMapper
+    from hilbert_quantization.core.streaming_index_builder import StreamingHilbertIndexGenerator
+    from hilbert_quantization.core.search_engine import ProgressiveSimilaritySearchEngine
+    from hilbert_quantization.models import QuantizedModel, ModelMetadata
+    m = HilbertCurveMapper()
+    sg = StreamingHilbertIndexGenerator()
+    out = {}
+    rng = np.random.default_rng(2024)
+    for tag, n, N in [("L64", 64, 160), ("L32", 32, 96)]:
+        C = np.zeros((N, n), dtype=np.float64)
+        for i in range(N):
+            p = rng.standard_normal(n * n if n == 32 else 1536).astype(np.float32)
+            pp = np.zeros(n * n, np.float32)
+            pp[: len(p)] = p
+            C[i] = sg.generate_optimized_indices(m.map_to_2d(pp, (n, n)), n)
+        # degenerate rows (SURVEY.md §8a hazards 5/6): zeros, constant 0.1 (np.std != 0), exact
+        # constants, duplicates, negations, a constant level-0 segment.
+        C[1] = 0.0
+        C[2] = 0.1
+        C[3] = 0.5
+        C[4] = C[10]
+        C[5] = -C[11]
+        C[6, : n // 2] = 0.25
+        C[7] = C[10]
+        C[8] = C[12] * 2.0 + 1.0
+        Q = np.stack([C[10] + rng.normal(0, 0.01, n), C[20].copy(), np.full(n, 0.5), rng.standard_normal(n),
+                      C[2].copy(), C[6].copy()])
+        eng = ProgressiveSimilaritySearchEngine(similarity_threshold=0.1, max_candidates_per_level=20)
+        levels = eng._parse_index_structure(Q[0], n)
+        nl = len(levels)
+        per = np.zeros((len(Q), N, nl))
+        for a in range(len(Q)):
+            for b in range(N):
+                for lv in range(nl):
+                    per[a, b, lv] = eng.compare_indices_at_level(Q[a], C[b], lv)
+        ov = np.zeros((len(Q), N))
+        for a in range(len(Q)):
+            for b in range(N):
+                ov[a, b] = eng._calculate_overall_similarity(Q[a], C[b])[0]
+        models = []
+        for b in range(N):
+            md = ModelMetadata(model_name=f"m{b}", original_size_bytes=1, compressed_size_bytes=1,
+                               compression_ratio=1.0, quantization_timestamp="t")
+            models.append(QuantizedModel(compressed_data=b"x", original_dimensions=(n, n), parameter_count=1,
+                                         compression_quality=0.8, hierarchical_indices=C[b], metadata=md))
+        K = 10
+        bf_ids = np.full((len(Q), K), -1, np.int64)
+        bf_sc = np.zeros((len(Q), K))
+        pg_ids = np.full((len(Q), K), -1, np.int64)
+        pg_sc = np.zeros((len(Q), K))
+        pg_err = np.zeros((len(Q), K))
+        for a in range(len(Q)):
+            r = eng.brute_force_search(Q[a], models, K)
+            for j, x in enumerate(r):
+                bf_ids[a, j] = int(x.model.model_id[1:])
+                bf_sc[a, j] = x.similarity_score
+            r = eng.progressive_search(Q[a], models, K)
+            for j, x in enumerate(r):
+                pg_ids[a, j] = int(x.model.model_id[1:])
+                pg_sc[a, j] = x.similarity_score
+                pg_err[a, j] = x.reconstruction_error
+        # threshold-fallback case: every candidate scores below 0.1 -> first argmax survives
+        negC = -np.tile(Q[3], (30, 1)) * (1.0 + 0.01 * np.arange(30)[:, None])
+        negmodels = []
+        for b in range(30):
+            md = ModelMetadata(model_name=f"m{b}", original_size_bytes=1, compressed_size_bytes=1,
+                               compression_ratio=1.0, quantization_timestamp="t")
+            negmodels.append(QuantizedModel(compressed_data=b"x", original_dimensions=(n, n), parameter_count=1,
+                                            compression_quality=0.8, hierarchical_indices=negC[b], metadata=md))
+        r = eng.progressive_search(Q[3], negmodels, K)
+        out[f"{tag}_fallback_C"] = negC
+        out[f"{tag}_fallback_ids"] = np.array([int(x.model.model_id[1:]) for x in r], dtype=np.int64)
+        out[f"{tag}_fallback_sc"] = np.array([x.similarity_score for x in r])
+        out[f"{tag}_C"] = C
+        out[f"{tag}_Q"] = Q
+        out[f"{tag}_per_level"] = per
+        out[f"{tag}_overall"] = ov
+        out[f"{tag}_bf_ids"] = bf_ids
+        out[f"{tag}_bf_sc"] = bf_sc
+        out[f"{tag}_pg_ids"] = pg_ids
+        out[f"{tag}_pg_sc"] = pg_sc
+        out[f"{tag}_pg_err"] = pg_err
+    struct = []
+    for L in list(range(1, 130)) + [256, 1024, 4096]:
+        for lv in ProgressiveSimilaritySearchEngine()._parse_index_structure(np.zeros(L), L):
+            struct.append((L, lv.grid_size, lv.start_index, lv.end_index, int(lv.is_offset_sampling)))
+    out["parse_struct"] = np.array(struct, dtype=np.int64)
+    return out
+
+
+def rag_score_fixtures(hq):
+    from hilbert_quantization.rag.search import engine as E
+    cls = E.RAGSearchEngineImpl if hasattr(E, "RAGSearchEngineImpl") else None
+    if cls is None:
+        cands = [v for v in vars(E).values() if isinstance(v, type) and hasattr(v, "_compare_multi_level_indices")]
+        cls = cands[0]
+    obj = cls.__new__(cls)  # scoring helpers use no instance state beyond each other
+    rng = np.random.default_rng(5)
+    out = {}
+    A = rng.standard_normal((8, 32, 32)).astype(np.float32)
+    A[3] = 0.0
+    B = A[0] + rng.normal(0, 0.3, (32, 32)).astype(np.float32)
+    out["cos_A"] = A
+    out["cos_B"] = B
+    out["cos"] = np.array([obj._calculate_embedding_cosine_similarity(B, A[i]) for i in range(8)])
+    ML = rng.standard_normal((6, 3, 64))
+    out["ml_C"] = ML
+    out["ml_Q"] = ML[0] + rng.normal(0, 0.2, (3, 64))
+    out["ml"] = np.array([obj._compare_multi_level_indices(out["ml_Q"], ML[i]) for i in range(6)])
+    out["ml_w3"] = obj._calculate_granularity_weights(3)
+    out["ml_w5"] = obj._calculate_granularity_weights(5)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    a = ap.parse_args()
+    hq = _import_reference(a.ref)
+    for name, fn in [("mapper", mapper_fixtures), ("index", index_fixtures), ("quant", quant_fixtures),
+                     ("search", search_fixtures), ("rag_score", rag_score_fixtures)]:
+        d = fn(hq)
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **d)
+        print(f"wrote {path}: {len(d)} arrays, {os.path.getsize(path)} bytes")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,215 @@
+"""Pin the CPU oracle (oracle/hq_oracle.py) to the reference: golden vectors generated from the real
+reference (tests/golden/make_golden.py) and the reference's own known-answer tests.
+CPU only."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import hq_oracle as O
+
+# ---------------------------------------------------------------- NumPy-order reductions
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_np_order_sum_mean_std(dtype):
+    rng = np.random.default_rng(3)
+    for n in list(range(1, 140)) + [255, 256, 300, 1024]:
+        X = (rng.standard_normal((7, n)) * 10 ** rng.uniform(-3, 3)).astype(dtype)
+        s = O.np_sum_rows(X)
+        m = O.np_mean_rows(X)
+        sd = O.np_std_rows(X)
+        for i in range(7):
+            assert s[i] == np.add.reduce(X[i])
+            assert m[i] == np.mean(X[i])
+            assert sd[i] == np.std(X[i])
+
+
+def test_np_std_constant_point_one():
+    # SURVEY.md §8a hazard 5: np.std([0.1]*3) is 1.39e-17, not 0
+    x = np.full((1, 3), 0.1)
+    assert O.np_std_rows(x)[0] == np.std(x[0]) != 0.0
+
+
+# ---------------------------------------------------------------- M rows
+
+
+def test_reference_kats():
+    # tests/test_hilbert_mapper.py:23, :43-46; tests/test_rag_hilbert_mapper.py:317
+    xs, ys = O.hilbert_table(2)
+    assert list(zip(xs, ys)) == [(0, 0), (0, 1), (1, 1), (1, 0)]
+    xs, ys = O.hilbert_table(4)
+    assert list(zip(xs, ys))[:8] == [(0, 0), (1, 0), (1, 1), (0, 1), (0, 2), (0, 3), (1, 3), (1, 2)]
+    # tests/test_hilbert_mapper.py:173-182 and tests/test_rag_hilbert_mapper.py:694-701
+    assert list(O.map_from_2d(np.array([[1, 4], [2, 3]]))) == [1, 2, 3, 4]
+    assert list(O.map_from_2d(np.array([[1, 2], [3, 4]]))) == [1, 3, 4, 2]
+    with pytest.raises(ValueError, match="power of 2"):
+        O.hilbert_table(3)
+
+
+def test_coords_and_xy2d_golden(golden):
+    g = golden("mapper")
+    for n in [1, 2, 4, 8, 16, 32, 64, 128]:
+        xs, ys = O.hilbert_table(n)
+        np.testing.assert_array_equal(np.stack([xs, ys], 1), g[f"coords_n{n}"])
+    for n in [1, 2, 4, 8, 16, 32, 64]:
+        yy, xx = np.mgrid[0:n, 0:n]
+        np.testing.assert_array_equal(O.hilbert_xy2d(xx, yy, n), g[f"xy2d_n{n}"])
+
+
+def test_map_golden(golden):
+    g = golden("mapper")
+    k = 0
+    while f"map_in_{k}" in g:
+        p = g[f"map_in_{k}"]
+        img = g[f"map_out_{k}"]
+        n = img.shape[0]
+        out = O.map_to_2d(p, n)
+        assert out.dtype == img.dtype
+        assert out.tobytes() == img.tobytes()
+        assert g[f"rag_map_out_{k}"].tobytes() == img.tobytes()
+        un = O.map_from_2d(img)
+        assert un.tobytes() == g[f"unmap_out_{k}"].tobytes() == g[f"rag_unmap_out_{k}"].tobytes()
+        k += 1
+    assert k >= 8
+
+
+# ---------------------------------------------------------------- S1 / I rows
+
+
+def test_dimension_table(golden):
+    g = golden("quant")
+    for s, n, err in zip(g["dim_sizes"], g["dim_n"], g["dim_err"]):
+        assert O.optimal_dimensions(int(s)) == (n, n)
+        if err:
+            with pytest.raises(ValueError) as e:
+                O.check_efficiency(int(s), (n, n))
+            assert str(e.value) == str(err)
+        else:
+            O.check_efficiency(int(s), (n, n))
+
+
+def test_streaming_index_golden(golden):
+    g = golden("index")
+    k = 0
+    while f"stream_img_{k}" in g:
+        img = g[f"stream_img_{k}"]
+        L = int(g[f"stream_L_{k}"])
+        got = O.streaming_index(O.map_from_2d(img), L)
+        ref = g[f"stream_idx_{k}"]
+        assert got.dtype == np.float64
+        assert got.tobytes() == ref.tobytes(), k
+        k += 1
+    assert k == 10
+
+
+def test_streaming_allocations_known():
+    # n=64,L=64 -> [32,16,8,4,2,1,1]; n=32 -> [16,8,4,2,1,1]
+    assert [a for a in O.streaming_allocations([4096, 1024, 256, 64, 16, 4, 1, 0, 0, 0], 64) if a] == \
+        [32, 16, 8, 4, 2, 1, 1]
+    assert [a for a in O.streaming_allocations([1024, 256, 64, 16, 4, 1, 0, 0, 0, 0], 32) if a] == \
+        [16, 8, 4, 2, 1, 1]
+
+
+def test_traditional_index_golden(golden):
+    g = golden("index")
+    assert [tuple(x) for x in g["trad_alloc_32"]] == O.traditional_allocation(32)
+    assert [tuple(x) for x in g["trad_alloc_64"]] == O.traditional_allocation(64)
+    k = 0
+    while f"trad_img_{k}" in g:
+        got = O.traditional_index(g[f"trad_img_{k}"], int(g[f"trad_L_{k}"]))
+        ref = g[f"trad_idx_{k}"]
+        assert got.dtype == ref.dtype == np.float32
+        assert got.tobytes() == ref.tobytes(), k
+        k += 1
+    assert k == 7
+
+
+def test_rag_rows_golden(golden):
+    g = golden("index")
+    k = 0
+    while f"rag_img_{k}" in g:
+        got = O.rag_multi_level_indices(g[f"rag_img_{k}"])
+        ref = g[f"rag_rows_{k}"]
+        assert got.dtype == ref.dtype
+        assert got.tobytes() == ref.tobytes(), k
+        k += 1
+    assert k == 5
+
+
+def test_quantize_pipeline_golden(golden):
+    g = golden("quant")
+    for tag in ["d1536", "d1024", "d300", "d4096"]:
+        P = g[f"{tag}_params"]
+        n = O.optimal_dimensions(P.shape[1])[0]
+        img = O.map_to_2d(O.pad_parameters(P, n), n)
+        idx = O.streaming_index(O.map_from_2d(img), n)
+        assert idx.tobytes() == g[f"{tag}_idx"].tobytes()
+        enh = O.embed_index_row(img, idx)
+        u8, mn, mx = O.normalize_u8(enh)
+        assert u8.tobytes() == g[f"{tag}_frames"].tobytes(), tag
+        assert mn.tobytes() == g[f"{tag}_min"].tobytes()
+        assert mx.tobytes() == g[f"{tag}_max"].tobytes()
+        de = O.denormalize_u8(u8[0], mn[0], mx[0])
+        assert de.tobytes() == g[f"{tag}_denorm0"].tobytes()
+    u8, _, _ = O.normalize_u8(np.full((5, 4), 2.5, dtype=np.float32))
+    assert u8.tobytes() == g["const_frame"].tobytes()
+
+
+# ---------------------------------------------------------------- S rows
+
+
+def test_parse_structure_golden(golden):
+    g = golden("search")
+    got = []
+    for L in list(range(1, 130)) + [256, 1024, 4096]:
+        for (gr, s, e, off) in O.parse_index_structure(L):
+            got.append((L, gr, s, e, int(off)))
+    np.testing.assert_array_equal(np.array(got), g["parse_struct"])
+    assert O.segment_bounds(64) == [(0, 32), (32, 40), (40, 43), (43, 44), (44, 64)]
+    assert O.segment_bounds(32) == [(0, 16), (16, 20), (20, 21), (21, 32)]
+
+
+@pytest.mark.parametrize("tag", ["L64", "L32"])
+def test_scores_golden(golden, tag):
+    g = golden("search")
+    C, Q = g[f"{tag}_C"], g[f"{tag}_Q"]
+    per, ov = g[f"{tag}_per_level"], g[f"{tag}_overall"]
+    for a in range(len(Q)):
+        for lv in range(per.shape[2]):
+            s = O.level_similarity(Q[a], C, lv)
+            np.testing.assert_allclose(s, per[a, :, lv], rtol=0, atol=1e-12)
+            # exact-value branches are bit-exact
+            exact = np.isin(per[a, :, lv], [0.0, 0.1, 1.0])
+            assert np.array_equal(s[exact], per[a, exact, lv])
+        o, _ = O.overall_similarity(Q[a], C)
+        np.testing.assert_allclose(o, ov[a], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("tag", ["L64", "L32"])
+def test_search_orders_golden(golden, tag):
+    g = golden("search")
+    C, Q = g[f"{tag}_C"], g[f"{tag}_Q"]
+    for a in range(len(Q)):
+        ids, sc, _ = O.brute_force_search(Q[a], C, 10)
+        np.testing.assert_array_equal(ids, g[f"{tag}_bf_ids"][a][: len(ids)])
+        np.testing.assert_allclose(sc, g[f"{tag}_bf_sc"][a][: len(ids)], atol=1e-12)
+        ids, sc, _, err = O.progressive_search(Q[a], C, 10, 0.1, 20)
+        ref_ids = g[f"{tag}_pg_ids"][a]
+        ref_ids = ref_ids[ref_ids >= 0]
+        np.testing.assert_array_equal(ids, ref_ids)
+        np.testing.assert_allclose(sc, g[f"{tag}_pg_sc"][a][: len(ids)], atol=1e-12)
+        np.testing.assert_allclose(err, g[f"{tag}_pg_err"][a][: len(ids)], atol=1e-12)
+    ids, sc, _, _ = O.progressive_search(Q[3], g[f"{tag}_fallback_C"], 10, 0.1, 20)
+    np.testing.assert_array_equal(ids, g[f"{tag}_fallback_ids"])
+    np.testing.assert_allclose(sc, g[f"{tag}_fallback_sc"], atol=1e-12)
+
+
+def test_rag_scoring_golden(golden):
+    g = golden("rag_score")
+    got = O.rag_cosine(g["cos_B"], g["cos_A"])
+    np.testing.assert_allclose(got, g["cos"], atol=1e-7)
+    np.testing.assert_allclose(O.rag_granularity_weights(3), g["ml_w3"], atol=1e-15)
+    np.testing.assert_allclose(O.rag_granularity_weights(5), g["ml_w5"], atol=1e-15)
+    got = O.rag_multi_level_similarity(g["ml_Q"], g["ml_C"])
+    np.testing.assert_allclose(got, g["ml"], atol=1e-12)
