@@ -1,0 +1,882 @@
+// hq_search.hip — hierarchical-index similarity scan.
+//
+// Reference: core/search_engine.py:42-388 (ProgressiveSimilaritySearchEngine), core/video_search.py:
+// 215-264,1316-1328 (level-0 scan over stored frames), rag/search/engine.py:622-660,1025-1051 (cosine).
+//
+// compare_indices_at_level (search_engine.py:111-189) for one level segment of length m is
+//   both std 0 -> |mean_q - mean_c| < 1e-6 ? 1 : 0;  one std 0 -> 0.1;  otherwise
+//   corr = mean(zq*zc), sim = (corr+1)/2, dsim = max(0, 1 - mse/maxmse), clamp(0.7 sim + 0.3 dsim)
+// with zq = (q - mean_q)/std_q.  Everything except G = sum_j zq_j zc_j is a per-vector statistic, so
+// the scan is a segmented f64 GEMM (v_mfma_f64_16x16x4f64) plus an epilogue:
+//   corr = G/m;  sum q*c = std_q std_c G + m mean_q mean_c;
+//   1 - mse/maxmse = 2 (sum q*c) / (m (msq_q + msq_c))      (msq = mean of squares)
+// Zero-variance branches are decided by std values computed in NumPy's pairwise order
+// (k_seg_prepare), so the exact-constant outcomes (0, 0.1, 1) are bit-identical to the reference.
+//
+// Index vectors are stored "segment padded": each level segment starts at a multiple of 4 f64 and
+// is zero-filled to a multiple of 4 (Lp columns), so every MFMA k-step lies inside one segment.
+#include "hq_common.h"
+
+#include <math.h>
+
+namespace hq {
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------------
+// segment layout
+// ------------------------------------------------------------------------------------------------
+struct SegInfo {
+  int nseg;
+  int L, Lp;
+  int src[kMaxSeg];   // start in the raw index vector
+  int len[kMaxSeg];   // segment length m
+  int poff[kMaxSeg];  // start in the padded layout (multiple of 4)
+  int plen[kMaxSeg];  // padded length (multiple of 4)
+  double inv_m[kMaxSeg];
+  double w[kMaxSeg];  // 1/(l+1) (search_engine.py:205)
+  double wsum;
+};
+
+static void seg_info(int L, SegInfo& s) {
+  SegTable t;
+  parse_structure(L, L, t);
+  s.nseg = t.nseg;
+  s.L = L;
+  int off = 0;
+  s.wsum = 0.0;
+  for (int i = 0; i < t.nseg; ++i) {
+    s.src[i] = t.start[i];
+    s.len[i] = t.end[i] - t.start[i];
+    s.poff[i] = off;
+    s.plen[i] = (s.len[i] + 3) & ~3;
+    off += s.plen[i];
+    s.inv_m[i] = 1.0 / (double)s.len[i];
+    s.w[i] = 1.0 / (double)(i + 1);
+    s.wsum += s.w[i];
+  }
+  s.Lp = off;
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-segment statistics + normalised vectors (reference np.mean/np.std order)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_seg_prepare(const double* __restrict__ idx, int64_t N, SegInfo si,
+                                                     double* __restrict__ Z, double* __restrict__ stats) {
+  const int64_t total = N * si.nseg;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = t / si.nseg;
+    const int s = (int)(t % si.nseg);
+    const double* x = idx + row * si.L + si.src[s];
+    const int m = si.len[s];
+    auto fx = [=](int k) -> double { return x[k]; };
+    const double mean = np_sum<double>(fx, m) / (double)m;            // np.mean
+    auto fd = [=](int k) -> double { double d = x[k] - mean; return d * d; };
+    const double sd = sqrt(np_sum<double>(fd, m) / (double)m);        // np.std (_methods._var)
+    auto fs = [=](int k) -> double { return x[k] * x[k]; };
+    const double msq = np_sum<double>(fs, m) / (double)m;             // np.mean(q ** 2)
+    double* z = Z + row * si.Lp + si.poff[s];
+    if (sd == 0.0) {
+      for (int i = 0; i < si.plen[s]; ++i) z[i] = 0.0;
+    } else {
+      for (int i = 0; i < m; ++i) z[i] = (x[i] - mean) / sd;          // (q - mean(q)) / std (:150-151)
+      for (int i = m; i < si.plen[s]; ++i) z[i] = 0.0;
+    }
+    double* st = stats + (row * si.nseg + s) * 4;
+    st[0] = mean;
+    st[1] = sd;
+    st[2] = msq;
+    st[3] = 0.0;
+  }
+}
+
+// score of one level from the contraction G and the two vectors' segment statistics
+__device__ __forceinline__ double level_sim(double G, double qm, double qs, double qq, double cm, double cs,
+                                            double cq, double m, double inv_m) {
+  const bool fq = qs == 0.0, fc = cs == 0.0;
+  if (fq && fc) return fabs(qm - cm) < 1e-6 ? 1.0 : 0.0;
+  if (fq || fc) return 0.1;
+  const double corr = G * inv_m;
+  const double sim = (corr + 1.0) * 0.5;
+  const double t1 = (qs * cs) * G;
+  const double t2 = (qm * cm) * m;
+  const double dot = t1 + t2;                 // sum q*c
+  const double maxmse = qq + cq;              // > 0 here: both segments have a non-zero value
+  double dsim = (2.0 * inv_m) * dot / maxmse; // 1 - mse / maxmse
+  dsim = dsim > 0.0 ? dsim : 0.0;
+  double comb = 0.7 * sim + 0.3 * dsim;
+  comb = comb < 1.0 ? comb : 1.0;
+  return comb > 0.0 ? comb : 0.0;
+}
+
+// plain dot over a padded segment
+__device__ __forceinline__ double seg_dot(const double* a, const double* b, int n) {
+  double g = 0.0;
+  for (int i = 0; i < n; ++i) g = fma(a[i], b[i], g);
+  return g;
+}
+
+__device__ double pair_level(const double* zq, const double* sq, const double* zc, const double* sc,
+                             const SegInfo& si, int s) {
+  const double G = seg_dot(zq + si.poff[s], zc + si.poff[s], si.plen[s]);
+  const double* a = sq + 4 * s;
+  const double* b = sc + 4 * s;
+  return level_sim(G, a[0], a[1], a[2], b[0], b[1], b[2], (double)si.len[s], si.inv_m[s]);
+}
+
+__device__ double pair_overall(const double* zq, const double* sq, const double* zc, const double* sc,
+                               const SegInfo& si, double* lv) {
+  // search_engine.py:191-230: running weighted sum in level order, then divide and clamp
+  double tws = 0.0;
+  for (int s = 0; s < si.nseg; ++s) {
+    double v = pair_level(zq, sq, zc, sc, si, s);
+    if (lv) lv[s] = v;
+    tws = tws + v * si.w[s];
+  }
+  double ov = si.wsum > 0.0 ? tws / si.wsum : 0.0;
+  ov = ov < 1.0 ? ov : 1.0;
+  return ov > 0.0 ? ov : 0.0;
+}
+
+// dense Q x N scores (drop-in path for candidate lists held by Python)
+__global__ __launch_bounds__(256) void k_level_scores(const double* __restrict__ Zq, const double* __restrict__ Sq,
+                                                      int Q, const double* __restrict__ Zc,
+                                                      const double* __restrict__ Sc, int64_t N, SegInfo si,
+                                                      int level, double* __restrict__ out) {
+  const int64_t total = (int64_t)Q * N;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(t / N);
+    const int64_t c = t % N;
+    const double* zq = Zq + (int64_t)q * si.Lp;
+    const double* sq = Sq + (int64_t)q * si.nseg * 4;
+    const double* zc = Zc + c * si.Lp;
+    const double* sc = Sc + c * si.nseg * 4;
+    double v;
+    if (level < 0) v = pair_overall(zq, sq, zc, sc, si, nullptr);
+    else if (level >= si.nseg) v = 0.0;
+    else v = pair_level(zq, sq, zc, sc, si, level);
+    out[t] = v;
+  }
+}
+
+// overall + per-level for selected (query, candidate) pairs; ids are global, id_base subtracted
+__global__ __launch_bounds__(256) void k_rescore(const double* __restrict__ Zq, const double* __restrict__ Sq,
+                                                 int Q, const double* __restrict__ Zc,
+                                                 const double* __restrict__ Sc, int64_t N, SegInfo si,
+                                                 const int64_t* __restrict__ ids, int k, int64_t id_base,
+                                                 double* __restrict__ out) {
+  const int64_t total = (int64_t)Q * k;
+  const int W = 1 + si.nseg;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(t / k);
+    const int64_t gid = ids[t];
+    double* o = out + t * W;
+    const int64_t c = gid - id_base;
+    if (gid < 0 || c < 0 || c >= N) {
+      for (int i = 0; i < W; ++i) o[i] = 0.0;
+      continue;
+    }
+    double lv[kMaxSeg];
+    o[0] = pair_overall(Zq + (int64_t)q * si.Lp, Sq + (int64_t)q * si.nseg * 4, Zc + c * si.Lp,
+                        Sc + c * si.nseg * 4, si, lv);
+    for (int s = 0; s < si.nseg; ++s) o[1 + s] = lv[s];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// fused scan: MFMA f64 contraction + epilogue + per-query top-k (score desc, id asc)
+// WG = 4 waves; 64 queries (16 per wave) x one corpus chunk, 64 candidates per step.
+// ------------------------------------------------------------------------------------------------
+constexpr int kQB = 64;       // queries per workgroup
+constexpr int kCB = 64;       // candidates per step
+constexpr int kMaxTopK = 64;
+constexpr int kMaxFinal = 256;  // survivors handled by k_progressive_final
+
+struct ScanArgs {
+  const double* Zq; const double* Sq; int Q;
+  const double* Zc; const double* Sc; int64_t N;
+  SegInfo si;
+  int ks;          // k-steps (4 f64 each) processed: level0 -> plen[0]/4, overall -> Lp/4
+  int nseg_used;   // 1 (level0) or nseg (overall)
+  int rs;          // LDS row stride of the candidate tile (f64), == 2 mod 32, >= 4*ks
+  int K;           // top-k
+  double thr; int thr_mode;  // 0 none, 1 >=, 2 >
+  int64_t id_base;
+  int64_t chunk_len; int nchunks; int nqb;
+  double* ws_score; int64_t* ws_id; double* ws_best; int64_t* ws_best_id;
+};
+
+__device__ __forceinline__ bool better(double s, int64_t id, double s2, int64_t id2) {
+  return s > s2 || (s == s2 && id < id2);
+}
+
+template <int KSMAX, bool OVERALL>
+__global__ __launch_bounds__(256) void k_scan(ScanArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int nsu = a.nseg_used;
+  // LDS carve
+  double* btile = reinterpret_cast<double*>(smem);                         // kCB x rs
+  double* cstat = btile + kCB * a.rs;                                      // kCB x nsu x 4
+  double* qstat = cstat + kCB * nsu * 4;                                   // kQB x nsu x 4
+  double* stile = qstat + kQB * nsu * 4;                                   // 4 x 16 x kCB
+  double* lscore = stile + 4 * 16 * kCB;                                   // kQB x K
+  int64_t* lid = reinterpret_cast<int64_t*>(lscore + kQB * a.K);           // kQB x K
+  unsigned long long* mask = reinterpret_cast<unsigned long long*>(lid + kQB * a.K);  // kQB
+  double* tau = reinterpret_cast<double*>(mask + kQB);                     // kQB
+  int* lcnt = reinterpret_cast<int*>(tau + kQB);                           // kQB
+
+  // XCD-aware block -> (query block, chunk): the nqb blocks of one chunk share an XCD (same
+  // blockIdx % 8) and are dispatched back to back, so the chunk's candidate tiles come from L2.
+  const int b = blockIdx.x;
+  const int xcd = b & 7, slot = b >> 3;
+  const int chunk = xcd + 8 * (slot / a.nqb);
+  const int qb = slot % a.nqb;
+  if (chunk >= a.nchunks) return;
+  const int64_t c_begin = (int64_t)chunk * a.chunk_len;
+  int64_t c_end = c_begin + a.chunk_len;
+  if (c_end > a.N) c_end = a.N;
+
+  const int qw0 = qb * kQB + wave * 16;  // first query of this wave
+  const SegInfo& si = a.si;
+
+  // A fragments (kept in registers for the whole chunk): lane holds Zq[qw0 + (lane&15)][4t + (lane>>4)]
+  double af[KSMAX];
+  {
+    const int q = qw0 + (lane & 15);
+#pragma unroll
+    for (int t = 0; t < KSMAX; ++t) {
+      double v = 0.0;
+      if (t < a.ks && q < a.Q) v = a.Zq[(int64_t)q * si.Lp + 4 * t + (lane >> 4)];
+      af[t] = v;
+    }
+  }
+  // query stats -> LDS, list init
+  for (int i = tid; i < kQB * nsu; i += 256) {
+    const int ql = i / nsu, s = i % nsu;
+    const int q = qb * kQB + ql;
+    for (int j = 0; j < 4; ++j) qstat[i * 4 + j] = (q < a.Q) ? a.Sq[((int64_t)q * si.nseg + s) * 4 + j] : 1.0;
+  }
+  for (int i = tid; i < kQB; i += 256) {
+    mask[i] = 0ull;
+    tau[i] = -__builtin_huge_val();
+    lcnt[i] = 0;
+  }
+  // lane's best (first arg-max) for its 4 query rows
+  double best[4];
+  int64_t best_id[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { best[r] = -__builtin_huge_val(); best_id[r] = -1; }
+  __syncthreads();
+
+  const int pieces_per_row = 2 * a.ks;  // 16-byte pieces of the used K columns
+  for (int64_t cs = c_begin; cs < c_end; cs += kCB) {
+    // ---- stage candidate tile + stats -------------------------------------------------------
+    for (int p = tid; p < kCB * pieces_per_row; p += 256) {
+      const int c = p / pieces_per_row, kk = p % pieces_per_row;
+      const int64_t gc = cs + c;
+      double2 v = make_double2(0.0, 0.0);
+      if (gc < c_end) v = *reinterpret_cast<const double2*>(a.Zc + gc * si.Lp + 2 * kk);
+      *reinterpret_cast<double2*>(btile + c * a.rs + 2 * kk) = v;
+    }
+    for (int i = tid; i < kCB * nsu; i += 256) {
+      const int c = i / nsu, s = i % nsu;
+      const int64_t gc = cs + c;
+      for (int j = 0; j < 4; ++j) cstat[i * 4 + j] = (gc < c_end) ? a.Sc[(gc * si.nseg + s) * 4 + j] : 1.0;
+    }
+    __syncthreads();
+
+    // ---- contraction + epilogue ---------------------------------------------------------------
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int cl = cb * 16 + (lane & 15);        // candidate column of this lane
+      const double* brow = btile + cl * a.rs + (lane >> 4);
+      double score[4];
+      if constexpr (!OVERALL) {
+        dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int t = 0; t < KSMAX; ++t)
+          if (t < a.ks) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], brow[4 * t], acc, 0, 0, 0);
+        const double* cst = cstat + cl * nsu * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double* qst = qstat + (wave * 16 + (lane >> 4) + 4 * r) * nsu * 4;
+          score[r] = level_sim(acc[r], qst[0], qst[1], qst[2], cst[0], cst[1], cst[2], (double)si.len[0],
+                               si.inv_m[0]);
+        }
+      } else {
+        double tws[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int s = 0; s < si.nseg; ++s) {
+          dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+          const int t0 = si.poff[s] >> 2, t1 = (si.poff[s] + si.plen[s]) >> 2;
+#pragma unroll
+          for (int t = 0; t < KSMAX; ++t)
+            if (t >= t0 && t < t1) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], brow[4 * t], acc, 0, 0, 0);
+          const double* cst = cstat + (cl * nsu + s) * 4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const double* qst = qstat + ((wave * 16 + (lane >> 4) + 4 * r) * nsu + s) * 4;
+            double v = level_sim(acc[r], qst[0], qst[1], qst[2], cst[0], cst[1], cst[2], (double)si.len[s],
+                                 si.inv_m[s]);
+            tws[r] = tws[r] + v * si.w[s];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double ov = tws[r] / si.wsum;
+          ov = ov < 1.0 ? ov : 1.0;
+          score[r] = ov > 0.0 ? ov : 0.0;
+        }
+      }
+      const int64_t cid = cs + cl;
+      const bool cvalid = cid < c_end;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = wave * 16 + (lane >> 4) + 4 * r;  // query row inside the WG
+        const bool qvalid = qb * kQB + ql < a.Q;
+        const double s = score[r];
+        if (cvalid && qvalid) {
+          if (s > best[r]) { best[r] = s; best_id[r] = cid; }
+          const bool thr_ok = a.thr_mode == 0 || (a.thr_mode == 1 ? s >= a.thr : s > a.thr);
+          if (thr_ok && s > tau[ql]) {
+            stile[(wave * 16 + ((lane >> 4) + 4 * r)) * kCB + cl] = s;
+            atomicOr(&mask[ql], 1ull << cl);
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- owner lanes merge passing candidates into the sorted per-query lists -----------------
+    if (lane < 16) {
+      const int ql = wave * 16 + lane;
+      unsigned long long m = mask[ql];
+      if (m) {
+        double* ls = lscore + ql * a.K;
+        int64_t* li = lid + ql * a.K;
+        int cnt = lcnt[ql];
+        while (m) {
+          const int bit = __builtin_ctzll(m);
+          m &= m - 1;
+          const double s = stile[ql * kCB + bit];
+          const int64_t id = cs + bit;
+          if (cnt == a.K && !better(s, id, ls[a.K - 1], li[a.K - 1])) continue;
+          int pos = cnt < a.K ? cnt : a.K - 1;
+          while (pos > 0 && better(s, id, ls[pos - 1], li[pos - 1])) {
+            ls[pos] = ls[pos - 1];
+            li[pos] = li[pos - 1];
+            --pos;
+          }
+          ls[pos] = s;
+          li[pos] = id;
+          if (cnt < a.K) ++cnt;
+        }
+        lcnt[ql] = cnt;
+        tau[ql] = (cnt == a.K) ? ls[a.K - 1] : -__builtin_huge_val();
+        mask[ql] = 0ull;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- write this chunk's lists and arg-max ---------------------------------------------------
+  for (int i = tid; i < kQB * a.K; i += 256) {
+    const int ql = i / a.K, j = i % a.K;
+    const int q = qb * kQB + ql;
+    if (q >= a.Q) continue;
+    const int64_t o = ((int64_t)chunk * a.Q + q) * a.K + j;
+    if (j < lcnt[ql]) {
+      a.ws_score[o] = lscore[ql * a.K + j];
+      a.ws_id[o] = lid[ql * a.K + j] + a.id_base;
+    } else {
+      a.ws_score[o] = -__builtin_huge_val();
+      a.ws_id[o] = -1;
+    }
+  }
+  // reduce best across the 16 lanes sharing (lane >> 4): xor over the low 4 lane bits
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    double s = best[r];
+    int64_t id = best_id[r];
+    for (int o = 1; o < 16; o <<= 1) {
+      const double s2 = __shfl_xor(s, o, 64);
+      const int64_t id2 = __shfl_xor(id, o, 64);
+      if (id2 >= 0 && (id < 0 || better(s2, id2, s, id))) { s = s2; id = id2; }
+    }
+    const int q = qw0 + (lane >> 4) + 4 * r;
+    if ((lane & 15) == 0 && q < a.Q) {
+      a.ws_best[(int64_t)chunk * a.Q + q] = s;
+      a.ws_best_id[(int64_t)chunk * a.Q + q] = id >= 0 ? id + a.id_base : -1;
+    }
+  }
+}
+
+// merge nchunks sorted lists per query (one wave per query)
+__global__ __launch_bounds__(64) void k_merge(const double* __restrict__ ws_score, const int64_t* __restrict__ ws_id,
+                                              const double* __restrict__ ws_best, const int64_t* __restrict__ ws_best_id,
+                                              int nchunks, int Q, int K, double* __restrict__ out_score,
+                                              int64_t* __restrict__ out_id, double* __restrict__ out_best,
+                                              int64_t* __restrict__ out_best_id) {
+  const int lane = threadIdx.x;
+  constexpr int kPerLane = 8;  // nchunks <= 512
+  for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    int head[kPerLane];
+#pragma unroll
+    for (int i = 0; i < kPerLane; ++i) head[i] = 0;
+    for (int j = 0; j < K; ++j) {
+      // this lane's best head
+      double s = -__builtin_huge_val();
+      int64_t id = -1;
+      int which = -1;
+#pragma unroll
+      for (int i = 0; i < kPerLane; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nchunks && head[i] < K) {
+          const int64_t o = ((int64_t)c * Q + q) * K + head[i];
+          const int64_t id2 = ws_id[o];
+          const double s2 = ws_score[o];
+          if (id2 >= 0 && (id < 0 || better(s2, id2, s, id))) { s = s2; id = id2; which = i; }
+        }
+      }
+      double bs = s;
+      int64_t bid = id;
+      for (int o = 1; o < 64; o <<= 1) {
+        const double s2 = __shfl_xor(bs, o, 64);
+        const int64_t id2 = __shfl_xor(bid, o, 64);
+        if (id2 >= 0 && (bid < 0 || better(s2, id2, bs, bid))) { bs = s2; bid = id2; }
+      }
+      if (bid >= 0 && id == bid && which >= 0) {
+#pragma unroll
+        for (int i = 0; i < kPerLane; ++i)
+          if (i == which) head[i]++;
+      }
+      if (lane == 0) {
+        out_score[(int64_t)q * K + j] = bid >= 0 ? bs : -__builtin_huge_val();
+        out_id[(int64_t)q * K + j] = bid;
+      }
+    }
+    if (out_best) {
+      double s = -__builtin_huge_val();
+      int64_t id = -1;
+      for (int c = lane; c < nchunks; c += 64) {
+        const double s2 = ws_best[(int64_t)c * Q + q];
+        const int64_t id2 = ws_best_id[(int64_t)c * Q + q];
+        if (id2 >= 0 && (id < 0 || better(s2, id2, s, id))) { s = s2; id = id2; }
+      }
+      for (int o = 1; o < 64; o <<= 1) {
+        const double s2 = __shfl_xor(s, o, 64);
+        const int64_t id2 = __shfl_xor(id, o, 64);
+        if (id2 >= 0 && (id < 0 || better(s2, id2, s, id))) { s = s2; id = id2; }
+      }
+      if (lane == 0) { out_best[q] = s; out_best_id[q] = id; }
+    }
+  }
+}
+
+// progressive search final stage (search_engine.py:284-298 fallback, :340-388 re-rank), R-way.
+// lists are sorted by (level-0 score desc, id asc); det rows are [overall, level sims...].
+__global__ void k_progressive_final(int R, int Q, int M, int W, const double* __restrict__ s0,
+                                    const int64_t* __restrict__ ids, const double* __restrict__ det,
+                                    const double* __restrict__ best, const int64_t* __restrict__ best_id,
+                                    const double* __restrict__ best_det, int K, int64_t* __restrict__ out_id,
+                                    double* __restrict__ out_det, int* __restrict__ out_count) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  constexpr int kMaxR = 16;
+  int head[kMaxR];
+  for (int r = 0; r < R; ++r) head[r] = 0;
+  // survivors: global top-M by level-0; kept as (rank, slot) pairs
+  int sr[kMaxFinal], ss[kMaxFinal];
+  int n = 0;
+  for (int j = 0; j < M; ++j) {
+    int pick = -1;
+    double ps = 0.0;
+    int64_t pid = -1;
+    for (int r = 0; r < R; ++r) {
+      if (head[r] >= M) continue;
+      const int64_t o = ((int64_t)r * Q + q) * M + head[r];
+      const int64_t id = ids[o];
+      if (id < 0) continue;
+      const double s = s0[o];
+      if (pick < 0 || better(s, id, ps, pid)) { pick = r; ps = s; pid = id; }
+    }
+    if (pick < 0) break;
+    sr[n] = pick;
+    ss[n] = head[pick];
+    ++n;
+    head[pick]++;
+  }
+  const double* rowp[kMaxFinal];
+  int64_t idp[kMaxFinal];
+  if (n == 0) {
+    // none passed the threshold: keep the first arg-max of the level-0 score (:295-298)
+    int pick = -1;
+    double ps = 0.0;
+    int64_t pid = -1;
+    for (int r = 0; r < R; ++r) {
+      const int64_t id = best_id[(int64_t)r * Q + q];
+      if (id < 0) continue;
+      const double s = best[(int64_t)r * Q + q];
+      if (pick < 0 || better(s, id, ps, pid)) { pick = r; ps = s; pid = id; }
+    }
+    if (pick >= 0) {
+      rowp[0] = best_det + ((int64_t)pick * Q + q) * W;
+      idp[0] = pid;
+      n = 1;
+    }
+  } else {
+    for (int i = 0; i < n; ++i) {
+      const int64_t o = ((int64_t)sr[i] * Q + q) * M + ss[i];
+      rowp[i] = det + o * W;
+      idp[i] = ids[o];
+    }
+  }
+  // stable sort by overall score desc (insertion sort keeps the level-0 order on ties)
+  for (int i = 1; i < n; ++i) {
+    const double* rp = rowp[i];
+    const int64_t ip = idp[i];
+    int j = i;
+    while (j > 0 && rowp[j - 1][0] < rp[0]) {
+      rowp[j] = rowp[j - 1];
+      idp[j] = idp[j - 1];
+      --j;
+    }
+    rowp[j] = rp;
+    idp[j] = ip;
+  }
+  const int outn = n < K ? n : K;
+  for (int i = 0; i < K; ++i) {
+    out_id[(int64_t)q * K + i] = i < outn ? idp[i] : -1;
+    for (int w = 0; w < W; ++w) out_det[((int64_t)q * K + i) * W + w] = i < outn ? rowp[i][w] : 0.0;
+  }
+  out_count[q] = outn;
+}
+
+
+// top-k of a dense score matrix per query (one wave per query): (score desc, id asc) with the
+// threshold test, plus the first arg-max over all candidates.  Used when k exceeds the fused
+// scan's LDS lists (e.g. the reference engine's default max_candidates_per_level = 100).
+__global__ __launch_bounds__(64) void k_select(const double* __restrict__ sc, int Q, int64_t N, int k, double thr,
+                                               int thr_mode, int64_t id_base, double* __restrict__ out_s,
+                                               int64_t* __restrict__ out_id, double* __restrict__ best,
+                                               int64_t* __restrict__ best_id) {
+  const int lane = threadIdx.x;
+  for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    const double* row = sc + (int64_t)q * N;
+    // previous pick (strictly worse order follows it)
+    double ps = __builtin_huge_val();
+    int64_t pid = -1;
+    for (int j = 0; j < k; ++j) {
+      double bs = 0.0;
+      int64_t bi = -1;
+      for (int64_t c = lane; c < N; c += 64) {
+        const double s = row[c];
+        const bool ok = thr_mode == 0 || (thr_mode == 1 ? s >= thr : s > thr);
+        if (!ok) continue;
+        if (pid >= 0 && !better(ps, pid, s, c)) continue;  // must come after the previous pick
+        if (bi < 0 || better(s, c, bs, bi)) { bs = s; bi = c; }
+      }
+      for (int o = 1; o < 64; o <<= 1) {
+        const double s2 = __shfl_xor(bs, o, 64);
+        const int64_t i2 = __shfl_xor(bi, o, 64);
+        if (i2 >= 0 && (bi < 0 || better(s2, i2, bs, bi))) { bs = s2; bi = i2; }
+      }
+      if (lane == 0) {
+        out_s[(int64_t)q * k + j] = bi >= 0 ? bs : -__builtin_huge_val();
+        out_id[(int64_t)q * k + j] = bi >= 0 ? bi + id_base : -1;
+      }
+      if (bi < 0) {
+        for (int jj = j + 1 + lane; jj < k; jj += 64) {
+          out_s[(int64_t)q * k + jj] = -__builtin_huge_val();
+          out_id[(int64_t)q * k + jj] = -1;
+        }
+        break;
+      }
+      ps = bs;
+      pid = bi;
+    }
+    if (best) {
+      double bs = 0.0;
+      int64_t bi = -1;
+      for (int64_t c = lane; c < N; c += 64)
+        if (bi < 0 || better(row[c], c, bs, bi)) { bs = row[c]; bi = c; }
+      for (int o = 1; o < 64; o <<= 1) {
+        const double s2 = __shfl_xor(bs, o, 64);
+        const int64_t i2 = __shfl_xor(bi, o, 64);
+        if (i2 >= 0 && (bi < 0 || better(s2, i2, bs, bi))) { bs = s2; bi = i2; }
+      }
+      if (lane == 0) {
+        best[q] = bi >= 0 ? bs : -__builtin_huge_val();
+        best_id[q] = bi >= 0 ? bi + id_base : -1;
+      }
+    }
+  }
+}
+
+// compare_indices_at_level on raw equal-length segments (mixed-length candidate pools): the query
+// segment q[0..m) against each row of C (N x m), statistics computed in place in NumPy order.
+__global__ __launch_bounds__(256) void k_pair_raw(const double* __restrict__ q, const double* __restrict__ C, int64_t N,
+                                                  int m, double* __restrict__ out) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x) {
+    const double* x = C + c * m;
+    auto fq = [=](int k) -> double { return q[k]; };
+    auto fc = [=](int k) -> double { return x[k]; };
+    const double qm = np_sum<double>(fq, m) / (double)m;
+    const double cm = np_sum<double>(fc, m) / (double)m;
+    auto fqd = [=](int k) -> double { double d = q[k] - qm; return d * d; };
+    auto fcd = [=](int k) -> double { double d = x[k] - cm; return d * d; };
+    const double qs = sqrt(np_sum<double>(fqd, m) / (double)m);
+    const double cs = sqrt(np_sum<double>(fcd, m) / (double)m);
+    double G = 0.0;
+    if (qs != 0.0 && cs != 0.0)
+      for (int k = 0; k < m; ++k) G = fma((q[k] - qm) / qs, (x[k] - cm) / cs, G);
+    auto fqq = [=](int k) -> double { return q[k] * q[k]; };
+    auto fcc = [=](int k) -> double { return x[k] * x[k]; };
+    const double qq = np_sum<double>(fqq, m) / (double)m;
+    const double cq = np_sum<double>(fcc, m) / (double)m;
+    out[c] = level_sim(G, qm, qs, qq, cm, cs, cq, (double)m, 1.0 / (double)m);
+  }
+}
+
+// S7: (cos + 1) / 2, 0 if a norm is 0 (rag/search/engine.py:622-660, 1025-1051)
+__global__ __launch_bounds__(256) void k_cosine(const float* __restrict__ A, int Q, const float* __restrict__ B,
+                                                int64_t N, int K, double* __restrict__ out) {
+  const int64_t total = (int64_t)Q * N;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(t / N);
+    const int64_t c = t % N;
+    const float* a = A + (int64_t)q * K;
+    const float* b = B + c * K;
+    double dot = 0.0, na = 0.0, nb = 0.0;
+    for (int i = 0; i < K; ++i) {
+      const double x = a[i], y = b[i];
+      dot = fma(x, y, dot);
+      na = fma(x, x, na);
+      nb = fma(y, y, nb);
+    }
+    double r = 0.0;
+    if (na != 0.0 && nb != 0.0) r = (dot / (sqrt(na) * sqrt(nb)) + 1.0) / 2.0;
+    out[t] = r;
+  }
+}
+
+static int rs_for(int kp) {
+  int r = kp < 2 ? 2 : kp;
+  while ((r % 32) != 2) ++r;
+  return r;
+}
+
+static size_t scan_lds_bytes(int rs, int nsu, int K) {
+  return (size_t)8 * (kCB * rs + kCB * nsu * 4 + kQB * nsu * 4 + 4 * 16 * kCB + kQB * K) + (size_t)8 * kQB * K +
+         (size_t)8 * kQB + (size_t)8 * kQB + (size_t)4 * kQB + 64;
+}
+
+static void scan_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& chunk_len) {
+  nqb = (Q + kQB - 1) / kQB;
+  // aim for ~2 waves of workgroups over 256 CUs; nchunks multiple of 8 (XCD mapping), <= 512
+  int64_t target = (2048 + nqb - 1) / nqb;
+  if (target < 8) target = 8;
+  int64_t max_chunks = (N + kCB - 1) / kCB;
+  if (target > max_chunks) target = max_chunks;
+  if (target > 512) target = 512;
+  nchunks = (int)(((target + 7) / 8) * 8);
+  if (nchunks < 8) nchunks = 8;
+  chunk_len = (N + nchunks - 1) / nchunks;
+  chunk_len = ((chunk_len + kCB - 1) / kCB) * kCB;
+  if (chunk_len < kCB) chunk_len = kCB;
+}
+
+template <int KSMAX, bool OVERALL>
+static int launch_scan(const ScanArgs& a, hipStream_t s) {
+  const size_t lds = scan_lds_bytes(a.rs, a.nseg_used, a.K);
+  HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_scan<KSMAX, OVERALL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds));
+  const int grid = a.nqb * a.nchunks;
+  hipLaunchKernelGGL((k_scan<KSMAX, OVERALL>), dim3(grid), dim3(256), lds, s, a);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+}  // namespace hq
+
+using namespace hq;
+
+extern "C" {
+
+int hq_seg_count(int L) {
+  SegInfo si;
+  seg_info(L, si);
+  return si.nseg;
+}
+
+int hq_seg_padded_len(int L) {
+  SegInfo si;
+  seg_info(L, si);
+  return si.Lp;
+}
+
+int hq_seg_prepare(const double* idx, int64_t N, int L, double* Z, double* stats, hq_stream_t stream) {
+  if (L <= 0 || N < 0) return fail(HQ_E_INVALID, "bad shape N=%lld L=%d", (long long)N, L);
+  if (N == 0) return HQ_OK;
+  if (!idx || !Z || !stats) return fail(HQ_E_INVALID, "null buffer");
+  SegInfo si;
+  seg_info(L, si);
+  if (si.nseg == 0) return fail(HQ_E_INVALID, "no level structure for L=%d", L);
+  const int64_t total = N * si.nseg;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(k_seg_prepare, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, idx, N, si, Z, stats);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+int hq_level_scores(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc, int64_t N,
+                    int L, int level, double* scores, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || L <= 0) return fail(HQ_E_INVALID, "bad shape");
+  if (Q == 0 || N == 0) return HQ_OK;
+  if (!Zq || !Sq || !Zc || !Sc || !scores) return fail(HQ_E_INVALID, "null buffer");
+  SegInfo si;
+  seg_info(L, si);
+  const int64_t total = (int64_t)Q * N;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(k_level_scores, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, Zq, Sq, Q, Zc, Sc, N, si,
+                     level, scores);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+size_t hq_scan_workspace_size(int Q, int64_t N, int k) {
+  int nqb, nchunks;
+  int64_t chunk_len;
+  scan_geometry(Q, N, nqb, nchunks, chunk_len);
+  return (size_t)nchunks * Q * k * 16 + (size_t)nchunks * Q * 16 + 256;
+}
+
+int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc, int64_t N, int L,
+                 int mode, int k, double threshold, int thr_mode, int64_t id_base, void* workspace,
+                 size_t workspace_bytes, double* out_score, int64_t* out_id, double* out_best,
+                 int64_t* out_best_id, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || L <= 0) return fail(HQ_E_INVALID, "bad shape");
+  if (k <= 0 || k > kMaxTopK) return fail(HQ_E_UNSUPPORTED, "k=%d (1..%d)", k, kMaxTopK);
+  if (mode != 0 && mode != 1) return fail(HQ_E_INVALID, "mode %d", mode);
+  if (Q == 0) return HQ_OK;
+  if (!out_score || !out_id) return fail(HQ_E_INVALID, "null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  if (N == 0) {
+    HQ_CHECK_HIP(hipMemsetAsync(out_id, 0xFF, sizeof(int64_t) * Q * k, s));
+    if (out_best_id) HQ_CHECK_HIP(hipMemsetAsync(out_best_id, 0xFF, sizeof(int64_t) * Q, s));
+    return HQ_OK;
+  }
+  if (!Zq || !Sq || !Zc || !Sc || !workspace) return fail(HQ_E_INVALID, "null buffer");
+  if (workspace_bytes < hq_scan_workspace_size(Q, N, k)) return fail(HQ_E_INVALID, "workspace too small");
+  ScanArgs a;
+  a.Zq = Zq; a.Sq = Sq; a.Q = Q; a.Zc = Zc; a.Sc = Sc; a.N = N;
+  seg_info(L, a.si);
+  const int kp = mode == 0 ? a.si.plen[0] : a.si.Lp;
+  a.ks = kp / 4;
+  a.nseg_used = mode == 0 ? 1 : a.si.nseg;
+  a.rs = rs_for(kp);
+  a.K = k;
+  a.thr = threshold;
+  a.thr_mode = thr_mode;
+  a.id_base = id_base;
+  scan_geometry(Q, N, a.nqb, a.nchunks, a.chunk_len);
+  uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
+  a.ws_score = reinterpret_cast<double*>(ws);
+  a.ws_id = reinterpret_cast<int64_t*>(ws + (size_t)a.nchunks * Q * k * 8);
+  a.ws_best = reinterpret_cast<double*>(ws + (size_t)a.nchunks * Q * k * 16);
+  a.ws_best_id = reinterpret_cast<int64_t*>(ws + (size_t)a.nchunks * Q * k * 16 + (size_t)a.nchunks * Q * 8);
+  int rc;
+  if (mode == 0) {
+    if (a.ks <= 8) rc = launch_scan<8, false>(a, s);
+    else if (a.ks <= 16) rc = launch_scan<16, false>(a, s);
+    else if (a.ks <= 32) rc = launch_scan<32, false>(a, s);
+    else if (a.ks <= 64) rc = launch_scan<64, false>(a, s);
+    else return fail(HQ_E_UNSUPPORTED, "level-0 segment too long (%d)", kp);
+  } else {
+    if (a.ks <= 8) rc = launch_scan<8, true>(a, s);
+    else if (a.ks <= 16) rc = launch_scan<16, true>(a, s);
+    else if (a.ks <= 32) rc = launch_scan<32, true>(a, s);
+    else if (a.ks <= 64) rc = launch_scan<64, true>(a, s);
+    else return fail(HQ_E_UNSUPPORTED, "index too long for the fused scan (Lp=%d)", kp);
+  }
+  if (rc) return rc;
+  int mg = Q < 4096 ? Q : 4096;
+  hipLaunchKernelGGL(k_merge, dim3(mg), dim3(64), 0, s, a.ws_score, a.ws_id, a.ws_best, a.ws_best_id, a.nchunks, Q,
+                     k, out_score, out_id, out_best, out_best_id);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+int hq_rescore(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc, int64_t N, int L,
+               const int64_t* ids, int k, int64_t id_base, double* out, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || L <= 0 || k < 0) return fail(HQ_E_INVALID, "bad shape");
+  if (Q == 0 || k == 0) return HQ_OK;
+  if (!Zq || !Sq || !ids || !out || (N > 0 && (!Zc || !Sc))) return fail(HQ_E_INVALID, "null buffer");
+  SegInfo si;
+  seg_info(L, si);
+  const int64_t total = (int64_t)Q * k;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(k_rescore, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, Zq, Sq, Q, Zc, Sc, N, si, ids, k,
+                     id_base, out);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+int hq_progressive_final(int R, int Q, int M, int nseg, const double* s0, const int64_t* ids, const double* det,
+                         const double* best, const int64_t* best_id, const double* best_det, int K,
+                         int64_t* out_id, double* out_det, int* out_count, hq_stream_t stream) {
+  if (R <= 0 || R > 16 || Q < 0 || M <= 0 || M > kMaxFinal || K <= 0 || nseg < 0 || nseg >= kMaxSeg)
+    return fail(HQ_E_INVALID, "bad sizes R=%d Q=%d M=%d K=%d", R, Q, M, K);
+  if (Q == 0) return HQ_OK;
+  if (!s0 || !ids || !det || !best || !best_id || !best_det || !out_id || !out_det || !out_count)
+    return fail(HQ_E_INVALID, "null buffer");
+  const int W = 1 + nseg;
+  hipLaunchKernelGGL(k_progressive_final, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, R, Q, M, W, s0, ids,
+                     det, best, best_id, best_det, K, out_id, out_det, out_count);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+int hq_select_topk(const double* scores, int Q, int64_t N, int k, double threshold, int thr_mode, int64_t id_base,
+                   double* out_score, int64_t* out_id, double* out_best, int64_t* out_best_id, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || k <= 0) return fail(HQ_E_INVALID, "bad shape");
+  if (Q == 0) return HQ_OK;
+  if (!out_score || !out_id || (N > 0 && !scores)) return fail(HQ_E_INVALID, "null buffer");
+  int grid = Q < 4096 ? Q : 4096;
+  hipLaunchKernelGGL(k_select, dim3(grid), dim3(64), 0, (hipStream_t)stream, scores, Q, N, k, threshold, thr_mode,
+                     id_base, out_score, out_id, out_best, out_best_id);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+int hq_pair_scores_raw(const double* q, const double* C, int64_t N, int m, double* out, hq_stream_t stream) {
+  if (N < 0 || m <= 0) return fail(HQ_E_INVALID, "bad shape");
+  if (N == 0) return HQ_OK;
+  if (!q || !C || !out) return fail(HQ_E_INVALID, "null buffer");
+  int64_t blocks = (N + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_pair_raw, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, q, C, N, m, out);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+int hq_cosine_scores(const float* a, int Q, const float* b, int64_t N, int K, double* out, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || K < 0) return fail(HQ_E_INVALID, "bad shape");
+  if (Q == 0 || N == 0) return HQ_OK;
+  if (!a || !b || !out) return fail(HQ_E_INVALID, "null buffer");
+  const int64_t total = (int64_t)Q * N;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(k_cosine, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, a, Q, b, N, K, out);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,117 @@
+"""ctypes binding of libhq_mi355x.so (include/hq_mi355x.h).
+
+The library is built in-tree (`make -C hilbert-quantization_amd/csrc`, or `__graft_entry__.build()`)
+and loaded from this directory.  There is no fallback: if the library is missing or the process has
+no GPU, every product entry point raises instead of computing anything on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhq_mi355x.so")
+
+HQ_OK = 0
+HQ_E_INVALID = -1
+HQ_E_NOT_POW2 = -2
+HQ_E_TOO_MANY = -3
+HQ_E_HIP = -4
+HQ_E_UNSUPPORTED = -5
+
+DT = {"float32": 0, "float64": 1, "float16": 2, "bfloat16": 3, "int8": 4, "uint8": 5, "int16": 6,
+      "int32": 7, "int64": 8, "uint16": 6, "uint32": 7, "uint64": 8, "bool": 5}
+
+_c = ctypes
+_i = _c.c_int
+_i64 = _c.c_int64
+_p = _c.c_void_p
+_d = _c.c_double
+_sz = _c.c_size_t
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "hq_version": (_i, []),
+    "hq_last_error": (_c.c_char_p, []),
+    "hq_hilbert_table": (_i, [_i, _p, _p, _p, _p]),
+    "hq_map_to_2d": (_i, [_i, _p, _i64, _i64, _i, _i, _p, _p]),
+    "hq_map_from_2d": (_i, [_i, _p, _i64, _i, _i, _p, _p]),
+    "hq_index_streaming": (_i, [_i, _p, _i64, _i, _i, _i, _p, _p]),
+    "hq_index_traditional_f32": (_i, [_p, _i64, _i, _i, _p, _p]),
+    "hq_rag_index_rows": (_i, [_i]),
+    "hq_block_means_f32": (_i, [_p, _i64, _i, _i, _i, _p, _p]),
+    "hq_index_rag_f32": (_i, [_p, _i64, _i, _p, _p]),
+    "hq_quantize_u8": (_i, [_p, _i64, _i, _i, _p, _p, _p]),
+    "hq_dequantize_u8": (_i, [_p, _i64, _i, _i, _p, _p, _p]),
+    "hq_map_index_quantize": (_i, [_p, _i64, _i64, _i, _i, _i, _p, _p, _p, _p]),
+    "hq_chunk_encode_f16": (_i, [_p, _i64, _i, _p, _p, _p, _p]),
+    "hq_parse_structure": (_i, [_i, _p, _i]),
+    "hq_seg_count": (_i, [_i]),
+    "hq_seg_padded_len": (_i, [_i]),
+    "hq_seg_prepare": (_i, [_p, _i64, _i, _p, _p, _p]),
+    "hq_level_scores": (_i, [_p, _p, _i, _p, _p, _i64, _i, _i, _p, _p]),
+    "hq_scan_workspace_size": (_sz, [_i, _i64, _i]),
+    "hq_scan_topk": (_i, [_p, _p, _i, _p, _p, _i64, _i, _i, _i, _d, _i, _i64, _p, _sz, _p, _p, _p, _p, _p]),
+    "hq_rescore": (_i, [_p, _p, _i, _p, _p, _i64, _i, _p, _i, _i64, _p, _p]),
+    "hq_progressive_final": (_i, [_i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
+    "hq_cosine_scores": (_i, [_p, _i, _p, _i64, _i, _p, _p]),
+    "hq_select_topk": (_i, [_p, _i, _i64, _i, _d, _i, _i64, _p, _p, _p, _p, _p]),
+    "hq_pair_scores_raw": (_i, [_p, _p, _i64, _i, _p, _p]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class NativeLibraryError(RuntimeError):
+    """The HIP library is missing or failed; no CPU fallback exists."""
+
+
+def load(path: str = LIB_PATH):
+    """Load the shared library (no device needed: used by the CPU export test too)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise NativeLibraryError(
+                f"{path} not found: build it with `make -C hilbert-quantization_amd/csrc` "
+                "(or __graft_entry__.build()); hq_mi355x has no CPU fallback")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def lib():
+    """The library, on a process that can run kernels (a GPU must be visible)."""
+    import torch
+    if not torch.cuda.is_available():
+        raise NativeLibraryError("hq_mi355x needs an MI355X (torch.cuda.is_available() is False); "
+                                 "there is no CPU fallback")
+    return load()
+
+
+def last_error() -> str:
+    l = load()
+    msg = l.hq_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, exc=None):
+    """Raise `exc` (or NativeLibraryError) with the library's message when rc != 0."""
+    if rc == HQ_OK:
+        return
+    msg = last_error()
+    if exc is None:
+        raise NativeLibraryError(f"libhq_mi355x error {rc}: {msg}")
+    raise exc(msg)
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,66 @@
+"""MPEGAICompressorImpl on MI355X: the uint8 normalise stage.
+
+`_normalize_for_compression` / `_denormalize_from_compression` keep the reference's instance-state
+semantics (core/compressor.py:256-303): a non-constant image stores (min, max) on the instance, a
+constant image returns 128s and leaves the state untouched, and de-normalising without state is
+u8 / 255.  The arithmetic runs in hq_quantize_u8 / hq_dequantize_u8.  The JPEG ("MPEG-AI") codec
+after it is outside the hot path; `compress`/`decompress` wrap PIL on the host
+exactly where the reference does so the pipeline stays usable end to end.
+"""
+from __future__ import annotations
+
+import io
+from typing import Optional
+
+import numpy as np
+
+from .. import kernels as K
+from .._dev import to_dev, to_np
+from ..exceptions import CompressionError
+
+
+class MPEGAICompressorImpl:
+    def __init__(self, config: Optional[object] = None):
+        self.config = config
+        self._last_compression_metrics = None
+
+    def _normalize_for_compression(self, image):
+        img = np.asarray(image)
+        if img.dtype != np.float32:
+            raise CompressionError(f"GPU normalise implements the float32 frame path, got {img.dtype}")
+        u8, mm = K.quantize_u8(to_dev(img), CompressionError)
+        mm = to_np(mm)
+        if mm[1] != mm[0]:
+            self._norm_min = np.float32(mm[0])
+            self._norm_max = np.float32(mm[1])
+        return to_np(u8)
+
+    def _denormalize_from_compression(self, image):
+        u8 = np.asarray(image, dtype=np.uint8)
+        if not hasattr(self, "_norm_min") or not hasattr(self, "_norm_max"):
+            mm = np.array([0.0, 1.0], dtype=np.float32)   # u8 / 255 * 1 + 0 == u8 / 255 exactly
+        else:
+            mm = np.array([self._norm_min, self._norm_max], dtype=np.float32)
+        return to_np(K.dequantize_u8(to_dev(u8), to_dev(mm), CompressionError))
+
+    def compress(self, image, quality: float) -> bytes:
+        if not 0.0 <= quality <= 1.0:
+            raise CompressionError(f"Quality must be between 0.0 and 1.0, got {quality}")
+        try:
+            from PIL import Image
+        except ImportError as e:  # codec is optional, the normalise stage is not
+            raise CompressionError(f"JPEG codec unavailable: {e}")
+        u8 = self._normalize_for_compression(image)
+        buf = io.BytesIO()
+        Image.fromarray(u8, mode="L").save(buf, format="JPEG", quality=int(quality * 95), optimize=True)
+        return buf.getvalue()
+
+    def decompress(self, compressed_data: bytes):
+        from PIL import Image
+        u8 = np.array(Image.open(io.BytesIO(compressed_data)))
+        return self._denormalize_from_compression(u8)
+
+    def estimate_compression_ratio(self, original_size: int, compressed_size: int) -> float:
+        if compressed_size <= 0:
+            raise ValueError("Compressed size must be positive")
+        return original_size / compressed_size

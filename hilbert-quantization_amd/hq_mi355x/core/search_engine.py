@@ -1,0 +1,263 @@
+"""Progressive similarity search on MI355X.
+
+`ProgressiveSimilaritySearchEngine` is the drop-in for the reference's core/search_engine.py:23-388
+(same constructor, methods, ordering and result objects); `IndexCorpus` is the batched device-
+resident form: index vectors are prepared once (hq_seg_prepare) and a query batch is answered by the
+fused MFMA scan (hq_scan_topk) + re-scoring (hq_rescore) + final ranking (hq_progressive_final).
+
+Ordering contract (reference): candidates are ranked by score descending with Python's stable sort,
+i.e. ties keep candidate-pool order — (score desc, pool index asc).  Progressive search keeps the
+level-0 top `max_candidates_per_level` among sims >= threshold (first arg-max if none pass), then
+stable-sorts those survivors by the overall score.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .. import kernels as K
+from .._dev import is_tensor, to_dev, to_np, torch
+from ..models import QuantizedModel, SearchResult
+
+MAX_FUSED_K = 64
+
+
+@dataclass
+class LevelConfig:
+    grid_size: int
+    start_index: int
+    end_index: int
+    is_offset_sampling: bool = False
+
+
+def _f64(x):
+    t = torch()
+    return to_dev(x, t.float64)
+
+
+class IndexCorpus:
+    """A corpus of equal-length hierarchical index vectors resident in HBM.
+
+    `indices`: [N, L] (NumPy or device tensor); `id_base`: global id of row 0 (corpus shards)."""
+
+    def __init__(self, indices, id_base: int = 0):
+        x = _f64(indices)
+        if x.dim() != 2:
+            raise ValueError("IndexCorpus expects a 2-D [N, L] array of index vectors")
+        self.N, self.L = int(x.shape[0]), int(x.shape[1])
+        self.id_base = int(id_base)
+        self.prep = K.seg_prepare(x)
+        self.nseg = self.prep.nseg
+
+    def prepare_queries(self, queries) -> "K.Prepared":
+        q = _f64(queries)
+        if q.dim() == 1:
+            q = q.view(1, -1)
+        if q.shape[1] != self.L:
+            raise ValueError(f"query index length {q.shape[1]} != corpus index length {self.L}")
+        return K.seg_prepare(q)
+
+    # ---- scores ------------------------------------------------------------------------------
+    def level_scores(self, queries, level: int):
+        """Dense [Q, N]: level >= 0 -> compare_indices_at_level, -1 -> overall similarity."""
+        return K.level_scores(self.prepare_queries(queries), self.prep, level)
+
+    def _topk(self, qp, mode: int, k: int, thr: float, thr_mode: int):
+        if k <= MAX_FUSED_K:
+            return K.scan_topk(qp, self.prep, mode, k, thr, thr_mode, self.id_base)
+        sc = K.level_scores(qp, self.prep, 0 if mode == 0 else -1)
+        return K.select_topk(sc, k, thr, thr_mode, self.id_base)
+
+    # ---- searches ----------------------------------------------------------------------------
+    def brute_force(self, queries, max_results: int):
+        """search_engine.py:302-338 for a query batch -> (ids [Q, K], overall [Q, K], levels [Q, K, nseg])."""
+        qp = self.prepare_queries(queries)
+        k = max(1, min(int(max_results), self.N)) if self.N else 1
+        sc, ids, _, _ = self._topk(qp, 1, k, 0.0, 0)
+        det = K.rescore(qp, self.prep, ids, self.id_base)
+        return ids, det[..., 0], det[..., 1:]
+
+    def progressive(self, queries, max_results: int, threshold: float = 0.1, max_candidates_per_level: int = 100):
+        """search_engine.py:232-300 + :340-388 for a query batch.
+        Returns (ids [Q, K], overall [Q, K], levels [Q, K, nseg], count [Q]) with K = max_results;
+        rows are padded with id -1 beyond count."""
+        t = torch()
+        qp = self.prepare_queries(queries)
+        Q = qp.N
+        K_out = max(1, int(max_results))
+        M = int(max_candidates_per_level)
+        if self.N <= M:
+            # the level loop never filters (:298): every candidate is re-scored and stable-sorted
+            ids, ov, lv = self.brute_force(queries, min(K_out, max(self.N, 1)))
+            cnt = (ids >= 0).sum(dim=1).to(t.int32)
+            return ids, ov, lv, cnt
+        s0, ids, best, bid = self._topk(qp, 0, M, float(threshold), 1)
+        det = K.rescore(qp, self.prep, ids, self.id_base)
+        bdet = K.rescore(qp, self.prep, bid.view(Q, 1), self.id_base).view(Q, -1)
+        oid, odet, cnt = K.progressive_final(s0.unsqueeze(0), ids.unsqueeze(0), det.unsqueeze(0), best.unsqueeze(0),
+                                             bid.unsqueeze(0), bdet.unsqueeze(0), K_out)
+        return oid, odet[..., 0], odet[..., 1:], cnt
+
+    def frame_search(self, queries, max_results: int, threshold: float = 0.1):
+        """core/video_search.py:215-264: level-0 sim > threshold (strict), stable sort, top-k."""
+        qp = self.prepare_queries(queries)
+        k = max(1, int(max_results))
+        sc, ids, _, _ = self._topk(qp, 0, k, float(threshold), 2)
+        return ids, sc
+
+
+class ProgressiveSimilaritySearchEngine:
+    """Drop-in for core/search_engine.py:23 (interfaces.py:191-225 SimilaritySearchEngine)."""
+
+    def __init__(self, similarity_threshold: float = 0.1, max_candidates_per_level: int = 100):
+        self.similarity_threshold = similarity_threshold
+        self.max_candidates_per_level = max_candidates_per_level
+
+    # ---- structure -----------------------------------------------------------------------------
+    def _parse_index_structure(self, indices, total_space: int) -> List[LevelConfig]:
+        if len(indices) == 0 or total_space <= 0:
+            return []
+        levels = [LevelConfig(g, s, e, off) for (g, s, e, off) in K.parse_structure(int(total_space))]
+        # the reference stops consuming at len(indices) (:115, :142-147); callers pass len(indices)
+        return [lv for lv in levels if lv.start_index < len(indices)]
+
+    # ---- pair scores ---------------------------------------------------------------------------
+    def _scores_at_level(self, q: np.ndarray, cands: Sequence[np.ndarray], level: int) -> np.ndarray:
+        """compare_indices_at_level(q, c, level) for every candidate, on the GPU."""
+        N = len(cands)
+        out = np.zeros(N)
+        if len(q) == 0 or N == 0:
+            return out
+        ql = self._parse_index_structure(q, len(q))
+        if level >= len(ql):
+            return out
+        groups: Dict[int, List[int]] = {}
+        for i, c in enumerate(cands):
+            groups.setdefault(len(c), []).append(i)
+        for Lc, members in groups.items():
+            if Lc == 0:
+                continue
+            C = np.stack([np.asarray(cands[i], dtype=np.float64) for i in members])
+            if Lc == len(q):
+                corpus = IndexCorpus(C)
+                s = to_np(corpus.level_scores(np.asarray(q, dtype=np.float64)[None], level))[0]
+            else:
+                cl = self._parse_index_structure(C[0], Lc)
+                if level >= len(cl):
+                    continue
+                qs, qe = ql[level].start_index, ql[level].end_index
+                cs, ce = cl[level].start_index, cl[level].end_index
+                m = min(qe - qs, ce - cs)
+                if m <= 0:
+                    continue
+                qseg = np.asarray(q, dtype=np.float64)[qs:qs + m]
+                s = to_np(K.pair_scores_raw(_f64(qseg), _f64(np.ascontiguousarray(C[:, cs:cs + m]))))
+            out[members] = s
+        return out
+
+    def compare_indices_at_level(self, query_indices, candidate_indices, level: int) -> float:
+        if len(query_indices) == 0 or len(candidate_indices) == 0:
+            return 0.0
+        return float(self._scores_at_level(np.asarray(query_indices), [np.asarray(candidate_indices)], level)[0])
+
+    def _calculate_overall_similarity(self, query_indices, candidate_indices) -> Tuple[float, Dict[int, float]]:
+        ov, lv = self._overall_many(np.asarray(query_indices), [np.asarray(candidate_indices)])
+        if lv.shape[1] == 0:
+            return 0.0, {}
+        return float(ov[0]), {i: float(lv[0, i]) for i in range(lv.shape[1])}
+
+    def _overall_many(self, q: np.ndarray, cands: Sequence[np.ndarray]):
+        ql = self._parse_index_structure(q, len(q))
+        N = len(cands)
+        if not ql:
+            return np.zeros(N), np.zeros((N, 0))
+        if all(len(c) == len(q) for c in cands) and N:
+            corpus = IndexCorpus(np.stack([np.asarray(c, dtype=np.float64) for c in cands]))
+            qp = corpus.prepare_queries(np.asarray(q, dtype=np.float64)[None])
+            ids = torch().arange(N, device=qp.Z.device).view(1, N)
+            det = to_np(K.rescore(qp, corpus.prep, ids))[0]
+            return det[:, 0], det[:, 1:]
+        lv = np.stack([self._scores_at_level(q, cands, l) for l in range(len(ql))], axis=1)
+        tws = np.zeros(N)
+        tw = 0.0
+        for l in range(len(ql)):
+            w = 1.0 / (l + 1)
+            tws = tws + lv[:, l] * w
+            tw += w
+        return np.clip(tws / tw, 0.0, 1.0), lv
+
+    # ---- searches ------------------------------------------------------------------------------
+    @staticmethod
+    def _uniform(q, pool) -> bool:
+        return all(len(c.hierarchical_indices) == len(q) for c in pool)
+
+    def _results(self, pool, ids, ov, lv, count=None, with_error=True) -> List[SearchResult]:
+        out = []
+        n = len(ids) if count is None else int(count)
+        for j in range(n):
+            i = int(ids[j])
+            if i < 0:
+                break
+            sim = float(min(1.0, max(0.0, ov[j])))
+            err = max(0.0, 1.0 - float(ov[j])) if with_error else 0.0
+            out.append(SearchResult(model=pool[i], similarity_score=sim,
+                                    matching_indices={l: float(lv[j, l]) for l in range(lv.shape[1])},
+                                    reconstruction_error=err))
+        return out
+
+    def brute_force_search(self, query_indices, candidate_pool: List[QuantizedModel],
+                           max_results: int) -> List[SearchResult]:
+        if len(query_indices) == 0 or not candidate_pool:
+            return []
+        q = np.asarray(query_indices, dtype=np.float64)
+        if self._uniform(q, candidate_pool):
+            corpus = IndexCorpus(np.stack([np.asarray(c.hierarchical_indices, dtype=np.float64)
+                                           for c in candidate_pool]))
+            ids, ov, lv = corpus.brute_force(q[None], min(max_results, len(candidate_pool)))
+            return self._results(candidate_pool, to_np(ids)[0], to_np(ov)[0], to_np(lv)[0], with_error=False)
+        ov, lv = self._overall_many(q, [c.hierarchical_indices for c in candidate_pool])
+        order = np.argsort(-ov, kind="stable")[:max_results]
+        return self._results(candidate_pool, order, ov[order], lv[order], with_error=False)
+
+    def progressive_search(self, query_indices, candidate_pool: List[QuantizedModel],
+                           max_results: int) -> List[SearchResult]:
+        if len(query_indices) == 0 or not candidate_pool:
+            return []
+        q = np.asarray(query_indices, dtype=np.float64)
+        if not self._parse_index_structure(q, len(q)):
+            return []
+        if self._uniform(q, candidate_pool):
+            corpus = IndexCorpus(np.stack([np.asarray(c.hierarchical_indices, dtype=np.float64)
+                                           for c in candidate_pool]))
+            ids, ov, lv, cnt = corpus.progressive(q[None], max_results, self.similarity_threshold,
+                                                  self.max_candidates_per_level)
+            return self._results(candidate_pool, to_np(ids)[0], to_np(ov)[0], to_np(lv)[0], int(to_np(cnt)[0]))
+        return self._progressive_mixed(q, candidate_pool, max_results)
+
+    def _progressive_mixed(self, q, pool, max_results):
+        """Candidate pools of mixed index length: scores from the GPU, the reference's level loop
+        (:254-300) applied to them."""
+        cands = [np.asarray(c.hierarchical_indices) for c in pool]
+        nl = len(self._parse_index_structure(q, len(q)))
+        cur = np.arange(len(pool))
+        prev: Dict[int, np.ndarray] = {}
+        for lv in range(nl):
+            if len(cur) <= self.max_candidates_per_level:
+                break
+            s = self._scores_at_level(q, [cands[i] for i in cur], lv)
+            now = dict(prev)
+            now[lv] = s
+            tw = sum(1.0 / (i + 1) for i in now)
+            comb = sum(now[i] * (1.0 / (i + 1)) for i in now) / tw
+            keep = np.nonzero(s >= self.similarity_threshold)[0]
+            if len(keep):
+                keep = keep[np.argsort(-comb[keep], kind="stable")][: self.max_candidates_per_level]
+            else:
+                keep = np.array([int(np.argmax(s))])
+            cur = cur[keep]
+            prev = {k: v[keep] for k, v in now.items()}
+        ov, lvs = self._overall_many(q, [cands[i] for i in cur])
+        order = np.argsort(-ov, kind="stable")[:max_results]
+        return self._results(pool, cur[order], ov[order], lvs[order])

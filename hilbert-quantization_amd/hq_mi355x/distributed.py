@@ -1,0 +1,120 @@
+"""Corpus sharding across GPUs: one process per GPU, the corpus split into contiguous
+global-id ranges, every rank answering the whole query batch against its shard, and ONE all-gather
+(torch.distributed, backend "nccl" = RCCL over xGMI) of fixed-size per-shard records, merged on
+every rank by the same (score desc, global id asc) rule that reproduces the single-GPU order.
+
+The reference has no distributed component; its closest analogue is the per-video thread fan-out
+plus list-concatenation merge of core/video_search.py:722-875.
+
+Record layout per (query, slot), float64: [score, id, det_0 .. det_{W-1}] where det = [overall,
+level sims...] from hq_rescore; ids are integers < 2^53 so the f64 round trip is exact.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+from . import kernels as K
+from ._dev import torch
+from .core.search_engine import IndexCorpus, MAX_FUSED_K
+
+
+def shard_range(n_total: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous [start, end) global-id range of a rank (balanced, ranks in order)."""
+    base, extra = divmod(n_total, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def pack(scores, ids, det):
+    """[Q, M] scores, [Q, M] ids, [Q, M, W] det -> f64 [Q, M, 2 + W] records."""
+    t = torch()
+    return t.cat([scores.unsqueeze(-1).to(t.float64), ids.unsqueeze(-1).to(t.float64), det.to(t.float64)], dim=-1)
+
+
+def unpack(rec):
+    """[..., 2 + W] records -> (scores, ids int64, det)."""
+    t = torch()
+    return rec[..., 0].contiguous(), rec[..., 1].round().to(t.int64).contiguous(), rec[..., 2:].contiguous()
+
+
+def all_gather(x, group=None):
+    """Stack of every rank's tensor [R, ...] (one collective; RCCL on GPU tensors, gloo on CPU)."""
+    t = torch()
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
+        return x.unsqueeze(0)
+    world = dist.get_world_size(group)
+    out = [t.empty_like(x) for _ in range(world)]
+    dist.all_gather(out, x.contiguous(), group=group)
+    return t.stack(out, 0)
+
+
+class ShardedIndexCorpus:
+    """This rank's shard of a global corpus of index vectors (global ids start at `id_base`)."""
+
+    def __init__(self, local_indices, id_base: int, n_total: int, group=None):
+        self.local = IndexCorpus(local_indices, id_base=id_base)
+        self.n_total = int(n_total)
+        self.group = group
+
+    def _local_lists(self, qp, mode: int, k: int, thr: float, thr_mode: int):
+        c = self.local
+        if k <= MAX_FUSED_K:
+            return K.scan_topk(qp, c.prep, mode, k, thr, thr_mode, c.id_base)
+        sc = K.level_scores(qp, c.prep, 0 if mode == 0 else -1)
+        return K.select_topk(sc, k, thr, thr_mode, c.id_base)
+
+    def progressive(self, queries, max_results: int, threshold: float = 0.1, max_candidates_per_level: int = 100):
+        """Global progressive search; every rank returns the same (ids, overall, levels, count)."""
+        t = torch()
+        c = self.local
+        qp = c.prepare_queries(queries)
+        Q = qp.N
+        M = int(max_candidates_per_level)
+        if self.n_total <= M:
+            return self.brute_force(queries, max_results)
+        s0, ids, best, bid = self._local_lists(qp, 0, M, float(threshold), 1)
+        det = K.rescore(qp, c.prep, ids, c.id_base)
+        bdet = K.rescore(qp, c.prep, bid.view(Q, 1), c.id_base)
+        rec = t.cat([pack(s0, ids, det), pack(best.view(Q, 1), bid.view(Q, 1), bdet)], dim=1)  # [Q, M+1, 2+W]
+        g = all_gather(rec, self.group)  # [R, Q, M+1, 2+W]
+        gs, gi, gd = unpack(g[:, :, :M])
+        bs, bi, bd = unpack(g[:, :, M])
+        oid, odet, cnt = K.progressive_final(gs, gi, gd, bs, bi, bd, int(max_results))
+        return oid, odet[..., 0], odet[..., 1:], cnt
+
+    def brute_force(self, queries, max_results: int):
+        """Global top-k by the overall score: local top-k, all-gather, R-way merge."""
+        t = torch()
+        c = self.local
+        qp = c.prepare_queries(queries)
+        Q = qp.N
+        k = max(1, int(max_results))
+        sc, ids, _, _ = self._local_lists(qp, 1, k, 0.0, 0)
+        det = K.rescore(qp, c.prep, ids, c.id_base)
+        g = all_gather(pack(sc, ids, det), self.group)
+        gs, gi, gd = unpack(g)
+        R = g.shape[0]
+        none_s = t.full((R, Q), -float("inf"), dtype=t.float64, device=g.device)
+        none_i = t.full((R, Q), -1, dtype=t.int64, device=g.device)
+        none_d = t.zeros((R, Q, gd.shape[-1]), dtype=t.float64, device=g.device)
+        # lists are sorted by overall (score desc, id asc); the final stable sort by overall keeps it
+        oid, odet, cnt = K.progressive_final(gs, gi, gd, none_s, none_i, none_d, k)
+        return oid, odet[..., 0], odet[..., 1:], cnt
+
+    def frame_search(self, queries, max_results: int, threshold: float = 0.1):
+        """Global level-0 scan (> threshold), merged across shards."""
+        t = torch()
+        c = self.local
+        qp = c.prepare_queries(queries)
+        Q = qp.N
+        k = max(1, int(max_results))
+        sc, ids, _, _ = self._local_lists(qp, 0, k, float(threshold), 2)
+        g = all_gather(pack(sc, ids, sc.unsqueeze(-1)), self.group)
+        gs, gi, gd = unpack(g)
+        R = g.shape[0]
+        none_s = t.full((R, Q), -float("inf"), dtype=t.float64, device=g.device)
+        none_i = t.full((R, Q), -1, dtype=t.int64, device=g.device)
+        none_d = t.zeros((R, Q, 1), dtype=t.float64, device=g.device)
+        oid, odet, cnt = K.progressive_final(gs, gi, gd, none_s, none_i, none_d, k)
+        return oid, odet[..., 0], cnt

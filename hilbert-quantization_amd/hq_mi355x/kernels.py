@@ -1,0 +1,336 @@
+"""Tensor-level entry points: one function per C-ABI call of libhq_mi355x (include/hq_mi355x.h).
+
+Inputs and outputs are device tensors (torch on ROCm, used only as HBM buffers); every function
+launches HIP kernels on the current stream and never computes on the host.  These are the batched
+entry points the reference lacks (`map_to_2d_batch`, `quantize_batch`, `search_batch` in
+SURVEY.md §7); the reference-shaped classes in `hq_mi355x.core` / `hq_mi355x.rag` wrap them.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._dev import device, dtype_code, ptr, stream, torch
+
+
+def _L():
+    return _lib.lib()
+
+
+def _chk(rc, exc=None):
+    _lib.check(rc, exc)
+
+
+def _contig(x):
+    return x if x.is_contiguous() else x.contiguous()
+
+
+# ---------------------------------------------------------------------------------------------- M
+
+
+def hilbert_table(n: int, exc=None):
+    """(xs, ys, xy2d) int32 device tensors for an n x n grid (core/hilbert_mapper.py:17-113)."""
+    t = torch()
+    if n <= 0 or (n & (n - 1)) != 0:
+        _chk(_L().hq_hilbert_table(n, None, None, None, None), exc)
+    xs = t.empty(n * n, dtype=t.int32, device=device())
+    ys = t.empty_like(xs)
+    tab = t.empty_like(xs)
+    _chk(_L().hq_hilbert_table(n, ptr(xs), ptr(ys), ptr(tab), stream()), exc)
+    return xs, ys, tab.view(n, n)
+
+
+def map_to_2d(x, n: int, exc=None):
+    """[N, d] (or [d]) -> [N, n, n]: out[y][x] = in[d2xy^-1(x, y)] (core/hilbert_mapper.py:115-174)."""
+    t = torch()
+    squeeze = x.dim() == 1
+    x2 = x.view(1, -1) if squeeze else x
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    N, d = x2.shape
+    out = t.empty((N, n, n), dtype=x.dtype, device=x.device)
+    _chk(_L().hq_map_to_2d(dtype_code(x.dtype), ptr(x2), N, x2.stride(0) if N > 1 else d, d, n, ptr(out),
+                           stream()), exc)
+    return out[0] if squeeze else out
+
+
+def map_from_2d(img, d_out: Optional[int] = None, exc=None):
+    """[N, n, n] (or [n, n]) -> [N, d_out] in curve order (core/hilbert_mapper.py:176-205)."""
+    t = torch()
+    squeeze = img.dim() == 2
+    im = _contig(img.unsqueeze(0) if squeeze else img)
+    N, n, _ = im.shape
+    if d_out is None:
+        d_out = n * n
+    out = t.empty((N, d_out), dtype=img.dtype, device=img.device)
+    _chk(_L().hq_map_from_2d(dtype_code(img.dtype), ptr(im), N, n, d_out, ptr(out), stream()), exc)
+    return out[0] if squeeze else out
+
+
+# ---------------------------------------------------------------------------------------------- I
+
+
+def index_streaming(img, L: int, stream_len: Optional[int] = None, exc=None):
+    """Streaming index of [N, n, n] f32/f64 images -> f64 [N, L] (core/streaming_index_builder.py:315-343).
+    The tree covers the first `stream_len` curve positions (default n*n)."""
+    t = torch()
+    squeeze = img.dim() == 2
+    im = _contig(img.unsqueeze(0) if squeeze else img)
+    N, n, _ = im.shape
+    if stream_len is None:
+        stream_len = n * n
+    out = t.zeros((N, L), dtype=t.float64, device=im.device)
+    _chk(_L().hq_index_streaming(dtype_code(im.dtype), ptr(im), N, n, int(stream_len), L, ptr(out), stream()), exc)
+    return out[0] if squeeze else out
+
+
+def index_traditional(img, L: int, exc=None):
+    """Traditional index of [N, n, n] f32 images -> f32 [N, L] (core/index_generator.py:313-356)."""
+    t = torch()
+    squeeze = img.dim() == 2
+    im = _contig((img.unsqueeze(0) if squeeze else img).to(t.float32))
+    N, n, _ = im.shape
+    out = t.zeros((N, L), dtype=t.float32, device=im.device)
+    _chk(_L().hq_index_traditional_f32(ptr(im), N, n, L, ptr(out), stream()), exc)
+    return out[0] if squeeze else out
+
+
+def block_means(img, grid: int, order: int = 0, exc=None):
+    """np.mean of each block: order 0 row-major sections, 1 RAG Hilbert order -> f32 [N, cnt]."""
+    t = torch()
+    squeeze = img.dim() == 2
+    im = _contig((img.unsqueeze(0) if squeeze else img).to(t.float32))
+    N, n, _ = im.shape
+    cnt = 1 if n // grid == 0 else grid * grid
+    out = t.empty((N, cnt), dtype=t.float32, device=im.device)
+    _chk(_L().hq_block_means_f32(ptr(im), N, n, int(grid), int(order), ptr(out), stream()), exc)
+    return out[0] if squeeze else out
+
+
+def rag_index_rows(n: int) -> int:
+    return _lib.load().hq_rag_index_rows(n)
+
+
+def index_rag(img, exc=None):
+    """RAG multi-row index: [N, n, n] f32 -> [N, n + R, n] (hierarchical_index_generator.py:103-146)."""
+    t = torch()
+    squeeze = img.dim() == 2
+    im = _contig(img.unsqueeze(0) if squeeze else img)
+    if im.dtype != t.float32:
+        raise TypeError("index_rag: float32 images only")
+    N, n, _ = im.shape
+    R = rag_index_rows(n)
+    out = t.empty((N, n + R, n), dtype=t.float32, device=im.device)
+    _chk(_L().hq_index_rag_f32(ptr(im), N, n, ptr(out), stream()), exc)
+    return out[0] if squeeze else out
+
+
+# ---------------------------------------------------------------------------------------------- Q
+
+
+def quantize_u8(enh, exc=None):
+    """[N, r, c] f32 -> (u8 [N, r, c], minmax f32 [N, 2]) (core/compressor.py:256-280)."""
+    t = torch()
+    squeeze = enh.dim() == 2
+    e = _contig(enh.unsqueeze(0) if squeeze else enh)
+    N, r, c = e.shape
+    out = t.empty((N, r, c), dtype=t.uint8, device=e.device)
+    mm = t.empty((N, 2), dtype=t.float32, device=e.device)
+    _chk(_L().hq_quantize_u8(ptr(e), N, r, c, ptr(out), ptr(mm), stream()), exc)
+    return (out[0], mm[0]) if squeeze else (out, mm)
+
+
+def dequantize_u8(u8, minmax, exc=None):
+    """u8 [N, r, c] with minmax [N, 2] -> f32 (core/compressor.py:282-303)."""
+    t = torch()
+    squeeze = u8.dim() == 2
+    u = _contig(u8.unsqueeze(0) if squeeze else u8)
+    mm = _contig(minmax.view(-1, 2).to(t.float32))
+    N, r, c = u.shape
+    out = t.empty((N, r, c), dtype=t.float32, device=u.device)
+    _chk(_L().hq_dequantize_u8(ptr(u), N, r, c, ptr(mm), ptr(out), stream()), exc)
+    return out[0] if squeeze else out
+
+
+def map_index_quantize(x, n: int, L: Optional[int] = None, want_idx: bool = True, want_minmax: bool = True,
+                       out: Optional[Tuple] = None, exc=None):
+    """The fused north-star kernel: f32 [N, d] -> (u8 frames [N, n+1, n], f64 idx [N, L], f32 minmax [N, 2]).
+    Equivalent to pad -> map_to_2d -> streaming index(L) -> embed -> normalise of core/pipeline.py:97-146."""
+    t = torch()
+    if L is None:
+        L = n
+    x2 = x if x.dim() == 2 else x.view(1, -1)
+    if x2.dtype != t.float32:
+        raise TypeError("map_index_quantize expects float32 parameters")
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    N, d = x2.shape
+    if out is not None:
+        frames, idx, mm = out
+    else:
+        frames = t.empty((N, n + 1, n), dtype=t.uint8, device=x2.device)
+        idx = t.empty((N, L), dtype=t.float64, device=x2.device) if want_idx else None
+        mm = t.empty((N, 2), dtype=t.float32, device=x2.device) if want_minmax else None
+    _chk(_L().hq_map_index_quantize(ptr(x2), N, x2.stride(0) if N > 1 else d, d, n, L, ptr(frames), ptr(idx),
+                                    ptr(mm), stream()), exc)
+    return frames, idx, mm
+
+
+def chunk_encode_f16(x, chunk: int = 1024, exc=None):
+    """Config 5: flat f16 stream -> per-chunk (u8 frame, f32 traditional index, minmax)
+    (core/streaming_processor.py:539-582, 877-913).  The last (shorter) chunk uses its own
+    geometry inside its slot; unused slot bytes are zero."""
+    t = torch()
+    x1 = _contig(x.reshape(-1))
+    if x1.dtype != t.float16:
+        raise TypeError("chunk_encode_f16 expects float16")
+    total = x1.numel()
+    from .core.dimension_calculator import _optimal_side
+    ns = _optimal_side(chunk)
+    nch = (total + chunk - 1) // chunk
+    frames = t.zeros((nch, ns + 1, ns), dtype=t.uint8, device=x1.device)
+    idx = t.zeros((nch, ns), dtype=t.float32, device=x1.device)
+    mm = t.zeros((nch, 2), dtype=t.float32, device=x1.device)
+    _chk(_L().hq_chunk_encode_f16(ptr(x1), total, chunk, ptr(frames), ptr(idx), ptr(mm), stream()), exc)
+    return frames, idx, mm
+
+
+# ---------------------------------------------------------------------------------------------- S
+
+
+def parse_structure(L: int):
+    """[(grid, start, end, is_offset)] (core/search_engine.py:42-109), computed by the library."""
+    buf = (ctypes.c_int32 * 64)()
+    n = _lib.load().hq_parse_structure(int(L), buf, 16)
+    return [(buf[4 * i], buf[4 * i + 1], buf[4 * i + 2], bool(buf[4 * i + 3])) for i in range(min(n, 16))]
+
+
+def seg_count(L: int) -> int:
+    return _lib.load().hq_seg_count(int(L))
+
+
+def seg_padded_len(L: int) -> int:
+    return _lib.load().hq_seg_padded_len(int(L))
+
+
+class Prepared:
+    """Device-resident prepared index vectors: Z [N, Lp] f64 (segment padded, normalised) and
+    stats [N, nseg, 4] (mean, std, mean of squares).  Built once per corpus (an index build)."""
+
+    __slots__ = ("Z", "S", "L", "N", "nseg", "Lp")
+
+    def __init__(self, Z, S, L):
+        self.Z, self.S, self.L = Z, S, int(L)
+        self.N = Z.shape[0]
+        self.nseg = S.shape[1]
+        self.Lp = Z.shape[1]
+
+
+def seg_prepare(idx, exc=None) -> Prepared:
+    t = torch()
+    i2 = _contig((idx if idx.dim() == 2 else idx.view(1, -1)).to(t.float64))
+    N, L = i2.shape
+    Lp, ns = seg_padded_len(L), seg_count(L)
+    Z = t.empty((N, Lp), dtype=t.float64, device=i2.device)
+    S = t.empty((N, ns, 4), dtype=t.float64, device=i2.device)
+    if N:
+        _chk(_L().hq_seg_prepare(ptr(i2), N, L, ptr(Z), ptr(S), stream()), exc)
+    return Prepared(Z, S, L)
+
+
+def level_scores(q: Prepared, c: Prepared, level: int, exc=None):
+    """Dense [Q, N] level (>= 0) or overall (level = -1) scores."""
+    t = torch()
+    out = t.empty((q.N, c.N), dtype=t.float64, device=q.Z.device)
+    _chk(_L().hq_level_scores(ptr(q.Z), ptr(q.S), q.N, ptr(c.Z), ptr(c.S), c.N, c.L, level, ptr(out), stream()),
+         exc)
+    return out
+
+
+def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.0, thr_mode: int = 0,
+              id_base: int = 0, exc=None):
+    """Fused MFMA scan + per-query top-k.  mode 0: level-0 score, 1: overall.
+    thr_mode 0 none / 1 >= / 2 >.  Returns (scores [Q, k], ids [Q, k], best [Q], best_id [Q])."""
+    t = torch()
+    Q, N = q.N, c.N
+    dev = q.Z.device
+    ws_bytes = int(_lib.load().hq_scan_workspace_size(Q, N, k))
+    ws = t.empty(ws_bytes, dtype=t.uint8, device=dev)
+    sc = t.empty((Q, k), dtype=t.float64, device=dev)
+    ids = t.empty((Q, k), dtype=t.int64, device=dev)
+    best = t.empty(Q, dtype=t.float64, device=dev)
+    bid = t.empty(Q, dtype=t.int64, device=dev)
+    _chk(_L().hq_scan_topk(ptr(q.Z), ptr(q.S), Q, ptr(c.Z), ptr(c.S), N, c.L, mode, k, float(threshold), thr_mode,
+                           int(id_base), ptr(ws), ws_bytes, ptr(sc), ptr(ids), ptr(best), ptr(bid), stream()), exc)
+    return sc, ids, best, bid
+
+
+def rescore(q: Prepared, c: Prepared, ids, id_base: int = 0, exc=None):
+    """[overall, level_0..] for the (query, global id) pairs in ids [Q, k] -> f64 [Q, k, 1 + nseg]."""
+    t = torch()
+    ids = _contig(ids.to(t.int64))
+    Q, k = ids.shape
+    out = t.empty((Q, k, 1 + q.nseg), dtype=t.float64, device=ids.device)
+    _chk(_L().hq_rescore(ptr(q.Z), ptr(q.S), Q, ptr(c.Z), ptr(c.S), c.N, c.L, ptr(ids), k, int(id_base), ptr(out),
+                         stream()), exc)
+    return out
+
+
+def progressive_final(s0, ids, det, best, best_id, best_det, K: int, exc=None):
+    """R-way final stage of progressive search.  s0/ids [R, Q, M], det [R, Q, M, W], best/best_id
+    [R, Q], best_det [R, Q, W].  Returns (out_id [Q, K], out_det [Q, K, W], count [Q])."""
+    t = torch()
+    R, Q, M = ids.shape
+    W = det.shape[-1]
+    dev = ids.device
+    oid = t.empty((Q, K), dtype=t.int64, device=dev)
+    odet = t.empty((Q, K, W), dtype=t.float64, device=dev)
+    cnt = t.empty(Q, dtype=t.int32, device=dev)
+    _chk(_L().hq_progressive_final(R, Q, M, W - 1, ptr(_contig(s0)), ptr(_contig(ids)), ptr(_contig(det)),
+                                   ptr(_contig(best)), ptr(_contig(best_id)), ptr(_contig(best_det)), K, ptr(oid),
+                                   ptr(odet), ptr(cnt), stream()), exc)
+    return oid, odet, cnt
+
+
+def cosine_scores(a, b, exc=None):
+    """(cos + 1) / 2 of rows of a [Q, K] against rows of b [N, K] (rag/search/engine.py:622-660)."""
+    t = torch()
+    a2 = _contig(a.reshape(a.shape[0], -1).to(t.float32))
+    b2 = _contig(b.reshape(b.shape[0], -1).to(t.float32))
+    K = min(a2.shape[1], b2.shape[1])
+    if a2.shape[1] != K:
+        a2 = _contig(a2[:, :K])
+    if b2.shape[1] != K:
+        b2 = _contig(b2[:, :K])
+    out = t.empty((a2.shape[0], b2.shape[0]), dtype=t.float64, device=a2.device)
+    _chk(_L().hq_cosine_scores(ptr(a2), a2.shape[0], ptr(b2), b2.shape[0], K, ptr(out), stream()), exc)
+    return out
+
+
+def select_topk(scores, k: int, threshold: float = 0.0, thr_mode: int = 0, id_base: int = 0, exc=None):
+    """Top-k (score desc, id asc) of a dense f64 [Q, N] score matrix + first arg-max."""
+    t = torch()
+    sc = _contig(scores.to(t.float64))
+    Q, N = sc.shape
+    dev = sc.device
+    os_ = t.empty((Q, k), dtype=t.float64, device=dev)
+    oi = t.empty((Q, k), dtype=t.int64, device=dev)
+    b = t.empty(Q, dtype=t.float64, device=dev)
+    bi = t.empty(Q, dtype=t.int64, device=dev)
+    _chk(_L().hq_select_topk(ptr(sc), Q, N, k, float(threshold), thr_mode, int(id_base), ptr(os_), ptr(oi), ptr(b),
+                             ptr(bi), stream()), exc)
+    return os_, oi, b, bi
+
+
+def pair_scores_raw(q, C, exc=None):
+    """compare_indices_at_level on raw equal-length segments: q [m] vs C [N, m] -> f64 [N]."""
+    t = torch()
+    q1 = _contig(q.reshape(-1).to(t.float64))
+    C2 = _contig(C.to(t.float64))
+    N, m = C2.shape
+    out = t.empty(N, dtype=t.float64, device=C2.device)
+    _chk(_L().hq_pair_scores_raw(ptr(q1), ptr(C2), N, m, ptr(out), stream()), exc)
+    return out

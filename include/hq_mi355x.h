@@ -1,0 +1,208 @@
+/* hq_mi355x.h — C-ABI of libhq_mi355x.so, the MI355X (gfx950) hot path of hilbert_quantization.
+ *
+ * The reference (Tylerlhess/hilbert-quantization v1.3.0) is pure Python/NumPy and has no FFI: its
+ * plugin boundary is a set of Python ABCs injected into the pipelines.  Each entry
+ * point below replaces the arithmetic behind one of those ABC methods; the Python package
+ * `hq_mi355x` (hilbert-quantization_amd/hq_mi355x) binds them with ctypes and keeps the reference's
+ * method names, argument meaning, exceptions and messages.  Replaced reference interfaces are cited
+ * as file:line in the reference's `hilbert_quantization/` tree.
+ *
+ * Conventions (all entry points):
+ *   - every buffer argument is a caller-owned DEVICE pointer; nothing here allocates device memory
+ *     (hq_scan_topk takes a caller-sized workspace: hq_scan_workspace_size);
+ *   - `stream` is a hipStream_t (NULL = default stream); calls are asynchronous on that stream;
+ *   - return HQ_OK (0) or a negative HQ_E_* code; hq_last_error() is thread-local;
+ *   - no global mutable state: calls are re-entrant from any host thread.
+ */
+#ifndef HQ_MI355X_H
+#define HQ_MI355X_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* hq_stream_t; /* hipStream_t */
+
+/* error codes */
+#define HQ_OK 0
+#define HQ_E_INVALID (-1)     /* bad argument (shape, pointer, size) */
+#define HQ_E_NOT_POW2 (-2)    /* grid side is not a positive power of two */
+#define HQ_E_TOO_MANY (-3)    /* more values than n*n cells */
+#define HQ_E_HIP (-4)         /* HIP runtime / launch error */
+#define HQ_E_UNSUPPORTED (-5) /* valid request outside what this build implements */
+
+/* dtype codes (element type of copy-only buffers) */
+#define HQ_F32 0
+#define HQ_F64 1
+#define HQ_F16 2
+#define HQ_BF16 3
+#define HQ_I8 4
+#define HQ_U8 5
+#define HQ_I16 6
+#define HQ_I32 7
+#define HQ_I64 8
+
+int hq_version(void);
+const char* hq_last_error(void);
+
+/* ---- M1/M2/M4: coordinate tables ------------------------------------------------------------
+ * replaces core/hilbert_mapper.py:17-40 generate_hilbert_coordinates (+ :42-113 d2xy/xy2d/rotate)
+ * and rag/embedding_generation/hilbert_mapper.py:122-204.
+ * xs, ys: int32[n*n] in curve order (d2xy); xy2d: int32[n*n] row-major (index of cell (x,y) at
+ * y*n+x).  Any of the three may be NULL.                                                        */
+int hq_hilbert_table(int n, int32_t* xs, int32_t* ys, int32_t* xy2d, hq_stream_t stream);
+
+/* ---- M5: 1-D -> 2-D scatter ---------------------------------------------------------------
+ * replaces core/hilbert_mapper.py:115-174 map_to_2d (and rag/.../hilbert_mapper.py:16-75).
+ * in: N rows of d elements (row stride in_stride elements); out: N x n x n row-major (row = y),
+ * out[y][x] = in[i] for the i with d2xy(i) = (x,y), i < d; zero elsewhere.  Bit copy, any dtype.  */
+int hq_map_to_2d(int dtype, const void* in, int64_t N, int64_t in_stride, int d, int n, void* out,
+                 hq_stream_t stream);
+
+/* ---- M6: 2-D -> 1-D gather ----------------------------------------------------------------
+ * replaces core/hilbert_mapper.py:176-205 map_from_2d (and rag/.../hilbert_mapper.py:77-120,
+ * rag/embedding_generation/reconstructor.py:100-131).  img: N x n x n; out: N x d_out with
+ * out[i] = img[y_i][x_i], d_out <= n*n (callers truncate, core/pipeline.py:219).               */
+int hq_map_from_2d(int dtype, const void* img, int64_t N, int n, int d_out, void* out,
+                   hq_stream_t stream);
+
+/* ---- I1: streaming hierarchical index ------------------------------------------------------
+ * replaces core/streaming_index_builder.py:315-343 StreamingHilbertIndexGenerator.
+ * generate_optimized_indices(image, L) (default index of HilbertQuantizer, core/pipeline.py:59-63).
+ * img: N x n x n (dtype HQ_F32 or HQ_F64); the tree is built over the first stream_len values of
+ * the Hilbert-ordered stream (n*n for generate_optimized_indices; len(parameters) for
+ * generate_indices_during_mapping, :287-313, where partial groups of 4 never promote).
+ * idx_out: float64 N x L.                                                                       */
+int hq_index_streaming(int dtype, const void* img, int64_t N, int n, int stream_len, int L,
+                       double* idx_out, hq_stream_t stream);
+
+/* ---- I2: traditional index -----------------------------------------------------------------
+ * replaces core/index_generator.py:313-356 _generate_traditional_indices (used by the chunk
+ * encoder, core/streaming_processor.py:858-860,897-899).  img: f32 N x n x n; out: f32 N x L.   */
+int hq_index_traditional_f32(const float* img, int64_t N, int n, int L, float* out,
+                             hq_stream_t stream);
+
+/* ---- I2/I4 building block: block means ---------------------------------------------------------
+ * np.mean of each (n/grid)^2 block of f32 N x n x n images (NumPy pairwise order, f32 result):
+ * order 0 = row-major sections (core/index_generator.py:100-144 calculate_spatial_averages);
+ * order 1 = the RAG generator's Hilbert order (hierarchical_index_generator.py:204-244).
+ * out: f32 N x cnt with cnt = grid*grid (1 = whole-image mean when grid > n).                   */
+int hq_block_means_f32(const float* img, int64_t N, int n, int grid, int order, float* out,
+                       hq_stream_t stream);
+
+/* ---- I4: RAG multi-row index ---------------------------------------------------------------
+ * replaces rag/embedding_generation/hierarchical_index_generator.py:103-146
+ * generate_multi_level_indices.  img: f32 N x n x n; out: f32 N x (n + R) x n where
+ * R = hq_rag_index_rows(n) (image copied, one row per granularity appended, zero filled).       */
+int hq_rag_index_rows(int n);
+int hq_index_rag_f32(const float* img, int64_t N, int n, float* out, hq_stream_t stream);
+
+/* ---- Q1/Q2: uint8 quantize / de-normalise ---------------------------------------------------
+ * replaces core/compressor.py:256-280 _normalize_for_compression and :282-303
+ * _denormalize_from_compression.  enh: f32 N x rows x cols; out u8 same shape;
+ * minmax: f32 N x 2 (min, max) written.  Constant images give 128 everywhere.                  */
+int hq_quantize_u8(const float* enh, int64_t N, int rows, int cols, uint8_t* out, float* minmax,
+                   hq_stream_t stream);
+int hq_dequantize_u8(const uint8_t* u8, int64_t N, int rows, int cols, const float* minmax,
+                     float* out, hq_stream_t stream);
+
+/* ---- fused map + streaming index + embed + uint8 quantize (the north-star kernel) -----------
+ * replaces the component sequence of core/pipeline.py:97-146 quantize_model up to the codec:
+ * pad (:325-349) -> map_to_2d -> streaming index (L) -> embed_indices_in_image
+ * (core/index_generator.py:221-253) -> _normalize_for_compression.
+ * in: f32 N x d (row stride in_stride elements), d <= n*n, 2 <= n <= 128;
+ * frame: u8 N x (n+1) x n; idx: f64 N x L (may be NULL); minmax: f32 N x 2 (may be NULL).      */
+int hq_map_index_quantize(const float* in, int64_t N, int64_t in_stride, int d, int n, int L,
+                          uint8_t* frame, double* idx, float* minmax, hq_stream_t stream);
+
+/* ---- config 5: f16 parameter stream, chunked (core/streaming_processor.py:539-582,877-972) ---
+ * Consecutive chunks of `chunk` fp16 values (the last may be shorter, >= chunk/2) are each padded
+ * to n*n (n = side of chunk), Hilbert-mapped, given the TRADITIONAL index (L = min(chunk, n)),
+ * embedded and quantized: frame u8 nchunks x (n+1) x n, idx f32 nchunks x L, minmax f32 x 2.     */
+int hq_chunk_encode_f16(const uint16_t* in, int64_t total, int chunk, uint8_t* frame, float* idx,
+                        float* minmax, hq_stream_t stream);
+
+/* ---- S2: level structure of an index vector of length L (host function) -------------------
+ * replaces core/search_engine.py:42-109 _parse_index_structure.  Writes up to max_levels rows of
+ * (grid, start, end, is_offset) into out[4*max_levels]; returns the number of levels.           */
+int hq_parse_structure(int L, int32_t* out, int max_levels);
+
+/* ---- S3 support: per-segment statistics of index vectors -----------------------------------
+ * Level segments are those of hq_parse_structure(L).  Vectors are stored "segment padded": segment s
+ * starts at a multiple of 4 and is zero-filled to a multiple of 4, Lp = hq_seg_padded_len(L)
+ * columns, nseg = hq_seg_count(L).  For every row of idx (f64 N x L):
+ *   Z[row][poff_s + j] = (c_j - mean_s) / std_s   (0 where std_s == 0)     f64 N x Lp
+ *   stats[row][s]      = {mean_s, std_s, mean(c^2)_s, 0}                  f64 N x nseg x 4
+ * mean/std follow NumPy's pairwise summation order so the std == 0 branches of
+ * core/search_engine.py:137-147 match bit-for-bit.                                              */
+int hq_seg_count(int L);
+int hq_seg_padded_len(int L);
+int hq_seg_prepare(const double* idx, int64_t N, int L, double* Z, double* stats, hq_stream_t stream);
+
+/* ---- S3/S4: dense scores ----------------------------------------------------------------------
+ * replaces core/search_engine.py:111-189 compare_indices_at_level (level >= 0) and :191-230
+ * _calculate_overall_similarity (level == -1) for Q queries against N candidates of equal L,
+ * from the hq_seg_prepare outputs of queries (Zq, Sq) and corpus (Zc, Sc).  scores: f64 Q x N.    */
+int hq_level_scores(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc,
+                    int64_t N, int L, int level, double* scores, hq_stream_t stream);
+
+/* ---- S5/S6: fused scan with per-query top-k ---------------------------------------------------
+ * One pass over the corpus: MFMA f64 contraction (v_mfma_f64_16x16x4f64) + score epilogue +
+ * per-query top-k ordered by (score desc, id asc) — Python's stable sort by score, reverse=True.
+ *   mode 0: level-0 score (progressive filter, search_engine.py:232-300; video hierarchical scan,
+ *           core/video_search.py:215-264); mode 1: overall score (brute_force_search :302-338).
+ *   thr_mode 0: keep all; 1: score >= threshold; 2: score > threshold.
+ * Also the first arg-max of the score over all candidates (out_best, may be NULL): the
+ * reference's "none pass" fallback (:295-298).  id_base is added to local row ids (sharding).
+ * out_score/out_id: Q x k (-inf / -1 in empty slots).  1 <= k <= 64.
+ * workspace: hq_scan_workspace_size(Q, N, k) bytes of device memory.                            */
+size_t hq_scan_workspace_size(int Q, int64_t N, int k);
+int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc,
+                 int64_t N, int L, int mode, int k, double threshold, int thr_mode, int64_t id_base,
+                 void* workspace, size_t workspace_bytes, double* out_score, int64_t* out_id,
+                 double* out_best, int64_t* out_best_id, hq_stream_t stream);
+
+/* ---- S4 on candidate lists: overall + per-level scores of selected pairs ---------------------
+ * ids: int64 Q x k GLOBAL ids (row = id - id_base; out of range / < 0 -> zeros);
+ * out: f64 Q x k x (1 + nseg) = [overall, level_0 .. level_{nseg-1}] (search_engine.py:191-230). */
+int hq_rescore(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc,
+               int64_t N, int L, const int64_t* ids, int k, int64_t id_base, double* out,
+               hq_stream_t stream);
+
+/* ---- S5 final stage, R-way (R = number of corpus shards) -------------------------------------
+ * Inputs per shard r: level-0 top-M lists s0/ids (R x Q x M, sorted), their rescored rows det
+ * (R x Q x M x (1+nseg)), and the shard's level-0 arg-max best/best_id (R x Q) with its row
+ * best_det (R x Q x (1+nseg)).  Forms the global level-0 top-M, falls back to the global first
+ * arg-max when no candidate passed (search_engine.py:295-298), stable-sorts the survivors by the
+ * overall score (:386-388) and writes the top K: out_id (Q x K, -1 padded), out_det
+ * (Q x K x (1+nseg)), out_count (Q).                                                            */
+int hq_progressive_final(int R, int Q, int M, int nseg, const double* s0, const int64_t* ids,
+                         const double* det, const double* best, const int64_t* best_id,
+                         const double* best_det, int K, int64_t* out_id, double* out_det,
+                         int* out_count, hq_stream_t stream);
+
+/* ---- S5 support: top-k of a dense score matrix (k > 64, e.g. max_candidates_per_level = 100) -----
+ * scores f64 Q x N -> out_score/out_id Q x k ordered (score desc, id asc) among candidates passing
+ * thr_mode (0 none, 1 >=, 2 >); out_best/out_best_id (may be NULL): first arg-max.               */
+int hq_select_topk(const double* scores, int Q, int64_t N, int k, double threshold, int thr_mode,
+                   int64_t id_base, double* out_score, int64_t* out_id, double* out_best,
+                   int64_t* out_best_id, hq_stream_t stream);
+
+/* ---- S3 on raw segments (candidate pools of mixed index length) -------------------------------
+ * compare_indices_at_level for the level segments already sliced and truncated to a common length
+ * m (search_engine.py:122-135): q f64[m] against C f64 N x m -> out f64[N].                      */
+int hq_pair_scores_raw(const double* q, const double* C, int64_t N, int m, double* out,
+                       hq_stream_t stream);
+
+/* ---- S7: RAG cosine scores (rag/search/engine.py:622-660, 1025-1051) --------------------------
+ * a: f32 Q x K, b: f32 N x K -> out f64 Q x N of (cos + 1) / 2 (0 if a norm is 0).               */
+int hq_cosine_scores(const float* a, int Q, const float* b, int64_t N, int K, double* out,
+                     hq_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HQ_MI355X_H */

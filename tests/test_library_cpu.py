@@ -1,0 +1,110 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol include/hq_mi355x.h declares,
+and its host-only entry points (level structure, segment layout, argument validation) agree with the
+reference.  No kernel is launched here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "hq_mi355x.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|size_t|const char\*)\s+(hq_[a-z0-9_]+)\(", txt, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from hq_mi355x import _lib
+    return _lib.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    names = declared_symbols()
+    assert len(names) >= 25
+    for n in names:
+        assert hasattr(lib, n), n
+    from hq_mi355x._lib import SIGNATURES
+    assert set(SIGNATURES) == set(names)
+
+
+def test_parse_structure_matches_reference(lib, golden):
+    g = golden("search")
+    got = []
+    buf = (ctypes.c_int32 * 64)()
+    for L in list(range(1, 130)) + [256, 1024, 4096]:
+        n = lib.hq_parse_structure(L, buf, 16)
+        for i in range(n):
+            got.append((L, buf[4 * i], buf[4 * i + 1], buf[4 * i + 2], buf[4 * i + 3]))
+    np.testing.assert_array_equal(np.array(got), g["parse_struct"])
+
+
+def test_segment_layout(lib):
+    assert lib.hq_seg_count(64) == 5 and lib.hq_seg_padded_len(64) == 68
+    assert lib.hq_seg_count(32) == 4 and lib.hq_seg_padded_len(32) == 36
+    assert lib.hq_rag_index_rows(64) == 3 and lib.hq_rag_index_rows(32) == 2
+    assert lib.hq_scan_workspace_size(1000, 1_000_000, 20) > 0
+
+
+def test_validation_messages_match_reference(lib):
+    # core/hilbert_mapper.py:136-143 messages, returned before any device work
+    from hq_mi355x import _lib
+    rc = lib.hq_map_to_2d(0, None, 1, 4, 4, 3, None, None)
+    assert rc == _lib.HQ_E_NOT_POW2
+    assert _lib.last_error() == "Dimension must be a power of 2, got 3"
+    rc = lib.hq_map_to_2d(0, None, 1, 20, 20, 4, None, None)
+    assert rc == _lib.HQ_E_TOO_MANY
+    assert _lib.last_error() == "Too many parameters (20) for dimensions 4x4 (16 cells)"
+    rc = lib.hq_hilbert_table(6, None, None, None, None)
+    assert _lib.last_error() == "Grid size must be a power of 2, got 6"
+    rc = lib.hq_map_index_quantize(None, 1, 4, 4, 256, 16, None, None, None, None)
+    assert rc == _lib.HQ_E_UNSUPPORTED
+
+
+def test_host_dimension_logic(golden):
+    from hq_mi355x.core.dimension_calculator import PowerOf4DimensionCalculator
+    g = golden("quant")
+    dc = PowerOf4DimensionCalculator()
+    for s, n, err in zip(g["dim_sizes"], g["dim_n"], g["dim_err"]):
+        assert dc.calculate_optimal_dimensions(int(s)) == (n, n)
+        if err:
+            with pytest.raises(ValueError) as e:
+                dc.calculate_padding_strategy(int(s), (n, n))
+            assert str(e.value) == str(err)
+
+
+def test_host_allocation_logic(golden):
+    from hq_mi355x.core.index_generator import level_allocation
+    from hq_mi355x.rag.hierarchical_index_generator import HierarchicalIndexGenerator
+    g = golden("index")
+    assert [tuple(x) for x in g["trad_alloc_32"]] == level_allocation(32)
+    assert [tuple(x) for x in g["trad_alloc_64"]] == level_allocation(64)
+    gen = HierarchicalIndexGenerator()
+    assert gen.calculate_optimal_granularity((64, 64))["granularity_levels"] == [8, 4, 2]
+    assert gen.calculate_optimal_granularity((32, 32))["granularity_levels"] == [4, 2]
+    for k in range(5):
+        img = g[f"rag_img_{k}"]
+        rows = g[f"rag_rows_{k}"]
+        info = gen.calculate_optimal_granularity((img.shape[1], img.shape[0]))
+        assert rows.shape[0] == img.shape[0] + info["index_rows_needed"]
+
+
+def test_product_has_no_cpu_fallback():
+    """The product package must not import the oracle or compute on the host when no GPU exists."""
+    import hq_mi355x
+    pkg = os.path.dirname(hq_mi355x.__file__)
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in src.replace("oracle/", ""), f
+    import torch
+    if not torch.cuda.is_available():
+        from hq_mi355x import _lib
+        from hq_mi355x.core import HilbertCurveMapper
+        with pytest.raises(_lib.NativeLibraryError):
+            HilbertCurveMapper().map_to_2d(np.arange(16, dtype=np.float32), (4, 4))
