@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X hot path (BASELINE.json configs 2-4).
+
+Headline `value` (BASELINE.json metric, first half): embeddings/sec of the fused Hilbert map +
+streaming index + index-row embed + uint8 quantize (hq_map_index_quantize) on 1M x 1536-d float32
+embeddings per GPU (config 2, n = 64, L = 64, min_efficiency_ratio = 0.2), inputs resident in HBM.
+A step = one launch over the whole 1M batch.  Weak scaling: every rank processes its own 1M batch.
+
+Second half of the metric, reported in "search": queries/sec @ top-10 of the reference's
+progressive search (threshold 0.1, max_candidates_per_level 20 as HilbertQuantizer sets it) over a
+1M-frame corpus per GPU (config 3; config 4 = 1M per GPU x N GPUs with the RCCL all-gather merge).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "hilbert-quantization_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_MATRIX_PEAK_TFS = 78.6    # MI355X FP64 matrix peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n-emb", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=1536)
+    ap.add_argument("--corpus", type=int, default=1_000_000)
+    ap.add_argument("--queries", type=int, default=1000)
+    ap.add_argument("--search-steps", type=int, default=5)
+    ap.add_argument("--no-search", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed(fn, steps, warmup, world):
+    for _ in range(warmup):
+        fn()
+    barrier(world)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(steps):
+        fn()
+    ev1.record()
+    barrier(world)
+    wall = time.perf_counter() - t0
+    return max_over_ranks(wall, world), ev0.elapsed_time(ev1) / 1e3 / steps
+
+
+def load_traffic(name):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (tools/pmc_traffic.py), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get(name, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline_quantize(dim, seconds):
+    """The NumPy oracle (oracle/hq_oracle.py, a restatement of the reference) on host cores."""
+    from oracle import hq_oracle as O
+    rng = np.random.default_rng(1)
+    n = O.optimal_dimensions(dim)[0]
+    B = 256
+    P = rng.standard_normal((B, dim)).astype(np.float32)
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        img = O.map_to_2d(O.pad_parameters(P, n), n)
+        idx = O.streaming_index(O.map_from_2d(img), n)
+        O.normalize_u8(O.embed_index_row(img, idx))
+        done += B
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "embeddings/sec", "cores": 1, "kind": "port",
+            "sample": f"{done} x {dim}-d f32 embeddings through oracle map+streaming index+embed+u8 normalise "
+                      f"(NumPy, single thread) in {dt:.1f}s"}
+
+
+def cpu_baseline_search(C, Q, seconds):
+    from oracle import hq_oracle as O
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds and done < len(Q):
+        O.progressive_search(Q[done], C, 10, 0.1, 20)
+        done += 1
+    dt = time.perf_counter() - t0
+    cand_per_s = done * len(C) / dt
+    return {"value": cand_per_s / 1_000_000, "unit": "queries/sec over a 1M corpus (extrapolated)",
+            "cores": 1, "kind": "port",
+            "sample": f"{done} queries x {len(C)} candidates, oracle progressive_search (NumPy, single thread) "
+                      f"in {dt:.1f}s, linear in corpus size"}
+
+
+def main():
+    args = parse()
+    world, rank = dist_setup(args)
+    from hq_mi355x import kernels as K
+    from hq_mi355x.core.pipeline import quantize_batch
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    N, d = args.n_emb, args.dim
+    n, L = 64, 64
+    g = torch.Generator(device=dev).manual_seed(1 + 1000 * rank)
+    X = torch.randn((N, d), generator=g, device=dev, dtype=torch.float32)
+    frames = torch.empty((N, n + 1, n), dtype=torch.uint8, device=dev)
+    idx = torch.empty((N, L), dtype=torch.float64, device=dev)
+    mm = torch.empty((N, 2), dtype=torch.float32, device=dev)
+    out = (frames, idx, mm)
+
+    def step():
+        quantize_batch(X, min_efficiency_ratio=0.2, index_space_size=L, out=out)
+
+    wall, kern = timed(step, args.steps, args.warmup, world)
+    ms = wall / args.steps * 1e3
+    value = N * world * args.steps / wall
+    bytes_per_emb = 4 * d + (n + 1) * n + 8 * L + 8
+    achieved = bytes_per_emb * N / kern / 1e9
+    traffic = load_traffic("k_fused64")
+    rec = {
+        "metric": "embeddings/sec Hilbert map+quantize (1536D)", "value": value, "unit": "embeddings/sec",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic N(0,1) float32 embeddings generated on device (seed 1 + 1000*rank)",
+        "config": {"workload": "cfg2: 1M x 1536-d embeddings per GPU, order-64 Hilbert map + streaming index "
+                               "(L=64, f64) + index-row embed + uint8 quantize (fused hq_map_index_quantize)",
+                   "embeddings_per_gpu": N, "dim": d, "grid": n, "index_len": L,
+                   "parallelism": f"dp{world} (independent shards, no collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes_per_embedding": bytes_per_emb, "kernel_ms": kern * 1e3},
+    }
+
+    if not args.no_search:
+        from hq_mi355x.core.search_engine import IndexCorpus
+        from hq_mi355x.distributed import ShardedIndexCorpus
+        Nc, Qn = args.corpus, args.queries
+        gc = torch.Generator(device=dev).manual_seed(2 + 1000 * rank)
+        Xc = torch.randn((Nc, d), generator=gc, device=dev, dtype=torch.float32)
+        _, corpus_idx, _ = K.map_index_quantize(Xc, n, L)
+        del Xc
+        # queries = global corpus rows 0..Q-1 (rank 0's shard) + N(0, 0.01) noise, identical on all ranks
+        g0 = torch.Generator(device=dev).manual_seed(2)
+        X0 = torch.randn((Qn, d), generator=g0, device=dev, dtype=torch.float32)
+        _, q0, _ = K.map_index_quantize(X0, n, L)
+        gq = torch.Generator(device=dev).manual_seed(3)
+        queries = q0 + 0.01 * torch.randn(q0.shape, generator=gq, device=dev, dtype=torch.float64)
+        torch.cuda.synchronize()
+        tp0 = time.perf_counter()
+        if world > 1:
+            sharded = ShardedIndexCorpus(corpus_idx, id_base=rank * Nc, n_total=Nc * world)
+            run = lambda: sharded.progressive(queries, 10, 0.1, 20)  # noqa: E731
+        else:
+            corpus = IndexCorpus(corpus_idx)
+            run = lambda: corpus.progressive(queries, 10, 0.1, 20)  # noqa: E731
+        torch.cuda.synchronize()
+        prep_s = time.perf_counter() - tp0
+        swall, skern = timed(run, args.search_steps, 1, world)
+        qps = Qn * args.search_steps / swall
+        pairs = Qn * Nc  # level-0 pairs scored per rank per step
+        flops = 2.0 * pairs * 32
+        ids, ov, _, cnt = run()
+        rec["search"] = {
+            "metric": "queries/sec@top-10 over 1M corpus", "value": qps, "unit": "queries/sec",
+            "corpus_per_gpu": Nc, "corpus_total": Nc * world, "queries": Qn, "steps": args.search_steps,
+            "ms_per_step": swall / args.search_steps * 1e3, "index_prepare_s": prep_s,
+            "mode": "progressive (level-0 MFMA scan top-20 >= 0.1, exact re-rank, overall re-score, top-10)",
+            "roofline": {"bound": "mfma", "achieved": flops / skern / 1e12, "peak": FP64_MATRIX_PEAK_TFS,
+                         "unit": "TFLOP/s", "frac": flops / skern / 1e12 / FP64_MATRIX_PEAK_TFS,
+                         "note": "algorithmic 2*Q*N*32 flops of the level-0 contraction per step / step time"},
+            "self_match_rate": float((ids[:, 0].cpu() == torch.arange(Qn)).float().mean()),
+        }
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        rec["cpu_baseline"] = cpu_baseline_quantize(d, args.cpu_seconds)
+        rec["cpu_baseline"]["threads_available"] = os.cpu_count()
+        if "search" in rec:
+            from hq_mi355x._dev import to_np
+            C = to_np(corpus_idx[:100_000])
+            Qh = to_np(queries[:50])
+            rec["search"]["cpu_baseline"] = cpu_baseline_search(C, Qh, args.cpu_seconds / 2)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

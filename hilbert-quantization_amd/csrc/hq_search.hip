@@ -110,68 +110,90 @@ __device__ __forceinline__ double level_sim(double G, double qm, double qs, doub
   return comb > 0.0 ? comb : 0.0;
 }
 
-// plain dot over a padded segment
-__device__ __forceinline__ double seg_dot(const double* a, const double* b, int n) {
-  double g = 0.0;
-  for (int i = 0; i < n; ++i) g = fma(a[i], b[i], g);
-  return g;
-}
+// ------------------------------------------------------------------------------------------------
+// EXACT scores: compare_indices_at_level (search_engine.py:111-189) in the reference's operation
+// order — products and squared differences summed in NumPy's pairwise order, then the same Python
+// float expression.  Used for dense scores, re-scoring and the final re-rank of the MFMA scan's
+// candidate lists, so rankings (including noise-level ties) match the reference bit for bit.
+// ------------------------------------------------------------------------------------------------
+struct VecSet {
+  const double* raw;  // N x L  (original index vectors)
+  const double* Z;    // N x Lp (segment-padded normalised vectors)
+  const double* S;    // N x nseg x 4 (mean, std, mean of squares, 0)
+};
 
-__device__ double pair_level(const double* zq, const double* sq, const double* zc, const double* sc,
-                             const SegInfo& si, int s) {
-  const double G = seg_dot(zq + si.poff[s], zc + si.poff[s], si.plen[s]);
-  const double* a = sq + 4 * s;
-  const double* b = sc + 4 * s;
-  return level_sim(G, a[0], a[1], a[2], b[0], b[1], b[2], (double)si.len[s], si.inv_m[s]);
-}
-
-__device__ double pair_overall(const double* zq, const double* sq, const double* zc, const double* sc,
-                               const SegInfo& si, double* lv) {
-  // search_engine.py:191-230: running weighted sum in level order, then divide and clamp
-  double tws = 0.0;
-  for (int s = 0; s < si.nseg; ++s) {
-    double v = pair_level(zq, sq, zc, sc, si, s);
-    if (lv) lv[s] = v;
-    tws = tws + v * si.w[s];
+__device__ double exact_level(const double* q, const double* zq, const double* sq, const double* c,
+                              const double* zc, const double* sc, int m) {
+  const double qs = sq[1], cs = sc[1];
+  if (qs == 0.0 && cs == 0.0) return fabs(sq[0] - sc[0]) < 1e-6 ? 1.0 : 0.0;   // :141-145
+  if (qs == 0.0 || cs == 0.0) return 0.1;                                        // :146-148
+  auto fp = [=](int k) -> double { return zq[k] * zc[k]; };
+  const double corr = np_sum<double>(fp, m) / (double)m;                         // :154
+  const double sim = (corr + 1.0) / 2.0;                                         // :158
+  auto fd = [=](int k) -> double { double d = q[k] - c[k]; return d * d; };
+  const double mse = np_sum<double>(fd, m) / (double)m;                          // :161
+  const double maxmse = sq[2] + sc[2];                                           // :162
+  double ds = 1.0;
+  if (maxmse > 0.0) {
+    ds = 1.0 - (mse / maxmse);
+    ds = ds > 0.0 ? ds : 0.0;
   }
-  double ov = si.wsum > 0.0 ? tws / si.wsum : 0.0;
+  const double a = 0.7 * sim;
+  const double b = 0.3 * ds;
+  double comb = a + b;                                                           // :171
+  comb = comb < 1.0 ? comb : 1.0;
+  return comb > 0.0 ? comb : 0.0;
+}
+
+__device__ double exact_pair(const VecSet& A, int64_t ia, const VecSet& B, int64_t ib, const SegInfo& si, int level,
+                             double* lv) {
+  const double* ra = A.raw + ia * si.L;
+  const double* rb = B.raw + ib * si.L;
+  const double* za = A.Z + ia * si.Lp;
+  const double* zb = B.Z + ib * si.Lp;
+  const double* sa = A.S + ia * si.nseg * 4;
+  const double* sb = B.S + ib * si.nseg * 4;
+  if (level >= 0) {
+    if (level >= si.nseg) return 0.0;
+    const int s = level;
+    return exact_level(ra + si.src[s], za + si.poff[s], sa + 4 * s, rb + si.src[s], zb + si.poff[s], sb + 4 * s,
+                       si.len[s]);
+  }
+  // search_engine.py:191-230: running weighted sum in level order, divide, clamp
+  double tws = 0.0, tw = 0.0;
+  for (int s = 0; s < si.nseg; ++s) {
+    const double v = exact_level(ra + si.src[s], za + si.poff[s], sa + 4 * s, rb + si.src[s], zb + si.poff[s],
+                                 sb + 4 * s, si.len[s]);
+    if (lv) lv[s] = v;
+    const double w = 1.0 / (double)(s + 1);
+    tws = tws + v * w;
+    tw = tw + w;
+  }
+  double ov = tw > 0.0 ? tws / tw : 0.0;
   ov = ov < 1.0 ? ov : 1.0;
   return ov > 0.0 ? ov : 0.0;
 }
 
-// dense Q x N scores (drop-in path for candidate lists held by Python)
-__global__ __launch_bounds__(256) void k_level_scores(const double* __restrict__ Zq, const double* __restrict__ Sq,
-                                                      int Q, const double* __restrict__ Zc,
-                                                      const double* __restrict__ Sc, int64_t N, SegInfo si,
-                                                      int level, double* __restrict__ out) {
+// dense Q x N exact scores (drop-in path and rare exact fallbacks)
+__global__ __launch_bounds__(256) void k_level_scores(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si, int level,
+                                                      double* __restrict__ out) {
   const int64_t total = (int64_t)Q * N;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(t / N);
-    const int64_t c = t % N;
-    const double* zq = Zq + (int64_t)q * si.Lp;
-    const double* sq = Sq + (int64_t)q * si.nseg * 4;
-    const double* zc = Zc + c * si.Lp;
-    const double* sc = Sc + c * si.nseg * 4;
-    double v;
-    if (level < 0) v = pair_overall(zq, sq, zc, sc, si, nullptr);
-    else if (level >= si.nseg) v = 0.0;
-    else v = pair_level(zq, sq, zc, sc, si, level);
-    out[t] = v;
+    const int64_t q = t / N, c = t % N;
+    out[t] = exact_pair(Qs, q, Cs, c, si, level, nullptr);
   }
 }
 
-// overall + per-level for selected (query, candidate) pairs; ids are global, id_base subtracted
-__global__ __launch_bounds__(256) void k_rescore(const double* __restrict__ Zq, const double* __restrict__ Sq,
-                                                 int Q, const double* __restrict__ Zc,
-                                                 const double* __restrict__ Sc, int64_t N, SegInfo si,
+// exact overall + per-level for selected (query, candidate) pairs; ids are global, id_base subtracted
+__global__ __launch_bounds__(256) void k_rescore(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si,
                                                  const int64_t* __restrict__ ids, int k, int64_t id_base,
                                                  double* __restrict__ out) {
   const int64_t total = (int64_t)Q * k;
   const int W = 1 + si.nseg;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(t / k);
+    const int64_t q = t / k;
     const int64_t gid = ids[t];
     double* o = out + t * W;
     const int64_t c = gid - id_base;
@@ -180,8 +202,7 @@ __global__ __launch_bounds__(256) void k_rescore(const double* __restrict__ Zq, 
       continue;
     }
     double lv[kMaxSeg];
-    o[0] = pair_overall(Zq + (int64_t)q * si.Lp, Sq + (int64_t)q * si.nseg * 4, Zc + c * si.Lp,
-                        Sc + c * si.nseg * 4, si, lv);
+    o[0] = exact_pair(Qs, q, Cs, c, si, -1, lv);
     for (int s = 0; s < si.nseg; ++s) o[1 + s] = lv[s];
   }
 }
@@ -641,6 +662,72 @@ __global__ __launch_bounds__(256) void k_pair_raw(const double* __restrict__ q, 
   }
 }
 
+// Exact re-rank of an approximate (MFMA) candidate list, one wave per query.  cand lists [Q, kp] are
+// sorted by approximate score (id -1 = empty slot).  Output: the exact top-k (score desc, id asc)
+// among listed candidates passing the exact threshold test, their count, and resolved = 1 when no
+// unlisted candidate can belong to the exact top-k given |approx - exact| <= eps:
+//   list not full (every candidate with approx >= thr - eps is listed), or
+//   last listed approx + eps < k-th exact score (enough passed), or < / <= thr (too few passed).
+__global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si, int mode,
+                                               const double* __restrict__ cs, const int64_t* __restrict__ cid, int kp,
+                                               int k, double thr, int thr_mode, double eps, int64_t id_base,
+                                               double* __restrict__ os, int64_t* __restrict__ oid,
+                                               int* __restrict__ ocnt, int* __restrict__ ores) {
+  __shared__ double es[kMaxTopK];
+  __shared__ int64_t ei[kMaxTopK];
+  const int lane = threadIdx.x;
+  for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    const int64_t base = (int64_t)q * kp;
+    if (lane < kp) {
+      double e = -__builtin_huge_val();
+      int64_t id = cid[base + lane];
+      const int64_t c = id - id_base;
+      if (id >= 0 && c >= 0 && c < N) {
+        e = exact_pair(Qs, q, Cs, c, si, mode == 0 ? 0 : -1, nullptr);
+        const bool pass = thr_mode == 0 || (thr_mode == 1 ? e >= thr : e > thr);
+        if (!pass) id = -1;
+      } else {
+        id = -1;
+      }
+      es[lane] = e;
+      ei[lane] = id;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      int n = 0;
+      for (int j = 0; j < kp; ++j) {  // compact valid entries, then insertion sort
+        if (ei[j] < 0) continue;
+        double s = es[j];
+        int64_t id = ei[j];
+        int p = n++;
+        while (p > 0 && better(s, id, es[p - 1], ei[p - 1])) {
+          es[p] = es[p - 1];
+          ei[p] = ei[p - 1];
+          --p;
+        }
+        es[p] = s;
+        ei[p] = id;
+      }
+      const int cnt = n < k ? n : k;
+      for (int j = 0; j < k; ++j) {
+        os[(int64_t)q * k + j] = j < cnt ? es[j] : -__builtin_huge_val();
+        oid[(int64_t)q * k + j] = j < cnt ? ei[j] : -1;
+      }
+      ocnt[q] = cnt;
+      const bool full = cid[base + kp - 1] >= 0;
+      int res = 1;
+      if (full) {
+        const double bound = cs[base + kp - 1] + eps;
+        if (n >= k) res = bound < es[k - 1];
+        else if (thr_mode == 0) res = 0;
+        else res = thr_mode == 1 ? (bound < thr) : (bound <= thr);
+      }
+      ores[q] = res;
+    }
+    __syncthreads();
+  }
+}
+
 // S7: (cos + 1) / 2, 0 if a norm is 0 (rag/search/engine.py:622-660, 1025-1051)
 __global__ __launch_bounds__(256) void k_cosine(const float* __restrict__ A, int Q, const float* __restrict__ B,
                                                 int64_t N, int K, double* __restrict__ out) {
@@ -734,18 +821,38 @@ int hq_seg_prepare(const double* idx, int64_t N, int L, double* Z, double* stats
   return HQ_OK;
 }
 
-int hq_level_scores(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc, int64_t N,
-                    int L, int level, double* scores, hq_stream_t stream) {
+int hq_level_scores(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc, const double* Zc,
+                    const double* Sc, int64_t N, int L, int level, double* scores, hq_stream_t stream) {
   if (Q < 0 || N < 0 || L <= 0) return fail(HQ_E_INVALID, "bad shape");
   if (Q == 0 || N == 0) return HQ_OK;
-  if (!Zq || !Sq || !Zc || !Sc || !scores) return fail(HQ_E_INVALID, "null buffer");
+  if (!Rq || !Zq || !Sq || !Rc || !Zc || !Sc || !scores) return fail(HQ_E_INVALID, "null buffer");
   SegInfo si;
   seg_info(L, si);
   const int64_t total = (int64_t)Q * N;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(k_level_scores, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, Zq, Sq, Q, Zc, Sc, N, si,
-                     level, scores);
+  hipLaunchKernelGGL(k_level_scores, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
+                     VecSet{Rc, Zc, Sc}, N, si, level, scores);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+int hq_refine_topk(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc, const double* Zc,
+                   const double* Sc, int64_t N, int L, int mode, const double* cand_score, const int64_t* cand_id,
+                   int kp, int k, double threshold, int thr_mode, double eps, int64_t id_base, double* out_score,
+                   int64_t* out_id, int* out_count, int* out_resolved, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || L <= 0 || kp <= 0 || kp > kMaxTopK || k <= 0 || k > kp)
+    return fail(HQ_E_INVALID, "bad sizes kp=%d k=%d", kp, k);
+  if (Q == 0) return HQ_OK;
+  if (!Rq || !Zq || !Sq || !cand_score || !cand_id || !out_score || !out_id || !out_count || !out_resolved ||
+      (N > 0 && (!Rc || !Zc || !Sc)))
+    return fail(HQ_E_INVALID, "null buffer");
+  SegInfo si;
+  seg_info(L, si);
+  int grid = Q < 8192 ? Q : 8192;
+  hipLaunchKernelGGL(k_refine, dim3(grid), dim3(64), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
+                     VecSet{Rc, Zc, Sc}, N, si, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base,
+                     out_score, out_id, out_count, out_resolved);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
@@ -813,18 +920,19 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
   return HQ_OK;
 }
 
-int hq_rescore(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc, int64_t N, int L,
-               const int64_t* ids, int k, int64_t id_base, double* out, hq_stream_t stream) {
+int hq_rescore(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc, const double* Zc,
+               const double* Sc, int64_t N, int L, const int64_t* ids, int k, int64_t id_base, double* out,
+               hq_stream_t stream) {
   if (Q < 0 || N < 0 || L <= 0 || k < 0) return fail(HQ_E_INVALID, "bad shape");
   if (Q == 0 || k == 0) return HQ_OK;
-  if (!Zq || !Sq || !ids || !out || (N > 0 && (!Zc || !Sc))) return fail(HQ_E_INVALID, "null buffer");
+  if (!Rq || !Zq || !Sq || !ids || !out || (N > 0 && (!Rc || !Zc || !Sc))) return fail(HQ_E_INVALID, "null buffer");
   SegInfo si;
   seg_info(L, si);
   const int64_t total = (int64_t)Q * k;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(k_rescore, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, Zq, Sq, Q, Zc, Sc, N, si, ids, k,
-                     id_base, out);
+  hipLaunchKernelGGL(k_rescore, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
+                     VecSet{Rc, Zc, Sc}, N, si, ids, k, id_base, out);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }

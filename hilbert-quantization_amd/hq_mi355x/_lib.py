@@ -50,10 +50,11 @@ SIGNATURES = {
     "hq_seg_count": (_i, [_i]),
     "hq_seg_padded_len": (_i, [_i]),
     "hq_seg_prepare": (_i, [_p, _i64, _i, _p, _p, _p]),
-    "hq_level_scores": (_i, [_p, _p, _i, _p, _p, _i64, _i, _i, _p, _p]),
+    "hq_level_scores": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _p, _p]),
+    "hq_refine_topk": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _p, _p, _i, _i, _d, _i, _d, _i64, _p, _p, _p, _p, _p]),
     "hq_scan_workspace_size": (_sz, [_i, _i64, _i]),
     "hq_scan_topk": (_i, [_p, _p, _i, _p, _p, _i64, _i, _i, _i, _d, _i, _i64, _p, _sz, _p, _p, _p, _p, _p]),
-    "hq_rescore": (_i, [_p, _p, _i, _p, _p, _i64, _i, _p, _i, _i64, _p, _p]),
+    "hq_rescore": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _p, _i, _i64, _p, _p]),
     "hq_progressive_final": (_i, [_i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
     "hq_cosine_scores": (_i, [_p, _i, _p, _i64, _i, _p, _p]),
     "hq_select_topk": (_i, [_p, _i, _i64, _i, _d, _i, _i64, _p, _p, _p, _p, _p]),

@@ -40,7 +40,15 @@ def _f64(x):
 class IndexCorpus:
     """A corpus of equal-length hierarchical index vectors resident in HBM.
 
-    `indices`: [N, L] (NumPy or device tensor); `id_base`: global id of row 0 (corpus shards)."""
+    `indices`: [N, L] (NumPy or device tensor); `id_base`: global id of row 0 (corpus shards).
+
+    Every ranking is EXACT: the fused MFMA scan (approximate scores, |err| << EPS) produces a list
+    of SLACK extra candidates per query, hq_refine_topk re-scores the list in the reference's
+    operation order and proves (or not) that nothing outside the list can enter the exact top-k;
+    unproven queries and the "none passed" fallback are answered by the dense exact path."""
+
+    EPS = 1e-9      # bound on |approximate - exact| score (observed < 1e-13 at L = 64)
+    SLACK = 16
 
     def __init__(self, indices, id_base: int = 0):
         x = _f64(indices)
@@ -61,21 +69,56 @@ class IndexCorpus:
 
     # ---- scores ------------------------------------------------------------------------------
     def level_scores(self, queries, level: int):
-        """Dense [Q, N]: level >= 0 -> compare_indices_at_level, -1 -> overall similarity."""
+        """Dense exact [Q, N]: level >= 0 -> compare_indices_at_level, -1 -> overall similarity."""
         return K.level_scores(self.prepare_queries(queries), self.prep, level)
 
-    def _topk(self, qp, mode: int, k: int, thr: float, thr_mode: int):
-        if k <= MAX_FUSED_K:
-            return K.scan_topk(qp, self.prep, mode, k, thr, thr_mode, self.id_base)
-        sc = K.level_scores(qp, self.prep, 0 if mode == 0 else -1)
-        return K.select_topk(sc, k, thr, thr_mode, self.id_base)
+    def _dense(self, qp, sel, mode: int, k: int, thr: float, thr_mode: int):
+        """Dense exact path for the queries `sel` (device int64): scores, select top-k + arg-max."""
+        sub = qp.rows(sel)
+        outs = []
+        chunk = max(1, (1 << 27) // max(1, self.N))  # <= 1 GiB of scores per launch
+        for i in range(0, sub.N, chunk):
+            part = sub.rows(torch().arange(i, min(sub.N, i + chunk), device=sel.device))
+            sc = K.level_scores(part, self.prep, 0 if mode == 0 else -1)
+            outs.append(K.select_topk(sc, k, thr, thr_mode, self.id_base))
+        return [torch().cat([o[j] for o in outs], 0) for j in range(4)]
+
+    def exact_topk(self, qp, mode: int, k: int, thr: float = 0.0, thr_mode: int = 0, need_best: bool = False):
+        """Exact per-query top-k (score desc, id asc) among candidates passing the threshold test;
+        with need_best, also the exact first arg-max for queries where nothing passed.
+        Returns (scores [Q, k], ids [Q, k], count [Q], best [Q], best_id [Q])."""
+        t = torch()
+        Q = qp.N
+        dev = qp.Z.device
+        best = t.full((Q,), -float("inf"), dtype=t.float64, device=dev)
+        bid = t.full((Q,), -1, dtype=t.int64, device=dev)
+        kp = k + self.SLACK
+        if kp > MAX_FUSED_K:
+            sc, ids, b, bi = self._dense(qp, t.arange(Q, device=dev), mode, k, thr, thr_mode)
+            cnt = (ids >= 0).sum(1).to(t.int32)
+            return sc, ids, cnt, b, bi
+        lo_mode = 0 if thr_mode == 0 else 1
+        asc, aid, _, _ = K.scan_topk(qp, self.prep, mode, kp, thr - self.EPS, lo_mode, self.id_base)
+        sc, ids, cnt, res = K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, thr_mode, self.EPS, self.id_base)
+        redo = (res == 0)
+        if need_best:
+            redo = redo | (cnt == 0)
+        sel = t.nonzero(redo).view(-1)
+        if sel.numel():
+            s2, i2, b2, bi2 = self._dense(qp, sel, mode, k, thr, thr_mode)
+            sc[sel] = s2
+            ids[sel] = i2
+            cnt[sel] = (i2 >= 0).sum(1).to(t.int32)
+            best[sel] = b2
+            bid[sel] = bi2
+        return sc, ids, cnt, best, bid
 
     # ---- searches ----------------------------------------------------------------------------
     def brute_force(self, queries, max_results: int):
         """search_engine.py:302-338 for a query batch -> (ids [Q, K], overall [Q, K], levels [Q, K, nseg])."""
         qp = self.prepare_queries(queries)
         k = max(1, min(int(max_results), self.N)) if self.N else 1
-        sc, ids, _, _ = self._topk(qp, 1, k, 0.0, 0)
+        _, ids, _, _, _ = self.exact_topk(qp, 1, k)
         det = K.rescore(qp, self.prep, ids, self.id_base)
         return ids, det[..., 0], det[..., 1:]
 
@@ -93,18 +136,17 @@ class IndexCorpus:
             ids, ov, lv = self.brute_force(queries, min(K_out, max(self.N, 1)))
             cnt = (ids >= 0).sum(dim=1).to(t.int32)
             return ids, ov, lv, cnt
-        s0, ids, best, bid = self._topk(qp, 0, M, float(threshold), 1)
+        s0, ids, cnt, best, bid = self.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)
         det = K.rescore(qp, self.prep, ids, self.id_base)
         bdet = K.rescore(qp, self.prep, bid.view(Q, 1), self.id_base).view(Q, -1)
-        oid, odet, cnt = K.progressive_final(s0.unsqueeze(0), ids.unsqueeze(0), det.unsqueeze(0), best.unsqueeze(0),
-                                             bid.unsqueeze(0), bdet.unsqueeze(0), K_out)
-        return oid, odet[..., 0], odet[..., 1:], cnt
+        oid, odet, ocnt = K.progressive_final(s0.unsqueeze(0), ids.unsqueeze(0), det.unsqueeze(0),
+                                              best.unsqueeze(0), bid.unsqueeze(0), bdet.unsqueeze(0), K_out)
+        return oid, odet[..., 0], odet[..., 1:], ocnt
 
     def frame_search(self, queries, max_results: int, threshold: float = 0.1):
         """core/video_search.py:215-264: level-0 sim > threshold (strict), stable sort, top-k."""
         qp = self.prepare_queries(queries)
-        k = max(1, int(max_results))
-        sc, ids, _, _ = self._topk(qp, 0, k, float(threshold), 2)
+        sc, ids, _, _, _ = self.exact_topk(qp, 0, max(1, int(max_results)), float(threshold), 2)
         return ids, sc
 
 

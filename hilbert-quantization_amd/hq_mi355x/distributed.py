@@ -15,7 +15,7 @@ from typing import Optional, Tuple
 
 from . import kernels as K
 from ._dev import torch
-from .core.search_engine import IndexCorpus, MAX_FUSED_K
+from .core.search_engine import IndexCorpus
 
 
 def shard_range(n_total: int, rank: int, world: int) -> Tuple[int, int]:
@@ -57,13 +57,6 @@ class ShardedIndexCorpus:
         self.n_total = int(n_total)
         self.group = group
 
-    def _local_lists(self, qp, mode: int, k: int, thr: float, thr_mode: int):
-        c = self.local
-        if k <= MAX_FUSED_K:
-            return K.scan_topk(qp, c.prep, mode, k, thr, thr_mode, c.id_base)
-        sc = K.level_scores(qp, c.prep, 0 if mode == 0 else -1)
-        return K.select_topk(sc, k, thr, thr_mode, c.id_base)
-
     def progressive(self, queries, max_results: int, threshold: float = 0.1, max_candidates_per_level: int = 100):
         """Global progressive search; every rank returns the same (ids, overall, levels, count)."""
         t = torch()
@@ -73,7 +66,7 @@ class ShardedIndexCorpus:
         M = int(max_candidates_per_level)
         if self.n_total <= M:
             return self.brute_force(queries, max_results)
-        s0, ids, best, bid = self._local_lists(qp, 0, M, float(threshold), 1)
+        s0, ids, _, best, bid = c.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)
         det = K.rescore(qp, c.prep, ids, c.id_base)
         bdet = K.rescore(qp, c.prep, bid.view(Q, 1), c.id_base)
         rec = t.cat([pack(s0, ids, det), pack(best.view(Q, 1), bid.view(Q, 1), bdet)], dim=1)  # [Q, M+1, 2+W]
@@ -90,7 +83,7 @@ class ShardedIndexCorpus:
         qp = c.prepare_queries(queries)
         Q = qp.N
         k = max(1, int(max_results))
-        sc, ids, _, _ = self._local_lists(qp, 1, k, 0.0, 0)
+        sc, ids, _, _, _ = c.exact_topk(qp, 1, k)
         det = K.rescore(qp, c.prep, ids, c.id_base)
         g = all_gather(pack(sc, ids, det), self.group)
         gs, gi, gd = unpack(g)
@@ -109,7 +102,7 @@ class ShardedIndexCorpus:
         qp = c.prepare_queries(queries)
         Q = qp.N
         k = max(1, int(max_results))
-        sc, ids, _, _ = self._local_lists(qp, 0, k, float(threshold), 2)
+        sc, ids, _, _, _ = c.exact_topk(qp, 0, k, float(threshold), 2)
         g = all_gather(pack(sc, ids, sc.unsqueeze(-1)), self.group)
         gs, gi, gd = unpack(g)
         R = g.shape[0]

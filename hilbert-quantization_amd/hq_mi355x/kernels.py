@@ -217,16 +217,20 @@ def seg_padded_len(L: int) -> int:
 
 
 class Prepared:
-    """Device-resident prepared index vectors: Z [N, Lp] f64 (segment padded, normalised) and
-    stats [N, nseg, 4] (mean, std, mean of squares).  Built once per corpus (an index build)."""
+    """Device-resident prepared index vectors: raw R [N, L] f64, Z [N, Lp] f64 (segment padded,
+    normalised) and stats S [N, nseg, 4] (mean, std, mean of squares).  Built once per corpus."""
 
-    __slots__ = ("Z", "S", "L", "N", "nseg", "Lp")
+    __slots__ = ("R", "Z", "S", "L", "N", "nseg", "Lp")
 
-    def __init__(self, Z, S, L):
-        self.Z, self.S, self.L = Z, S, int(L)
+    def __init__(self, R, Z, S, L):
+        self.R, self.Z, self.S, self.L = R, Z, S, int(L)
         self.N = Z.shape[0]
         self.nseg = S.shape[1]
         self.Lp = Z.shape[1]
+
+    def rows(self, sel):
+        """Sub-set of rows (device index tensor) as a new Prepared."""
+        return Prepared(self.R.index_select(0, sel), self.Z.index_select(0, sel), self.S.index_select(0, sel), self.L)
 
 
 def seg_prepare(idx, exc=None) -> Prepared:
@@ -238,21 +242,21 @@ def seg_prepare(idx, exc=None) -> Prepared:
     S = t.empty((N, ns, 4), dtype=t.float64, device=i2.device)
     if N:
         _chk(_L().hq_seg_prepare(ptr(i2), N, L, ptr(Z), ptr(S), stream()), exc)
-    return Prepared(Z, S, L)
+    return Prepared(i2, Z, S, L)
 
 
 def level_scores(q: Prepared, c: Prepared, level: int, exc=None):
-    """Dense [Q, N] level (>= 0) or overall (level = -1) scores."""
+    """Dense EXACT [Q, N] level (>= 0) or overall (level = -1) scores (reference operation order)."""
     t = torch()
     out = t.empty((q.N, c.N), dtype=t.float64, device=q.Z.device)
-    _chk(_L().hq_level_scores(ptr(q.Z), ptr(q.S), q.N, ptr(c.Z), ptr(c.S), c.N, c.L, level, ptr(out), stream()),
-         exc)
+    _chk(_L().hq_level_scores(ptr(q.R), ptr(q.Z), ptr(q.S), q.N, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L, level,
+                              ptr(out), stream()), exc)
     return out
 
 
 def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.0, thr_mode: int = 0,
               id_base: int = 0, exc=None):
-    """Fused MFMA scan + per-query top-k.  mode 0: level-0 score, 1: overall.
+    """Fused MFMA scan + per-query top-k on APPROXIMATE scores.  mode 0: level-0 score, 1: overall.
     thr_mode 0 none / 1 >= / 2 >.  Returns (scores [Q, k], ids [Q, k], best [Q], best_id [Q])."""
     t = torch()
     Q, N = q.N, c.N
@@ -268,14 +272,30 @@ def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.
     return sc, ids, best, bid
 
 
+def refine_topk(q: Prepared, c: Prepared, mode: int, cand_score, cand_id, k: int, threshold: float = 0.0,
+                thr_mode: int = 0, eps: float = 1e-9, id_base: int = 0, exc=None):
+    """Exact re-rank of a scan list -> (scores [Q, k], ids [Q, k], count [Q], resolved [Q])."""
+    t = torch()
+    Q, kp = cand_id.shape
+    dev = cand_id.device
+    os_ = t.empty((Q, k), dtype=t.float64, device=dev)
+    oi = t.empty((Q, k), dtype=t.int64, device=dev)
+    cnt = t.empty(Q, dtype=t.int32, device=dev)
+    res = t.empty(Q, dtype=t.int32, device=dev)
+    _chk(_L().hq_refine_topk(ptr(q.R), ptr(q.Z), ptr(q.S), Q, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L, mode,
+                             ptr(_contig(cand_score)), ptr(_contig(cand_id)), kp, k, float(threshold), thr_mode,
+                             float(eps), int(id_base), ptr(os_), ptr(oi), ptr(cnt), ptr(res), stream()), exc)
+    return os_, oi, cnt, res
+
+
 def rescore(q: Prepared, c: Prepared, ids, id_base: int = 0, exc=None):
-    """[overall, level_0..] for the (query, global id) pairs in ids [Q, k] -> f64 [Q, k, 1 + nseg]."""
+    """EXACT [overall, level_0..] for (query, global id) pairs in ids [Q, k] -> f64 [Q, k, 1 + nseg]."""
     t = torch()
     ids = _contig(ids.to(t.int64))
     Q, k = ids.shape
     out = t.empty((Q, k, 1 + q.nseg), dtype=t.float64, device=ids.device)
-    _chk(_L().hq_rescore(ptr(q.Z), ptr(q.S), Q, ptr(c.Z), ptr(c.S), c.N, c.L, ptr(ids), k, int(id_base), ptr(out),
-                         stream()), exc)
+    _chk(_L().hq_rescore(ptr(q.R), ptr(q.Z), ptr(q.S), Q, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L, ptr(ids), k,
+                         int(id_base), ptr(out), stream()), exc)
     return out
 
 

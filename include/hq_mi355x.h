@@ -142,22 +142,25 @@ int hq_seg_count(int L);
 int hq_seg_padded_len(int L);
 int hq_seg_prepare(const double* idx, int64_t N, int L, double* Z, double* stats, hq_stream_t stream);
 
-/* ---- S3/S4: dense scores ----------------------------------------------------------------------
+/* ---- S3/S4: dense EXACT scores ---------------------------------------------------------------
  * replaces core/search_engine.py:111-189 compare_indices_at_level (level >= 0) and :191-230
- * _calculate_overall_similarity (level == -1) for Q queries against N candidates of equal L,
- * from the hq_seg_prepare outputs of queries (Zq, Sq) and corpus (Zc, Sc).  scores: f64 Q x N.    */
-int hq_level_scores(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc,
-                    int64_t N, int L, int level, double* scores, hq_stream_t stream);
+ * _calculate_overall_similarity (level == -1) for Q queries against N candidates of equal L.
+ * Scores are evaluated in the reference's operation order (products and squared differences
+ * summed in NumPy's pairwise order), so they are bit-identical to the reference.  Inputs per side:
+ * the raw index vectors R (f64 x L) and their hq_seg_prepare outputs (Z, S).  scores: f64 Q x N. */
+int hq_level_scores(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
+                    const double* Zc, const double* Sc, int64_t N, int L, int level, double* scores,
+                    hq_stream_t stream);
 
-/* ---- S5/S6: fused scan with per-query top-k ---------------------------------------------------
- * One pass over the corpus: MFMA f64 contraction (v_mfma_f64_16x16x4f64) + score epilogue +
- * per-query top-k ordered by (score desc, id asc) — Python's stable sort by score, reverse=True.
- *   mode 0: level-0 score (progressive filter, search_engine.py:232-300; video hierarchical scan,
- *           core/video_search.py:215-264); mode 1: overall score (brute_force_search :302-338).
- *   thr_mode 0: keep all; 1: score >= threshold; 2: score > threshold.
- * Also the first arg-max of the score over all candidates (out_best, may be NULL): the
- * reference's "none pass" fallback (:295-298).  id_base is added to local row ids (sharding).
- * out_score/out_id: Q x k (-inf / -1 in empty slots).  1 <= k <= 64.
+/* ---- S5/S6: fused MFMA scan with per-query top-k (APPROXIMATE scores) ------------------------
+ * One pass over the corpus: f64 MFMA contraction (v_mfma_f64_16x16x4f64) of the normalised
+ * vectors + algebraic score epilogue (|score - exact| < 1e-12 for L <= 64) + per-query top-k by
+ * (score desc, id asc).  mode 0: level-0 score (progressive filter, search_engine.py:232-300;
+ * video hierarchical scan, core/video_search.py:215-264); mode 1: overall score
+ * (brute_force_search :302-338).  thr_mode 0: keep all; 1: score >= threshold; 2: > threshold.
+ * Also the first arg-max of the approximate score (out_best, may be NULL).  id_base is added to
+ * local row ids (sharding).  out_score/out_id: Q x k (-inf / -1 in empty slots), 1 <= k <= 64.
+ * The exact ranking is obtained with hq_refine_topk on a slightly larger list.
  * workspace: hq_scan_workspace_size(Q, N, k) bytes of device memory.                            */
 size_t hq_scan_workspace_size(int Q, int64_t N, int k);
 int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc,
@@ -165,12 +168,24 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
                  void* workspace, size_t workspace_bytes, double* out_score, int64_t* out_id,
                  double* out_best, int64_t* out_best_id, hq_stream_t stream);
 
-/* ---- S4 on candidate lists: overall + per-level scores of selected pairs ---------------------
+/* ---- S5/S6: exact re-rank of a scan list -----------------------------------------------------
+ * cand_score/cand_id: Q x kp list from hq_scan_topk (approximate, sorted).  Re-scores every listed
+ * candidate exactly (as hq_level_scores), applies the threshold test exactly and writes the exact
+ * top-k (score desc, id asc): out_score/out_id Q x k, out_count Q, and out_resolved Q = 1 when the
+ * result is provably the exact top-k over the whole corpus given |approx - exact| <= eps (else the
+ * caller re-runs that query on the dense exact path).  kp <= 64, k <= kp.                        */
+int hq_refine_topk(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
+                   const double* Zc, const double* Sc, int64_t N, int L, int mode,
+                   const double* cand_score, const int64_t* cand_id, int kp, int k,
+                   double threshold, int thr_mode, double eps, int64_t id_base, double* out_score,
+                   int64_t* out_id, int* out_count, int* out_resolved, hq_stream_t stream);
+
+/* ---- S4 on candidate lists: EXACT overall + per-level scores of selected pairs ---------------
  * ids: int64 Q x k GLOBAL ids (row = id - id_base; out of range / < 0 -> zeros);
  * out: f64 Q x k x (1 + nseg) = [overall, level_0 .. level_{nseg-1}] (search_engine.py:191-230). */
-int hq_rescore(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc,
-               int64_t N, int L, const int64_t* ids, int k, int64_t id_base, double* out,
-               hq_stream_t stream);
+int hq_rescore(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
+               const double* Zc, const double* Sc, int64_t N, int L, const int64_t* ids, int k,
+               int64_t id_base, double* out, hq_stream_t stream);
 
 /* ---- S5 final stage, R-way (R = number of corpus shards) -------------------------------------
  * Inputs per shard r: level-0 top-M lists s0/ids (R x Q x M, sorted), their rescored rows det

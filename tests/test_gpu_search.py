@@ -59,10 +59,8 @@ def test_level_and_overall_scores_golden(hq_lib, golden, tag):
     corpus = IndexCorpus(C)
     for lv in range(per.shape[2]):
         got = _np(corpus.level_scores(Q, lv))
-        np.testing.assert_allclose(got, per[:, :, lv], rtol=0, atol=TOL)
-        exact = np.isin(per[:, :, lv], [0.0, 0.1, 1.0])
-        assert np.array_equal(got[exact], per[:, :, lv][exact])
-    np.testing.assert_allclose(_np(corpus.level_scores(Q, -1)), ov, rtol=0, atol=TOL)
+        assert np.array_equal(got, per[:, :, lv])          # exact scores are bit-identical
+    assert np.array_equal(_np(corpus.level_scores(Q, -1)), ov)
 
 
 @pytest.mark.parametrize("tag", ["L64", "L32"])
@@ -162,7 +160,7 @@ def test_sharded_merge_equals_single(hq_lib):
         a, b = shard_range(len(C), r, R)
         sh = IndexCorpus(C[a:b], id_base=a)
         qp = sh.prepare_queries(Q)
-        s0, ids, best, bid = K.scan_topk(qp, sh.prep, 0, 20, 0.1, 1, a)
+        s0, ids, _, best, bid = sh.exact_topk(qp, 0, 20, 0.1, 1, need_best=True)
         det = K.rescore(qp, sh.prep, ids, a)
         bdet = K.rescore(qp, sh.prep, bid.view(-1, 1), a)
         recs.append(torch.cat([pack(s0, ids, det), pack(best.view(-1, 1), bid.view(-1, 1), bdet)], dim=1))
