@@ -177,9 +177,10 @@ def main():
         _, corpus_idx, _ = K.map_index_quantize(Xc, n, L)
         del Xc
         # queries = global corpus rows 0..Q-1 (rank 0's shard) + N(0, 0.01) noise, identical on all ranks
-        g0 = torch.Generator(device=dev).manual_seed(2)
-        X0 = torch.randn((Qn, d), generator=g0, device=dev, dtype=torch.float32)
-        _, q0, _ = K.map_index_quantize(X0, n, L)
+        q0 = corpus_idx[:Qn].clone()
+        if world > 1:
+            import torch.distributed as dist
+            dist.broadcast(q0, src=0)
         gq = torch.Generator(device=dev).manual_seed(3)
         queries = q0 + 0.01 * torch.randn(q0.shape, generator=gq, device=dev, dtype=torch.float64)
         torch.cuda.synchronize()

@@ -1,0 +1,312 @@
+// hq_fused.hip — software-pipelined fused map + streaming index + embed + uint8 quantize for the
+// common grid sides (16, 32, 64) and index lengths L <= 64.  Same contract and bit-exact results
+// as k_fused (hq_quant.hip); SURVEY.md §8a rows M5, P1, I1, I3, Q1.
+//
+// Reference sequence: core/pipeline.py:97-146 (pad -> map_to_2d -> streaming index -> embed ->
+// _normalize_for_compression), index tree core/streaming_index_builder.py:45-243.
+//
+// Structure (one wave64 per embedding, persistent grid, HBM-bound):
+//   * lane j owns float4 groups j + 64t (t < ND = data groups per lane); loads are coalesced 1 KiB
+//     wave instructions and the NEXT embedding's groups are loaded before the current one is
+//     processed (explicit A/B register ping-pong), so HBM latency overlaps the arithmetic;
+//   * tree level 1 is a float4 group (registers), level 2 is a quad reduction with DPP quad_perm
+//     broadcasts (same left-to-right f64 order), levels >= 3 are tiny LDS reductions;
+//   * every index slot i < L is owned by lane i, which knows its (level, position) from a host
+//     plan: level-0 / level-1 slots load their own element / group with the prefetch, deeper slots
+//     read the LDS tree — no global re-reads and no second min/max reduction (all index values lie
+//     inside [min, max] of the padded data, core/index_generator.py:247 casts them to f32; only the
+//     zero fill of unused index-row slots can extend the range, decided on the host);
+//   * 2x2 blocks of the image are float4 groups, so each lane scatters two u16 pairs into a
+//     row-major LDS frame that is streamed out with 16-byte stores.
+#include "hq_common.h"
+
+namespace hq {
+
+struct FastPlan {
+  int8_t lev[64];   // slot level (-1: zero fill)
+  int32_t pos[64];  // position inside the level
+  int zero_row;     // index row holds zero-fill slots among its first n entries
+};
+
+template <int CTRL>
+__device__ __forceinline__ double quad_bcast(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ float wmin64(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wmax64(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ uint32_t qz(float x, float mn, float rng) {
+  float t = (x - mn) / rng;  // IEEE f32 division (no fast-math), then * 255 and truncate
+  t = t * 255.0f;
+  return (uint32_t)t;
+}
+
+template <int NS>
+struct FastGeo {
+  static constexpr int G = NS * NS / 4;
+  static constexpr int NT = G / 64;
+  static constexpr int FB = (NS + 1) * NS;
+  static constexpr int levels() {
+    int k = 0, s = NS * NS;
+    while (k < kStreamMaxLevels && s > 0) { ++k; s >>= 2; }
+    return k;
+  }
+  // LDS tree holds levels >= 2; level l (>= 2) has G >> (2(l-1)) values
+  static constexpr int off(int l) {
+    int t = 0, s = G >> 2;
+    for (int k = 2; k < l; ++k) { t += s; s >>= 2; }
+    return t;
+  }
+  static constexpr int tree_len() { return off(levels()); }
+  static constexpr int frame_off() { return ((tree_len() * 8 + G * 4) + 15) & ~15; }
+  static constexpr size_t lds_bytes() { return (size_t)frame_off() + ((FB + 15) & ~15); }
+};
+
+template <int NS, int ND>
+struct Buf {
+  float4 g[ND];
+  float4 slot;
+};
+
+template <int NS, int ND>
+__device__ __forceinline__ void load_emb(const float* __restrict__ src, int d, int lane, int slev, int spos,
+                                         Buf<NS, ND>& b) {
+#pragma unroll
+  for (int t = 0; t < ND; ++t) {
+    const int j = lane + 64 * t;
+    if (4 * j + 3 < d) {
+      b.g[t] = *reinterpret_cast<const float4*>(src + 4 * j);
+    } else {
+      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (4 * j + 0 < d) x.x = src[4 * j + 0];
+      if (4 * j + 1 < d) x.y = src[4 * j + 1];
+      if (4 * j + 2 < d) x.z = src[4 * j + 2];
+      b.g[t] = x;
+    }
+  }
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (slev == 0) {
+    if (spos < d) s.x = src[spos];
+  } else if (slev == 1) {
+    const int p = 4 * spos;
+    if (p + 3 < d) {
+      s = *reinterpret_cast<const float4*>(src + p);
+    } else {
+      if (p + 0 < d) s.x = src[p + 0];
+      if (p + 1 < d) s.y = src[p + 1];
+      if (p + 2 < d) s.z = src[p + 2];
+    }
+  }
+  b.slot = s;
+}
+
+template <int NS, int ND>
+__device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int d, int L, int lane, int slev,
+                                            int spos, bool pad0, double* tree, const uint32_t* lut, uint8_t* frame,
+                                            uint8_t* __restrict__ frame_out, double* __restrict__ idx_out,
+                                            float* __restrict__ mm_out) {
+  using Geo = FastGeo<NS>;
+  constexpr int NLEV = Geo::levels();
+  // ---- min / max over the real elements --------------------------------------------------------
+  float lmin = __builtin_huge_valf(), lmax = -__builtin_huge_valf();
+#pragma unroll
+  for (int t = 0; t < ND; ++t) {
+    const int j = lane + 64 * t;
+    const float4 x = b.g[t];
+    if (4 * j + 3 < d) {
+      lmin = fminf(lmin, fminf(fminf(x.x, x.y), fminf(x.z, x.w)));
+      lmax = fmaxf(lmax, fmaxf(fmaxf(x.x, x.y), fmaxf(x.z, x.w)));
+    } else {
+      if (4 * j + 0 < d) { lmin = fminf(lmin, x.x); lmax = fmaxf(lmax, x.x); }
+      if (4 * j + 1 < d) { lmin = fminf(lmin, x.y); lmax = fmaxf(lmax, x.y); }
+      if (4 * j + 2 < d) { lmin = fminf(lmin, x.z); lmax = fmaxf(lmax, x.z); }
+    }
+  }
+  float mn = wmin64(lmin), mx = wmax64(lmax);
+  if (pad0) { mn = fminf(mn, 0.f); mx = fmaxf(mx, 0.f); }
+
+  // ---- tree: level 1 in registers, level 2 by quad DPP, deeper levels in LDS ---------------------
+  if (NLEV > 2) {
+#pragma unroll
+    for (int t = 0; t < ND; ++t) {
+      const float4 x = b.g[t];
+      const double l1 = ((((double)x.x + (double)x.y) + (double)x.z) + (double)x.w) * 0.25;
+      const double a0 = quad_bcast<0x00>(l1), a1 = quad_bcast<0x55>(l1);
+      const double a2 = quad_bcast<0xAA>(l1), a3 = quad_bcast<0xFF>(l1);
+      const double l2 = (((a0 + a1) + a2) + a3) * 0.25;
+      if ((lane & 3) == 0) tree[Geo::off(2) + (lane >> 2) + 16 * t] = l2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int l = 3; l < NLEV; ++l) {
+      const int S = Geo::G >> (2 * (l - 1));
+      const double* a = tree + Geo::off(l - 1);
+      double* o = tree + Geo::off(l);
+      for (int k = lane; k < S; k += 64) o[k] = (((a[4 * k] + a[4 * k + 1]) + a[4 * k + 2]) + a[4 * k + 3]) * 0.25;
+      __syncthreads();
+    }
+  }
+
+  // ---- this lane's index slot ------------------------------------------------------------------
+  double val = 0.0;
+  if (slev == 0) {
+    val = (double)b.slot.x;
+  } else if (slev == 1) {
+    val = ((((double)b.slot.x + (double)b.slot.y) + (double)b.slot.z) + (double)b.slot.w) * 0.25;
+  } else if (slev >= 2) {
+    val = tree[Geo::off(slev) + spos];
+  }
+  if (lane < L) idx_out[e * (int64_t)L + lane] = val;
+  const float rv = (float)val;
+
+  // ---- quantize into the LDS frame, stream out --------------------------------------------------
+  const bool flat = mx == mn;
+  const float rng = mx - mn;
+  const uint32_t q0 = flat ? 128u : qz(0.f, mn, rng);
+  const int groups_data = (d + 3) >> 2;
+  if (d < NS * NS || flat) {
+    const uint32_t w = q0 * 0x01010101u;
+    const uint4 w4 = make_uint4(w, w, w, w);
+#pragma unroll
+    for (int c = lane; c < NS * NS / 16; c += 64) reinterpret_cast<uint4*>(frame)[c] = w4;
+  }
+  if (!flat) {
+#pragma unroll
+    for (int t = 0; t < ND; ++t) {
+      const int j = lane + 64 * t;
+      if (j < groups_data) {
+        const float4 x = b.g[t];
+        const uint32_t e0 = qz(x.x, mn, rng);
+        const uint32_t e1 = (4 * j + 1 < d) ? qz(x.y, mn, rng) : q0;
+        const uint32_t e2 = (4 * j + 2 < d) ? qz(x.z, mn, rng) : q0;
+        const uint32_t e3 = (4 * j + 3 < d) ? qz(x.w, mn, rng) : q0;
+        const uint32_t ent = lut[j];
+        const uint32_t code = ent >> 16;
+        const uint32_t w = (e0 << (8 * (code & 3))) | (e1 << (8 * ((code >> 2) & 3))) |
+                           (e2 << (8 * ((code >> 4) & 3))) | (e3 << (8 * ((code >> 6) & 3)));
+        const uint32_t off = ent & 0xFFFFu;
+        *reinterpret_cast<uint16_t*>(frame + off) = (uint16_t)(w & 0xFFFFu);
+        *reinterpret_cast<uint16_t*>(frame + off + NS) = (uint16_t)(w >> 16);
+      }
+    }
+  }
+  if (lane < NS) frame[NS * NS + lane] = flat ? (uint8_t)128 : (uint8_t)qz(rv, mn, rng);
+  __syncthreads();
+  uint8_t* dst = frame_out + e * (int64_t)Geo::FB;
+#pragma unroll
+  for (int c = lane; c < Geo::FB / 16; c += 64)
+    reinterpret_cast<uint4*>(dst)[c] = reinterpret_cast<const uint4*>(frame)[c];
+  if (mm_out && lane == 0) {
+    mm_out[2 * e] = mn;
+    mm_out[2 * e + 1] = mx;
+  }
+  __syncthreads();
+}
+
+template <int NS, int ND>
+__global__ __launch_bounds__(64) void k_fused_fast(const float* __restrict__ in, int64_t N, int64_t stride, int d,
+                                                   int L, FastPlan plan, uint8_t* __restrict__ frame_out,
+                                                   double* __restrict__ idx_out, float* __restrict__ mm_out) {
+  using Geo = FastGeo<NS>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  double* tree = reinterpret_cast<double*>(smem);
+  uint32_t* lut = reinterpret_cast<uint32_t*>(smem + Geo::tree_len() * 8);
+  uint8_t* frame = smem + Geo::frame_off();
+  const int lane = threadIdx.x;
+  for (int j = lane; j < Geo::G; j += 64) {
+    uint32_t code = 0, off = 0;
+    for (uint32_t m = 0; m < 4; ++m) {
+      uint32_t x, y;
+      d2xy(NS, 4 * j + m, x, y);
+      if (m == 0) off = (y & ~1u) * NS + (x & ~1u);
+      code |= ((x & 1u) + 2u * (y & 1u)) << (2 * m);
+    }
+    lut[j] = off | (code << 16);
+  }
+  // level-2 nodes of all-padding groups (t >= ND) are 0.0 for every embedding: zero once
+  for (int k = lane; k < Geo::tree_len(); k += 64) tree[k] = 0.0;
+  __syncthreads();
+
+  const int slev = lane < L ? (int)plan.lev[lane] : -1;
+  const int spos = lane < L ? plan.pos[lane] : 0;
+  const bool pad0 = (d < NS * NS) || plan.zero_row;
+  Buf<NS, ND> A, B;
+  int64_t e = blockIdx.x;
+  if (e < N) load_emb<NS, ND>(in + e * stride, d, lane, slev, spos, A);
+  while (e < N) {
+    int64_t e2 = e + gridDim.x;
+    if (e2 < N) load_emb<NS, ND>(in + e2 * stride, d, lane, slev, spos, B);
+    process_emb<NS, ND>(e, A, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
+    e = e2;
+    if (e >= N) break;
+    e2 = e + gridDim.x;
+    if (e2 < N) load_emb<NS, ND>(in + e2 * stride, d, lane, slev, spos, A);
+    process_emb<NS, ND>(e, B, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
+    e = e2;
+  }
+}
+
+template <int NS, int ND>
+static int launch_ff(const float* in, int64_t N, int64_t stride, int d, int L, const FastPlan& plan, uint8_t* frame,
+                     double* idx, float* mm, hipStream_t s) {
+  using Geo = FastGeo<NS>;
+  const size_t lds = Geo::lds_bytes();
+  const int grid = persistent_grid((const void*)k_fused_fast<NS, ND>, 64, lds, N);
+  hipLaunchKernelGGL((k_fused_fast<NS, ND>), dim3(grid), dim3(64), lds, s, in, N, stride, d, L, plan, frame, idx, mm);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+template <int NS, int ND>
+static int pick_nd(int nd, const float* in, int64_t N, int64_t stride, int d, int L, const FastPlan& plan,
+                   uint8_t* frame, double* idx, float* mm, hipStream_t s) {
+  if constexpr (ND > FastGeo<NS>::NT) {
+    return HQ_E_UNSUPPORTED;
+  } else {
+    if (nd == ND) return launch_ff<NS, ND>(in, N, stride, d, L, plan, frame, idx, mm, s);
+    return pick_nd<NS, ND + 1>(nd, in, N, stride, d, L, plan, frame, idx, mm, s);
+  }
+}
+
+// Returns HQ_E_UNSUPPORTED (without launching) when the fast path does not apply.
+int fused_fast(const float* in, int64_t N, int64_t stride, int d, int n, int L, uint8_t* frame, double* idx,
+               float* mm, hipStream_t s) {
+  if (!(n == 16 || n == 32 || n == 64)) return HQ_E_UNSUPPORTED;
+  if (L < 1 || L > 64 || !idx || d < 1) return HQ_E_UNSUPPORTED;
+  if ((reinterpret_cast<uintptr_t>(in) & 15) || (stride % 4) || (reinterpret_cast<uintptr_t>(frame) & 15))
+    return HQ_E_UNSUPPORTED;
+  StreamSchedule sched;
+  stream_schedule((int64_t)n * n, L, sched);
+  FastPlan plan;
+  plan.zero_row = 0;
+  for (int i = 0; i < 64; ++i) {
+    int lev = -1;
+    int64_t pos = 0;
+    if (i < L && stream_sample(sched, i, lev, pos)) {
+      plan.lev[i] = (int8_t)lev;
+      plan.pos[i] = (int32_t)pos;
+    } else {
+      plan.lev[i] = -1;
+      plan.pos[i] = 0;
+      if (i < n) plan.zero_row = 1;
+    }
+  }
+  if (L < n) plan.zero_row = 1;
+  const int nd = (((d + 3) / 4) + 63) / 64;
+  switch (n) {
+    case 16: return pick_nd<16, 1>(nd, in, N, stride, d, L, plan, frame, idx, mm, s);
+    case 32: return pick_nd<32, 1>(nd, in, N, stride, d, L, plan, frame, idx, mm, s);
+    case 64: return pick_nd<64, 1>(nd, in, N, stride, d, L, plan, frame, idx, mm, s);
+  }
+  return HQ_E_UNSUPPORTED;
+}
+
+}  // namespace hq

@@ -334,16 +334,17 @@ static int dispatch_chunk(int ns, const uint16_t* in, int64_t total, int chunk, 
 
 // block means in row-major section order (core/index_generator.py:100-144) or in the RAG
 // generator's Hilbert order (hierarchical_index_generator.py:204-244); one thread per block
-__global__ __launch_bounds__(256) void k_block_means(const float* __restrict__ img, int64_t N, int n, int g,
-                                                     int order, float* __restrict__ out) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_block_means(const T* __restrict__ img, int64_t N, int n, int g,
+                                                     int order, T* __restrict__ out) {
   const int sh = n / g;
   const int cnt = sh == 0 ? 1 : g * g;
   const int64_t total = N * cnt;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = t / cnt;
     const int k = (int)(t % cnt);
-    const float* im = img + e * (int64_t)n * n;
-    float v;
+    const T* im = img + e * (int64_t)n * n;
+    T v;
     if (sh == 0) {
       v = np_mean_block(im, n, n, n);
     } else {
@@ -385,14 +386,22 @@ int hq_index_traditional_f32(const float* img, int64_t N, int n, int L, float* o
   return HQ_OK;
 }
 
-int hq_block_means_f32(const float* img, int64_t N, int n, int grid, int order, float* out, hq_stream_t stream) {
+int hq_block_means(int dtype, const void* img, int64_t N, int n, int grid, int order, void* out,
+                   hq_stream_t stream) {
   if (n <= 0 || grid <= 0 || N < 0) return fail(HQ_E_INVALID, "bad shape n=%d grid=%d", n, grid);
   if (N == 0) return HQ_OK;
   if (!img || !out) return fail(HQ_E_INVALID, "null buffer");
   const int cnt = (n / grid == 0) ? 1 : grid * grid;
   int64_t blocks = (N * cnt + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(k_block_means, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, img, N, n, grid, order, out);
+  if (dtype == HQ_F32)
+    hipLaunchKernelGGL(k_block_means<float>, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (const float*)img, N,
+                       n, grid, order, (float*)out);
+  else if (dtype == HQ_F64)
+    hipLaunchKernelGGL(k_block_means<double>, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (const double*)img,
+                       N, n, grid, order, (double*)out);
+  else
+    return fail(HQ_E_UNSUPPORTED, "block means dtype %d (f32/f64)", dtype);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }

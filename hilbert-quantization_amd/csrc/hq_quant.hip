@@ -21,6 +21,8 @@
 //   * f32 quantize uses IEEE division (-ffp-contract=off, no fast-math) => bit-exact frames.
 #include "hq_common.h"
 
+#include <stdlib.h>
+
 namespace hq {
 
 __device__ __forceinline__ float wave_min(float v) {
@@ -371,6 +373,11 @@ __global__ void k_dequantize(const uint8_t* __restrict__ u8, int64_t N, int64_t 
 
 }  // namespace hq
 
+namespace hq {
+int fused_fast(const float* in, int64_t N, int64_t stride, int d, int n, int L, uint8_t* frame, double* idx,
+               float* mm, hipStream_t s);  // hq_fused.hip
+}
+
 using namespace hq;
 
 extern "C" {
@@ -386,6 +393,10 @@ int hq_map_index_quantize(const float* in, int64_t N, int64_t in_stride, int d, 
   if (N == 0) return HQ_OK;
   if (!frame || (d > 0 && !in)) return fail(HQ_E_INVALID, "null buffer");
   hipStream_t s = (hipStream_t)stream;
+  if (!getenv("HQ_FUSED_GENERIC")) {  // software-pipelined path for n in {16, 32, 64}, L <= 64
+    const int rc = fused_fast(in, N, in_stride, d, n, L, frame, idx, minmax, s);
+    if (rc != HQ_E_UNSUPPORTED) return rc;
+  }
   switch (n) {
     case 2: return launch_fused<2>(in, N, in_stride, d, L, frame, idx, minmax, s);
     case 4: return launch_fused<4>(in, N, in_stride, d, L, frame, idx, minmax, s);

@@ -286,6 +286,10 @@ __global__ __launch_bounds__(256) void k_scan(ScanArgs a) {
     tau[i] = -__builtin_huge_val();
     lcnt[i] = 0;
   }
+  for (int i = tid; i < kQB * a.K; i += 256) {
+    lscore[i] = -__builtin_huge_val();
+    lid[i] = -1;
+  }
   // lane's best (first arg-max) for its 4 query rows
   double best[4];
   int64_t best_id[4];
@@ -294,21 +298,74 @@ __global__ __launch_bounds__(256) void k_scan(ScanArgs a) {
   __syncthreads();
 
   const int pieces_per_row = 2 * a.ks;  // 16-byte pieces of the used K columns
+  const int npieces = kCB * pieces_per_row;
+  const int nstat = kCB * nsu * 4;
+  // register prefetch of the next candidate tile (software pipelining) for the short-K scans
+  constexpr bool PREF = KSMAX <= 16;
+  constexpr int PMAX = PREF ? (kCB * 2 * KSMAX + 255) / 256 : 1;
+  constexpr int SMAX = PREF ? (kCB * 4 + 255) / 256 : 1;
+  double2 pf[PMAX];
+  double ps[SMAX];
+  auto fetch = [&](int64_t cs) {
+#pragma unroll
+    for (int u = 0; u < PMAX; ++u) {
+      const int p = tid + 256 * u;
+      double2 v = make_double2(0.0, 0.0);
+      if (p < npieces) {
+        const int c = p / pieces_per_row, kk = p % pieces_per_row;
+        const int64_t gc = cs + c;
+        if (gc < c_end) v = *reinterpret_cast<const double2*>(a.Zc + gc * si.Lp + 2 * kk);
+      }
+      pf[u] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < SMAX; ++u) {
+      const int i = tid + 256 * u;
+      double v = 1.0;
+      if (i < nstat) {
+        const int c = i / 4, j = i % 4;  // nsu == 1 on this path
+        const int64_t gc = cs + c;
+        if (gc < c_end) v = a.Sc[gc * si.nseg * 4 + j];
+      }
+      ps[u] = v;
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int u = 0; u < PMAX; ++u) {
+      const int p = tid + 256 * u;
+      if (p < npieces) {
+        const int c = p / pieces_per_row, kk = p % pieces_per_row;
+        *reinterpret_cast<double2*>(btile + c * a.rs + 2 * kk) = pf[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SMAX; ++u) {
+      const int i = tid + 256 * u;
+      if (i < nstat) cstat[i] = ps[u];
+    }
+  };
+  if (PREF && nsu == 1 && c_begin < c_end) fetch(c_begin);
   for (int64_t cs = c_begin; cs < c_end; cs += kCB) {
     // ---- stage candidate tile + stats -------------------------------------------------------
-    for (int p = tid; p < kCB * pieces_per_row; p += 256) {
-      const int c = p / pieces_per_row, kk = p % pieces_per_row;
-      const int64_t gc = cs + c;
-      double2 v = make_double2(0.0, 0.0);
-      if (gc < c_end) v = *reinterpret_cast<const double2*>(a.Zc + gc * si.Lp + 2 * kk);
-      *reinterpret_cast<double2*>(btile + c * a.rs + 2 * kk) = v;
-    }
-    for (int i = tid; i < kCB * nsu; i += 256) {
-      const int c = i / nsu, s = i % nsu;
-      const int64_t gc = cs + c;
-      for (int j = 0; j < 4; ++j) cstat[i * 4 + j] = (gc < c_end) ? a.Sc[(gc * si.nseg + s) * 4 + j] : 1.0;
+    if (PREF && nsu == 1) {
+      stash();
+    } else {
+      for (int p = tid; p < npieces; p += 256) {
+        const int c = p / pieces_per_row, kk = p % pieces_per_row;
+        const int64_t gc = cs + c;
+        double2 v = make_double2(0.0, 0.0);
+        if (gc < c_end) v = *reinterpret_cast<const double2*>(a.Zc + gc * si.Lp + 2 * kk);
+        *reinterpret_cast<double2*>(btile + c * a.rs + 2 * kk) = v;
+      }
+      for (int i = tid; i < kCB * nsu; i += 256) {
+        const int c = i / nsu, s = i % nsu;
+        const int64_t gc = cs + c;
+        for (int j = 0; j < 4; ++j) cstat[i * 4 + j] = (gc < c_end) ? a.Sc[(gc * si.nseg + s) * 4 + j] : 1.0;
+      }
     }
     __syncthreads();
+    if (PREF && nsu == 1 && cs + kCB < c_end) fetch(cs + kCB);  // next tile in flight during compute
 
     // ---- contraction + epilogue ---------------------------------------------------------------
 #pragma unroll
@@ -371,32 +428,36 @@ __global__ __launch_bounds__(256) void k_scan(ScanArgs a) {
     }
     __syncthreads();
 
-    // ---- owner lanes merge passing candidates into the sorted per-query lists -----------------
-    if (lane < 16) {
-      const int ql = wave * 16 + lane;
+    // ---- merge passing candidates into the sorted per-query lists, one wave per query ---------
+    // (lists sorted by (score desc, id asc); a candidate's slot = #entries better than it, found with
+    // one ballot; the tail shifts by one lane)
+    for (int qq = 0; qq < 16; ++qq) {
+      const int ql = wave * 16 + qq;
       unsigned long long m = mask[ql];
-      if (m) {
-        double* ls = lscore + ql * a.K;
-        int64_t* li = lid + ql * a.K;
-        int cnt = lcnt[ql];
-        while (m) {
-          const int bit = __builtin_ctzll(m);
-          m &= m - 1;
-          const double s = stile[ql * kCB + bit];
-          const int64_t id = cs + bit;
-          if (cnt == a.K && !better(s, id, ls[a.K - 1], li[a.K - 1])) continue;
-          int pos = cnt < a.K ? cnt : a.K - 1;
-          while (pos > 0 && better(s, id, ls[pos - 1], li[pos - 1])) {
-            ls[pos] = ls[pos - 1];
-            li[pos] = li[pos - 1];
-            --pos;
-          }
-          ls[pos] = s;
-          li[pos] = id;
-          if (cnt < a.K) ++cnt;
-        }
-        lcnt[ql] = cnt;
-        tau[ql] = (cnt == a.K) ? ls[a.K - 1] : -__builtin_huge_val();
+      if (m == 0ull) continue;
+      double es = lane < a.K ? lscore[ql * a.K + lane] : -__builtin_huge_val();
+      int64_t ei = lane < a.K ? lid[ql * a.K + lane] : -1;
+      while (m) {
+        const int bit = __builtin_ctzll(m);
+        m &= m - 1;
+        const double sc = stile[ql * kCB + bit];
+        const int64_t id = cs + bit;
+        const bool bt = (ei >= 0) && better(es, ei, sc, id);
+        const int p = __popcll(__ballot(bt));
+        if (p >= a.K) continue;
+        const double us = __shfl_up(es, 1, 64);
+        const int64_t ui = __shfl_up(ei, 1, 64);
+        if (lane > p) { es = us; ei = ui; }
+        if (lane == p) { es = sc; ei = id; }
+      }
+      if (lane < a.K) {
+        lscore[ql * a.K + lane] = es;
+        lid[ql * a.K + lane] = ei;
+      }
+      const double wsc = __shfl(es, a.K - 1, 64);
+      const int64_t wid = __shfl(ei, a.K - 1, 64);
+      if (lane == 0) {
+        tau[ql] = wid >= 0 ? wsc : -__builtin_huge_val();
         mask[ql] = 0ull;
       }
     }
@@ -409,7 +470,7 @@ __global__ __launch_bounds__(256) void k_scan(ScanArgs a) {
     const int q = qb * kQB + ql;
     if (q >= a.Q) continue;
     const int64_t o = ((int64_t)chunk * a.Q + q) * a.K + j;
-    if (j < lcnt[ql]) {
+    if (lid[ql * a.K + j] >= 0) {
       a.ws_score[o] = lscore[ql * a.K + j];
       a.ws_id[o] = lid[ql * a.K + j] + a.id_base;
     } else {

@@ -40,7 +40,7 @@ SIGNATURES = {
     "hq_index_streaming": (_i, [_i, _p, _i64, _i, _i, _i, _p, _p]),
     "hq_index_traditional_f32": (_i, [_p, _i64, _i, _i, _p, _p]),
     "hq_rag_index_rows": (_i, [_i]),
-    "hq_block_means_f32": (_i, [_p, _i64, _i, _i, _i, _p, _p]),
+    "hq_block_means": (_i, [_i, _p, _i64, _i, _i, _i, _p, _p]),
     "hq_index_rag_f32": (_i, [_p, _i64, _i, _p, _p]),
     "hq_quantize_u8": (_i, [_p, _i64, _i, _i, _p, _p, _p]),
     "hq_dequantize_u8": (_i, [_p, _i64, _i, _i, _p, _p, _p]),

@@ -64,7 +64,9 @@ class HierarchicalIndexGeneratorImpl:
     def calculate_spatial_averages(self, image, grid_size: int) -> List[float]:
         if image.size == 0 or grid_size <= 0:
             return []
-        img = np.asarray(image, dtype=np.float32)
+        img = np.asarray(image)
+        if img.dtype not in (np.float32, np.float64):
+            img = img.astype(np.float64)
         return [float(v) for v in to_np(K.block_means(to_dev(img), int(grid_size), 0))]
 
     def calculate_offset_samples(self, image, section_size: int, available_space: int) -> List[float]:

@@ -102,11 +102,13 @@ def block_means(img, grid: int, order: int = 0, exc=None):
     """np.mean of each block: order 0 row-major sections, 1 RAG Hilbert order -> f32 [N, cnt]."""
     t = torch()
     squeeze = img.dim() == 2
-    im = _contig((img.unsqueeze(0) if squeeze else img).to(t.float32))
+    im = _contig(img.unsqueeze(0) if squeeze else img)
+    if im.dtype not in (t.float32, t.float64):
+        im = im.to(t.float32)
     N, n, _ = im.shape
     cnt = 1 if n // grid == 0 else grid * grid
-    out = t.empty((N, cnt), dtype=t.float32, device=im.device)
-    _chk(_L().hq_block_means_f32(ptr(im), N, n, int(grid), int(order), ptr(out), stream()), exc)
+    out = t.empty((N, cnt), dtype=im.dtype, device=im.device)
+    _chk(_L().hq_block_means(dtype_code(im.dtype), ptr(im), N, n, int(grid), int(order), ptr(out), stream()), exc)
     return out[0] if squeeze else out
 
 

@@ -81,8 +81,8 @@ class HierarchicalIndexGenerator:
     def _calculate_hilbert_order_averages(self, image, granularity: int) -> np.ndarray:
         img = np.asarray(image)
         h, w = img.shape
-        if h != w or img.dtype != np.float32:
-            raise ValueError("GPU block means need a square float32 image")
+        if h != w or img.dtype not in (np.float32, np.float64):
+            raise ValueError("GPU block means need a square float32/float64 image")
         return to_np(K.block_means(to_dev(img), int(granularity), 1))
 
     def embed_multi_level_indices(self, image, index_rows: List[np.ndarray]):

@@ -86,12 +86,13 @@ int hq_index_traditional_f32(const float* img, int64_t N, int n, int L, float* o
                              hq_stream_t stream);
 
 /* ---- I2/I4 building block: block means ---------------------------------------------------------
- * np.mean of each (n/grid)^2 block of f32 N x n x n images (NumPy pairwise order, f32 result):
+ * np.mean of each (n/grid)^2 block of N x n x n images (dtype HQ_F32 or HQ_F64, NumPy pairwise
+ * order in that dtype, result in that dtype):
  * order 0 = row-major sections (core/index_generator.py:100-144 calculate_spatial_averages);
  * order 1 = the RAG generator's Hilbert order (hierarchical_index_generator.py:204-244).
- * out: f32 N x cnt with cnt = grid*grid (1 = whole-image mean when grid > n).                   */
-int hq_block_means_f32(const float* img, int64_t N, int n, int grid, int order, float* out,
-                       hq_stream_t stream);
+ * out: N x cnt with cnt = grid*grid (1 = whole-image mean when grid > n).                       */
+int hq_block_means(int dtype, const void* img, int64_t N, int n, int grid, int order, void* out,
+                   hq_stream_t stream);
 
 /* ---- I4: RAG multi-row index ---------------------------------------------------------------
  * replaces rag/embedding_generation/hierarchical_index_generator.py:103-146

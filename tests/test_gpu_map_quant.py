@@ -200,6 +200,30 @@ def test_fused_kernel_vs_oracle(hq_lib, n, d, L):
     assert np.array_equal(got[:, 0], mn) and np.array_equal(got[:, 1], mx)
 
 
+@pytest.mark.parametrize("n,d,L", [(32, 1000, 32), (64, 1536, 64), (64, 4096, 30), (16, 256, 16)])
+def test_fused_generic_path_vs_oracle(hq_lib, n, d, L, monkeypatch):
+    """The non-pipelined kernel (n outside {16,32,64}, L > 64, unaligned rows) stays bit-exact too."""
+    from hq_mi355x import kernels as K
+    monkeypatch.setenv("HQ_FUSED_GENERIC", "1")
+    rng = np.random.default_rng(d + L)
+    P = rng.standard_normal((19, d)).astype(np.float32)
+    fr, idx, mm = K.map_index_quantize(_t(P), n, L)
+    u8, ridx, mn, mx = _oracle_fused(P, n, L)
+    assert _np(fr).tobytes() == u8.tobytes()
+    assert _np(idx).tobytes() == ridx.tobytes()
+
+
+def test_fused_unaligned_rows(hq_lib):
+    """Row stride not a multiple of 4 floats: the fast path declines, results still exact."""
+    from hq_mi355x import kernels as K
+    import torch
+    x = torch.randn(23, 1537, device="cuda")
+    sub = x[:, :1536]
+    fr, idx, _ = K.map_index_quantize(sub, 64, 64)
+    u8, ridx, _, _ = _oracle_fused(sub.cpu().numpy(), 64, 64)
+    assert _np(fr).tobytes() == u8.tobytes() and _np(idx).tobytes() == ridx.tobytes()
+
+
 def test_quantize_dequantize_vs_oracle(hq_lib, golden):
     from hq_mi355x.core import MPEGAICompressorImpl
     from hq_mi355x import kernels as K
