@@ -20,6 +20,8 @@
 //     row-major LDS frame that is streamed out with 16-byte stores.
 #include "hq_common.h"
 
+#include <stdlib.h>
+
 namespace hq {
 
 struct FastPlan {
@@ -35,18 +37,50 @@ __device__ __forceinline__ double quad_bcast(double v) {
   return __hiloint2double(hi, lo);
 }
 
+// wave64 all-reduce through DPP (xor 1, xor 2, half-row mirror, row mirror) and four readlanes: no
+// LDS round trips on the per-embedding critical path
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lanef(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 __device__ __forceinline__ float wmin64(float v) {
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fminf(v, dppf<0xB1>(v));
+  v = fminf(v, dppf<0x4E>(v));
+  v = fminf(v, dppf<0x141>(v));
+  v = fminf(v, dppf<0x140>(v));
+  return fminf(fminf(lanef(v, 0), lanef(v, 16)), fminf(lanef(v, 32), lanef(v, 48)));
 }
 __device__ __forceinline__ float wmax64(float v) {
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  v = fmaxf(v, dppf<0x140>(v));
+  return fmaxf(fmaxf(lanef(v, 0), lanef(v, 16)), fmaxf(lanef(v, 32), lanef(v, 48)));
 }
 __device__ __forceinline__ uint32_t qz(float x, float mn, float rng) {
   float t = (x - mn) / rng;  // IEEE f32 division (no fast-math), then * 255 and truncate
   t = t * 255.0f;
   return (uint32_t)t;
+}
+// Fast form of qz: y' = ((x - mn) * fl(1/rng)) * 255 differs from the reference's
+// fl(fl((x - mn) / rng) * 255) by < 1e-4 (two roundings of relative 2^-24 on a value <= 255), so
+// trunc(y') == trunc(y) whenever y' is more than 1e-3 away from an integer; otherwise `slow` is set
+// and the caller recomputes that element with the exact division.
+__device__ __forceinline__ uint32_t qfast(float x, float mn, float rcp, bool& slow) {
+  const float y = ((x - mn) * rcp) * 255.0f;
+  const float fl = floorf(y);
+  const float f = y - fl;
+  slow |= (f < 1e-3f) | (f > 0.999f);
+  return (uint32_t)fl;
+}
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_stream(const float* p) {  // read-once stream: non-temporal
+  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
 }
 
 template <int NS>
@@ -76,14 +110,15 @@ struct Buf {
   float4 slot;
 };
 
-template <int NS, int ND>
+template <int NS, int ND, int V>
 __device__ __forceinline__ void load_emb(const float* __restrict__ src, int d, int lane, int slev, int spos,
                                          Buf<NS, ND>& b) {
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
     const int j = lane + 64 * t;
     if (4 * j + 3 < d) {
-      b.g[t] = *reinterpret_cast<const float4*>(src + 4 * j);
+      if constexpr ((V & 1) != 0) b.g[t] = ld_stream(src + 4 * j);
+      else b.g[t] = *reinterpret_cast<const float4*>(src + 4 * j);
     } else {
       float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
       if (4 * j + 0 < d) x.x = src[4 * j + 0];
@@ -108,7 +143,7 @@ __device__ __forceinline__ void load_emb(const float* __restrict__ src, int d, i
   b.slot = s;
 }
 
-template <int NS, int ND>
+template <int NS, int ND, int V>
 __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int d, int L, int lane, int slev,
                                             int spos, bool pad0, double* tree, const uint32_t* lut, uint8_t* frame,
                                             uint8_t* __restrict__ frame_out, double* __restrict__ idx_out,
@@ -179,15 +214,34 @@ __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int
     for (int c = lane; c < NS * NS / 16; c += 64) reinterpret_cast<uint4*>(frame)[c] = w4;
   }
   if (!flat) {
+    const float rcp = 1.0f / rng;
+    (void)rcp;
 #pragma unroll
     for (int t = 0; t < ND; ++t) {
       const int j = lane + 64 * t;
       if (j < groups_data) {
         const float4 x = b.g[t];
-        const uint32_t e0 = qz(x.x, mn, rng);
-        const uint32_t e1 = (4 * j + 1 < d) ? qz(x.y, mn, rng) : q0;
-        const uint32_t e2 = (4 * j + 2 < d) ? qz(x.z, mn, rng) : q0;
-        const uint32_t e3 = (4 * j + 3 < d) ? qz(x.w, mn, rng) : q0;
+        uint32_t e0, e1, e2, e3;
+        if constexpr ((V & 2) != 0) {
+          bool slow = false;
+          e0 = qfast(x.x, mn, rcp, slow);
+          e1 = (4 * j + 1 < d) ? qfast(x.y, mn, rcp, slow) : q0;
+          e2 = (4 * j + 2 < d) ? qfast(x.z, mn, rcp, slow) : q0;
+          e3 = (4 * j + 3 < d) ? qfast(x.w, mn, rcp, slow) : q0;
+          if (__builtin_amdgcn_ballot_w64(slow)) {  // rare: some lane is within 1e-3 of a level edge
+            if (slow) {
+              e0 = qz(x.x, mn, rng);
+              e1 = (4 * j + 1 < d) ? qz(x.y, mn, rng) : q0;
+              e2 = (4 * j + 2 < d) ? qz(x.z, mn, rng) : q0;
+              e3 = (4 * j + 3 < d) ? qz(x.w, mn, rng) : q0;
+            }
+          }
+        } else {
+          e0 = qz(x.x, mn, rng);
+          e1 = (4 * j + 1 < d) ? qz(x.y, mn, rng) : q0;
+          e2 = (4 * j + 2 < d) ? qz(x.z, mn, rng) : q0;
+          e3 = (4 * j + 3 < d) ? qz(x.w, mn, rng) : q0;
+        }
         const uint32_t ent = lut[j];
         const uint32_t code = ent >> 16;
         const uint32_t w = (e0 << (8 * (code & 3))) | (e1 << (8 * ((code >> 2) & 3))) |
@@ -211,7 +265,7 @@ __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int
   __syncthreads();
 }
 
-template <int NS, int ND>
+template <int NS, int ND, int V>
 __global__ __launch_bounds__(64) void k_fused_fast(const float* __restrict__ in, int64_t N, int64_t stride, int d,
                                                    int L, FastPlan plan, uint8_t* __restrict__ frame_out,
                                                    double* __restrict__ idx_out, float* __restrict__ mm_out) {
@@ -238,41 +292,79 @@ __global__ __launch_bounds__(64) void k_fused_fast(const float* __restrict__ in,
   const int slev = lane < L ? (int)plan.lev[lane] : -1;
   const int spos = lane < L ? plan.pos[lane] : 0;
   const bool pad0 = (d < NS * NS) || plan.zero_row;
-  Buf<NS, ND> A, B;
+  // V & 4: three register buffers — while embedding e is processed, e+G and e+2G are in flight (HBM
+  // latency under full load is several microseconds; one embedding of prefetch left waves ~70%
+  // stalled); otherwise two buffers.
+  const int64_t G = gridDim.x;
   int64_t e = blockIdx.x;
-  if (e < N) load_emb<NS, ND>(in + e * stride, d, lane, slev, spos, A);
-  while (e < N) {
-    int64_t e2 = e + gridDim.x;
-    if (e2 < N) load_emb<NS, ND>(in + e2 * stride, d, lane, slev, spos, B);
-    process_emb<NS, ND>(e, A, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
-    e = e2;
-    if (e >= N) break;
-    e2 = e + gridDim.x;
-    if (e2 < N) load_emb<NS, ND>(in + e2 * stride, d, lane, slev, spos, A);
-    process_emb<NS, ND>(e, B, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
-    e = e2;
+  if constexpr ((V & 4) != 0) {
+    Buf<NS, ND> A, B, C;
+    if (e < N) load_emb<NS, ND, V>(in + e * stride, d, lane, slev, spos, A);
+    if (e + G < N) load_emb<NS, ND, V>(in + (e + G) * stride, d, lane, slev, spos, B);
+    while (e < N) {
+      if (e + 2 * G < N) load_emb<NS, ND, V>(in + (e + 2 * G) * stride, d, lane, slev, spos, C);
+      process_emb<NS, ND, V>(e, A, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
+      e += G;
+      if (e >= N) break;
+      if (e + 2 * G < N) load_emb<NS, ND, V>(in + (e + 2 * G) * stride, d, lane, slev, spos, A);
+      process_emb<NS, ND, V>(e, B, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
+      e += G;
+      if (e >= N) break;
+      if (e + 2 * G < N) load_emb<NS, ND, V>(in + (e + 2 * G) * stride, d, lane, slev, spos, B);
+      process_emb<NS, ND, V>(e, C, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
+      e += G;
+    }
+  } else {
+    Buf<NS, ND> A, B;
+    if (e < N) load_emb<NS, ND, V>(in + e * stride, d, lane, slev, spos, A);
+    while (e < N) {
+      if (e + G < N) load_emb<NS, ND, V>(in + (e + G) * stride, d, lane, slev, spos, B);
+      process_emb<NS, ND, V>(e, A, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
+      e += G;
+      if (e >= N) break;
+      if (e + G < N) load_emb<NS, ND, V>(in + (e + G) * stride, d, lane, slev, spos, A);
+      process_emb<NS, ND, V>(e, B, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
+      e += G;
+    }
   }
 }
 
-template <int NS, int ND>
+template <int NS, int ND, int V>
 static int launch_ff(const float* in, int64_t N, int64_t stride, int d, int L, const FastPlan& plan, uint8_t* frame,
                      double* idx, float* mm, hipStream_t s) {
   using Geo = FastGeo<NS>;
   const size_t lds = Geo::lds_bytes();
-  const int grid = persistent_grid((const void*)k_fused_fast<NS, ND>, 64, lds, N);
-  hipLaunchKernelGGL((k_fused_fast<NS, ND>), dim3(grid), dim3(64), lds, s, in, N, stride, d, L, plan, frame, idx, mm);
+  const int grid = persistent_grid((const void*)k_fused_fast<NS, ND, V>, 64, lds, N);
+  hipLaunchKernelGGL((k_fused_fast<NS, ND, V>), dim3(grid), dim3(64), lds, s, in, N, stride, d, L, plan, frame, idx,
+                     mm);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
 
+constexpr int kDefaultV = 4;  // triple buffering, plain loads, exact quantize
+
 template <int NS, int ND>
-static int pick_nd(int nd, const float* in, int64_t N, int64_t stride, int d, int L, const FastPlan& plan,
+static int pick_nd(int variant, int nd, const float* in, int64_t N, int64_t stride, int d, int L, const FastPlan& plan,
                    uint8_t* frame, double* idx, float* mm, hipStream_t s) {
   if constexpr (ND > FastGeo<NS>::NT) {
     return HQ_E_UNSUPPORTED;
   } else {
-    if (nd == ND) return launch_ff<NS, ND>(in, N, stride, d, L, plan, frame, idx, mm, s);
-    return pick_nd<NS, ND + 1>(nd, in, N, stride, d, L, plan, frame, idx, mm, s);
+    if (nd == ND) {
+      if constexpr (NS == 64 && ND == 6) {  // A/B variants of the headline shape (HQ_FUSED_V, bench)
+        switch (variant) {
+          case 0: return launch_ff<NS, ND, 0>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 1: return launch_ff<NS, ND, 1>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 2: return launch_ff<NS, ND, 2>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 3: return launch_ff<NS, ND, 3>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 5: return launch_ff<NS, ND, 5>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 6: return launch_ff<NS, ND, 6>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 7: return launch_ff<NS, ND, 7>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          default: break;
+        }
+      }
+      return launch_ff<NS, ND, kDefaultV>(in, N, stride, d, L, plan, frame, idx, mm, s);
+    }
+    return pick_nd<NS, ND + 1>(variant, nd, in, N, stride, d, L, plan, frame, idx, mm, s);
   }
 }
 
@@ -301,10 +393,12 @@ int fused_fast(const float* in, int64_t N, int64_t stride, int d, int n, int L, 
   }
   if (L < n) plan.zero_row = 1;
   const int nd = (((d + 3) / 4) + 63) / 64;
+  const char* ev = getenv("HQ_FUSED_V");
+  const int variant = ev ? atoi(ev) : kDefaultV;
   switch (n) {
-    case 16: return pick_nd<16, 1>(nd, in, N, stride, d, L, plan, frame, idx, mm, s);
-    case 32: return pick_nd<32, 1>(nd, in, N, stride, d, L, plan, frame, idx, mm, s);
-    case 64: return pick_nd<64, 1>(nd, in, N, stride, d, L, plan, frame, idx, mm, s);
+    case 16: return pick_nd<16, 1>(variant, nd, in, N, stride, d, L, plan, frame, idx, mm, s);
+    case 32: return pick_nd<32, 1>(variant, nd, in, N, stride, d, L, plan, frame, idx, mm, s);
+    case 64: return pick_nd<64, 1>(variant, nd, in, N, stride, d, L, plan, frame, idx, mm, s);
   }
   return HQ_E_UNSUPPORTED;
 }
