@@ -9,6 +9,7 @@ hilbert_quantization.api and .rag.
 from .exceptions import (HilbertQuantizationError, QuantizationError, ReconstructionError, SearchError,
                          ValidationError, CompressionError)
 from .models import QuantizedModel, SearchResult, ModelMetadata, PaddingConfig
+from ._lib import NativeLibraryError
 from . import kernels
 
 __version__ = "0.1.0"
