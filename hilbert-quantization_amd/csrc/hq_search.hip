@@ -496,6 +496,397 @@ __global__ __launch_bounds__(256) void k_scan(ScanArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// level-0 scan, wave-independent (the progressive search's filtering stage; k_scan handles the
+// overall mode and the arg-max).  One wave = 64 queries (4 MFMA column blocks of 16) x one corpus
+// chunk, 16 candidates per step:
+//   D[cand][query] = sum_k Zc[cand][k] Zq[query][k] with v_mfma_f64_16x16x4f64, A = candidates,
+//   B = queries.  Lane group g = lane >> 4 feeds the contiguous k range [g*KS, g*KS + KS), so each
+//   lane loads its candidate fragment with KS/2 16-byte loads straight from HBM/L2 (no LDS staging,
+//   no barriers); the query fragments stay in registers for the whole chunk.
+// Lane (g, j) owns queries 16b + j (b < 4) and candidates g + 4r (r < 4) of the step.
+// Filter without division: with base = 0.35 + 0.35 G/m, num = 0.6 (qs cs G / m + qm cm) and
+// den = msq_q + msq_c, score >= th  <=>  th - base <= 0  or  num >= (th - base) den.
+// th(query) = max(threshold, own K-th best, best K-th of any other wave for that query); the last
+// is exchanged through a per-query atomicMax in global memory (scores >= 0 order like their bit
+// patterns), so after the first chunks almost nothing reaches the insert path.  Every pruned
+// candidate is below the K-th best of some complete list, so the merged top-K is unchanged.
+// ------------------------------------------------------------------------------------------------
+constexpr int kQW = 64;  // queries per wave
+constexpr int kCS = 16;  // candidates per step
+
+struct Scan0Args {
+  const double* Zq; const double* Sq; int Q;
+  const double* Zc; const double* Sc; int64_t N;
+  int Lp, nseg;
+  double inv_m, c1;  // 1/m, 0.35/m
+  int K;
+  double thr0;       // initial threshold (-inf: none)
+  const double* th0; // per-query lower bound of the K-th best approximate score (sample pass) or null
+  int64_t id_base;
+  int64_t chunk_len; int nchunks; int nqb;
+  double* ws_score; int64_t* ws_id; unsigned long long* gtau;
+};
+
+__device__ __forceinline__ double rl_f64(double v, int l) {
+  const int2 p = *reinterpret_cast<int2*>(&v);
+  int2 r;
+  r.x = __builtin_amdgcn_readlane(p.x, l);
+  r.y = __builtin_amdgcn_readlane(p.y, l);
+  return *reinterpret_cast<double*>(&r);
+}
+
+// lane i <- lane i-1 (lane 0 keeps its own value): DPP wave_shr:1
+__device__ __forceinline__ int shr1_i32(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false); }
+__device__ __forceinline__ double shr1_f64(double v) {
+  int2 p = *reinterpret_cast<int2*>(&v);
+  p.x = shr1_i32(p.x);
+  p.y = shr1_i32(p.y);
+  return *reinterpret_cast<double*>(&p);
+}
+
+// approximate level-0 score of a pair with both stds non-zero (the insert path and the sample pass
+// use this same expression, so their values agree bit for bit)
+__device__ __forceinline__ double approx0(double G, double c1, double qA, double qB, double qQ, double cs, double cm,
+                                          double cq) {
+  const double base = fma(G, c1, 0.35);
+  const double num = fma(G, qA * cs, qB * cm);
+  double t = num / (qQ + cq);
+  t = t > 0.0 ? t : 0.0;
+  double s = base + t;
+  s = s < 1.0 ? s : 1.0;
+  return s > 0.0 ? s : 0.0;
+}
+
+// constant branches of compare_indices_at_level (search_engine.py:141-148)
+__device__ __forceinline__ double const0(bool zq, bool zc, double qm, double cm) {
+  if (zq && zc) return fabs(qm - cm) < 1e-6 ? 1.0 : 0.0;
+  return 0.1;
+}
+
+template <int KS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_scan0(Scan0Args a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  double* ls = reinterpret_cast<double*>(smem);     // kQW x K approx scores
+  int* li = reinterpret_cast<int*>(ls + kQW * a.K);  // kQW x K corpus rows
+  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
+  const int chunk = xcd + 8 * (slot / a.nqb);
+  const int qb = slot % a.nqb;
+  if (chunk >= a.nchunks) return;
+  const int64_t c_begin = (int64_t)chunk * a.chunk_len;
+  int64_t c_end = c_begin + a.chunk_len;
+  if (c_end > a.N) c_end = a.N;
+  const int q0 = qb * kQW;
+  const int K = a.K;
+
+  // query fragments and constants
+  double qf[4][KS];
+  double qA[4], qB[4], qQ[4], th[4];
+  int qz = 0;  // bit b: query 16b + j has zero std
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int q = q0 + 16 * b + j;
+    const bool v = q < a.Q;
+    const double* zr = a.Zq + (int64_t)(v ? q : 0) * a.Lp + g * KS;
+#pragma unroll
+    for (int t = 0; t < KS; ++t) qf[b][t] = v ? zr[t] : 0.0;
+    const double* st = a.Sq + (int64_t)(v ? q : 0) * a.nseg * 4;
+    const double qm = st[0], qs = st[1], qq = st[2];
+    qA[b] = (0.6 * a.inv_m) * qs;
+    qB[b] = 0.6 * qm;
+    qQ[b] = qq;
+    double t0 = a.thr0;
+    if (v && a.th0 && a.th0[q] > t0) t0 = a.th0[q];
+    th[b] = v ? t0 : __builtin_huge_val();
+    if (v && qs == 0.0) qz |= 1 << b;
+  }
+  for (int i = lane; i < kQW * K; i += 64) {
+    ls[i] = -__builtin_huge_val();
+    li[i] = -1;
+  }
+  const bool myq = q0 + lane < a.Q;  // lane's query for the global-threshold exchange
+
+  // candidate fragment: row c = cs + j, k range [g*KS, g*KS + KS)
+  typedef double dbl2v __attribute__((ext_vector_type(2)));
+  double cf[KS];
+  auto load_frag = [&](int64_t cs, double* dst) {
+    int64_t c = cs + j;
+    if (c >= c_end) c = c_end - 1;
+    const double* p = a.Zc + c * a.Lp + g * KS;
+    if constexpr ((KS & 1) == 0) {
+#pragma unroll
+      for (int t = 0; t < KS; t += 2) {
+        const dbl2v v = *reinterpret_cast<const dbl2v*>(p + t);
+        dst[t] = v.x;
+        dst[t + 1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < KS; ++t) dst[t] = p[t];
+    }
+  };
+  // candidate statistics for rows g + 4r
+  double cm[4], csd[4], cq[4];
+  auto load_stats = [&](int64_t cs) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int64_t c = cs + g + 4 * r;
+      if (c >= c_end) c = c_end - 1;
+      const double* st = a.Sc + c * a.nseg * 4;
+      const dbl2v v = *reinterpret_cast<const dbl2v*>(st);
+      cm[r] = v.x;
+      csd[r] = v.y;
+      cq[r] = st[2];
+    }
+  };
+  load_frag(c_begin, cf);
+  load_stats(c_begin);
+  unsigned long long gt_bits = 0ull;
+
+  int step = 0;
+  for (int64_t cs = c_begin; cs < c_end; cs += kCS, ++step) {
+    // ---- contraction ----
+    dbl4 acc[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      acc[b] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int t = 0; t < KS; ++t) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(cf[t], qf[b][t], acc[b], 0, 0, 0);
+    }
+    // next fragment in flight during the epilogue; the global thresholds every 4 steps
+    const bool more = cs + kCS < c_end;
+    double cfn[KS];
+    if (more) load_frag(cs + kCS, cfn);
+    if ((step & 3) == 0) {
+      if (gt_bits != 0ull) {
+        const double gd = __longlong_as_double((long long)gt_bits);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const double v = __shfl(gd, 16 * b + j, 64);
+          th[b] = v > th[b] ? v : th[b];
+        }
+      }
+      if (myq) gt_bits = __atomic_load_n(a.gtau + q0 + lane, __ATOMIC_RELAXED);
+    }
+
+    // ---- filter ----
+    int cz = 0;  // bit r: candidate g+4r has zero std or lies past the chunk end
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (csd[r] == 0.0 || cs + g + 4 * r >= c_end) cz |= 1 << r;
+    const bool slow = __ballot((qz | cz) != 0) != 0ull;
+    // pass test of pair (b, r) for this lane (re-evaluated by the insert path)
+    auto passes = [&](int b, int r) -> bool {
+      const double G = acc[b][r];
+      const double R = th[b] - fma(G, a.c1, 0.35);
+      const double num = fma(G, qA[b] * csd[r], qB[b] * cm[r]);
+      const double den = qQ[b] + cq[r];
+      bool p = (R <= 0.0) || (num >= R * den);
+      if (slow) {
+        const bool inval = cs + g + 4 * r >= c_end;
+        const bool spec = ((qz >> b) & 1) || csd[r] == 0.0;
+        p = !inval && (spec || p);
+      }
+      return p;
+    };
+    bool anyl = false;
+    if (!slow) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) anyl |= passes(b, r);
+    } else {
+      // a zero-variance query/candidate or the chunk's ragged end is in this step: constant-score
+      // pairs go to the insert path, which evaluates and tests them exactly
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) anyl |= passes(b, r);
+    }
+
+    // ---- insert (rare once the thresholds are up) ----
+    if (__ballot(anyl)) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          unsigned long long m = __ballot(passes(b, r));
+          if (m == 0ull) continue;
+          // this lane's full approximate score for pair (b, r)
+          const bool zq = (qz >> b) & 1, zc = csd[r] == 0.0;
+          double s;
+          if (zq || zc) {
+            const int q = q0 + 16 * b + j;
+            s = const0(zq, zc, a.Sq[(int64_t)(q < a.Q ? q : 0) * a.nseg * 4], cm[r]);
+          } else {
+            s = approx0(acc[b][r], a.c1, qA[b], qB[b], qQ[b], csd[r], cm[r], cq[r]);
+          }
+          while (m) {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            const int c_off = (l >> 4) + 4 * r;
+            if (cs + c_off >= c_end) continue;
+            const double sc = rl_f64(s, l);
+            if (!(sc >= rl_f64(th[b], l))) continue;
+            const int qi = 16 * b + (l & 15);
+            const int id = (int)(cs + c_off);
+            double es = lane < K ? ls[qi * K + lane] : -__builtin_huge_val();
+            int ei = lane < K ? li[qi * K + lane] : -1;
+            const bool bt = (ei >= 0) && (es > sc || (es == sc && ei < id));
+            const int p = __popcll(__ballot(bt));
+            if (p >= K) continue;
+            const double us = shr1_f64(es);
+            const int ui = shr1_i32(ei);
+            if (lane > p) { es = us; ei = ui; }
+            if (lane == p) { es = sc; ei = id; }
+            if (lane < K) {
+              ls[qi * K + lane] = es;
+              li[qi * K + lane] = ei;
+            }
+            if (__builtin_amdgcn_readlane(ei, K - 1) >= 0) {
+              const double tau = rl_f64(es, K - 1);
+              if (j == (l & 15)) th[b] = tau > th[b] ? tau : th[b];
+              if (lane == 0 && tau > 0.0)
+                atomicMax(a.gtau + q0 + qi, (unsigned long long)__double_as_longlong(tau));
+            }
+          }
+        }
+    }
+    if (more) {
+#pragma unroll
+      for (int t = 0; t < KS; ++t) cf[t] = cfn[t];
+      load_stats(cs + kCS);
+    }
+  }
+
+  // ---- this chunk's lists ----
+  for (int i = lane; i < kQW * K; i += 64) {
+    const int ql = i / K, jj = i % K;
+    const int q = q0 + ql;
+    if (q >= a.Q) continue;
+    const int64_t o = ((int64_t)chunk * a.Q + q) * K + jj;
+    const int id = li[i];
+    a.ws_score[o] = id >= 0 ? ls[i] : -__builtin_huge_val();
+    a.ws_id[o] = id >= 0 ? (int64_t)id + a.id_base : -1;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// sample pass for k_scan0: a strided subset of the corpus (row i*stride) is scored with the same
+// MFMA contraction and the same approximate-score expression; each query gets a 256-bin histogram of
+// its sample scores over [0, 1].  The highest bin edge e/256 with >= K sample scores at or above it
+// is a lower bound of the K-th best score over the whole corpus (the sample is a subset), which
+// k_scan0 uses as its starting threshold, so only ~stride*K candidates per query reach its lists.
+// ------------------------------------------------------------------------------------------------
+constexpr int kBins = 256;
+
+struct SampleArgs {
+  const double* Zq; const double* Sq; int Q;
+  const double* Zc; const double* Sc; int64_t N;
+  int Lp, nseg;
+  double inv_m, c1;
+  int64_t stride, S;
+  int64_t chunk_len; int nchunks; int nqb;
+  unsigned int* hist;  // Q x kBins
+};
+
+template <int KS>
+__global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* hs = reinterpret_cast<uint32_t*>(smem);  // kQW x kBins/2, two u16 counters per word
+  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
+  const int chunk = xcd + 8 * (slot / a.nqb);
+  const int qb = slot % a.nqb;
+  if (chunk >= a.nchunks) return;
+  const int64_t c_begin = (int64_t)chunk * a.chunk_len;
+  int64_t c_end = c_begin + a.chunk_len;
+  if (c_end > a.S) c_end = a.S;
+  const int q0 = qb * kQW;
+  for (int i = lane; i < kQW * kBins / 2; i += 64) hs[i] = 0u;
+
+  double qf[4][KS];
+  double qA[4], qB[4], qQ[4], qm[4];
+  int qz = 0, qv = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int q = q0 + 16 * b + j;
+    const bool v = q < a.Q;
+    const double* zr = a.Zq + (int64_t)(v ? q : 0) * a.Lp + g * KS;
+#pragma unroll
+    for (int t = 0; t < KS; ++t) qf[b][t] = v ? zr[t] : 0.0;
+    const double* st = a.Sq + (int64_t)(v ? q : 0) * a.nseg * 4;
+    qm[b] = st[0];
+    qA[b] = (0.6 * a.inv_m) * st[1];
+    qB[b] = 0.6 * st[0];
+    qQ[b] = st[2];
+    if (v) qv |= 1 << b;
+    if (st[1] == 0.0) qz |= 1 << b;
+  }
+  __syncthreads();
+  for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
+    double cf[KS];
+    {
+      int64_t i = cs + j;
+      if (i >= c_end) i = c_end - 1;
+      const double* p = a.Zc + i * a.stride * a.Lp + g * KS;
+#pragma unroll
+      for (int t = 0; t < KS; ++t) cf[t] = p[t];
+    }
+    dbl4 acc[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      acc[b] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int t = 0; t < KS; ++t) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(cf[t], qf[b][t], acc[b], 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t i = cs + g + 4 * r;
+      if (i >= c_end) continue;
+      const double* st = a.Sc + i * a.stride * a.nseg * 4;
+      const double cm = st[0], csd = st[1], cq = st[2];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (!((qv >> b) & 1)) continue;
+        const bool zq = (qz >> b) & 1, zc = csd == 0.0;
+        const double sc = (zq || zc) ? const0(zq, zc, qm[b], cm)
+                                     : approx0(acc[b][r], a.c1, qA[b], qB[b], qQ[b], csd, cm, cq);
+        int bin = (int)(sc * (double)kBins);
+        bin = bin < 0 ? 0 : (bin >= kBins ? kBins - 1 : bin);
+        atomicAdd(&hs[(16 * b + j) * (kBins / 2) + (bin >> 1)], 1u << (16 * (bin & 1)));
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = lane; i < kQW * kBins / 2; i += 64) {
+    const uint32_t v = hs[i];
+    if (v == 0u) continue;
+    const int q = q0 + i / (kBins / 2);
+    if (q >= a.Q) continue;
+    unsigned int* h = a.hist + (int64_t)q * kBins + 2 * (i % (kBins / 2));
+    if (v & 0xFFFFu) atomicAdd(h, v & 0xFFFFu);
+    if (v >> 16) atomicAdd(h + 1, v >> 16);
+  }
+}
+
+// per-query starting threshold from the sample histogram (-inf when the sample has < K scores)
+__global__ void k_hist_tau(const unsigned int* __restrict__ hist, int Q, int K, double* __restrict__ th0) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  unsigned int cum = 0;
+  double t = -__builtin_huge_val();
+  for (int e = kBins - 1; e >= 0; --e) {
+    cum += hist[(int64_t)q * kBins + e];
+    if (cum >= (unsigned int)K) {
+      t = (double)e / (double)kBins - 1e-12;  // margin >> rounding differences between the two passes
+      break;
+    }
+  }
+  th0[q] = t;
+}
+
 // merge nchunks sorted lists per query (one wave per query)
 __global__ __launch_bounds__(64) void k_merge(const double* __restrict__ ws_score, const int64_t* __restrict__ ws_id,
                                               const double* __restrict__ ws_best, const int64_t* __restrict__ ws_best_id,
@@ -838,6 +1229,63 @@ static void scan_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& chu
   if (chunk_len < kCB) chunk_len = kCB;
 }
 
+// k_scan0: ~16 resident waves per CU-pair of rounds; nchunks multiple of 8 (XCD mapping), <= 512
+static void scan0_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& chunk_len) {
+  nqb = (Q + kQW - 1) / kQW;
+  int64_t target = (4096 + nqb - 1) / nqb;
+  int64_t max_chunks = (N + kCS - 1) / kCS;
+  if (target > max_chunks) target = max_chunks;
+  if (target > 512) target = 512;
+  nchunks = (int)(((target + 7) / 8) * 8);
+  if (nchunks < 8) nchunks = 8;
+  chunk_len = (N + nchunks - 1) / nchunks;
+  chunk_len = ((chunk_len + kCS - 1) / kCS) * kCS;
+  if (chunk_len < kCS) chunk_len = kCS;
+}
+
+static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
+  int nqb, nchunks;
+  int64_t chunk_len;
+  scan0_geometry(Q, N, nqb, nchunks, chunk_len);
+  // lists + global thresholds + sample histogram + starting thresholds
+  return (size_t)nchunks * Q * k * 16 + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 8 + 256;
+}
+
+// sample pass: stride 16 once the corpus is large, else a sample of ~4096 rows (the whole corpus
+// below that); chunks of <= 65520 rows (u16 histogram counters), ~1024 waves
+static void sample_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, int& nqb, int& nchunks,
+                            int64_t& chunk_len) {
+  stride = N >= 16 * 4096 ? 16 : (N / 4096 > 1 ? N / 4096 : 1);
+  S = (N + stride - 1) / stride;
+  nqb = (Q + kQW - 1) / kQW;
+  int64_t target = (1024 + nqb - 1) / nqb;
+  const int64_t max_chunks = (S + kCS - 1) / kCS;
+  if (target > max_chunks) target = max_chunks;
+  if (target < (S + 65519) / 65520) target = (S + 65519) / 65520;
+  nchunks = (int)(((target + 7) / 8) * 8);
+  chunk_len = (S + nchunks - 1) / nchunks;
+  chunk_len = ((chunk_len + kCS - 1) / kCS) * kCS;
+}
+
+template <int KS>
+static int launch_sample(const SampleArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)kQW * kBins / 2 * 4;
+  HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_sample_hist<KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds));
+  hipLaunchKernelGGL((k_sample_hist<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+template <int KS>
+static int launch_scan0(const Scan0Args& a, hipStream_t s) {
+  const size_t lds = (size_t)kQW * a.K * 12;
+  HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_scan0<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((k_scan0<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
 template <int KSMAX, bool OVERALL>
 static int launch_scan(const ScanArgs& a, hipStream_t s) {
   const size_t lds = scan_lds_bytes(a.rs, a.nseg_used, a.K);
@@ -922,7 +1370,9 @@ size_t hq_scan_workspace_size(int Q, int64_t N, int k) {
   int nqb, nchunks;
   int64_t chunk_len;
   scan_geometry(Q, N, nqb, nchunks, chunk_len);
-  return (size_t)nchunks * Q * k * 16 + (size_t)nchunks * Q * 16 + 256;
+  const size_t w1 = (size_t)nchunks * Q * k * 16 + (size_t)nchunks * Q * 16 + 256;
+  const size_t w0 = scan0_ws_bytes(Q, N, k);
+  return w0 > w1 ? w0 : w1;
 }
 
 int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc, int64_t N, int L,
@@ -942,6 +1392,71 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
   }
   if (!Zq || !Sq || !Zc || !Sc || !workspace) return fail(HQ_E_INVALID, "null buffer");
   if (workspace_bytes < hq_scan_workspace_size(Q, N, k)) return fail(HQ_E_INVALID, "workspace too small");
+  if (mode == 0 && !out_best && !out_best_id && N < 0x7FFFFFFF && getenv("HQ_SCAN_V1") == nullptr) {
+    SegInfo si;
+    seg_info(L, si);
+    const int ks = si.plen[0] / 4;
+    if (ks >= 1 && ks <= 8) {
+      Scan0Args b;
+      b.Zq = Zq; b.Sq = Sq; b.Q = Q; b.Zc = Zc; b.Sc = Sc; b.N = N;
+      b.Lp = si.Lp; b.nseg = si.nseg;
+      b.inv_m = si.inv_m[0];
+      b.c1 = 0.35 * si.inv_m[0];
+      b.K = k;
+      b.thr0 = thr_mode == 0 ? -__builtin_huge_val() : threshold;
+      b.id_base = id_base;
+      scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len);
+      uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
+      b.ws_score = reinterpret_cast<double*>(ws);
+      b.ws_id = reinterpret_cast<int64_t*>(ws + (size_t)b.nchunks * Q * k * 8);
+      b.gtau = reinterpret_cast<unsigned long long*>(ws + (size_t)b.nchunks * Q * k * 16);
+      HQ_CHECK_HIP(hipMemsetAsync(b.gtau, 0, sizeof(unsigned long long) * Q, s));
+      unsigned int* hist = reinterpret_cast<unsigned int*>(ws + (size_t)b.nchunks * Q * k * 16 + (size_t)Q * 8);
+      double* th0 = reinterpret_cast<double*>(ws + (size_t)b.nchunks * Q * k * 16 + (size_t)Q * 8 +
+                                              (size_t)Q * kBins * 4);
+      b.th0 = nullptr;
+      int rc;
+      if (getenv("HQ_SCAN_NOSAMPLE") == nullptr) {
+        SampleArgs sa;
+        sa.Zq = Zq; sa.Sq = Sq; sa.Q = Q; sa.Zc = Zc; sa.Sc = Sc; sa.N = N;
+        sa.Lp = b.Lp; sa.nseg = b.nseg; sa.inv_m = b.inv_m; sa.c1 = b.c1;
+        sample_geometry(Q, N, sa.stride, sa.S, sa.nqb, sa.nchunks, sa.chunk_len);
+        sa.hist = hist;
+        HQ_CHECK_HIP(hipMemsetAsync(hist, 0, sizeof(unsigned int) * kBins * Q, s));
+        switch (ks) {
+          case 1: rc = launch_sample<1>(sa, s); break;
+          case 2: rc = launch_sample<2>(sa, s); break;
+          case 3: rc = launch_sample<3>(sa, s); break;
+          case 4: rc = launch_sample<4>(sa, s); break;
+          case 5: rc = launch_sample<5>(sa, s); break;
+          case 6: rc = launch_sample<6>(sa, s); break;
+          case 7: rc = launch_sample<7>(sa, s); break;
+          default: rc = launch_sample<8>(sa, s); break;
+        }
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_hist_tau, dim3((Q + 255) / 256), dim3(256), 0, s, (const unsigned int*)hist, Q, k, th0);
+        HQ_CHECK_LAUNCH();
+        b.th0 = th0;
+      }
+      switch (ks) {
+        case 1: rc = launch_scan0<1>(b, s); break;
+        case 2: rc = launch_scan0<2>(b, s); break;
+        case 3: rc = launch_scan0<3>(b, s); break;
+        case 4: rc = launch_scan0<4>(b, s); break;
+        case 5: rc = launch_scan0<5>(b, s); break;
+        case 6: rc = launch_scan0<6>(b, s); break;
+        case 7: rc = launch_scan0<7>(b, s); break;
+        default: rc = launch_scan0<8>(b, s); break;
+      }
+      if (rc) return rc;
+      int mg = Q < 4096 ? Q : 4096;
+      hipLaunchKernelGGL(k_merge, dim3(mg), dim3(64), 0, s, b.ws_score, b.ws_id, (const double*)nullptr,
+                         (const int64_t*)nullptr, b.nchunks, Q, k, out_score, out_id, (double*)nullptr,
+                         (int64_t*)nullptr);
+      HQ_CHECK_LAUNCH();
+      return HQ_OK;
+    }
+  }
   ScanArgs a;
   a.Zq = Zq; a.Sq = Sq; a.Q = Q; a.Zc = Zc; a.Sc = Sc; a.N = N;
   seg_info(L, a.si);

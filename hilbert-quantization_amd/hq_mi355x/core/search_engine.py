@@ -48,7 +48,7 @@ class IndexCorpus:
     unproven queries and the "none passed" fallback are answered by the dense exact path."""
 
     EPS = 1e-9      # bound on |approximate - exact| score (observed < 1e-13 at L = 64)
-    SLACK = 16
+    SLACK = 8
 
     def __init__(self, indices, id_base: int = 0):
         x = _f64(indices)

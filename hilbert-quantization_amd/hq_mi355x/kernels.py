@@ -257,9 +257,11 @@ def level_scores(q: Prepared, c: Prepared, level: int, exc=None):
 
 
 def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.0, thr_mode: int = 0,
-              id_base: int = 0, exc=None):
+              id_base: int = 0, need_best: bool = False, exc=None):
     """Fused MFMA scan + per-query top-k on APPROXIMATE scores.  mode 0: level-0 score, 1: overall.
-    thr_mode 0 none / 1 >= / 2 >.  Returns (scores [Q, k], ids [Q, k], best [Q], best_id [Q])."""
+    thr_mode 0 none / 1 >= / 2 >.  Returns (scores [Q, k], ids [Q, k], best [Q], best_id [Q]); best and
+    best_id (first arg-max of the approximate score) are None unless need_best (the level-0 scan without
+    the arg-max runs the wave-independent k_scan0 kernel)."""
     t = torch()
     Q, N = q.N, c.N
     dev = q.Z.device
@@ -267,8 +269,8 @@ def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.
     ws = t.empty(ws_bytes, dtype=t.uint8, device=dev)
     sc = t.empty((Q, k), dtype=t.float64, device=dev)
     ids = t.empty((Q, k), dtype=t.int64, device=dev)
-    best = t.empty(Q, dtype=t.float64, device=dev)
-    bid = t.empty(Q, dtype=t.int64, device=dev)
+    best = t.empty(Q, dtype=t.float64, device=dev) if need_best else None
+    bid = t.empty(Q, dtype=t.int64, device=dev) if need_best else None
     _chk(_L().hq_scan_topk(ptr(q.Z), ptr(q.S), Q, ptr(c.Z), ptr(c.S), N, c.L, mode, k, float(threshold), thr_mode,
                            int(id_base), ptr(ws), ws_bytes, ptr(sc), ptr(ids), ptr(best), ptr(bid), stream()), exc)
     return sc, ids, best, bid

@@ -183,3 +183,42 @@ def test_rag_scores(hq_lib, golden):
     a = g["cos_A"][0]
     b = g["cos_B"]
     assert abs(S.calculate_spatial_locality_similarity(a, b) - O.rag_spatial_locality_similarity(a, b)) < 1e-6
+
+
+def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, monkeypatch):
+    """The wave-independent level-0 scan (k_scan0: global threshold exchange, division-free filter,
+    exact constant branches) gives the same exact top-k as the LDS-tiled k_scan (HQ_SCAN_V1) and as
+    the oracle, on a corpus with a ragged chunk tail, zero-variance level-0 segments on both sides,
+    duplicate runs across chunks and a query count that is not a multiple of 64."""
+    from hq_mi355x.core.search_engine import IndexCorpus
+    rng = np.random.default_rng(77)
+    N, L = 40_003, 64
+    C = rng.standard_normal((N, L))
+    C[100:140, :32] = 0.5                      # constant level-0 segments (std 0)
+    C[200:210, :32] = 0.5 + 1e-7               # |mean diff| < 1e-6 -> score 1 vs a constant query
+    C[39_990:] = C[7]                          # duplicates in the last (ragged) chunk
+    C[20_000:20_030] = C[7]                    # ... and in a middle chunk
+    Q = np.concatenate([C[[7, 100, 300, 5000]], C[400:530] + rng.normal(0, 0.05, (130, L))])
+    Q[1, :32] = 0.5                            # constant query segment
+    corpus = IndexCorpus(C)
+    qp = corpus.prepare_queries(Q)
+    res = {}
+    for tag in ("v0", "v0-nosample", "v1"):
+        if tag == "v0-nosample":
+            monkeypatch.setenv("HQ_SCAN_NOSAMPLE", "1")
+        if tag == "v1":
+            monkeypatch.setenv("HQ_SCAN_V1", "1")
+        for thr, tm in ((0.1, 1), (0.6, 1), (0.1, 2)):
+            sc, ids, cnt, _, _ = corpus.exact_topk(qp, 0, 20, thr, tm)
+            res[(tag, thr, tm)] = (_np(sc), _np(ids), _np(cnt))
+    for key in ((0.1, 1), (0.6, 1), (0.1, 2)):
+        for tag in ("v0-nosample", "v1"):
+            a, b = res[("v0",) + key], res[(tag,) + key]
+            assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]), (tag, key)
+            np.testing.assert_array_equal(a[0][a[1] >= 0], b[0][b[1] >= 0])
+    s_ids, s_cnt = res[("v0", 0.1, 1)][1], res[("v0", 0.1, 1)][2]
+    for a in list(range(6)) + [50, 133]:
+        s = O.level_similarity(Q[a], C, 0)
+        pos = np.nonzero(s >= 0.1)[0]
+        ref = pos[np.argsort(-s[pos], kind="stable")][:20]
+        assert list(s_ids[a][: s_cnt[a]]) == list(ref), a
