@@ -518,7 +518,9 @@ constexpr int kCS = 16;  // candidates per step
 struct Scan0Args {
   const double* Zq; const double* Sq; int Q;
   const double* Zc; const double* Sc; int64_t N;
-  int Lp, nseg;
+  const float* Zq32; const float* Zc32;  // f32 kernels: level-0 segments, rows of P0 (+kPad0 pad rows)
+  const float* Sq32; const float* Sc32;  // f32 kernels: level-0 (std, mean, msq, flag bits) per row
+  int Lp, nseg, P0;
   double inv_m, c1;  // 1/m, 0.35/m
   int K;
   double thr0;       // initial threshold (-inf: none)
@@ -564,11 +566,37 @@ __device__ __forceinline__ double const0(bool zq, bool zc, double qm, double cm)
   return 0.1;
 }
 
+typedef float flt4 __attribute__((ext_vector_type(4)));
+
+// Z operand types of the two contraction precisions: f64 (v_mfma_f64_16x16x4f64, C/D row
+// (lane>>4) + 4r) and f32 (v_mfma_f32_16x16x4f32, C/D row 4(lane>>4) + r).
+template <bool F32> struct ZOps;
+template <> struct ZOps<false> {
+  typedef double T;
+  typedef dbl4 Acc;
+  static __device__ __forceinline__ Acc mfma(T a, T b, Acc c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+  static __device__ __forceinline__ int row(int g, int r) { return g + 4 * r; }
+  static __device__ __forceinline__ const T* zq(const Scan0Args& a, int64_t q) { return a.Zq + q * a.Lp; }
+  static __device__ __forceinline__ const T* zc(const Scan0Args& a, int64_t c) { return a.Zc + c * a.Lp; }
+};
+template <> struct ZOps<true> {
+  typedef float T;
+  typedef flt4 Acc;
+  static __device__ __forceinline__ Acc mfma(T a, T b, Acc c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+  static __device__ __forceinline__ int row(int g, int r) { return 4 * g + r; }
+  static __device__ __forceinline__ const T* zq(const Scan0Args& a, int64_t q) { return a.Zq32 + q * a.P0; }
+  static __device__ __forceinline__ const T* zc(const Scan0Args& a, int64_t c) { return a.Zc32 + c * a.P0; }
+};
+
 template <int KS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_scan0(Scan0Args a) {
+  typedef ZOps<false> Z;
+  typedef typename Z::T ZT;
+  typedef typename Z::Acc AccT;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  double* ls = reinterpret_cast<double*>(smem);     // kQW x K approx scores
-  int* li = reinterpret_cast<int*>(ls + kQW * a.K);  // kQW x K corpus rows
+  double* qc = reinterpret_cast<double*>(smem);      // kQW x 4: 0.6 qs / m, 0.6 qm, msq, mean
+  double* ls = qc + kQW * 4;                          // kQW x K approx scores
+  int* li = reinterpret_cast<int*>(ls + kQW * a.K);   // kQW x K corpus rows
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
   const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
   const int chunk = xcd + 8 * (slot / a.nqb);
@@ -580,22 +608,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int q0 = qb * kQW;
   const int K = a.K;
 
-  // query fragments and constants
-  double qf[4][KS];
-  double qA[4], qB[4], qQ[4], th[4];
+  // query fragments (registers, whole chunk), constants (LDS), thresholds (registers)
+  ZT qf[4][KS];
+  double th[4];
   int qz = 0;  // bit b: query 16b + j has zero std
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     const int q = q0 + 16 * b + j;
     const bool v = q < a.Q;
-    const double* zr = a.Zq + (int64_t)(v ? q : 0) * a.Lp + g * KS;
+    const ZT* zr = Z::zq(a, v ? q : 0) + g * KS;
 #pragma unroll
-    for (int t = 0; t < KS; ++t) qf[b][t] = v ? zr[t] : 0.0;
+    for (int t = 0; t < KS; ++t) qf[b][t] = v ? zr[t] : (ZT)0;
     const double* st = a.Sq + (int64_t)(v ? q : 0) * a.nseg * 4;
     const double qm = st[0], qs = st[1], qq = st[2];
-    qA[b] = (0.6 * a.inv_m) * qs;
-    qB[b] = 0.6 * qm;
-    qQ[b] = qq;
+    if (g == 0) {
+      double* c = qc + (16 * b + j) * 4;
+      c[0] = (0.6 * a.inv_m) * qs;
+      c[1] = 0.6 * qm;
+      c[2] = qq;
+      c[3] = qm;
+    }
     double t0 = a.thr0;
     if (v && a.th0 && a.th0[q] > t0) t0 = a.th0[q];
     th[b] = v ? t0 : __builtin_huge_val();
@@ -607,57 +639,164 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   }
   const bool myq = q0 + lane < a.Q;  // lane's query for the global-threshold exchange
 
-  // candidate fragment: row c = cs + j, k range [g*KS, g*KS + KS)
+  // candidate fragment of a step: row cs + j, k range [g*KS, g*KS + KS)
   typedef double dbl2v __attribute__((ext_vector_type(2)));
-  double cf[KS];
-  auto load_frag = [&](int64_t cs, double* dst) {
+  auto load_frag = [&](int64_t cs, ZT* dst) {
     int64_t c = cs + j;
     if (c >= c_end) c = c_end - 1;
-    const double* p = a.Zc + c * a.Lp + g * KS;
-    if constexpr ((KS & 1) == 0) {
+    const ZT* p = Z::zc(a, c) + g * KS;
+    constexpr int W = 16 / sizeof(ZT);  // elements per 16-byte load
+    if constexpr ((KS % W) == 0) {
+      typedef ZT vec __attribute__((ext_vector_type(16 / sizeof(ZT))));
 #pragma unroll
-      for (int t = 0; t < KS; t += 2) {
-        const dbl2v v = *reinterpret_cast<const dbl2v*>(p + t);
-        dst[t] = v.x;
-        dst[t + 1] = v.y;
+      for (int t = 0; t < KS; t += W) {
+        const vec v = *reinterpret_cast<const vec*>(p + t);
+#pragma unroll
+        for (int e = 0; e < W; ++e) dst[t + e] = v[e];
       }
     } else {
 #pragma unroll
       for (int t = 0; t < KS; ++t) dst[t] = p[t];
     }
   };
-  // candidate statistics for rows g + 4r
-  double cm[4], csd[4], cq[4];
-  auto load_stats = [&](int64_t cs) {
+  // candidate statistics of a step for the lane's rows Z::row(g, r): mean, std, msq
+  auto load_stats = [&](int64_t cs, double* dst) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      int64_t c = cs + g + 4 * r;
+      int64_t c = cs + Z::row(g, r);
       if (c >= c_end) c = c_end - 1;
       const double* st = a.Sc + c * a.nseg * 4;
       const dbl2v v = *reinterpret_cast<const dbl2v*>(st);
-      cm[r] = v.x;
-      csd[r] = v.y;
-      cq[r] = st[2];
+      dst[3 * r] = v.x;
+      dst[3 * r + 1] = v.y;
+      dst[3 * r + 2] = st[2];
     }
   };
-  load_frag(c_begin, cf);
-  load_stats(c_begin);
-  unsigned long long gt_bits = 0ull;
+  // MFMAs of one half (two 16-query blocks) of a step
+  auto mfma_half = [&](const int h, const ZT* f, AccT* acc) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      acc[u] = AccT{0, 0, 0, 0};
+#pragma unroll
+      for (int t = 0; t < KS; ++t) acc[u] = Z::mfma(f[t], qf[2 * h + u][t], acc[u]);
+    }
+  };
+  // filter of one half of the step starting at row cs: branch-free, so the scheduler can interleave
+  // it with the other half's MFMAs.  Returns the lane's pass bits (bit 4u + r).
+  auto filter_half = [&](const int h, const AccT* acc, const int64_t cs, const double* cst,
+                         double* qa, double* qbv, double* qqv) -> int {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const double* c = qc + (16 * (2 * h + u) + j) * 4;
+      const dbl2v v0 = *reinterpret_cast<const dbl2v*>(c);
+      qa[u] = v0.x;
+      qbv[u] = v0.y;
+      qqv[u] = c[2];
+    }
+    int bits = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool inval = cs + Z::row(g, r) >= c_end;
+      const bool zc = cst[3 * r + 1] == 0.0;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int b = 2 * h + u;
+        const double G = (double)acc[u][r];
+        const double R = th[b] - fma(G, a.c1, 0.35);
+        const double num = fma(G, qa[u] * cst[3 * r + 1], qbv[u] * cst[3 * r]);
+        const double den = qqv[u] + cst[3 * r + 2];
+        // zero-variance pairs go to the insert path, which evaluates and tests them exactly;
+        // rows past the chunk end never pass
+        const bool spec = zc | (((qz >> b) & 1) != 0);
+        const bool p = ((R <= 0.0) | (num >= R * den) | spec) & !inval;
+        bits |= (int)p << (4 * u + r);
+      }
+    }
+    return bits;
+  };
+  // insert the passing pairs of one half (rare once the thresholds are up)
+  auto insert_half = [&](const int h, const AccT* acc, const int64_t cs, const double* cst, const double* qa,
+                         const double* qbv, const double* qqv, const int bits) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = 2 * h + u;
+        unsigned long long m = __ballot((bits >> (4 * u + r)) & 1);
+        if (m == 0ull) continue;
+        const double csd = cst[3 * r + 1], cm = cst[3 * r];
+        const bool zq = (qz >> b) & 1, zc = csd == 0.0;
+        const double s = (zq || zc) ? const0(zq, zc, qc[(16 * b + j) * 4 + 3], cm)
+                                    : approx0((double)acc[u][r], a.c1, qa[u], qbv[u], qqv[u], csd, cm, cst[3 * r + 2]);
+        while (m) {
+          const int l = __builtin_ctzll(m);
+          m &= m - 1;
+          const int c_off = Z::row(l >> 4, r);
+          const double sc = rl_f64(s, l);
+          if (!(sc >= rl_f64(th[b], l))) continue;
+          const int qi = 16 * b + (l & 15);
+          const int id = (int)(cs + c_off);
+          double es = lane < K ? ls[qi * K + lane] : -__builtin_huge_val();
+          int ei = lane < K ? li[qi * K + lane] : -1;
+          const bool bt = (ei >= 0) && (es > sc || (es == sc && ei < id));
+          const int p = __popcll(__ballot(bt));
+          if (p >= K) continue;
+          const double us = shr1_f64(es);
+          const int ui = shr1_i32(ei);
+          if (lane > p) { es = us; ei = ui; }
+          if (lane == p) { es = sc; ei = id; }
+          if (lane < K) {
+            ls[qi * K + lane] = es;
+            li[qi * K + lane] = ei;
+          }
+          if (__builtin_amdgcn_readlane(ei, K - 1) >= 0) {
+            const double tau = rl_f64(es, K - 1);
+            if (j == (l & 15)) th[b] = tau > th[b] ? tau : th[b];
+            if (lane == 0 && tau > 0.0)
+              atomicMax(a.gtau + q0 + qi, (unsigned long long)__double_as_longlong(tau));
+          }
+        }
+      }
+  };
+  // 16 MFMAs interleaved with the filter's VALU work
+  auto interleave = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2 * KS; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+    }
+  };
 
+  // Software pipeline: the MFMAs of one half run while the VALU filters the other half
+  //   block A: MFMA(step i, half 1)   || filter(step i, half 0)
+  //   block B: MFMA(step i+1, half 0) || filter(step i, half 1)
+  ZT cf[KS];
+  double cst[12];
+  load_frag(c_begin, cf);
+  load_stats(c_begin, cst);
+  AccT acc0[2], acc1[2];
+  mfma_half(0, cf, acc0);
+  unsigned long long gt_bits = 0ull;
   int step = 0;
   for (int64_t cs = c_begin; cs < c_end; cs += kCS, ++step) {
-    // ---- contraction ----
-    dbl4 acc[4];
+    ZT cfn[KS];
+    double cstn[12];
+    load_frag(cs + kCS, cfn);  // unconditional (rows clamp to the chunk): keeps the wait counts exact
+    load_stats(cs + kCS, cstn);
+    double qa[2], qbv[2], qqv[2];
+    mfma_half(1, cf, acc1);
+    const int bits0 = filter_half(0, acc0, cs, cst, qa, qbv, qqv);
+    interleave();
+    if (__ballot(bits0 != 0)) insert_half(0, acc0, cs, cst, qa, qbv, qqv, bits0);
+    mfma_half(0, cfn, acc0);  // next step's first half (a harmless repeat of the last row at the end)
+    const int bits1 = filter_half(1, acc1, cs, cst, qa, qbv, qqv);
+    interleave();
+    if (__ballot(bits1 != 0)) insert_half(1, acc1, cs, cst, qa, qbv, qqv, bits1);
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      acc[b] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < KS; ++t) cf[t] = cfn[t];
 #pragma unroll
-      for (int t = 0; t < KS; ++t) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(cf[t], qf[b][t], acc[b], 0, 0, 0);
-    }
-    // next fragment in flight during the epilogue; the global thresholds every 4 steps
-    const bool more = cs + kCS < c_end;
-    double cfn[KS];
-    if (more) load_frag(cs + kCS, cfn);
+    for (int t = 0; t < 12; ++t) cst[t] = cstn[t];
+    // ---- global thresholds, every 4 steps (applied from the next step) ----
     if ((step & 3) == 0) {
       if (gt_bits != 0ull) {
         const double gd = __longlong_as_double((long long)gt_bits);
@@ -668,95 +807,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         }
       }
       if (myq) gt_bits = __atomic_load_n(a.gtau + q0 + lane, __ATOMIC_RELAXED);
-    }
-
-    // ---- filter ----
-    int cz = 0;  // bit r: candidate g+4r has zero std or lies past the chunk end
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (csd[r] == 0.0 || cs + g + 4 * r >= c_end) cz |= 1 << r;
-    const bool slow = __ballot((qz | cz) != 0) != 0ull;
-    // pass test of pair (b, r) for this lane (re-evaluated by the insert path)
-    auto passes = [&](int b, int r) -> bool {
-      const double G = acc[b][r];
-      const double R = th[b] - fma(G, a.c1, 0.35);
-      const double num = fma(G, qA[b] * csd[r], qB[b] * cm[r]);
-      const double den = qQ[b] + cq[r];
-      bool p = (R <= 0.0) || (num >= R * den);
-      if (slow) {
-        const bool inval = cs + g + 4 * r >= c_end;
-        const bool spec = ((qz >> b) & 1) || csd[r] == 0.0;
-        p = !inval && (spec || p);
-      }
-      return p;
-    };
-    bool anyl = false;
-    if (!slow) {
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) anyl |= passes(b, r);
-    } else {
-      // a zero-variance query/candidate or the chunk's ragged end is in this step: constant-score
-      // pairs go to the insert path, which evaluates and tests them exactly
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) anyl |= passes(b, r);
-    }
-
-    // ---- insert (rare once the thresholds are up) ----
-    if (__ballot(anyl)) {
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          unsigned long long m = __ballot(passes(b, r));
-          if (m == 0ull) continue;
-          // this lane's full approximate score for pair (b, r)
-          const bool zq = (qz >> b) & 1, zc = csd[r] == 0.0;
-          double s;
-          if (zq || zc) {
-            const int q = q0 + 16 * b + j;
-            s = const0(zq, zc, a.Sq[(int64_t)(q < a.Q ? q : 0) * a.nseg * 4], cm[r]);
-          } else {
-            s = approx0(acc[b][r], a.c1, qA[b], qB[b], qQ[b], csd[r], cm[r], cq[r]);
-          }
-          while (m) {
-            const int l = __builtin_ctzll(m);
-            m &= m - 1;
-            const int c_off = (l >> 4) + 4 * r;
-            if (cs + c_off >= c_end) continue;
-            const double sc = rl_f64(s, l);
-            if (!(sc >= rl_f64(th[b], l))) continue;
-            const int qi = 16 * b + (l & 15);
-            const int id = (int)(cs + c_off);
-            double es = lane < K ? ls[qi * K + lane] : -__builtin_huge_val();
-            int ei = lane < K ? li[qi * K + lane] : -1;
-            const bool bt = (ei >= 0) && (es > sc || (es == sc && ei < id));
-            const int p = __popcll(__ballot(bt));
-            if (p >= K) continue;
-            const double us = shr1_f64(es);
-            const int ui = shr1_i32(ei);
-            if (lane > p) { es = us; ei = ui; }
-            if (lane == p) { es = sc; ei = id; }
-            if (lane < K) {
-              ls[qi * K + lane] = es;
-              li[qi * K + lane] = ei;
-            }
-            if (__builtin_amdgcn_readlane(ei, K - 1) >= 0) {
-              const double tau = rl_f64(es, K - 1);
-              if (j == (l & 15)) th[b] = tau > th[b] ? tau : th[b];
-              if (lane == 0 && tau > 0.0)
-                atomicMax(a.gtau + q0 + qi, (unsigned long long)__double_as_longlong(tau));
-            }
-          }
-        }
-    }
-    if (more) {
-#pragma unroll
-      for (int t = 0; t < KS; ++t) cf[t] = cfn[t];
-      load_stats(cs + kCS);
     }
   }
 
@@ -784,7 +834,9 @@ constexpr int kBins = 256;
 struct SampleArgs {
   const double* Zq; const double* Sq; int Q;
   const double* Zc; const double* Sc; int64_t N;
-  int Lp, nseg;
+  const float* Zq32; const float* Zc32;
+  const float* Sq32; const float* Sc32;
+  int Lp, nseg, P0;
   double inv_m, c1;
   int64_t stride, S;
   int64_t chunk_len; int nchunks; int nqb;
@@ -793,6 +845,10 @@ struct SampleArgs {
 
 template <int KS>
 __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
+  typedef ZOps<false> Z;
+  typedef typename Z::T ZT;
+  typedef typename Z::Acc AccT;
+  auto zrow = [&](const double* p64, const float*, int64_t row) -> const ZT* { return p64 + row * a.Lp; };
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* hs = reinterpret_cast<uint32_t*>(smem);  // kQW x kBins/2, two u16 counters per word
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
@@ -806,16 +862,16 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
   const int q0 = qb * kQW;
   for (int i = lane; i < kQW * kBins / 2; i += 64) hs[i] = 0u;
 
-  double qf[4][KS];
+  ZT qf[4][KS];
   double qA[4], qB[4], qQ[4], qm[4];
   int qz = 0, qv = 0;
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     const int q = q0 + 16 * b + j;
     const bool v = q < a.Q;
-    const double* zr = a.Zq + (int64_t)(v ? q : 0) * a.Lp + g * KS;
+    const ZT* zr = zrow(a.Zq, a.Zq32, v ? q : 0) + g * KS;
 #pragma unroll
-    for (int t = 0; t < KS; ++t) qf[b][t] = v ? zr[t] : 0.0;
+    for (int t = 0; t < KS; ++t) qf[b][t] = v ? zr[t] : (ZT)0;
     const double* st = a.Sq + (int64_t)(v ? q : 0) * a.nseg * 4;
     qm[b] = st[0];
     qA[b] = (0.6 * a.inv_m) * st[1];
@@ -825,39 +881,55 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
     if (st[1] == 0.0) qz |= 1 << b;
   }
   __syncthreads();
+  typedef double dbl2v __attribute__((ext_vector_type(2)));
+  auto load_frag = [&](int64_t cs, ZT* dst) {
+    int64_t i = cs + j;
+    if (i >= c_end) i = c_end - 1;
+    const ZT* p = zrow(a.Zc, a.Zc32, i * a.stride) + g * KS;
+#pragma unroll
+    for (int t = 0; t < KS; ++t) dst[t] = p[t];
+  };
+  ZT cf[KS];
+  load_frag(c_begin, cf);
   for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
-    double cf[KS];
-    {
-      int64_t i = cs + j;
-      if (i >= c_end) i = c_end - 1;
-      const double* p = a.Zc + i * a.stride * a.Lp + g * KS;
-#pragma unroll
-      for (int t = 0; t < KS; ++t) cf[t] = p[t];
-    }
-    dbl4 acc[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      acc[b] = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int t = 0; t < KS; ++t) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(cf[t], qf[b][t], acc[b], 0, 0, 0);
-    }
+    double cst[12];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t i = cs + g + 4 * r;
-      if (i >= c_end) continue;
+      int64_t i = cs + Z::row(g, r);
+      if (i >= c_end) i = c_end - 1;
       const double* st = a.Sc + i * a.stride * a.nseg * 4;
-      const double cm = st[0], csd = st[1], cq = st[2];
+      const dbl2v v = *reinterpret_cast<const dbl2v*>(st);
+      cst[3 * r] = v.x;
+      cst[3 * r + 1] = v.y;
+      cst[3 * r + 2] = st[2];
+    }
+    ZT cfn[KS];
+    load_frag(cs + kCS, cfn);
+    AccT acc[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      acc[b] = AccT{0, 0, 0, 0};
+#pragma unroll
+      for (int t = 0; t < KS; ++t) acc[b] = Z::mfma(cf[t], qf[b][t], acc[b]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (cs + Z::row(g, r) >= c_end) continue;
+      const double cm = cst[3 * r], csd = cst[3 * r + 1], cq = cst[3 * r + 2];
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         if (!((qv >> b) & 1)) continue;
         const bool zq = (qz >> b) & 1, zc = csd == 0.0;
         const double sc = (zq || zc) ? const0(zq, zc, qm[b], cm)
-                                     : approx0(acc[b][r], a.c1, qA[b], qB[b], qQ[b], csd, cm, cq);
+                                     : approx0((double)acc[b][r], a.c1, qA[b], qB[b], qQ[b], csd, cm, cq);
         int bin = (int)(sc * (double)kBins);
         bin = bin < 0 ? 0 : (bin >= kBins ? kBins - 1 : bin);
         atomicAdd(&hs[(16 * b + j) * (kBins / 2) + (bin >> 1)], 1u << (16 * (bin & 1)));
       }
     }
+#pragma unroll
+    for (int t = 0; t < KS; ++t) cf[t] = cfn[t];
   }
   __syncthreads();
   for (int i = lane; i < kQW * kBins / 2; i += 64) {
@@ -871,8 +943,317 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// f32 level-0 scan (default): v_mfma_f32_16x16x4f32 on f32 copies of the level-0 segments and an f32
+// division-free filter; passing pairs are re-scored in f64 (approx0 on the f32 contraction) and kept
+// in f32 lists.  Error budget: |G_f32 - G| <= (m+2) 2^-24 sum|zq zc| <= (m+2) 2^-24 m (Cauchy-Schwarz,
+// sum z^2 = m), i.e. <= 6.5e-5 at m = 32, so the score moves by <= 0.02 * 6.5e-5 ~ 1.3e-6; the f32
+// epilogue adds < 1e-6.  The filter therefore passes every pair within kMarginF of the threshold, and
+// the lists' scores are within 1.5e-6 of the exact ones (callers re-rank with eps = 1e-5).
+// Vectors whose level-0 statistics are zero-variance or outside [2^-60, 2^60] (f32-unsafe) carry a
+// flag and always take the f64 insert path.
+// ------------------------------------------------------------------------------------------------
+constexpr float kMarginF = 3e-5f;
+constexpr int kPad0 = 2 * kCS;  // pad rows of the f32 copies (hq_seg_pack0_f32)
+
+__device__ __forceinline__ float lower_f32(double x) {  // largest float <= x (x finite or +-inf)
+  float f = (float)x;
+  if ((double)f > x) {  // step one ulp towards -inf
+    const int i = __float_as_int(f);
+    f = f > 0.0f ? __int_as_float(i - 1) : (f == 0.0f ? -__int_as_float(1) : __int_as_float(i + 1));
+  }
+  return f;
+}
+__device__ __forceinline__ int shr1_f32i(float v) { return shr1_i32(__float_as_int(v)); }
+
+template <int KS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_scan0f(Scan0Args a) {
+  typedef ZOps<true> Z;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  float* ls = reinterpret_cast<float*>(smem);         // kQW x K approx scores
+  int* li = reinterpret_cast<int*>(ls + kQW * a.K);   // kQW x K corpus rows
+  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
+  const int chunk = xcd + 8 * (slot / a.nqb);
+  const int qb = slot % a.nqb;
+  if (chunk >= a.nchunks) return;
+  const int64_t c_begin = (int64_t)chunk * a.chunk_len;
+  int64_t c_end = c_begin + a.chunk_len;
+  if (c_end > a.N) c_end = a.N;
+  const int q0 = qb * kQW;
+  const int K = a.K;
+  const float c1f = (float)a.c1;
+
+  // queries: fragments, f32 constants, list thresholds (f32, exact list values)
+  float qf[4][KS];
+  float qA[4], qB[4], qQ[4], thl[4];
+  int qsp = 0;  // bit b: query 16b + j is flagged (zero variance / f32-unsafe)
+  int qvb = 0;  // bit b: query 16b + j exists
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int q = q0 + 16 * b + j;
+    const bool v = q < a.Q;
+    const int qq = v ? q : 0;
+    const float* zr = a.Zq32 + (int64_t)qq * a.P0 + g * KS;
+#pragma unroll
+    for (int t = 0; t < KS; ++t) qf[b][t] = v ? zr[t] : 0.0f;
+    const flt4 st = *reinterpret_cast<const flt4*>(a.Sq32 + (int64_t)qq * 4);
+    qA[b] = (float)(0.6 * a.inv_m) * st.x;
+    qB[b] = 0.6f * st.y;
+    qQ[b] = st.z;
+    if (v && __float_as_int(st.w) != 0) qsp |= 1 << b;
+    if (v) qvb |= 1 << b;
+    double t0 = a.thr0;
+    if (v && a.th0 && a.th0[q] > t0) t0 = a.th0[q];
+    thl[b] = v ? lower_f32(t0) : __builtin_huge_valf();
+  }
+  for (int i = lane; i < kQW * K; i += 64) {
+    ls[i] = -__builtin_huge_valf();
+    li[i] = -1;
+  }
+  const bool myq = q0 + lane < a.Q;
+
+  // candidate rows are padded by 16 (hq_seg_pack0_f32): no clamping, rows past c_end are masked
+  auto load_frag = [&](int64_t cs, float* dst) {
+    const float* p = a.Zc32 + (cs + j) * a.P0 + g * KS;
+    if constexpr ((KS % 4) == 0) {
+#pragma unroll
+      for (int t = 0; t < KS; t += 4) {
+        const flt4 v = *reinterpret_cast<const flt4*>(p + t);
+        dst[t] = v.x; dst[t + 1] = v.y; dst[t + 2] = v.z; dst[t + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < KS; ++t) dst[t] = p[t];
+    }
+  };
+  auto load_stats = [&](int64_t cs, flt4* dst) {
+    const flt4* p = reinterpret_cast<const flt4*>(a.Sc32) + cs + 4 * g;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dst[r] = p[r];
+  };
+  auto mfma_half = [&](const int h, const float* f, flt4* acc) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      acc[u] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int t = 0; t < KS; ++t) acc[u] = Z::mfma(f[t], qf[2 * h + u][t], acc[u]);
+    }
+  };
+  // branch-free f32 filter of one half; bit 4u + r = pass of pair (query 16(2h+u)+j, row 4g+r)
+  auto filter_half = [&](const int h, const flt4* acc, const flt4* cst, const int rem) -> int {
+    int bits = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool inval = 4 * g + r >= rem;
+      const bool fc = __float_as_int(cst[r].w) != 0;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int b = 2 * h + u;
+        const float G = acc[u][r];
+        const float R = (thl[b] - kMarginF) - fmaf(G, c1f, 0.35f);
+        const float num = fmaf(G, qA[b] * cst[r].x, qB[b] * cst[r].y);
+        const float den = qQ[b] + cst[r].z;
+        const bool spec = fc | (((qsp >> b) & 1) != 0);
+        const bool p = ((R <= 0.0f) | (num >= R * den) | spec) & !inval & (((qvb >> b) & 1) != 0);
+        bits |= (int)p << (4 * u + r);
+      }
+    }
+    return bits;
+  };
+  // f64 re-score of the passing pairs and list insertion (rare once the thresholds are up)
+  auto insert_half = [&](const int h, const flt4* acc, const int64_t cs, const int bits) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = 2 * h + u;
+        unsigned long long m = __ballot((bits >> (4 * u + r)) & 1);
+        if (m == 0ull) continue;
+        float s = -__builtin_huge_valf();
+        if ((bits >> (4 * u + r)) & 1) {
+          const int q = q0 + 16 * b + j;
+          const double* sq = a.Sq + (int64_t)q * a.nseg * 4;
+          const double* sc = a.Sc + (cs + 4 * g + r) * a.nseg * 4;
+          const double qm = sq[0], qs = sq[1], qq = sq[2], cm = sc[0], csd = sc[1], cq = sc[2];
+          const double v = (qs == 0.0 || csd == 0.0)
+                               ? const0(qs == 0.0, csd == 0.0, qm, cm)
+                               : approx0((double)acc[u][r], a.c1, (0.6 * a.inv_m) * qs, 0.6 * qm, qq, csd, cm, cq);
+          s = (float)v;
+        }
+        while (m) {
+          const int l = __builtin_ctzll(m);
+          m &= m - 1;
+          const float sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), l));
+          const float tl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thl[b]), l));
+          if (!(sc >= tl)) continue;
+          const int qi = 16 * b + (l & 15);
+          const int id = (int)(cs + 4 * (l >> 4) + r);
+          float es = lane < K ? ls[qi * K + lane] : -__builtin_huge_valf();
+          int ei = lane < K ? li[qi * K + lane] : -1;
+          const bool bt = (ei >= 0) && (es > sc || (es == sc && ei < id));
+          const int p = __popcll(__ballot(bt));
+          if (p >= K) continue;
+          const float us = __int_as_float(shr1_f32i(es));
+          const int ui = shr1_i32(ei);
+          if (lane > p) { es = us; ei = ui; }
+          if (lane == p) { es = sc; ei = id; }
+          if (lane < K) {
+            ls[qi * K + lane] = es;
+            li[qi * K + lane] = ei;
+          }
+          if (__builtin_amdgcn_readlane(ei, K - 1) >= 0) {
+            const float tau = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(es), K - 1));
+            if (j == (l & 15)) thl[b] = tau > thl[b] ? tau : thl[b];
+            if (lane == 0 && tau > 0.0f)
+              atomicMax(a.gtau + q0 + qi, (unsigned long long)__double_as_longlong((double)tau));
+          }
+        }
+      }
+  };
+
+  // software pipeline as in k_scan0
+  float cf[KS];
+  flt4 cst[4];
+  load_frag(c_begin, cf);
+  load_stats(c_begin, cst);
+  flt4 acc0[2], acc1[2];
+  mfma_half(0, cf, acc0);
+  unsigned long long gt_bits = 0ull;
+  int step = 0;
+  for (int64_t cs = c_begin; cs < c_end; cs += kCS, ++step) {
+    const int rem = (int)(c_end - cs);
+    float cfn[KS];
+    flt4 cstn[4];
+    load_frag(cs + kCS, cfn);
+    load_stats(cs + kCS, cstn);
+    mfma_half(1, cf, acc1);
+    const int bits0 = filter_half(0, acc0, cst, rem);
+    if (__ballot(bits0 != 0)) insert_half(0, acc0, cs, bits0);
+    mfma_half(0, cfn, acc0);
+    const int bits1 = filter_half(1, acc1, cst, rem);
+    if (__ballot(bits1 != 0)) insert_half(1, acc1, cs, bits1);
+#pragma unroll
+    for (int t = 0; t < KS; ++t) cf[t] = cfn[t];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cst[r] = cstn[r];
+    if ((step & 3) == 0) {
+      if (gt_bits != 0ull) {
+        const float gf = (float)__longlong_as_double((long long)gt_bits);  // exact: list values are f32
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const float v = __shfl(gf, 16 * b + j, 64);
+          thl[b] = v > thl[b] ? v : thl[b];
+        }
+      }
+      if (myq) gt_bits = __atomic_load_n(a.gtau + q0 + lane, __ATOMIC_RELAXED);
+    }
+  }
+
+  for (int i = lane; i < kQW * K; i += 64) {
+    const int ql = i / K, jj = i % K;
+    const int q = q0 + ql;
+    if (q >= a.Q) continue;
+    const int64_t o = ((int64_t)chunk * a.Q + q) * K + jj;
+    const int id = li[i];
+    a.ws_score[o] = id >= 0 ? (double)ls[i] : -__builtin_huge_val();
+    a.ws_id[o] = id >= 0 ? (int64_t)id + a.id_base : -1;
+  }
+}
+
+// f32 sample pass: f32 scores of a strided subset into per-query histograms; flagged pairs are not
+// counted (which only lowers the bound)
+template <int KS>
+__global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
+  typedef ZOps<true> Z;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* hs = reinterpret_cast<uint32_t*>(smem);  // kQW x kBins/2, two u16 counters per word
+  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
+  const int chunk = xcd + 8 * (slot / a.nqb);
+  const int qb = slot % a.nqb;
+  if (chunk >= a.nchunks) return;
+  const int64_t c_begin = (int64_t)chunk * a.chunk_len;
+  int64_t c_end = c_begin + a.chunk_len;
+  if (c_end > a.S) c_end = a.S;
+  const int q0 = qb * kQW;
+  const float c1f = (float)a.c1;
+  for (int i = lane; i < kQW * kBins / 2; i += 64) hs[i] = 0u;
+
+  float qf[4][KS];
+  float qA[4], qB[4], qQ[4];
+  int qok = 0;  // bit b: valid, unflagged query
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int q = q0 + 16 * b + j;
+    const bool v = q < a.Q;
+    const int qq = v ? q : 0;
+    const float* zr = a.Zq32 + (int64_t)qq * a.P0 + g * KS;
+#pragma unroll
+    for (int t = 0; t < KS; ++t) qf[b][t] = zr[t];
+    const flt4 st = *reinterpret_cast<const flt4*>(a.Sq32 + (int64_t)qq * 4);
+    qA[b] = (float)(0.6 * a.inv_m) * st.x;
+    qB[b] = 0.6f * st.y;
+    qQ[b] = st.z;
+    if (v && __float_as_int(st.w) == 0) qok |= 1 << b;
+  }
+  __syncthreads();
+  auto row_of = [&](int64_t i) -> int64_t { return (i < a.S ? i : a.S - 1) * a.stride; };
+  auto load_frag = [&](int64_t cs, float* dst) {
+    const float* p = a.Zc32 + row_of(cs + j) * a.P0 + g * KS;
+#pragma unroll
+    for (int t = 0; t < KS; ++t) dst[t] = p[t];
+  };
+  float cf[KS];
+  load_frag(c_begin, cf);
+  for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
+    flt4 cst[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cst[r] = reinterpret_cast<const flt4*>(a.Sc32)[row_of(cs + 4 * g + r)];
+    float cfn[KS];
+    load_frag(cs + kCS, cfn);
+    flt4 acc[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      acc[b] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int t = 0; t < KS; ++t) acc[b] = Z::mfma(cf[t], qf[b][t], acc[b]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool ok = cs + 4 * g + r < c_end && __float_as_int(cst[r].w) == 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (!ok || !((qok >> b) & 1)) continue;
+        const float G = acc[b][r];
+        const float num = fmaf(G, qA[b] * cst[r].x, qB[b] * cst[r].y);
+        float t = num / (qQ[b] + cst[r].z);
+        t = t > 0.0f ? t : 0.0f;
+        const float sc = fmaf(G, c1f, 0.35f) + t;
+        int bin = (int)(sc * (float)kBins);
+        bin = bin < 0 ? 0 : (bin >= kBins ? kBins - 1 : bin);
+        atomicAdd(&hs[(16 * b + j) * (kBins / 2) + (bin >> 1)], 1u << (16 * (bin & 1)));
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < KS; ++t) cf[t] = cfn[t];
+  }
+  __syncthreads();
+  for (int i = lane; i < kQW * kBins / 2; i += 64) {
+    const uint32_t v = hs[i];
+    if (v == 0u) continue;
+    const int q = q0 + i / (kBins / 2);
+    if (q >= a.Q) continue;
+    unsigned int* hh = a.hist + (int64_t)q * kBins + 2 * (i % (kBins / 2));
+    if (v & 0xFFFFu) atomicAdd(hh, v & 0xFFFFu);
+    if (v >> 16) atomicAdd(hh + 1, v >> 16);
+  }
+}
+
 // per-query starting threshold from the sample histogram (-inf when the sample has < K scores)
-__global__ void k_hist_tau(const unsigned int* __restrict__ hist, int Q, int K, double* __restrict__ th0) {
+__global__ void k_hist_tau(const unsigned int* __restrict__ hist, int Q, int K, double margin,
+                           double* __restrict__ th0) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= Q) return;
   unsigned int cum = 0;
@@ -880,7 +1261,7 @@ __global__ void k_hist_tau(const unsigned int* __restrict__ hist, int Q, int K, 
   for (int e = kBins - 1; e >= 0; --e) {
     cum += hist[(int64_t)q * kBins + e];
     if (cum >= (unsigned int)K) {
-      t = (double)e / (double)kBins - 1e-12;  // margin >> rounding differences between the two passes
+      t = (double)e / (double)kBins - margin;  // margin > the score error of the sample pass
       break;
     }
   }
@@ -1252,13 +1633,13 @@ static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
 }
 
 // sample pass: stride 16 once the corpus is large, else a sample of ~4096 rows (the whole corpus
-// below that); chunks of <= 65520 rows (u16 histogram counters), ~1024 waves
+// below that); chunks of <= 65520 rows (u16 histogram counters), ~2048 waves
 static void sample_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, int& nqb, int& nchunks,
                             int64_t& chunk_len) {
   stride = N >= 16 * 4096 ? 16 : (N / 4096 > 1 ? N / 4096 : 1);
   S = (N + stride - 1) / stride;
   nqb = (Q + kQW - 1) / kQW;
-  int64_t target = (1024 + nqb - 1) / nqb;
+  int64_t target = (2048 + nqb - 1) / nqb;
   const int64_t max_chunks = (S + kCS - 1) / kCS;
   if (target > max_chunks) target = max_chunks;
   if (target < (S + 65519) / 65520) target = (S + 65519) / 65520;
@@ -1267,23 +1648,135 @@ static void sample_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, int& 
   chunk_len = ((chunk_len + kCS - 1) / kCS) * kCS;
 }
 
-template <int KS>
+template <int KS, bool F32>
 static int launch_sample(const SampleArgs& a, hipStream_t s) {
   const size_t lds = (size_t)kQW * kBins / 2 * 4;
-  HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_sample_hist<KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds));
-  hipLaunchKernelGGL((k_sample_hist<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
+  const void* fn = F32 ? (const void*)k_sample_histf<KS> : (const void*)k_sample_hist<KS>;
+  HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  if constexpr (F32) hipLaunchKernelGGL((k_sample_histf<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
+  else hipLaunchKernelGGL((k_sample_hist<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
 
-template <int KS>
+template <int KS, bool F32>
 static int launch_scan0(const Scan0Args& a, hipStream_t s) {
-  const size_t lds = (size_t)kQW * a.K * 12;
+  if constexpr (F32) {
+    const size_t lds = (size_t)kQW * a.K * 8;
+    HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_scan0f<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_scan0f<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
+    HQ_CHECK_LAUNCH();
+    return HQ_OK;
+  }
+  const size_t lds = (size_t)kQW * 32 + (size_t)kQW * a.K * 12;
   HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_scan0<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL((k_scan0<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
+}
+
+template <bool F32>
+static int scan0_dispatch(int ks, const Scan0Args& b, const SampleArgs* sa, hipStream_t s) {
+  int rc;
+  if (sa) {
+    switch (ks) {
+      case 1: rc = launch_sample<1, F32>(*sa, s); break;
+      case 2: rc = launch_sample<2, F32>(*sa, s); break;
+      case 3: rc = launch_sample<3, F32>(*sa, s); break;
+      case 4: rc = launch_sample<4, F32>(*sa, s); break;
+      case 5: rc = launch_sample<5, F32>(*sa, s); break;
+      case 6: rc = launch_sample<6, F32>(*sa, s); break;
+      case 7: rc = launch_sample<7, F32>(*sa, s); break;
+      default: rc = launch_sample<8, F32>(*sa, s); break;
+    }
+    return rc;
+  }
+  switch (ks) {
+    case 1: rc = launch_scan0<1, F32>(b, s); break;
+    case 2: rc = launch_scan0<2, F32>(b, s); break;
+    case 3: rc = launch_scan0<3, F32>(b, s); break;
+    case 4: rc = launch_scan0<4, F32>(b, s); break;
+    case 5: rc = launch_scan0<5, F32>(b, s); break;
+    case 6: rc = launch_scan0<6, F32>(b, s); break;
+    case 7: rc = launch_scan0<7, F32>(b, s); break;
+    default: rc = launch_scan0<8, F32>(b, s); break;
+  }
+  return rc;
+}
+
+// level-0 scan (sample pass -> thresholds -> k_scan0 -> k_merge); f32 selects the f32 contraction
+static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const float* Zq32, const float* Sq32,
+                     int Q, const double* Zc, const double* Sc, const float* Zc32, const float* Sc32, int64_t N,
+                     const SegInfo& si, int k, double threshold, int thr_mode, int64_t id_base, void* workspace,
+                     double* out_score, int64_t* out_id, hipStream_t s) {
+  Scan0Args b;
+  b.Zq = Zq; b.Sq = Sq; b.Q = Q; b.Zc = Zc; b.Sc = Sc; b.N = N;
+  b.Zq32 = Zq32; b.Zc32 = Zc32; b.Sq32 = Sq32; b.Sc32 = Sc32;
+  b.Lp = si.Lp; b.nseg = si.nseg; b.P0 = si.plen[0];
+  b.inv_m = si.inv_m[0];
+  b.c1 = 0.35 * si.inv_m[0];
+  b.K = k;
+  b.thr0 = thr_mode == 0 ? -__builtin_huge_val() : threshold;
+  b.id_base = id_base;
+  scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len);
+  uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
+  b.ws_score = reinterpret_cast<double*>(ws);
+  b.ws_id = reinterpret_cast<int64_t*>(ws + (size_t)b.nchunks * Q * k * 8);
+  b.gtau = reinterpret_cast<unsigned long long*>(ws + (size_t)b.nchunks * Q * k * 16);
+  HQ_CHECK_HIP(hipMemsetAsync(b.gtau, 0, sizeof(unsigned long long) * Q, s));
+  unsigned int* hist = reinterpret_cast<unsigned int*>(ws + (size_t)b.nchunks * Q * k * 16 + (size_t)Q * 8);
+  double* th0 = reinterpret_cast<double*>(ws + (size_t)b.nchunks * Q * k * 16 + (size_t)Q * 8 +
+                                          (size_t)Q * kBins * 4);
+  b.th0 = nullptr;
+  int rc;
+  if (getenv("HQ_SCAN_NOSAMPLE") == nullptr) {
+    SampleArgs sa;
+    sa.Zq = Zq; sa.Sq = Sq; sa.Q = Q; sa.Zc = Zc; sa.Sc = Sc; sa.N = N;
+    sa.Zq32 = Zq32; sa.Zc32 = Zc32; sa.Sq32 = Sq32; sa.Sc32 = Sc32;
+    sa.Lp = b.Lp; sa.nseg = b.nseg; sa.P0 = b.P0; sa.inv_m = b.inv_m; sa.c1 = b.c1;
+    sample_geometry(Q, N, sa.stride, sa.S, sa.nqb, sa.nchunks, sa.chunk_len);
+    sa.hist = hist;
+    HQ_CHECK_HIP(hipMemsetAsync(hist, 0, sizeof(unsigned int) * kBins * Q, s));
+    rc = f32 ? scan0_dispatch<true>(ks, b, &sa, s) : scan0_dispatch<false>(ks, b, &sa, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_hist_tau, dim3((Q + 255) / 256), dim3(256), 0, s, (const unsigned int*)hist, Q, k,
+                       f32 ? (double)kMarginF : 1e-12, th0);
+    HQ_CHECK_LAUNCH();
+    b.th0 = th0;
+  }
+  rc = f32 ? scan0_dispatch<true>(ks, b, nullptr, s) : scan0_dispatch<false>(ks, b, nullptr, s);
+  if (rc) return rc;
+  int mg = Q < 4096 ? Q : 4096;
+  hipLaunchKernelGGL(k_merge, dim3(mg), dim3(64), 0, s, b.ws_score, b.ws_id, (const double*)nullptr,
+                     (const int64_t*)nullptr, b.nchunks, Q, k, out_score, out_id, (double*)nullptr, (int64_t*)nullptr);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+// f32 level-0 copies for the f32 scan: Z32 [N + kPad0, P0] (pad rows 0) and S32 [N + kPad0, 4] =
+// (std, mean, msq, flag bits: 1 zero variance, 2 msq outside [2^-60, 2^60], 4 pad row).  k_scan0f
+// reads up to 31 rows past a step start (the next step's prefetch) without clamping.
+__global__ void k_pack0(const double* __restrict__ Z, const double* __restrict__ S, int64_t N, int Lp, int P0,
+                        int nseg, float* __restrict__ Z32, float* __restrict__ S32) {
+  const int64_t rows = N + kPad0;
+  const int64_t total = rows * P0;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / P0;
+    const int c = (int)(t % P0);
+    Z32[t] = r < N ? (float)Z[r * Lp + c] : 0.0f;
+    if (c == 0) {
+      float* o = S32 + r * 4;
+      if (r < N) {
+        const double* st = S + r * nseg * 4;
+        const double sd = st[1], mean = st[0], msq = st[2];
+        int flag = sd == 0.0 ? 1 : 0;
+        if (!(msq >= 0x1p-60 && msq <= 0x1p60)) flag |= 2;
+        o[0] = (float)sd; o[1] = (float)mean; o[2] = (float)msq; o[3] = __int_as_float(flag);
+      } else {
+        o[0] = 0.0f; o[1] = 0.0f; o[2] = 1.0f; o[3] = __int_as_float(4);
+      }
+    }
+  }
 }
 
 template <int KSMAX, bool OVERALL>
@@ -1396,66 +1889,9 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
     SegInfo si;
     seg_info(L, si);
     const int ks = si.plen[0] / 4;
-    if (ks >= 1 && ks <= 8) {
-      Scan0Args b;
-      b.Zq = Zq; b.Sq = Sq; b.Q = Q; b.Zc = Zc; b.Sc = Sc; b.N = N;
-      b.Lp = si.Lp; b.nseg = si.nseg;
-      b.inv_m = si.inv_m[0];
-      b.c1 = 0.35 * si.inv_m[0];
-      b.K = k;
-      b.thr0 = thr_mode == 0 ? -__builtin_huge_val() : threshold;
-      b.id_base = id_base;
-      scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len);
-      uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
-      b.ws_score = reinterpret_cast<double*>(ws);
-      b.ws_id = reinterpret_cast<int64_t*>(ws + (size_t)b.nchunks * Q * k * 8);
-      b.gtau = reinterpret_cast<unsigned long long*>(ws + (size_t)b.nchunks * Q * k * 16);
-      HQ_CHECK_HIP(hipMemsetAsync(b.gtau, 0, sizeof(unsigned long long) * Q, s));
-      unsigned int* hist = reinterpret_cast<unsigned int*>(ws + (size_t)b.nchunks * Q * k * 16 + (size_t)Q * 8);
-      double* th0 = reinterpret_cast<double*>(ws + (size_t)b.nchunks * Q * k * 16 + (size_t)Q * 8 +
-                                              (size_t)Q * kBins * 4);
-      b.th0 = nullptr;
-      int rc;
-      if (getenv("HQ_SCAN_NOSAMPLE") == nullptr) {
-        SampleArgs sa;
-        sa.Zq = Zq; sa.Sq = Sq; sa.Q = Q; sa.Zc = Zc; sa.Sc = Sc; sa.N = N;
-        sa.Lp = b.Lp; sa.nseg = b.nseg; sa.inv_m = b.inv_m; sa.c1 = b.c1;
-        sample_geometry(Q, N, sa.stride, sa.S, sa.nqb, sa.nchunks, sa.chunk_len);
-        sa.hist = hist;
-        HQ_CHECK_HIP(hipMemsetAsync(hist, 0, sizeof(unsigned int) * kBins * Q, s));
-        switch (ks) {
-          case 1: rc = launch_sample<1>(sa, s); break;
-          case 2: rc = launch_sample<2>(sa, s); break;
-          case 3: rc = launch_sample<3>(sa, s); break;
-          case 4: rc = launch_sample<4>(sa, s); break;
-          case 5: rc = launch_sample<5>(sa, s); break;
-          case 6: rc = launch_sample<6>(sa, s); break;
-          case 7: rc = launch_sample<7>(sa, s); break;
-          default: rc = launch_sample<8>(sa, s); break;
-        }
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_hist_tau, dim3((Q + 255) / 256), dim3(256), 0, s, (const unsigned int*)hist, Q, k, th0);
-        HQ_CHECK_LAUNCH();
-        b.th0 = th0;
-      }
-      switch (ks) {
-        case 1: rc = launch_scan0<1>(b, s); break;
-        case 2: rc = launch_scan0<2>(b, s); break;
-        case 3: rc = launch_scan0<3>(b, s); break;
-        case 4: rc = launch_scan0<4>(b, s); break;
-        case 5: rc = launch_scan0<5>(b, s); break;
-        case 6: rc = launch_scan0<6>(b, s); break;
-        case 7: rc = launch_scan0<7>(b, s); break;
-        default: rc = launch_scan0<8>(b, s); break;
-      }
-      if (rc) return rc;
-      int mg = Q < 4096 ? Q : 4096;
-      hipLaunchKernelGGL(k_merge, dim3(mg), dim3(64), 0, s, b.ws_score, b.ws_id, (const double*)nullptr,
-                         (const int64_t*)nullptr, b.nchunks, Q, k, out_score, out_id, (double*)nullptr,
-                         (int64_t*)nullptr);
-      HQ_CHECK_LAUNCH();
-      return HQ_OK;
-    }
+    if (ks >= 1 && ks <= 8)
+      return scan0_run(false, ks, Zq, Sq, nullptr, nullptr, Q, Zc, Sc, nullptr, nullptr, N, si, k, threshold,
+                       thr_mode, id_base, workspace, out_score, out_id, s);
   }
   ScanArgs a;
   a.Zq = Zq; a.Sq = Sq; a.Q = Q; a.Zc = Zc; a.Sc = Sc; a.N = N;
@@ -1494,6 +1930,50 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
                      k, out_score, out_id, out_best, out_best_id);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
+}
+
+int hq_seg_level0_len(int L) {
+  SegInfo si;
+  seg_info(L, si);
+  return si.nseg > 0 ? si.plen[0] : 0;
+}
+
+int hq_seg_pack0_f32(const double* Z, const double* S, int64_t N, int L, float* Z32, float* S32, hq_stream_t stream) {
+  if (L <= 0 || N < 0) return fail(HQ_E_INVALID, "bad shape N=%lld L=%d", (long long)N, L);
+  if ((N > 0 && (!Z || !S)) || !Z32 || !S32) return fail(HQ_E_INVALID, "null buffer");
+  SegInfo si;
+  seg_info(L, si);
+  if (si.nseg == 0) return fail(HQ_E_INVALID, "no level structure for L=%d", L);
+  int64_t blocks = ((N + kPad0) * si.plen[0] + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(k_pack0, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, Z, S, N, si.Lp, si.plen[0],
+                     si.nseg, Z32, S32);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+int hq_scan0_topk_f32(const float* Zq32, const float* Sq32, const double* Sq, int Q, const float* Zc32,
+                      const float* Sc32, const double* Sc, int64_t N, int L, int k, double threshold, int thr_mode,
+                      int64_t id_base, void* workspace, size_t workspace_bytes, double* out_score, int64_t* out_id,
+                      hq_stream_t stream) {
+  if (Q < 0 || N < 0 || L <= 0) return fail(HQ_E_INVALID, "bad shape");
+  if (k <= 0 || k > kMaxTopK) return fail(HQ_E_UNSUPPORTED, "k=%d (1..%d)", k, kMaxTopK);
+  if (Q == 0) return HQ_OK;
+  if (!out_score || !out_id) return fail(HQ_E_INVALID, "null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  if (N == 0) {
+    HQ_CHECK_HIP(hipMemsetAsync(out_id, 0xFF, sizeof(int64_t) * Q * k, s));
+    return HQ_OK;
+  }
+  if (N >= 0x7FFFFFFF) return fail(HQ_E_UNSUPPORTED, "N=%lld rows (int32 row ids)", (long long)N);
+  if (!Zq32 || !Sq32 || !Sq || !Zc32 || !Sc32 || !Sc || !workspace) return fail(HQ_E_INVALID, "null buffer");
+  if (workspace_bytes < hq_scan_workspace_size(Q, N, k)) return fail(HQ_E_INVALID, "workspace too small");
+  SegInfo si;
+  seg_info(L, si);
+  const int ks = si.nseg > 0 ? si.plen[0] / 4 : 0;
+  if (ks < 1 || ks > 8) return fail(HQ_E_UNSUPPORTED, "level-0 segment of %d values (1..32)", si.plen[0]);
+  return scan0_run(true, ks, nullptr, Sq, Zq32, Sq32, Q, nullptr, Sc, Zc32, Sc32, N, si, k, threshold, thr_mode,
+                   id_base, workspace, out_score, out_id, s);
 }
 
 int hq_rescore(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc, const double* Zc,

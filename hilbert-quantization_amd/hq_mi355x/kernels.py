@@ -7,6 +7,8 @@ SURVEY.md §7); the reference-shaped classes in `hq_mi355x.core` / `hq_mi355x.ra
 """
 from __future__ import annotations
 
+import os
+
 import ctypes
 from typing import Optional, Tuple
 
@@ -222,17 +224,19 @@ class Prepared:
     """Device-resident prepared index vectors: raw R [N, L] f64, Z [N, Lp] f64 (segment padded,
     normalised) and stats S [N, nseg, 4] (mean, std, mean of squares).  Built once per corpus."""
 
-    __slots__ = ("R", "Z", "S", "L", "N", "nseg", "Lp")
+    __slots__ = ("R", "Z", "S", "L", "N", "nseg", "Lp", "Z32", "S32")
 
     def __init__(self, R, Z, S, L):
         self.R, self.Z, self.S, self.L = R, Z, S, int(L)
         self.N = Z.shape[0]
         self.nseg = S.shape[1]
         self.Lp = Z.shape[1]
+        self.Z32 = self.S32 = None  # f32 level-0 copies for the f32 level-0 scan (pack0_f32)
 
     def rows(self, sel):
-        """Sub-set of rows (device index tensor) as a new Prepared."""
-        return Prepared(self.R.index_select(0, sel), self.Z.index_select(0, sel), self.S.index_select(0, sel), self.L)
+        """Sub-set of rows (device index tensor) as a new Prepared (f32 copies re-packed on demand)."""
+        p = Prepared(self.R.index_select(0, sel), self.Z.index_select(0, sel), self.S.index_select(0, sel), self.L)
+        return pack0_f32(p) if self.Z32 is not None else p
 
 
 def seg_prepare(idx, exc=None) -> Prepared:
@@ -245,6 +249,19 @@ def seg_prepare(idx, exc=None) -> Prepared:
     if N:
         _chk(_L().hq_seg_prepare(ptr(i2), N, L, ptr(Z), ptr(S), stream()), exc)
     return Prepared(i2, Z, S, L)
+
+
+PAD0 = 32  # pad rows of the f32 level-0 copies (hq_mi355x.h: hq_seg_pack0_f32)
+
+
+def pack0_f32(p: Prepared, exc=None) -> Prepared:
+    """Attach the f32 copy of the level-0 segments (hq_seg_pack0_f32) used by the f32 level-0 scan."""
+    t = torch()
+    P0 = int(_L().hq_seg_level0_len(p.L))
+    p.Z32 = t.empty((p.N + PAD0, P0), dtype=t.float32, device=p.Z.device)
+    p.S32 = t.empty((p.N + PAD0, 4), dtype=t.float32, device=p.Z.device)
+    _chk(_L().hq_seg_pack0_f32(ptr(p.Z), ptr(p.S), p.N, p.L, ptr(p.Z32), ptr(p.S32), stream()), exc)
+    return p
 
 
 def level_scores(q: Prepared, c: Prepared, level: int, exc=None):
@@ -271,6 +288,12 @@ def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.
     ids = t.empty((Q, k), dtype=t.int64, device=dev)
     best = t.empty(Q, dtype=t.float64, device=dev) if need_best else None
     bid = t.empty(Q, dtype=t.int64, device=dev) if need_best else None
+    if (mode == 0 and not need_best and q.Z32 is not None and c.Z32 is not None
+            and not os.environ.get("HQ_SCAN_F64")):
+        _chk(_L().hq_scan0_topk_f32(ptr(q.Z32), ptr(q.S32), ptr(q.S), Q, ptr(c.Z32), ptr(c.S32), ptr(c.S), N, c.L, k,
+                                    float(threshold), thr_mode, int(id_base), ptr(ws), ws_bytes, ptr(sc), ptr(ids),
+                                    stream()), exc)
+        return sc, ids, best, bid
     _chk(_L().hq_scan_topk(ptr(q.Z), ptr(q.S), Q, ptr(c.Z), ptr(c.S), N, c.L, mode, k, float(threshold), thr_mode,
                            int(id_base), ptr(ws), ws_bytes, ptr(sc), ptr(ids), ptr(best), ptr(bid), stream()), exc)
     return sc, ids, best, bid

@@ -186,9 +186,9 @@ def test_rag_scores(hq_lib, golden):
 
 
 def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, monkeypatch):
-    """The wave-independent level-0 scan (k_scan0: global threshold exchange, division-free filter,
-    exact constant branches) gives the same exact top-k as the LDS-tiled k_scan (HQ_SCAN_V1) and as
-    the oracle, on a corpus with a ragged chunk tail, zero-variance level-0 segments on both sides,
+    """The wave-independent level-0 scan (k_scan0: sampled thresholds, global threshold exchange,
+    division-free filter, exact constant branches; f32 and f64 contractions) gives the same exact
+    top-k as the LDS-tiled k_scan (HQ_SCAN_V1) and as the oracle, on a corpus with a ragged chunk tail, zero-variance level-0 segments on both sides,
     duplicate runs across chunks and a query count that is not a multiple of 64."""
     from hq_mi355x.core.search_engine import IndexCorpus
     rng = np.random.default_rng(77)
@@ -203,7 +203,9 @@ def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, monkeypatch):
     corpus = IndexCorpus(C)
     qp = corpus.prepare_queries(Q)
     res = {}
-    for tag in ("v0", "v0-nosample", "v1"):
+    for tag in ("v0", "v0-f64", "v0-nosample", "v1"):
+        if tag == "v0-f64":
+            monkeypatch.setenv("HQ_SCAN_F64", "1")
         if tag == "v0-nosample":
             monkeypatch.setenv("HQ_SCAN_NOSAMPLE", "1")
         if tag == "v1":
@@ -212,7 +214,7 @@ def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, monkeypatch):
             sc, ids, cnt, _, _ = corpus.exact_topk(qp, 0, 20, thr, tm)
             res[(tag, thr, tm)] = (_np(sc), _np(ids), _np(cnt))
     for key in ((0.1, 1), (0.6, 1), (0.1, 2)):
-        for tag in ("v0-nosample", "v1"):
+        for tag in ("v0-f64", "v0-nosample", "v1"):
             a, b = res[("v0",) + key], res[(tag,) + key]
             assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]), (tag, key)
             np.testing.assert_array_equal(a[0][a[1] >= 0], b[0][b[1] >= 0])
