@@ -528,6 +528,9 @@ struct Scan0Args {
   int64_t id_base;
   int64_t chunk_len; int nchunks; int nqb;
   double* ws_score; int64_t* ws_id; unsigned long long* gtau;
+  float* pool_s; int* pool_i; int* pool_n; int pool_cap;  // k_scan0f: per-query candidate pools
+  int expt;          // performance experiments (HQ_SCAN_EXPT): 1 no filter, 2 no insert, 3 count
+  unsigned long long* dbg;  // expt 3: [entries, passing pairs, list inserts]
 };
 
 __device__ __forceinline__ double rl_f64(double v, int l) {
@@ -674,11 +677,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   };
   // MFMAs of one half (two 16-query blocks) of a step
   auto mfma_half = [&](const int h, const ZT* f, AccT* acc) {
+    acc[0] = AccT{0, 0, 0, 0};
+    acc[1] = AccT{0, 0, 0, 0};
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      acc[u] = AccT{0, 0, 0, 0};
-#pragma unroll
-      for (int t = 0; t < KS; ++t) acc[u] = Z::mfma(f[t], qf[2 * h + u][t], acc[u]);
+    for (int t = 0; t < KS; ++t) {  // two interleaved chains
+      acc[0] = Z::mfma(f[t], qf[2 * h][t], acc[0]);
+      acc[1] = Z::mfma(f[t], qf[2 * h + 1][t], acc[1]);
     }
   };
   // filter of one half of the step starting at row cs: branch-free, so the scheduler can interleave
@@ -907,11 +911,11 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
     load_frag(cs + kCS, cfn);
     AccT acc[4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      acc[b] = AccT{0, 0, 0, 0};
+    for (int b = 0; b < 4; ++b) acc[b] = AccT{0, 0, 0, 0};
 #pragma unroll
-      for (int t = 0; t < KS; ++t) acc[b] = Z::mfma(cf[t], qf[b][t], acc[b]);
-    }
+    for (int t = 0; t < KS; ++t)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[b] = Z::mfma(cf[t], qf[b][t], acc[b]);  // 4 interleaved chains
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -944,17 +948,17 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// f32 level-0 scan (default): v_mfma_f32_16x16x4f32 on f32 copies of the level-0 segments and an f32
-// division-free filter; passing pairs are re-scored in f64 (approx0 on the f32 contraction) and kept
-// in f32 lists.  Error budget: |G_f32 - G| <= (m+2) 2^-24 sum|zq zc| <= (m+2) 2^-24 m (Cauchy-Schwarz,
-// sum z^2 = m), i.e. <= 6.5e-5 at m = 32, so the score moves by <= 0.02 * 6.5e-5 ~ 1.3e-6; the f32
-// epilogue adds < 1e-6.  The filter therefore passes every pair within kMarginF of the threshold, and
-// the lists' scores are within 1.5e-6 of the exact ones (callers re-rank with eps = 1e-5).
-// Vectors whose level-0 statistics are zero-variance or outside [2^-60, 2^60] (f32-unsafe) carry a
-// flag and always take the f64 insert path.
+// f32 level-0 scan (default): v_mfma_f32_16x16x4f32 on f32 copies of the level-0 segments, an f32
+// division-free filter and f32 list scores.  Error budget: |G_f32 - G| <= (m+2) 2^-24 sum|zq zc| <=
+// (m+2) 2^-24 m (Cauchy-Schwarz, sum z^2 = m), i.e. <= 6.5e-5 at m = 32, so the score moves by
+// <= 0.02 * 6.5e-5 ~ 1.3e-6; the f32 epilogue adds < 1e-6 (each term of num is bounded by
+// 0.6 rho_q rho_c <= 0.3 den).  The filter passes every pair within kMarginF of the threshold, and
+// list scores are within ~3e-6 of the exact ones (callers re-rank with eps = 1e-5).  Vectors whose
+// level-0 statistics are zero-variance or outside [2^-60, 2^60] (f32-unsafe) carry a flag and are
+// scored from the f64 statistics.
 // ------------------------------------------------------------------------------------------------
 constexpr float kMarginF = 3e-5f;
-constexpr int kPad0 = 2 * kCS;  // pad rows of the f32 copies (hq_seg_pack0_f32)
+constexpr int kPad0 = 3 * kCS;  // pad rows of the f32 copies (hq_seg_pack0_f32)
 
 __device__ __forceinline__ float lower_f32(double x) {  // largest float <= x (x finite or +-inf)
   float f = (float)x;
@@ -983,6 +987,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int q0 = qb * kQW;
   const int K = a.K;
   const float c1f = (float)a.c1;
+  int cntr[4] = {0, 0, 0, 0};  // pairs offered to the list of query 16b + j (same in the 4 lanes g)
 
   // queries: fragments, f32 constants, list thresholds (f32, exact list values)
   float qf[4][KS];
@@ -1032,12 +1037,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
     for (int r = 0; r < 4; ++r) dst[r] = p[r];
   };
+  // two accumulation chains interleaved (dependent MFMAs two issues apart: no RAW stall)
   auto mfma_half = [&](const int h, const float* f, flt4* acc) {
+    acc[0] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
+    acc[1] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      acc[u] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int t = 0; t < KS; ++t) acc[u] = Z::mfma(f[t], qf[2 * h + u][t], acc[u]);
+    for (int t = 0; t < KS; ++t) {
+      acc[0] = Z::mfma(f[t], qf[2 * h][t], acc[0]);
+      acc[1] = Z::mfma(f[t], qf[2 * h + 1][t], acc[1]);
     }
   };
   // branch-free f32 filter of one half; bit 4u + r = pass of pair (query 16(2h+u)+j, row 4g+r)
@@ -1061,61 +1068,130 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
     return bits;
   };
-  // f64 re-score of the passing pairs and list insertion (rare once the thresholds are up)
-  auto insert_half = [&](const int h, const flt4* acc, const int64_t cs, const int bits) {
+  // List maintenance.  A query's list starts in APPEND mode: passing pairs are appended in parallel
+  // (LDS atomic slot, no ordering) while the list has room; the pair that fills it sorts it (rank
+  // sort), sets the query's threshold to its K-th score and switches it to SORTED mode, where later
+  // pairs are merged one at a time.  With the sampled starting thresholds most queries never leave
+  // append mode within a chunk.  cntr[b] counts the pairs ever offered (>= K: sorted mode); the slots
+  // of a batch follow from its ballot (pairs of query j sit in lanes j, j+16, j+32, j+48).
+  auto key_better = [](float s1, int i1, float s2, int i2) { return s1 > s2 || (s1 == s2 && i1 < i2); };
+  // rank sort of the first n (<= K <= 64) entries of list qi, in place
+  auto sort_list = [&](const int qi, const int n) {
+    float e = lane < n ? ls[qi * K + lane] : -__builtin_huge_valf();
+    int ei = lane < n ? li[qi * K + lane] : 0x7FFFFFFF;
+    int rank = 0;
+    for (int o = 0; o < n; ++o) {
+      const float so = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), o));
+      const int io = __builtin_amdgcn_readlane(ei, o);
+      rank += key_better(so, io, e, ei) ? 1 : 0;
+    }
+    if (lane < n) {
+      ls[qi * K + rank] = e;
+      li[qi * K + rank] = ei;
+    }
+  };
+  // raise query qi's threshold to tau (lanes holding it) and publish it
+  auto raise = [&](const int qi, const float tau) {
+    const int b = qi >> 4;
+    if (j == (qi & 15)) {
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+        if (bb == b) thl[bb] = tau > thl[bb] ? tau : thl[bb];
+    }
+    if (lane == 0 && tau > 0.0f) atomicMax(a.gtau + q0 + qi, (unsigned long long)__double_as_longlong((double)tau));
+  };
+  // merge one pair into the sorted list qi
+  auto merge_one = [&](const int qi, const float sc, const int id) {
+    float es = lane < K ? ls[qi * K + lane] : -__builtin_huge_valf();
+    int ei = lane < K ? li[qi * K + lane] : -1;
+    const bool bt = key_better(es, ei, sc, id);
+    const int p = __popcll(__ballot(bt));
+    if (p >= K) return;
+    const float us = __int_as_float(shr1_f32i(es));
+    const int ui = shr1_i32(ei);
+    if (lane > p) { es = us; ei = ui; }
+    if (lane == p) { es = sc; ei = id; }
+    if (lane < K) {
+      ls[qi * K + lane] = es;
+      li[qi * K + lane] = ei;
+    }
+    raise(qi, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(es), K - 1)));
+  };
+  // score, test and file the passing pairs of one half: f32 for plain pairs (the filter's expression
+  // with the division), f64 statistics for flagged pairs
+  auto insert_half = [&](const int h, const flt4* acc, const flt4* cst, const int64_t cs, const int bits) {
+    if (a.expt == 3 && lane == 0) atomicAdd(a.dbg, 1ull);
+    if (a.expt == 4) return;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = 2 * h + u;
-        unsigned long long m = __ballot((bits >> (4 * u + r)) & 1);
-        if (m == 0ull) continue;
+        const bool pb = (bits >> (4 * u + r)) & 1;
+        if (!__ballot(pb)) continue;
         float s = -__builtin_huge_valf();
-        if ((bits >> (4 * u + r)) & 1) {
-          const int q = q0 + 16 * b + j;
-          const double* sq = a.Sq + (int64_t)q * a.nseg * 4;
-          const double* sc = a.Sc + (cs + 4 * g + r) * a.nseg * 4;
-          const double qm = sq[0], qs = sq[1], qq = sq[2], cm = sc[0], csd = sc[1], cq = sc[2];
-          const double v = (qs == 0.0 || csd == 0.0)
-                               ? const0(qs == 0.0, csd == 0.0, qm, cm)
-                               : approx0((double)acc[u][r], a.c1, (0.6 * a.inv_m) * qs, 0.6 * qm, qq, csd, cm, cq);
-          s = (float)v;
+        const bool flagged = (((qsp >> b) & 1) != 0) | (__float_as_int(cst[r].w) != 0);
+        if (pb && !flagged) {
+          const float G = acc[u][r];
+          const float num = fmaf(G, qA[b] * cst[r].x, qB[b] * cst[r].y);
+          float t = num * __builtin_amdgcn_rcpf(qQ[b] + cst[r].z);  // 1 ulp
+          t = t > 0.0f ? t : 0.0f;
+          s = fmaf(G, c1f, 0.35f) + t;
+          s = s < 1.0f ? s : 1.0f;
+          s = s > 0.0f ? s : 0.0f;
         }
-        while (m) {
-          const int l = __builtin_ctzll(m);
-          m &= m - 1;
+        if (__ballot(pb && flagged)) {
+          if (pb && flagged) {
+            const int q = q0 + 16 * b + j;
+            const double* sq = a.Sq + (int64_t)q * a.nseg * 4;
+            const double* sc = a.Sc + (cs + 4 * g + r) * a.nseg * 4;
+            const double qm = sq[0], qs = sq[1], qq = sq[2], cm = sc[0], csd = sc[1], cq = sc[2];
+            const double v = (qs == 0.0 || csd == 0.0)
+                                 ? const0(qs == 0.0, csd == 0.0, qm, cm)
+                                 : approx0((double)acc[u][r], a.c1, (0.6 * a.inv_m) * qs, 0.6 * qm, qq, csd, cm, cq);
+            s = (float)v;
+          }
+        }
+        const bool ok = pb && s >= thl[b] && a.expt != 5;
+        if (a.expt == 3 && lane == 0) atomicAdd(a.dbg + 1, (unsigned long long)__popcll(__ballot(ok)));
+        const int qi = 16 * b + j;
+        const int id = (int)(cs + 4 * g + r);
+        const unsigned long long mok = __ballot(ok);
+        const unsigned long long mine = (mok >> j) & 0x0001000100010001ull;  // query j's pairs, bit 16g
+        const int pos = cntr[b] + __popcll(mine & ((1ull << (16 * g)) - 1ull));
+        cntr[b] += __popcll(mine);
+        if (ok && pos < K) {
+          ls[qi * K + pos] = s;
+          li[qi * K + pos] = id;
+        }
+        // lists that just filled: sort, threshold
+        unsigned long long mf = __ballot(ok && pos == K - 1);
+        while (mf) {
+          const int l = __builtin_ctzll(mf);
+          mf &= mf - 1;
+          const int qf = 16 * b + (l & 15);
+          sort_list(qf, K);
+          raise(qf, ls[qf * K + K - 1]);
+        }
+        // pairs offered to sorted lists
+        unsigned long long mo = __ballot(ok && pos >= K);
+        if (a.expt == 3 && lane == 0) atomicAdd(a.dbg + 2, (unsigned long long)__popcll(mo));
+        while (mo) {
+          const int l = __builtin_ctzll(mo);
+          mo &= mo - 1;
           const float sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), l));
-          const float tl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thl[b]), l));
-          if (!(sc >= tl)) continue;
-          const int qi = 16 * b + (l & 15);
-          const int id = (int)(cs + 4 * (l >> 4) + r);
-          float es = lane < K ? ls[qi * K + lane] : -__builtin_huge_valf();
-          int ei = lane < K ? li[qi * K + lane] : -1;
-          const bool bt = (ei >= 0) && (es > sc || (es == sc && ei < id));
-          const int p = __popcll(__ballot(bt));
-          if (p >= K) continue;
-          const float us = __int_as_float(shr1_f32i(es));
-          const int ui = shr1_i32(ei);
-          if (lane > p) { es = us; ei = ui; }
-          if (lane == p) { es = sc; ei = id; }
-          if (lane < K) {
-            ls[qi * K + lane] = es;
-            li[qi * K + lane] = ei;
-          }
-          if (__builtin_amdgcn_readlane(ei, K - 1) >= 0) {
-            const float tau = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(es), K - 1));
-            if (j == (l & 15)) thl[b] = tau > thl[b] ? tau : thl[b];
-            if (lane == 0 && tau > 0.0f)
-              atomicMax(a.gtau + q0 + qi, (unsigned long long)__double_as_longlong((double)tau));
-          }
+          const int qo = 16 * b + (l & 15);
+          if (!(sc >= ls[qo * K + K - 1])) continue;
+          merge_one(qo, sc, __builtin_amdgcn_readlane(id, l));
         }
       }
   };
 
-  // software pipeline as in k_scan0
-  float cf[KS];
+  // software pipeline as in k_scan0, fragments two steps ahead, statistics one step ahead
+  float cf[KS], cf1[KS];
   flt4 cst[4];
   load_frag(c_begin, cf);
+  load_frag(c_begin + kCS, cf1);
   load_stats(c_begin, cst);
   flt4 acc0[2], acc1[2];
   mfma_half(0, cf, acc0);
@@ -1123,18 +1199,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   int step = 0;
   for (int64_t cs = c_begin; cs < c_end; cs += kCS, ++step) {
     const int rem = (int)(c_end - cs);
-    float cfn[KS];
+    float cf2[KS];
     flt4 cstn[4];
-    load_frag(cs + kCS, cfn);
+    load_frag(cs + 2 * kCS, cf2);
     load_stats(cs + kCS, cstn);
     mfma_half(1, cf, acc1);
-    const int bits0 = filter_half(0, acc0, cst, rem);
-    if (__ballot(bits0 != 0)) insert_half(0, acc0, cs, bits0);
-    mfma_half(0, cfn, acc0);
-    const int bits1 = filter_half(1, acc1, cst, rem);
-    if (__ballot(bits1 != 0)) insert_half(1, acc1, cs, bits1);
+    int bits0 = a.expt == 1 ? 0 : filter_half(0, acc0, cst, rem);
+    if (a.expt == 2) bits0 = __ballot(bits0 != 0) ? 0 : 0;
+    if (__ballot(bits0 != 0)) insert_half(0, acc0, cst, cs, bits0);
+    mfma_half(0, cf1, acc0);
+    int bits1 = a.expt == 1 ? 0 : filter_half(1, acc1, cst, rem);
+    if (a.expt == 2) bits1 = __ballot(bits1 != 0) ? 0 : 0;
+    if (__ballot(bits1 != 0)) insert_half(1, acc1, cst, cs, bits1);
+    if (a.expt == 1) {  // keep the accumulators live
+      if (acc0[0][0] == 12345.0f && acc1[1][3] == 54321.0f) ls[0] = 1.0f;
+    }
 #pragma unroll
-    for (int t = 0; t < KS; ++t) cf[t] = cfn[t];
+    for (int t = 0; t < KS; ++t) {
+      cf[t] = cf1[t];
+      cf1[t] = cf2[t];
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) cst[r] = cstn[r];
     if ((step & 3) == 0) {
@@ -1150,14 +1234,130 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
   }
 
-  for (int i = lane; i < kQW * K; i += 64) {
-    const int ql = i / K, jj = i % K;
-    const int q = q0 + ql;
-    if (q >= a.Q) continue;
-    const int64_t o = ((int64_t)chunk * a.Q + q) * K + jj;
-    const int id = li[i];
-    a.ws_score[o] = id >= 0 ? (double)ls[i] : -__builtin_huge_val();
-    a.ws_id[o] = id >= 0 ? (int64_t)id + a.id_base : -1;
+  // hand the lists (unordered is fine) to the per-query pools: one atomic per query, lane-parallel
+  int nl = 0;  // entries of query `lane`
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int v = __shfl(cntr[b], lane & 15, 64);
+    if ((lane >> 4) == b) nl = v < K ? v : K;
+  }
+  int base = 0;
+  if (nl > 0 && myq) base = atomicAdd(a.pool_n + q0 + lane, nl);
+  for (int ql = 0; ql < kQW; ++ql) {
+    const int n = __builtin_amdgcn_readlane(nl, ql);
+    if (n == 0 || q0 + ql >= a.Q) continue;
+    const int bq = __builtin_amdgcn_readlane(base, ql);
+    if (lane < n) {
+      const int64_t o = (int64_t)(q0 + ql) * a.pool_cap + bq + lane;
+      a.pool_s[o] = ls[ql * K + lane];
+      a.pool_i[o] = li[ql * K + lane];
+    }
+  }
+}
+
+// Exact top-K of each query's pool (one wave per query): (score desc, row asc).  The K-th largest
+// score v is found by bisection on the f32 bit pattern (scores >= 0), ties at v by bisection on the
+// row, then the K selected entries are rank-sorted.  Pools of up to 64*kPoolReg entries stay in
+// registers; larger ones are re-read per bisection step.
+constexpr int kPoolReg = 16;
+
+__global__ __launch_bounds__(64) void k_pool_select(const float* __restrict__ pool_s, const int* __restrict__ pool_i,
+                                                    const int* __restrict__ pool_n, int cap, int Q, int K,
+                                                    int64_t id_base, double* __restrict__ out_score,
+                                                    int64_t* __restrict__ out_id) {
+  const int lane = threadIdx.x;
+  for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    const int T = pool_n[q];
+    const float* ps = pool_s + (int64_t)q * cap;
+    const int* pi = pool_i + (int64_t)q * cap;
+    const bool inreg = T <= 64 * kPoolReg;
+    float rs[kPoolReg];
+    int ri[kPoolReg];
+    if (inreg) {
+#pragma unroll
+      for (int e = 0; e < kPoolReg; ++e) {
+        const int x = lane + 64 * e;
+        rs[e] = x < T ? ps[x] : -1.0f;
+        ri[e] = x < T ? pi[x] : 0x7FFFFFFF;
+      }
+    }
+    // count entries with (score > sv) or (score == sv and row <= iv)  [iv = -1: score > sv only;
+    // iv = INT_MAX: score >= sv]
+    auto count = [&](float sv, int iv) -> int {
+      int c = 0;
+      if (inreg) {
+#pragma unroll
+        for (int e = 0; e < kPoolReg; ++e) c += (rs[e] > sv || (rs[e] == sv && ri[e] <= iv)) ? 1 : 0;
+      } else {
+        for (int x = lane; x < T; x += 64) {
+          const float s = ps[x];
+          c += (s > sv || (s == sv && pi[x] <= iv)) ? 1 : 0;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+      return c;
+    };
+    const int k = T < K ? T : K;
+    float sv = -1.0f;
+    int iv = 0x7FFFFFFF;  // select all
+    if (T > K) {
+      // largest sv (as bits) with count(score >= sv) >= K
+      unsigned lo = 0, hi = 0x7F800000u;  // [0, +inf]
+      while (lo < hi) {
+        const unsigned mid = lo + (hi - lo + 1) / 2;
+        if (count(__uint_as_float(mid), 0x7FFFFFFF) >= K) lo = mid; else hi = mid - 1;
+      }
+      sv = __uint_as_float(lo);
+      const int gt = count(sv, -1);  // strictly above sv
+      // smallest iv with count(score > sv or (== sv and row <= iv)) >= K
+      int a0 = 0, a1 = 0x7FFFFFFE;
+      if (gt < K) {
+        while (a0 < a1) {
+          const int mid = a0 + (a1 - a0) / 2;
+          if (count(sv, mid) >= K) a1 = mid; else a0 = mid + 1;
+        }
+      }
+      iv = gt < K ? a0 : -1;
+    }
+    // gather the k selected entries (rank among the selected by ballot prefix), then rank-sort
+    __shared__ float gs[64];
+    __shared__ int gi[64];
+    int filled = 0;
+    auto consider = [&](float s, int id, bool valid) {
+      const bool sel = valid && (s > sv || (s == sv && id <= iv));
+      const unsigned long long m = __ballot(sel);
+      const int pre = __popcll(m & ((1ull << lane) - 1ull));
+      if (sel && filled + pre < 64) { gs[filled + pre] = s; gi[filled + pre] = id; }
+      filled += __popcll(m);
+    };
+    if (inreg) {
+#pragma unroll
+      for (int e = 0; e < kPoolReg; ++e) consider(rs[e], ri[e], lane + 64 * e < T);
+    } else {
+      for (int x0 = 0; x0 < T; x0 += 64) {
+        const int x = x0 + lane;
+        consider(x < T ? ps[x] : -1.0f, x < T ? pi[x] : 0, x < T);
+      }
+    }
+    __syncthreads();
+    const float es = lane < k ? gs[lane] : -1.0f;
+    const int ei = lane < k ? gi[lane] : 0x7FFFFFFF;
+    int rank = 0;
+    for (int o = 0; o < k; ++o) {
+      const float so = __shfl(es, o, 64);
+      const int io = __shfl(ei, o, 64);
+      rank += (so > es || (so == es && io < ei)) ? 1 : 0;
+    }
+    if (lane < k) {
+      out_score[(int64_t)q * K + rank] = (double)es;
+      out_id[(int64_t)q * K + rank] = (int64_t)ei + id_base;
+    }
+    if (lane >= k && lane < K) {
+      out_score[(int64_t)q * K + lane] = -__builtin_huge_val();
+      out_id[(int64_t)q * K + lane] = -1;
+    }
+    __syncthreads();
   }
 }
 
@@ -1214,11 +1414,11 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
     load_frag(cs + kCS, cfn);
     flt4 acc[4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      acc[b] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int b = 0; b < 4; ++b) acc[b] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int t = 0; t < KS; ++t) acc[b] = Z::mfma(cf[t], qf[b][t], acc[b]);
-    }
+    for (int t = 0; t < KS; ++t)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[b] = Z::mfma(cf[t], qf[b][t], acc[b]);  // 4 interleaved chains
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1628,8 +1828,8 @@ static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
   int nqb, nchunks;
   int64_t chunk_len;
   scan0_geometry(Q, N, nqb, nchunks, chunk_len);
-  // lists + global thresholds + sample histogram + starting thresholds
-  return (size_t)nchunks * Q * k * 16 + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 8 + 256;
+  // lists / pools + global thresholds + sample histogram + starting thresholds + pool counts
+  return (size_t)nchunks * Q * k * 16 + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 8 + (size_t)Q * 4 + 256;
 }
 
 // sample pass: stride 16 once the corpus is large, else a sample of ~4096 rows (the whole corpus
@@ -1662,7 +1862,7 @@ static int launch_sample(const SampleArgs& a, hipStream_t s) {
 template <int KS, bool F32>
 static int launch_scan0(const Scan0Args& a, hipStream_t s) {
   if constexpr (F32) {
-    const size_t lds = (size_t)kQW * a.K * 8;
+    const size_t lds = (size_t)kQW * a.K * 8 + (size_t)kQW * 4;
     HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_scan0f<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL((k_scan0f<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
     HQ_CHECK_LAUNCH();
@@ -1718,6 +1918,13 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   b.K = k;
   b.thr0 = thr_mode == 0 ? -__builtin_huge_val() : threshold;
   b.id_base = id_base;
+  b.expt = getenv("HQ_SCAN_EXPT") ? atoi(getenv("HQ_SCAN_EXPT")) : 0;
+  static unsigned long long* dbg = nullptr;
+  if (b.expt == 3) {
+    if (!dbg) HQ_CHECK_HIP(hipMalloc(&dbg, 64));
+    HQ_CHECK_HIP(hipMemsetAsync(dbg, 0, 64, s));
+  }
+  b.dbg = dbg;
   scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len);
   uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
   b.ws_score = reinterpret_cast<double*>(ws);
@@ -1728,6 +1935,13 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   double* th0 = reinterpret_cast<double*>(ws + (size_t)b.nchunks * Q * k * 16 + (size_t)Q * 8 +
                                           (size_t)Q * kBins * 4);
   b.th0 = nullptr;
+  // f32 path: per-query pools in the list area (cap = nchunks * k entries, never overflows)
+  b.pool_cap = b.nchunks * k;
+  b.pool_s = reinterpret_cast<float*>(ws);
+  b.pool_i = reinterpret_cast<int*>(ws + (size_t)Q * b.pool_cap * 4);
+  b.pool_n = reinterpret_cast<int*>(ws + (size_t)b.nchunks * Q * k * 16 + (size_t)Q * 8 + (size_t)Q * kBins * 4 +
+                                    (size_t)Q * 8);
+  if (f32) HQ_CHECK_HIP(hipMemsetAsync(b.pool_n, 0, sizeof(int) * Q, s));
   int rc;
   if (getenv("HQ_SCAN_NOSAMPLE") == nullptr) {
     SampleArgs sa;
@@ -1746,16 +1960,32 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   }
   rc = f32 ? scan0_dispatch<true>(ks, b, nullptr, s) : scan0_dispatch<false>(ks, b, nullptr, s);
   if (rc) return rc;
-  int mg = Q < 4096 ? Q : 4096;
-  hipLaunchKernelGGL(k_merge, dim3(mg), dim3(64), 0, s, b.ws_score, b.ws_id, (const double*)nullptr,
-                     (const int64_t*)nullptr, b.nchunks, Q, k, out_score, out_id, (double*)nullptr, (int64_t*)nullptr);
-  HQ_CHECK_LAUNCH();
+  if (f32) {
+    const int mg = Q < 8192 ? Q : 8192;
+    hipLaunchKernelGGL(k_pool_select, dim3(mg), dim3(64), 0, s, (const float*)b.pool_s, (const int*)b.pool_i,
+                       (const int*)b.pool_n, b.pool_cap, Q, k, id_base, out_score, out_id);
+    HQ_CHECK_LAUNCH();
+  }
+  if (b.expt == 3) {
+    unsigned long long h[3];
+    HQ_CHECK_HIP(hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, s));
+    HQ_CHECK_HIP(hipStreamSynchronize(s));
+    fprintf(stderr, "k_scan0f: waves %d, insert entries %llu, passing pairs %llu, list inserts %llu\n",
+            b.nqb * b.nchunks, h[0], h[1], h[2]);
+  }
+  if (!f32) {
+    int mg = Q < 4096 ? Q : 4096;
+    hipLaunchKernelGGL(k_merge, dim3(mg), dim3(64), 0, s, b.ws_score, b.ws_id, (const double*)nullptr,
+                       (const int64_t*)nullptr, b.nchunks, Q, k, out_score, out_id, (double*)nullptr,
+                       (int64_t*)nullptr);
+    HQ_CHECK_LAUNCH();
+  }
   return HQ_OK;
 }
 
 // f32 level-0 copies for the f32 scan: Z32 [N + kPad0, P0] (pad rows 0) and S32 [N + kPad0, 4] =
 // (std, mean, msq, flag bits: 1 zero variance, 2 msq outside [2^-60, 2^60], 4 pad row).  k_scan0f
-// reads up to 31 rows past a step start (the next step's prefetch) without clamping.
+// reads up to 47 rows past a step start (prefetch two steps ahead) without clamping.
 __global__ void k_pack0(const double* __restrict__ Z, const double* __restrict__ S, int64_t N, int Lp, int P0,
                         int nseg, float* __restrict__ Z32, float* __restrict__ S32) {
   const int64_t rows = N + kPad0;

@@ -251,7 +251,7 @@ def seg_prepare(idx, exc=None) -> Prepared:
     return Prepared(i2, Z, S, L)
 
 
-PAD0 = 32  # pad rows of the f32 level-0 copies (hq_mi355x.h: hq_seg_pack0_f32)
+PAD0 = 48  # pad rows of the f32 level-0 copies (hq_mi355x.h: hq_seg_pack0_f32)
 
 
 def pack0_f32(p: Prepared, exc=None) -> Prepared:

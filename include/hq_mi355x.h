@@ -174,7 +174,7 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
  * v_mfma_f32_16x16x4f32 over f32 copies of the level-0 segments and the filter in f32; passing pairs
  * are re-scored in f64.  |approx - exact| <= ~1.5e-6 (|dG| <= (m+2) 2^-24 m), so callers re-rank
  * with hq_refine_topk at eps >= 1e-5.  hq_seg_pack0_f32 builds, from hq_seg_prepare's Z and S,
- * Z32 [N + 32, hq_seg_level0_len(L)] and S32 [N + 32, 4] (32 pad rows); Sq/Sc are the f64
+ * Z32 [N + 48, hq_seg_level0_len(L)] and S32 [N + 48, 4] (48 pad rows); Sq/Sc are the f64
  * statistics of hq_seg_prepare.  Level-0 segments of up to 32 values, N < 2^31.                  */
 int hq_seg_level0_len(int L);
 int hq_seg_pack0_f32(const double* Z, const double* S, int64_t N, int L, float* Z32, float* S32,
