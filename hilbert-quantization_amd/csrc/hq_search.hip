@@ -844,8 +844,30 @@ struct SampleArgs {
   double inv_m, c1;
   int64_t stride, S;
   int64_t chunk_len; int nchunks; int nqb;
+  int K;
   unsigned int* hist;  // Q x kBins
 };
+
+constexpr int kHRow = kBins / 2 + 1;  // LDS words per query histogram (odd: conflict-free rows)
+
+// Flush the top of a wave's per-query histograms (lane = query): bins from the top down until K
+// scores are covered.  Dropping lower bins only lowers global counts, so the edge k_hist_tau finds
+// stays a valid lower bound; the global top-K scores are all counted, so it stays as tight.
+__device__ void flush_hist_top(const uint32_t* hs, int q0, int Q, int K, unsigned int* hist) {
+  const int lane = threadIdx.x;
+  const int q = q0 + lane;
+  if (q >= Q) return;
+  const uint32_t* hq = hs + lane * kHRow;
+  unsigned int cum = 0;
+  for (int w = kBins / 2 - 1; w >= 0 && cum < (unsigned)K; --w) {
+    const uint32_t v = hq[w];
+    if (v == 0u) continue;
+    const unsigned hi = v >> 16, lo = v & 0xFFFFu;  // bins 2w + 1, 2w
+    unsigned int* h = hist + (int64_t)q * kBins + 2 * w;
+    if (hi) { atomicAdd(h + 1, hi); cum += hi; }
+    if (cum < (unsigned)K && lo) { atomicAdd(h, lo); cum += lo; }
+  }
+}
 
 template <int KS>
 __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
@@ -854,7 +876,7 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
   typedef typename Z::Acc AccT;
   auto zrow = [&](const double* p64, const float*, int64_t row) -> const ZT* { return p64 + row * a.Lp; };
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t* hs = reinterpret_cast<uint32_t*>(smem);  // kQW x kBins/2, two u16 counters per word
+  uint32_t* hs = reinterpret_cast<uint32_t*>(smem);  // kQW x kHRow words, two u16 counters per word
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
   const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
   const int chunk = xcd + 8 * (slot / a.nqb);
@@ -864,7 +886,7 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
   int64_t c_end = c_begin + a.chunk_len;
   if (c_end > a.S) c_end = a.S;
   const int q0 = qb * kQW;
-  for (int i = lane; i < kQW * kBins / 2; i += 64) hs[i] = 0u;
+  for (int i = lane; i < kQW * kHRow; i += 64) hs[i] = 0u;
 
   ZT qf[4][KS];
   double qA[4], qB[4], qQ[4], qm[4];
@@ -929,22 +951,14 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
                                      : approx0((double)acc[b][r], a.c1, qA[b], qB[b], qQ[b], csd, cm, cq);
         int bin = (int)(sc * (double)kBins);
         bin = bin < 0 ? 0 : (bin >= kBins ? kBins - 1 : bin);
-        atomicAdd(&hs[(16 * b + j) * (kBins / 2) + (bin >> 1)], 1u << (16 * (bin & 1)));
+        atomicAdd(&hs[(16 * b + j) * kHRow + (bin >> 1)], 1u << (16 * (bin & 1)));
       }
     }
 #pragma unroll
     for (int t = 0; t < KS; ++t) cf[t] = cfn[t];
   }
   __syncthreads();
-  for (int i = lane; i < kQW * kBins / 2; i += 64) {
-    const uint32_t v = hs[i];
-    if (v == 0u) continue;
-    const int q = q0 + i / (kBins / 2);
-    if (q >= a.Q) continue;
-    unsigned int* h = a.hist + (int64_t)q * kBins + 2 * (i % (kBins / 2));
-    if (v & 0xFFFFu) atomicAdd(h, v & 0xFFFFu);
-    if (v >> 16) atomicAdd(h + 1, v >> 16);
-  }
+  flush_hist_top(hs, q0, a.Q, a.K, a.hist);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1367,7 +1381,7 @@ template <int KS>
 __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
   typedef ZOps<true> Z;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t* hs = reinterpret_cast<uint32_t*>(smem);  // kQW x kBins/2, two u16 counters per word
+  uint32_t* hs = reinterpret_cast<uint32_t*>(smem);  // kQW x kHRow words, two u16 counters per word
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
   const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
   const int chunk = xcd + 8 * (slot / a.nqb);
@@ -1378,7 +1392,7 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
   if (c_end > a.S) c_end = a.S;
   const int q0 = qb * kQW;
   const float c1f = (float)a.c1;
-  for (int i = lane; i < kQW * kBins / 2; i += 64) hs[i] = 0u;
+  for (int i = lane; i < kQW * kHRow; i += 64) hs[i] = 0u;
 
   float qf[4][KS];
   float qA[4], qB[4], qQ[4];
@@ -1406,6 +1420,8 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
   };
   float cf[KS];
   load_frag(c_begin, cf);
+  float cut[4] = {-1.0f, -1.0f, -1.0f, -1.0f};  // per query: scores below need no counting
+  int step = 0;
   for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
     flt4 cst[4];
 #pragma unroll
@@ -1425,30 +1441,45 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
       const bool ok = cs + 4 * g + r < c_end && __float_as_int(cst[r].w) == 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        if (!ok || !((qok >> b) & 1)) continue;
         const float G = acc[b][r];
+        // division-free test against the cut first (most pairs stop here)
+        const float R = cut[b] - fmaf(G, c1f, 0.35f);
         const float num = fmaf(G, qA[b] * cst[r].x, qB[b] * cst[r].y);
-        float t = num / (qQ[b] + cst[r].z);
+        const float den = qQ[b] + cst[r].z;
+        if (!ok || !((qok >> b) & 1) || !((R <= 0.0f) || (num >= R * den))) continue;
+        float t = num * __builtin_amdgcn_rcpf(den);
         t = t > 0.0f ? t : 0.0f;
         const float sc = fmaf(G, c1f, 0.35f) + t;
         int bin = (int)(sc * (float)kBins);
         bin = bin < 0 ? 0 : (bin >= kBins ? kBins - 1 : bin);
-        atomicAdd(&hs[(16 * b + j) * (kBins / 2) + (bin >> 1)], 1u << (16 * (bin & 1)));
+        atomicAdd(&hs[(16 * b + j) * kHRow + (bin >> 1)], 1u << (16 * (bin & 1)));
       }
     }
 #pragma unroll
     for (int t = 0; t < KS; ++t) cf[t] = cfn[t];
+    // every 8 steps: cut = lower edge of the bin holding this wave's K-th best score of each query;
+    // lower bins would never be flushed (flush_hist_top stops at K), so they need not be counted
+    if ((++step & 7) == 0) {
+      const uint32_t* hq = hs + lane * kHRow;
+      unsigned int cum = 0;
+      int e = -1;
+      for (int w = kBins / 2 - 1; w >= 0; --w) {
+        const uint32_t v = hq[w];
+        cum += v >> 16;
+        if (cum >= (unsigned)a.K) { e = 2 * w + 1; break; }
+        cum += v & 0xFFFFu;
+        if (cum >= (unsigned)a.K) { e = 2 * w; break; }
+      }
+      const float cv = e > 0 ? (float)e / (float)kBins - 1e-6f : -1.0f;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float v = __shfl(cv, 16 * b + j, 64);
+        cut[b] = v > cut[b] ? v : cut[b];
+      }
+    }
   }
   __syncthreads();
-  for (int i = lane; i < kQW * kBins / 2; i += 64) {
-    const uint32_t v = hs[i];
-    if (v == 0u) continue;
-    const int q = q0 + i / (kBins / 2);
-    if (q >= a.Q) continue;
-    unsigned int* hh = a.hist + (int64_t)q * kBins + 2 * (i % (kBins / 2));
-    if (v & 0xFFFFu) atomicAdd(hh, v & 0xFFFFu);
-    if (v >> 16) atomicAdd(hh + 1, v >> 16);
-  }
+  flush_hist_top(hs, q0, a.Q, a.K, a.hist);
 }
 
 // per-query starting threshold from the sample histogram (-inf when the sample has < K scores)
@@ -1530,83 +1561,114 @@ __global__ __launch_bounds__(64) void k_merge(const double* __restrict__ ws_scor
   }
 }
 
-// progressive search final stage (search_engine.py:284-298 fallback, :340-388 re-rank), R-way.
-// lists are sorted by (level-0 score desc, id asc); det rows are [overall, level sims...].
-__global__ void k_progressive_final(int R, int Q, int M, int W, const double* __restrict__ s0,
-                                    const int64_t* __restrict__ ids, const double* __restrict__ det,
-                                    const double* __restrict__ best, const int64_t* __restrict__ best_id,
-                                    const double* __restrict__ best_det, int K, int64_t* __restrict__ out_id,
-                                    double* __restrict__ out_det, int* __restrict__ out_count) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= Q) return;
-  constexpr int kMaxR = 16;
-  int head[kMaxR];
-  for (int r = 0; r < R; ++r) head[r] = 0;
-  // survivors: global top-M by level-0; kept as (rank, slot) pairs
-  int sr[kMaxFinal], ss[kMaxFinal];
-  int n = 0;
-  for (int j = 0; j < M; ++j) {
-    int pick = -1;
-    double ps = 0.0;
-    int64_t pid = -1;
-    for (int r = 0; r < R; ++r) {
-      if (head[r] >= M) continue;
-      const int64_t o = ((int64_t)r * Q + q) * M + head[r];
-      const int64_t id = ids[o];
-      if (id < 0) continue;
-      const double s = s0[o];
-      if (pick < 0 || better(s, id, ps, pid)) { pick = r; ps = s; pid = id; }
+// progressive search final stage (search_engine.py:284-298 fallback, :340-388 re-rank), R-way,
+// one wave per query.  lists are sorted by (level-0 score desc, id asc); det rows are
+// [overall, level sims...].  Survivors = global top-M of the R lists (merged on (score, id), as the
+// reference's stable sort over the pool order); if none, the first arg-max of the level-0 score;
+// then a stable sort by overall score (ties keep the level-0 order) and the first K.
+__device__ __forceinline__ bool wave_better(double s, int64_t id, double s2, int64_t id2) {
+  return id >= 0 && (id2 < 0 || s > s2 || (s == s2 && id < id2));
+}
+
+__global__ __launch_bounds__(64) void k_progressive_final(int R, int Q, int M, int W, const double* __restrict__ s0,
+                                                          const int64_t* __restrict__ ids,
+                                                          const double* __restrict__ det,
+                                                          const double* __restrict__ best,
+                                                          const int64_t* __restrict__ best_id,
+                                                          const double* __restrict__ best_det, int K,
+                                                          int64_t* __restrict__ out_id, double* __restrict__ out_det,
+                                                          int* __restrict__ out_count) {
+  __shared__ int sel[kMaxFinal];  // survivor i -> (list r << 16) | slot
+  const int lane = threadIdx.x;
+  for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    // ---- R-way merge: lane r < R follows list r's head ----
+    int h = 0;
+    double hs = -__builtin_huge_val();
+    int64_t hid = -1;
+    auto load_head = [&]() {
+      hs = -__builtin_huge_val();
+      hid = -1;
+      if (lane < R && h < M) {
+        const int64_t o = ((int64_t)lane * Q + q) * M + h;
+        hid = ids[o];
+        if (hid >= 0) hs = s0[o];
+      }
+    };
+    load_head();
+    int n = 0;
+    for (; n < M; ++n) {
+      double bs = hs;
+      int64_t bid = hid;
+      int bl = lane;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double s2 = __shfl_xor(bs, o, 64);
+        const int64_t i2 = __shfl_xor(bid, o, 64);
+        const int l2 = __shfl_xor(bl, o, 64);
+        if (wave_better(s2, i2, bs, bid)) { bs = s2; bid = i2; bl = l2; }
+      }
+      if (bid < 0) break;
+      const int hb = __shfl(h, bl, 64);
+      if (lane == 0) sel[n] = (bl << 16) | hb;
+      if (lane == bl) {
+        h = hb + 1;
+        load_head();
+      }
     }
-    if (pick < 0) break;
-    sr[n] = pick;
-    ss[n] = head[pick];
-    ++n;
-    head[pick]++;
+    __syncthreads();
+    const double* rowbase = det;
+    int64_t fb_id = -1;
+    if (n == 0) {
+      // none passed the threshold: keep the first arg-max of the level-0 score (:295-298)
+      double bs = -__builtin_huge_val();
+      int64_t bid = -1;
+      int bl = lane;
+      if (lane < R) {
+        bid = best_id[(int64_t)lane * Q + q];
+        if (bid >= 0) bs = best[(int64_t)lane * Q + q];
+      }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double s2 = __shfl_xor(bs, o, 64);
+        const int64_t i2 = __shfl_xor(bid, o, 64);
+        const int l2 = __shfl_xor(bl, o, 64);
+        if (wave_better(s2, i2, bs, bid)) { bs = s2; bid = i2; bl = l2; }
+      }
+      if (bid >= 0) {
+        n = 1;
+        fb_id = bid;
+        rowbase = best_det;
+        if (lane == 0) sel[0] = bl << 16;
+      }
+      __syncthreads();
+    }
+    // ---- stable sort of the survivors by overall score ----
+    const int outn = n < K ? n : K;
+    // row of survivor i in rowbase: list rows (r Q + q) M + slot, or the fallback's best row r Q + q
+    auto row_of = [&](int v) -> int64_t {
+      const int64_t rq = (int64_t)(v >> 16) * Q + q;
+      return fb_id >= 0 ? rq : rq * M + (v & 0xFFFF);
+    };
+    for (int i = lane; i < n; i += 64) {
+      const int64_t oi = row_of(sel[i]);
+      const double ovi = rowbase[oi * W];
+      int rank = 0;
+      for (int jj = 0; jj < n; ++jj) {
+        const double ovj = rowbase[row_of(sel[jj]) * W];
+        rank += (ovj > ovi || (ovj == ovi && jj < i)) ? 1 : 0;
+      }
+      if (rank < K) {
+        out_id[(int64_t)q * K + rank] = fb_id >= 0 ? fb_id : ids[oi];
+        for (int w = 0; w < W; ++w) out_det[((int64_t)q * K + rank) * W + w] = rowbase[oi * W + w];
+      }
+    }
+    for (int i = outn + lane; i < K; i += 64) {
+      out_id[(int64_t)q * K + i] = -1;
+      for (int w = 0; w < W; ++w) out_det[((int64_t)q * K + i) * W + w] = 0.0;
+    }
+    if (lane == 0) out_count[q] = outn;
+    __syncthreads();
   }
-  const double* rowp[kMaxFinal];
-  int64_t idp[kMaxFinal];
-  if (n == 0) {
-    // none passed the threshold: keep the first arg-max of the level-0 score (:295-298)
-    int pick = -1;
-    double ps = 0.0;
-    int64_t pid = -1;
-    for (int r = 0; r < R; ++r) {
-      const int64_t id = best_id[(int64_t)r * Q + q];
-      if (id < 0) continue;
-      const double s = best[(int64_t)r * Q + q];
-      if (pick < 0 || better(s, id, ps, pid)) { pick = r; ps = s; pid = id; }
-    }
-    if (pick >= 0) {
-      rowp[0] = best_det + ((int64_t)pick * Q + q) * W;
-      idp[0] = pid;
-      n = 1;
-    }
-  } else {
-    for (int i = 0; i < n; ++i) {
-      const int64_t o = ((int64_t)sr[i] * Q + q) * M + ss[i];
-      rowp[i] = det + o * W;
-      idp[i] = ids[o];
-    }
-  }
-  // stable sort by overall score desc (insertion sort keeps the level-0 order on ties)
-  for (int i = 1; i < n; ++i) {
-    const double* rp = rowp[i];
-    const int64_t ip = idp[i];
-    int j = i;
-    while (j > 0 && rowp[j - 1][0] < rp[0]) {
-      rowp[j] = rowp[j - 1];
-      idp[j] = idp[j - 1];
-      --j;
-    }
-    rowp[j] = rp;
-    idp[j] = ip;
-  }
-  const int outn = n < K ? n : K;
-  for (int i = 0; i < K; ++i) {
-    out_id[(int64_t)q * K + i] = i < outn ? idp[i] : -1;
-    for (int w = 0; w < W; ++w) out_det[((int64_t)q * K + i) * W + w] = i < outn ? rowp[i][w] : 0.0;
-  }
-  out_count[q] = outn;
 }
 
 
@@ -1833,13 +1895,15 @@ static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
 }
 
 // sample pass: stride 16 once the corpus is large, else a sample of ~4096 rows (the whole corpus
-// below that); chunks of <= 65520 rows (u16 histogram counters), ~2048 waves
+// below that); chunks of <= 65520 rows (u16 histogram counters), ~1024 waves (a wave has a fixed
+// cost: histogram init and flush)
 static void sample_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, int& nqb, int& nchunks,
                             int64_t& chunk_len) {
   stride = N >= 16 * 4096 ? 16 : (N / 4096 > 1 ? N / 4096 : 1);
   S = (N + stride - 1) / stride;
   nqb = (Q + kQW - 1) / kQW;
-  int64_t target = (2048 + nqb - 1) / nqb;
+  const int waves = getenv("HQ_SAMPLE_WAVES") ? atoi(getenv("HQ_SAMPLE_WAVES")) : 1024;
+  int64_t target = (waves + nqb - 1) / nqb;
   const int64_t max_chunks = (S + kCS - 1) / kCS;
   if (target > max_chunks) target = max_chunks;
   if (target < (S + 65519) / 65520) target = (S + 65519) / 65520;
@@ -1850,7 +1914,7 @@ static void sample_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, int& 
 
 template <int KS, bool F32>
 static int launch_sample(const SampleArgs& a, hipStream_t s) {
-  const size_t lds = (size_t)kQW * kBins / 2 * 4;
+  const size_t lds = (size_t)kQW * kHRow * 4;
   const void* fn = F32 ? (const void*)k_sample_histf<KS> : (const void*)k_sample_hist<KS>;
   HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   if constexpr (F32) hipLaunchKernelGGL((k_sample_histf<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
@@ -1950,6 +2014,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     sa.Lp = b.Lp; sa.nseg = b.nseg; sa.P0 = b.P0; sa.inv_m = b.inv_m; sa.c1 = b.c1;
     sample_geometry(Q, N, sa.stride, sa.S, sa.nqb, sa.nchunks, sa.chunk_len);
     sa.hist = hist;
+    sa.K = k;
     HQ_CHECK_HIP(hipMemsetAsync(hist, 0, sizeof(unsigned int) * kBins * Q, s));
     rc = f32 ? scan0_dispatch<true>(ks, b, &sa, s) : scan0_dispatch<false>(ks, b, &sa, s);
     if (rc) return rc;
@@ -2232,8 +2297,9 @@ int hq_progressive_final(int R, int Q, int M, int nseg, const double* s0, const 
   if (!s0 || !ids || !det || !best || !best_id || !best_det || !out_id || !out_det || !out_count)
     return fail(HQ_E_INVALID, "null buffer");
   const int W = 1 + nseg;
-  hipLaunchKernelGGL(k_progressive_final, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, R, Q, M, W, s0, ids,
-                     det, best, best_id, best_det, K, out_id, out_det, out_count);
+  const int grid = Q < 8192 ? Q : 8192;
+  hipLaunchKernelGGL(k_progressive_final, dim3(grid), dim3(64), 0, (hipStream_t)stream, R, Q, M, W, s0, ids, det,
+                     best, best_id, best_det, K, out_id, out_det, out_count);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
