@@ -529,7 +529,7 @@ struct Scan0Args {
   int64_t chunk_len; int nchunks; int nqb;
   double* ws_score; int64_t* ws_id; unsigned long long* gtau;
   float* pool_s; int* pool_i; int* pool_n; int pool_cap;  // k_scan0f: per-query candidate pools
-  int expt;          // performance experiments (HQ_SCAN_EXPT): 1 no filter, 2 no insert, 3 count
+  int expt;          // HQ_SCAN_EXPT=3: count insert-path entries, passing pairs and list merges
   unsigned long long* dbg;  // expt 3: [entries, passing pairs, list inserts]
 };
 
@@ -972,7 +972,7 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
 // scored from the f64 statistics.
 // ------------------------------------------------------------------------------------------------
 constexpr float kMarginF = 3e-5f;
-constexpr int kPad0 = 3 * kCS;  // pad rows of the f32 copies (hq_seg_pack0_f32)
+constexpr int kPad0 = 3 * kCS;  // pad rows of the f32 copies (hq_seg_pack0_f32); reads reach cs + 31
 
 __device__ __forceinline__ float lower_f32(double x) {  // largest float <= x (x finite or +-inf)
   float f = (float)x;
@@ -985,7 +985,11 @@ __device__ __forceinline__ float lower_f32(double x) {  // largest float <= x (x
 __device__ __forceinline__ int shr1_f32i(float v) { return shr1_i32(__float_as_int(v)); }
 
 template <int KS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_scan0f(Scan0Args a) {
+#ifndef HQ_SCAN0F_WAVES
+#define HQ_SCAN0F_WAVES 2
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WAVES, HQ_SCAN0F_WAVES))) void k_scan0f(
+    Scan0Args a) {
   typedef ZOps<true> Z;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   float* ls = reinterpret_cast<float*>(smem);         // kQW x K approx scores
@@ -1135,7 +1139,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   // with the division), f64 statistics for flagged pairs
   auto insert_half = [&](const int h, const flt4* acc, const flt4* cst, const int64_t cs, const int bits) {
     if (a.expt == 3 && lane == 0) atomicAdd(a.dbg, 1ull);
-    if (a.expt == 4) return;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -1166,7 +1169,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             s = (float)v;
           }
         }
-        const bool ok = pb && s >= thl[b] && a.expt != 5;
+        const bool ok = pb && s >= thl[b];
         if (a.expt == 3 && lane == 0) atomicAdd(a.dbg + 1, (unsigned long long)__popcll(__ballot(ok)));
         const int qi = 16 * b + j;
         const int id = (int)(cs + 4 * g + r);
@@ -1201,11 +1204,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
   };
 
-  // software pipeline as in k_scan0, fragments two steps ahead, statistics one step ahead
-  float cf[KS], cf1[KS];
+  // ask the scheduler to spread the filter's VALU work between the other half's 16 MFMAs
+  auto interleave = [&]() {
+#ifndef HQ_NO_INTERLEAVE
+#pragma unroll
+    for (int i = 0; i < 2 * KS; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // 6 VALU
+    }
+#endif
+  };
+  // software pipeline as in k_scan0: next step's fragment and statistics in flight
+  float cf[KS];
   flt4 cst[4];
   load_frag(c_begin, cf);
-  load_frag(c_begin + kCS, cf1);
   load_stats(c_begin, cst);
   flt4 acc0[2], acc1[2];
   mfma_half(0, cf, acc0);
@@ -1213,26 +1225,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   int step = 0;
   for (int64_t cs = c_begin; cs < c_end; cs += kCS, ++step) {
     const int rem = (int)(c_end - cs);
-    float cf2[KS];
+    float cf1[KS];
     flt4 cstn[4];
-    load_frag(cs + 2 * kCS, cf2);
+    load_frag(cs + kCS, cf1);
     load_stats(cs + kCS, cstn);
     mfma_half(1, cf, acc1);
-    int bits0 = a.expt == 1 ? 0 : filter_half(0, acc0, cst, rem);
-    if (a.expt == 2) bits0 = __ballot(bits0 != 0) ? 0 : 0;
+    const int bits0 = filter_half(0, acc0, cst, rem);
+    interleave();
     if (__ballot(bits0 != 0)) insert_half(0, acc0, cst, cs, bits0);
     mfma_half(0, cf1, acc0);
-    int bits1 = a.expt == 1 ? 0 : filter_half(1, acc1, cst, rem);
-    if (a.expt == 2) bits1 = __ballot(bits1 != 0) ? 0 : 0;
+    const int bits1 = filter_half(1, acc1, cst, rem);
+    interleave();
     if (__ballot(bits1 != 0)) insert_half(1, acc1, cst, cs, bits1);
-    if (a.expt == 1) {  // keep the accumulators live
-      if (acc0[0][0] == 12345.0f && acc1[1][3] == 54321.0f) ls[0] = 1.0f;
-    }
 #pragma unroll
-    for (int t = 0; t < KS; ++t) {
-      cf[t] = cf1[t];
-      cf1[t] = cf2[t];
-    }
+    for (int t = 0; t < KS; ++t) cf[t] = cf1[t];
 #pragma unroll
     for (int r = 0; r < 4; ++r) cst[r] = cstn[r];
     if ((step & 3) == 0) {

@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhq_mi355x.so")
+LIB_PATH = os.environ.get("HQ_LIB_VARIANT") or os.path.join(_HERE, "libhq_mi355x.so")  # variant: A/B builds
 
 HQ_OK = 0
 HQ_E_INVALID = -1

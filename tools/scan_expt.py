@@ -17,9 +17,7 @@ g = torch.Generator(device="cuda").manual_seed(5)
 C = torch.randn((N, 64), generator=g, device="cuda", dtype=torch.float64).cumsum(1) * 0.1
 corpus = IndexCorpus(C)
 qp = corpus.prepare_queries(C[:Q] + 0.01 * torch.randn((Q, 64), generator=g, device="cuda", dtype=torch.float64))
-VARIANTS = [("count", {"HQ_SCAN_EXPT": "3"}), ("default", {}), ("no-filter", {"HQ_SCAN_EXPT": "1"}),
-                  ("no-insert", {"HQ_SCAN_EXPT": "2"}), ("entry-only", {"HQ_SCAN_EXPT": "4"}),
-                  ("score-only", {"HQ_SCAN_EXPT": "5"}),
+VARIANTS = [("count", {"HQ_SCAN_EXPT": "3"}), ("default", {}),
                   ("no-sample", {"HQ_SCAN_NOSAMPLE": "1"}), ("f64", {"HQ_SCAN_F64": "1"})]
 only = os.environ.get("SCAN_EXPT_ONLY")
 for name, env in VARIANTS:
