@@ -518,8 +518,9 @@ constexpr int kCS = 16;  // candidates per step
 struct Scan0Args {
   const double* Zq; const double* Sq; int Q;
   const double* Zc; const double* Sc; int64_t N;
-  const float* Zq32; const float* Zc32;  // f32 kernels: level-0 segments, rows of P0 (+kPad0 pad rows)
-  const float* Sq32; const float* Sc32;  // f32 kernels: level-0 (std, mean, msq, flag bits) per row
+  const float* Zq32; const float* Zc32;  // f64 kernels: unused
+  const _Float16* Zq16; const _Float16* Zc16;  // split kernels: level-0 rows [hi 32 | lo 32] (+kPad0 rows)
+  const float* Sq32; const float* Sc32;  // split kernels: level-0 (std, mean, msq, flag bits) per row
   int Lp, nseg, P0;
   double inv_m, c1;  // 1/m, 0.35/m
   int K;
@@ -571,8 +572,7 @@ __device__ __forceinline__ double const0(bool zq, bool zc, double qm, double cm)
 
 typedef float flt4 __attribute__((ext_vector_type(4)));
 
-// Z operand types of the two contraction precisions: f64 (v_mfma_f64_16x16x4f64, C/D row
-// (lane>>4) + 4r) and f32 (v_mfma_f32_16x16x4f32, C/D row 4(lane>>4) + r).
+// Z operand type of the f64 contraction (v_mfma_f64_16x16x4f64, C/D row (lane>>4) + 4r).
 template <bool F32> struct ZOps;
 template <> struct ZOps<false> {
   typedef double T;
@@ -581,14 +581,6 @@ template <> struct ZOps<false> {
   static __device__ __forceinline__ int row(int g, int r) { return g + 4 * r; }
   static __device__ __forceinline__ const T* zq(const Scan0Args& a, int64_t q) { return a.Zq + q * a.Lp; }
   static __device__ __forceinline__ const T* zc(const Scan0Args& a, int64_t c) { return a.Zc + c * a.Lp; }
-};
-template <> struct ZOps<true> {
-  typedef float T;
-  typedef flt4 Acc;
-  static __device__ __forceinline__ Acc mfma(T a, T b, Acc c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
-  static __device__ __forceinline__ int row(int g, int r) { return 4 * g + r; }
-  static __device__ __forceinline__ const T* zq(const Scan0Args& a, int64_t q) { return a.Zq32 + q * a.P0; }
-  static __device__ __forceinline__ const T* zc(const Scan0Args& a, int64_t c) { return a.Zc32 + c * a.P0; }
 };
 
 template <int KS>
@@ -839,6 +831,7 @@ struct SampleArgs {
   const double* Zq; const double* Sq; int Q;
   const double* Zc; const double* Sc; int64_t N;
   const float* Zq32; const float* Zc32;
+  const _Float16* Zq16; const _Float16* Zc16;
   const float* Sq32; const float* Sc32;
   int Lp, nseg, P0;
   double inv_m, c1;
@@ -962,16 +955,22 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// f32 level-0 scan (default): v_mfma_f32_16x16x4f32 on f32 copies of the level-0 segments, an f32
-// division-free filter and f32 list scores.  Error budget: |G_f32 - G| <= (m+2) 2^-24 sum|zq zc| <=
-// (m+2) 2^-24 m (Cauchy-Schwarz, sum z^2 = m), i.e. <= 6.5e-5 at m = 32, so the score moves by
-// <= 0.02 * 6.5e-5 ~ 1.3e-6; the f32 epilogue adds < 1e-6 (each term of num is bounded by
-// 0.6 rho_q rho_c <= 0.3 den).  The filter passes every pair within kMarginF of the threshold, and
-// list scores are within ~3e-6 of the exact ones (callers re-rank with eps = 1e-5).  Vectors whose
+// Split-f16 level-0 scan (default).  On gfx950 the f32/f64 MFMAs run on the vector ALUs (they never
+// co-execute with VALU work: SQ_VALU_MFMA_COEXEC_CYCLES = 0), so the contraction runs on the matrix
+// core instead: each normalised value z = hi + lo with hi = f16(z), lo = f16(z - hi), and
+//   G ~= hi_q.hi_c + hi_q.lo_c + lo_q.hi_c   (three v_mfma_f32_16x16x32_f16, f32 accumulation)
+// for 16 candidates x 16 queries x K = 32 (the level-0 segment zero-padded to 32).  Error budget:
+// split and dropped lo.lo <= 3 2^-22 |zq||zc| per term, f32 accumulation of 96 products <= 96 2^-24
+// sum|.|, with sum|zq zc| <= m (Cauchy-Schwarz, sum z^2 = m): |dG| <= 2.1e-4 at m = 32; the score
+// moves by <= (0.65 / m) |dG| <= 4.3e-6; the f32 epilogue adds < 1e-6 (each term of num is bounded
+// by 0.6 rho_q rho_c <= 0.3 den).  The filter passes every pair within kMarginF of the threshold;
+// list scores are within ~5.5e-6 of the exact ones (callers re-rank with eps = 2e-5).  Vectors whose
 // level-0 statistics are zero-variance or outside [2^-60, 2^60] (f32-unsafe) carry a flag and are
 // scored from the f64 statistics.
 // ------------------------------------------------------------------------------------------------
-constexpr float kMarginF = 3e-5f;
+constexpr float kMarginF = 6e-5f;
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+constexpr int kZ16Row = 64;  // halfs per split row: hi[32] then lo[32]
 constexpr int kPad0 = 3 * kCS;  // pad rows of the f32 copies (hq_seg_pack0_f32); reads reach cs + 31
 
 __device__ __forceinline__ float lower_f32(double x) {  // largest float <= x (x finite or +-inf)
@@ -984,13 +983,11 @@ __device__ __forceinline__ float lower_f32(double x) {  // largest float <= x (x
 }
 __device__ __forceinline__ int shr1_f32i(float v) { return shr1_i32(__float_as_int(v)); }
 
-template <int KS>
 #ifndef HQ_SCAN0F_WAVES
 #define HQ_SCAN0F_WAVES 2
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WAVES, HQ_SCAN0F_WAVES))) void k_scan0f(
     Scan0Args a) {
-  typedef ZOps<true> Z;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   float* ls = reinterpret_cast<float*>(smem);         // kQW x K approx scores
   int* li = reinterpret_cast<int*>(ls + kQW * a.K);   // kQW x K corpus rows
@@ -1008,7 +1005,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WA
   int cntr[4] = {0, 0, 0, 0};  // pairs offered to the list of query 16b + j (same in the 4 lanes g)
 
   // queries: fragments, f32 constants, list thresholds (f32, exact list values)
-  float qf[4][KS];
+  half8 qh[4], ql[4];  // query fragments: k range [8g, 8g + 8) of the hi and lo halves
   float qA[4], qB[4], qQ[4], thl[4];
   int qsp = 0;  // bit b: query 16b + j is flagged (zero variance / f32-unsafe)
   int qvb = 0;  // bit b: query 16b + j exists
@@ -1017,9 +1014,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WA
     const int q = q0 + 16 * b + j;
     const bool v = q < a.Q;
     const int qq = v ? q : 0;
-    const float* zr = a.Zq32 + (int64_t)qq * a.P0 + g * KS;
-#pragma unroll
-    for (int t = 0; t < KS; ++t) qf[b][t] = v ? zr[t] : 0.0f;
+    const _Float16* zr = a.Zq16 + (int64_t)qq * kZ16Row + 8 * g;
+    qh[b] = *reinterpret_cast<const half8*>(zr);
+    ql[b] = *reinterpret_cast<const half8*>(zr + 32);
     const flt4 st = *reinterpret_cast<const flt4*>(a.Sq32 + (int64_t)qq * 4);
     qA[b] = (float)(0.6 * a.inv_m) * st.x;
     qB[b] = 0.6f * st.y;
@@ -1036,34 +1033,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WA
   }
   const bool myq = q0 + lane < a.Q;
 
-  // candidate rows are padded by 16 (hq_seg_pack0_f32): no clamping, rows past c_end are masked
-  auto load_frag = [&](int64_t cs, float* dst) {
-    const float* p = a.Zc32 + (cs + j) * a.P0 + g * KS;
-    if constexpr ((KS % 4) == 0) {
-#pragma unroll
-      for (int t = 0; t < KS; t += 4) {
-        const flt4 v = *reinterpret_cast<const flt4*>(p + t);
-        dst[t] = v.x; dst[t + 1] = v.y; dst[t + 2] = v.z; dst[t + 3] = v.w;
-      }
-    } else {
-#pragma unroll
-      for (int t = 0; t < KS; ++t) dst[t] = p[t];
-    }
+  // candidate rows are padded (kPad0, hq_seg_pack0_split): no clamping, rows past c_end are masked
+  auto load_frag = [&](int64_t cs, half8* dst) {
+    const _Float16* p = a.Zc16 + (cs + j) * kZ16Row + 8 * g;
+    dst[0] = *reinterpret_cast<const half8*>(p);
+    dst[1] = *reinterpret_cast<const half8*>(p + 32);
   };
   auto load_stats = [&](int64_t cs, flt4* dst) {
     const flt4* p = reinterpret_cast<const flt4*>(a.Sc32) + cs + 4 * g;
 #pragma unroll
     for (int r = 0; r < 4; ++r) dst[r] = p[r];
   };
-  // two accumulation chains interleaved (dependent MFMAs two issues apart: no RAW stall)
-  auto mfma_half = [&](const int h, const float* f, flt4* acc) {
+  // G of two 16-query blocks: hi.hi + hi.lo + lo.hi, two accumulation chains interleaved
+  auto mfma_half = [&](const int h, const half8* f, flt4* acc) {
     acc[0] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
     acc[1] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int t = 0; t < KS; ++t) {
-      acc[0] = Z::mfma(f[t], qf[2 * h][t], acc[0]);
-      acc[1] = Z::mfma(f[t], qf[2 * h + 1][t], acc[1]);
-    }
+    for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[0], qh[2 * h + u], acc[u], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[0], ql[2 * h + u], acc[u], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[1], qh[2 * h + u], acc[u], 0, 0, 0);
   };
   // branch-free f32 filter of one half; bit 4u + r = pass of pair (query 16(2h+u)+j, row 4g+r)
   auto filter_half = [&](const int h, const flt4* acc, const flt4* cst, const int rem) -> int {
@@ -1204,18 +1194,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WA
       }
   };
 
-  // ask the scheduler to spread the filter's VALU work between the other half's 16 MFMAs
-  auto interleave = [&]() {
-#ifndef HQ_NO_INTERLEAVE
-#pragma unroll
-    for (int i = 0; i < 2 * KS; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // 6 VALU
-    }
-#endif
-  };
   // software pipeline as in k_scan0: next step's fragment and statistics in flight
-  float cf[KS];
+  half8 cf[2];
   flt4 cst[4];
   load_frag(c_begin, cf);
   load_stats(c_begin, cst);
@@ -1225,20 +1205,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WA
   int step = 0;
   for (int64_t cs = c_begin; cs < c_end; cs += kCS, ++step) {
     const int rem = (int)(c_end - cs);
-    float cf1[KS];
+    half8 cf1[2];
     flt4 cstn[4];
     load_frag(cs + kCS, cf1);
     load_stats(cs + kCS, cstn);
     mfma_half(1, cf, acc1);
     const int bits0 = filter_half(0, acc0, cst, rem);
-    interleave();
     if (__ballot(bits0 != 0)) insert_half(0, acc0, cst, cs, bits0);
     mfma_half(0, cf1, acc0);
     const int bits1 = filter_half(1, acc1, cst, rem);
-    interleave();
     if (__ballot(bits1 != 0)) insert_half(1, acc1, cst, cs, bits1);
-#pragma unroll
-    for (int t = 0; t < KS; ++t) cf[t] = cf1[t];
+    cf[0] = cf1[0];
+    cf[1] = cf1[1];
 #pragma unroll
     for (int r = 0; r < 4; ++r) cst[r] = cstn[r];
     if ((step & 3) == 0) {
@@ -1383,9 +1361,7 @@ __global__ __launch_bounds__(64) void k_pool_select(const float* __restrict__ po
 
 // f32 sample pass: f32 scores of a strided subset into per-query histograms; flagged pairs are not
 // counted (which only lowers the bound)
-template <int KS>
 __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
-  typedef ZOps<true> Z;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* hs = reinterpret_cast<uint32_t*>(smem);  // kQW x kHRow words, two u16 counters per word
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
@@ -1400,7 +1376,7 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
   const float c1f = (float)a.c1;
   for (int i = lane; i < kQW * kHRow; i += 64) hs[i] = 0u;
 
-  float qf[4][KS];
+  half8 qh[4], ql[4];
   float qA[4], qB[4], qQ[4];
   int qok = 0;  // bit b: valid, unflagged query
 #pragma unroll
@@ -1408,9 +1384,9 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
     const int q = q0 + 16 * b + j;
     const bool v = q < a.Q;
     const int qq = v ? q : 0;
-    const float* zr = a.Zq32 + (int64_t)qq * a.P0 + g * KS;
-#pragma unroll
-    for (int t = 0; t < KS; ++t) qf[b][t] = zr[t];
+    const _Float16* zr = a.Zq16 + (int64_t)qq * kZ16Row + 8 * g;
+    qh[b] = *reinterpret_cast<const half8*>(zr);
+    ql[b] = *reinterpret_cast<const half8*>(zr + 32);
     const flt4 st = *reinterpret_cast<const flt4*>(a.Sq32 + (int64_t)qq * 4);
     qA[b] = (float)(0.6 * a.inv_m) * st.x;
     qB[b] = 0.6f * st.y;
@@ -1419,12 +1395,12 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
   }
   __syncthreads();
   auto row_of = [&](int64_t i) -> int64_t { return (i < a.S ? i : a.S - 1) * a.stride; };
-  auto load_frag = [&](int64_t cs, float* dst) {
-    const float* p = a.Zc32 + row_of(cs + j) * a.P0 + g * KS;
-#pragma unroll
-    for (int t = 0; t < KS; ++t) dst[t] = p[t];
+  auto load_frag = [&](int64_t cs, half8* dst) {
+    const _Float16* p = a.Zc16 + row_of(cs + j) * kZ16Row + 8 * g;
+    dst[0] = *reinterpret_cast<const half8*>(p);
+    dst[1] = *reinterpret_cast<const half8*>(p + 32);
   };
-  float cf[KS];
+  half8 cf[2];
   load_frag(c_begin, cf);
   float cut[4] = {-1.0f, -1.0f, -1.0f, -1.0f};  // per query: scores below need no counting
   int step = 0;
@@ -1432,15 +1408,15 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
     flt4 cst[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) cst[r] = reinterpret_cast<const flt4*>(a.Sc32)[row_of(cs + 4 * g + r)];
-    float cfn[KS];
+    half8 cfn[2];
     load_frag(cs + kCS, cfn);
     flt4 acc[4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[b] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[0], qh[b], flt4{0, 0, 0, 0}, 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < KS; ++t)
+    for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[0], ql[b], acc[b], 0, 0, 0);
 #pragma unroll
-      for (int b = 0; b < 4; ++b) acc[b] = Z::mfma(cf[t], qf[b][t], acc[b]);  // 4 interleaved chains
+    for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[1], qh[b], acc[b], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1461,8 +1437,8 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
         atomicAdd(&hs[(16 * b + j) * kHRow + (bin >> 1)], 1u << (16 * (bin & 1)));
       }
     }
-#pragma unroll
-    for (int t = 0; t < KS; ++t) cf[t] = cfn[t];
+    cf[0] = cfn[0];
+    cf[1] = cfn[1];
     // every 8 steps: cut = lower edge of the bin holding this wave's K-th best score of each query;
     // lower bins would never be flushed (flush_hist_top stops at K), so they need not be counted
     if ((++step & 7) == 0) {
@@ -1921,9 +1897,9 @@ static void sample_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, int& 
 template <int KS, bool F32>
 static int launch_sample(const SampleArgs& a, hipStream_t s) {
   const size_t lds = (size_t)kQW * kHRow * 4;
-  const void* fn = F32 ? (const void*)k_sample_histf<KS> : (const void*)k_sample_hist<KS>;
+  const void* fn = F32 ? (const void*)k_sample_histf : (const void*)k_sample_hist<KS>;
   HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  if constexpr (F32) hipLaunchKernelGGL((k_sample_histf<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
+  if constexpr (F32) hipLaunchKernelGGL(k_sample_histf, dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
   else hipLaunchKernelGGL((k_sample_hist<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
@@ -1933,8 +1909,8 @@ template <int KS, bool F32>
 static int launch_scan0(const Scan0Args& a, hipStream_t s) {
   if constexpr (F32) {
     const size_t lds = (size_t)kQW * a.K * 8 + (size_t)kQW * 4;
-    HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_scan0f<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((k_scan0f<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
+    HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_scan0f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_scan0f, dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
     HQ_CHECK_LAUNCH();
     return HQ_OK;
   }
@@ -1975,13 +1951,13 @@ static int scan0_dispatch(int ks, const Scan0Args& b, const SampleArgs* sa, hipS
 }
 
 // level-0 scan (sample pass -> thresholds -> k_scan0 -> k_merge); f32 selects the f32 contraction
-static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const float* Zq32, const float* Sq32,
-                     int Q, const double* Zc, const double* Sc, const float* Zc32, const float* Sc32, int64_t N,
+static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const _Float16* Zq16, const float* Sq32,
+                     int Q, const double* Zc, const double* Sc, const _Float16* Zc16, const float* Sc32, int64_t N,
                      const SegInfo& si, int k, double threshold, int thr_mode, int64_t id_base, void* workspace,
                      double* out_score, int64_t* out_id, hipStream_t s) {
   Scan0Args b;
   b.Zq = Zq; b.Sq = Sq; b.Q = Q; b.Zc = Zc; b.Sc = Sc; b.N = N;
-  b.Zq32 = Zq32; b.Zc32 = Zc32; b.Sq32 = Sq32; b.Sc32 = Sc32;
+  b.Zq32 = nullptr; b.Zc32 = nullptr; b.Zq16 = Zq16; b.Zc16 = Zc16; b.Sq32 = Sq32; b.Sc32 = Sc32;
   b.Lp = si.Lp; b.nseg = si.nseg; b.P0 = si.plen[0];
   b.inv_m = si.inv_m[0];
   b.c1 = 0.35 * si.inv_m[0];
@@ -2016,7 +1992,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   if (getenv("HQ_SCAN_NOSAMPLE") == nullptr) {
     SampleArgs sa;
     sa.Zq = Zq; sa.Sq = Sq; sa.Q = Q; sa.Zc = Zc; sa.Sc = Sc; sa.N = N;
-    sa.Zq32 = Zq32; sa.Zc32 = Zc32; sa.Sq32 = Sq32; sa.Sc32 = Sc32;
+    sa.Zq32 = nullptr; sa.Zc32 = nullptr; sa.Zq16 = Zq16; sa.Zc16 = Zc16; sa.Sq32 = Sq32; sa.Sc32 = Sc32;
     sa.Lp = b.Lp; sa.nseg = b.nseg; sa.P0 = b.P0; sa.inv_m = b.inv_m; sa.c1 = b.c1;
     sample_geometry(Q, N, sa.stride, sa.S, sa.nqb, sa.nchunks, sa.chunk_len);
     sa.hist = hist;
@@ -2054,17 +2030,21 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   return HQ_OK;
 }
 
-// f32 level-0 copies for the f32 scan: Z32 [N + kPad0, P0] (pad rows 0) and S32 [N + kPad0, 4] =
-// (std, mean, msq, flag bits: 1 zero variance, 2 msq outside [2^-60, 2^60], 4 pad row).  k_scan0f
-// reads up to 47 rows past a step start (prefetch two steps ahead) without clamping.
+// Split-f16 level-0 copies for the default scan: Z16 [N + kPad0, 64] = (hi[32], lo[32]) of the
+// level-0 segment zero-padded to 32, and S32 [N + kPad0, 4] = (std, mean, msq, flag bits: 1 zero
+// variance, 2 msq outside [2^-60, 2^60], 4 pad row).  k_scan0f reads up to 31 rows past a step start.
 __global__ void k_pack0(const double* __restrict__ Z, const double* __restrict__ S, int64_t N, int Lp, int P0,
-                        int nseg, float* __restrict__ Z32, float* __restrict__ S32) {
+                        int nseg, _Float16* __restrict__ Z16, float* __restrict__ S32) {
   const int64_t rows = N + kPad0;
-  const int64_t total = rows * P0;
+  const int64_t total = rows * 32;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = t / P0;
-    const int c = (int)(t % P0);
-    Z32[t] = r < N ? (float)Z[r * Lp + c] : 0.0f;
+    const int64_t r = t / 32;
+    const int c = (int)(t % 32);
+    const double z = (r < N && c < P0) ? Z[r * Lp + c] : 0.0;
+    const _Float16 hi = (_Float16)z;
+    const _Float16 lo = (_Float16)(z - (double)hi);
+    Z16[r * kZ16Row + c] = hi;
+    Z16[r * kZ16Row + 32 + c] = lo;
     if (c == 0) {
       float* o = S32 + r * 4;
       if (r < N) {
@@ -2239,24 +2219,26 @@ int hq_seg_level0_len(int L) {
   return si.nseg > 0 ? si.plen[0] : 0;
 }
 
-int hq_seg_pack0_f32(const double* Z, const double* S, int64_t N, int L, float* Z32, float* S32, hq_stream_t stream) {
+int hq_seg_pack0_split(const double* Z, const double* S, int64_t N, int L, void* Z16, float* S32,
+                       hq_stream_t stream) {
   if (L <= 0 || N < 0) return fail(HQ_E_INVALID, "bad shape N=%lld L=%d", (long long)N, L);
-  if ((N > 0 && (!Z || !S)) || !Z32 || !S32) return fail(HQ_E_INVALID, "null buffer");
+  if ((N > 0 && (!Z || !S)) || !Z16 || !S32) return fail(HQ_E_INVALID, "null buffer");
   SegInfo si;
   seg_info(L, si);
   if (si.nseg == 0) return fail(HQ_E_INVALID, "no level structure for L=%d", L);
-  int64_t blocks = ((N + kPad0) * si.plen[0] + 255) / 256;
+  if (si.plen[0] > 32) return fail(HQ_E_UNSUPPORTED, "level-0 segment of %d values (<= 32)", si.plen[0]);
+  int64_t blocks = ((N + kPad0) * 32 + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(k_pack0, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, Z, S, N, si.Lp, si.plen[0],
-                     si.nseg, Z32, S32);
+                     si.nseg, reinterpret_cast<_Float16*>(Z16), S32);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
 
-int hq_scan0_topk_f32(const float* Zq32, const float* Sq32, const double* Sq, int Q, const float* Zc32,
-                      const float* Sc32, const double* Sc, int64_t N, int L, int k, double threshold, int thr_mode,
-                      int64_t id_base, void* workspace, size_t workspace_bytes, double* out_score, int64_t* out_id,
-                      hq_stream_t stream) {
+int hq_scan0_topk_split(const void* Zq16, const float* Sq32, const double* Sq, int Q, const void* Zc16,
+                        const float* Sc32, const double* Sc, int64_t N, int L, int k, double threshold, int thr_mode,
+                        int64_t id_base, void* workspace, size_t workspace_bytes, double* out_score,
+                        int64_t* out_id, hq_stream_t stream) {
   if (Q < 0 || N < 0 || L <= 0) return fail(HQ_E_INVALID, "bad shape");
   if (k <= 0 || k > kMaxTopK) return fail(HQ_E_UNSUPPORTED, "k=%d (1..%d)", k, kMaxTopK);
   if (Q == 0) return HQ_OK;
@@ -2267,14 +2249,15 @@ int hq_scan0_topk_f32(const float* Zq32, const float* Sq32, const double* Sq, in
     return HQ_OK;
   }
   if (N >= 0x7FFFFFFF) return fail(HQ_E_UNSUPPORTED, "N=%lld rows (int32 row ids)", (long long)N);
-  if (!Zq32 || !Sq32 || !Sq || !Zc32 || !Sc32 || !Sc || !workspace) return fail(HQ_E_INVALID, "null buffer");
+  if (!Zq16 || !Sq32 || !Sq || !Zc16 || !Sc32 || !Sc || !workspace) return fail(HQ_E_INVALID, "null buffer");
   if (workspace_bytes < hq_scan_workspace_size(Q, N, k)) return fail(HQ_E_INVALID, "workspace too small");
   SegInfo si;
   seg_info(L, si);
   const int ks = si.nseg > 0 ? si.plen[0] / 4 : 0;
   if (ks < 1 || ks > 8) return fail(HQ_E_UNSUPPORTED, "level-0 segment of %d values (1..32)", si.plen[0]);
-  return scan0_run(true, ks, nullptr, Sq, Zq32, Sq32, Q, nullptr, Sc, Zc32, Sc32, N, si, k, threshold, thr_mode,
-                   id_base, workspace, out_score, out_id, s);
+  return scan0_run(true, ks, nullptr, Sq, reinterpret_cast<const _Float16*>(Zq16), Sq32, Q, nullptr, Sc,
+                   reinterpret_cast<const _Float16*>(Zc16), Sc32, N, si, k, threshold, thr_mode, id_base, workspace,
+                   out_score, out_id, s);
 }
 
 int hq_rescore(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc, const double* Zc,

@@ -224,19 +224,19 @@ class Prepared:
     """Device-resident prepared index vectors: raw R [N, L] f64, Z [N, Lp] f64 (segment padded,
     normalised) and stats S [N, nseg, 4] (mean, std, mean of squares).  Built once per corpus."""
 
-    __slots__ = ("R", "Z", "S", "L", "N", "nseg", "Lp", "Z32", "S32")
+    __slots__ = ("R", "Z", "S", "L", "N", "nseg", "Lp", "Z16", "S32")
 
     def __init__(self, R, Z, S, L):
         self.R, self.Z, self.S, self.L = R, Z, S, int(L)
         self.N = Z.shape[0]
         self.nseg = S.shape[1]
         self.Lp = Z.shape[1]
-        self.Z32 = self.S32 = None  # f32 level-0 copies for the f32 level-0 scan (pack0_f32)
+        self.Z16 = self.S32 = None  # split-f16 level-0 copies for the level-0 scan (pack0)
 
     def rows(self, sel):
-        """Sub-set of rows (device index tensor) as a new Prepared (f32 copies re-packed on demand)."""
+        """Sub-set of rows (device index tensor) as a new Prepared (level-0 copies re-packed on demand)."""
         p = Prepared(self.R.index_select(0, sel), self.Z.index_select(0, sel), self.S.index_select(0, sel), self.L)
-        return pack0_f32(p) if self.Z32 is not None else p
+        return pack0(p) if self.Z16 is not None else p
 
 
 def seg_prepare(idx, exc=None) -> Prepared:
@@ -251,16 +251,18 @@ def seg_prepare(idx, exc=None) -> Prepared:
     return Prepared(i2, Z, S, L)
 
 
-PAD0 = 48  # pad rows of the f32 level-0 copies (hq_mi355x.h: hq_seg_pack0_f32)
+PAD0 = 48  # pad rows of the level-0 copies (hq_mi355x.h: hq_seg_pack0_split)
 
 
-def pack0_f32(p: Prepared, exc=None) -> Prepared:
-    """Attach the f32 copy of the level-0 segments (hq_seg_pack0_f32) used by the f32 level-0 scan."""
+def pack0(p: Prepared, exc=None) -> Prepared:
+    """Attach the split-f16 level-0 copies (hq_seg_pack0_split) used by the level-0 scan; indexes whose
+    level-0 segment is longer than 32 values keep the f64 scan."""
     t = torch()
-    P0 = int(_L().hq_seg_level0_len(p.L))
-    p.Z32 = t.empty((p.N + PAD0, P0), dtype=t.float32, device=p.Z.device)
+    if int(_L().hq_seg_level0_len(p.L)) > 32:
+        return p
+    p.Z16 = t.empty((p.N + PAD0, 64), dtype=t.float16, device=p.Z.device)
     p.S32 = t.empty((p.N + PAD0, 4), dtype=t.float32, device=p.Z.device)
-    _chk(_L().hq_seg_pack0_f32(ptr(p.Z), ptr(p.S), p.N, p.L, ptr(p.Z32), ptr(p.S32), stream()), exc)
+    _chk(_L().hq_seg_pack0_split(ptr(p.Z), ptr(p.S), p.N, p.L, ptr(p.Z16), ptr(p.S32), stream()), exc)
     return p
 
 
@@ -288,11 +290,11 @@ def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.
     ids = t.empty((Q, k), dtype=t.int64, device=dev)
     best = t.empty(Q, dtype=t.float64, device=dev) if need_best else None
     bid = t.empty(Q, dtype=t.int64, device=dev) if need_best else None
-    if (mode == 0 and not need_best and q.Z32 is not None and c.Z32 is not None
+    if (mode == 0 and not need_best and q.Z16 is not None and c.Z16 is not None
             and not os.environ.get("HQ_SCAN_F64")):
-        _chk(_L().hq_scan0_topk_f32(ptr(q.Z32), ptr(q.S32), ptr(q.S), Q, ptr(c.Z32), ptr(c.S32), ptr(c.S), N, c.L, k,
-                                    float(threshold), thr_mode, int(id_base), ptr(ws), ws_bytes, ptr(sc), ptr(ids),
-                                    stream()), exc)
+        _chk(_L().hq_scan0_topk_split(ptr(q.Z16), ptr(q.S32), ptr(q.S), Q, ptr(c.Z16), ptr(c.S32), ptr(c.S), N, c.L,
+                                      k, float(threshold), thr_mode, int(id_base), ptr(ws), ws_bytes, ptr(sc),
+                                      ptr(ids), stream()), exc)
         return sc, ids, best, bid
     _chk(_L().hq_scan_topk(ptr(q.Z), ptr(q.S), Q, ptr(c.Z), ptr(c.S), N, c.L, mode, k, float(threshold), thr_mode,
                            int(id_base), ptr(ws), ws_bytes, ptr(sc), ptr(ids), ptr(best), ptr(bid), stream()), exc)

@@ -169,20 +169,22 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
                  void* workspace, size_t workspace_bytes, double* out_score, int64_t* out_id,
                  double* out_best, int64_t* out_best_id, hq_stream_t stream);
 
-/* ---- S5/S6 level-0 scan with an f32 contraction (the progressive search's filtering stage) -------
- * Same result contract as hq_scan_topk(mode 0, no arg-max) but the contraction G = sum zq*zc runs on
- * v_mfma_f32_16x16x4f32 over f32 copies of the level-0 segments and the filter in f32; passing pairs
- * are re-scored in f64.  |approx - exact| <= ~1.5e-6 (|dG| <= (m+2) 2^-24 m), so callers re-rank
- * with hq_refine_topk at eps >= 1e-5.  hq_seg_pack0_f32 builds, from hq_seg_prepare's Z and S,
- * Z32 [N + 48, hq_seg_level0_len(L)] and S32 [N + 48, 4] (48 pad rows); Sq/Sc are the f64
- * statistics of hq_seg_prepare.  Level-0 segments of up to 32 values, N < 2^31.                  */
+/* ---- S5/S6 level-0 scan on the matrix cores (the progressive search's filtering stage) ----------
+ * Same result contract as hq_scan_topk(mode 0, no arg-max), but the contraction G = sum zq*zc runs as
+ * a split-f16 product (z = hi + lo, G ~= hi.hi + hi.lo + lo.hi with f32 accumulation, three
+ * v_mfma_f32_16x16x32_f16 per 16x16 tile) and the filter and list scores in f32.
+ * |approx - exact| <= ~5.5e-6, so callers re-rank with hq_refine_topk at eps >= 2e-5.
+ * hq_seg_pack0_split builds, from hq_seg_prepare's Z and S, Z16 [N + 48, 64] f16 (hi[32], lo[32]
+ * of the zero-padded level-0 segment) and S32 [N + 48, 4] f32 (std, mean, msq, flag bits), with 48
+ * pad rows; Sq/Sc are the f64 statistics of hq_seg_prepare.  Level-0 segments of up to 32 values,
+ * N < 2^31.                                                                                        */
 int hq_seg_level0_len(int L);
-int hq_seg_pack0_f32(const double* Z, const double* S, int64_t N, int L, float* Z32, float* S32,
-                     hq_stream_t stream);
-int hq_scan0_topk_f32(const float* Zq32, const float* Sq32, const double* Sq, int Q, const float* Zc32,
-                      const float* Sc32, const double* Sc, int64_t N, int L, int k, double threshold,
-                      int thr_mode, int64_t id_base, void* workspace, size_t workspace_bytes,
-                      double* out_score, int64_t* out_id, hq_stream_t stream);
+int hq_seg_pack0_split(const double* Z, const double* S, int64_t N, int L, void* Z16, float* S32,
+                       hq_stream_t stream);
+int hq_scan0_topk_split(const void* Zq16, const float* Sq32, const double* Sq, int Q, const void* Zc16,
+                        const float* Sc32, const double* Sc, int64_t N, int L, int k, double threshold,
+                        int thr_mode, int64_t id_base, void* workspace, size_t workspace_bytes,
+                        double* out_score, int64_t* out_id, hq_stream_t stream);
 
 /* ---- S5/S6: exact re-rank of a scan list -----------------------------------------------------
  * cand_score/cand_id: Q x kp list from hq_scan_topk (approximate, sorted).  Re-scores every listed
