@@ -983,14 +983,22 @@ __device__ __forceinline__ float lower_f32(double x) {  // largest float <= x (x
 }
 __device__ __forceinline__ int shr1_f32i(float v) { return shr1_i32(__float_as_int(v)); }
 
-#ifndef HQ_SCAN0F_WAVES
-#define HQ_SCAN0F_WAVES 2
+// NB = 16-query blocks per wave: 4 (64 queries, two pipelined halves, 2 waves/SIMD) or 2 (32
+// queries, one half, smaller register file: more waves per SIMD)
+template <int NB> struct Scan0fOcc;
+template <> struct Scan0fOcc<4> { static constexpr int waves = 2; };
+#ifndef HQ_NB2_WAVES
+#define HQ_NB2_WAVES 4
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WAVES, HQ_SCAN0F_WAVES))) void k_scan0f(
+template <> struct Scan0fOcc<2> { static constexpr int waves = HQ_NB2_WAVES; };
+
+template <int NB>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB>::waves))) void k_scan0f(
     Scan0Args a) {
+  constexpr int QW = 16 * NB;  // queries per wave
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  float* ls = reinterpret_cast<float*>(smem);         // kQW x K approx scores
-  int* li = reinterpret_cast<int*>(ls + kQW * a.K);   // kQW x K corpus rows
+  float* ls = reinterpret_cast<float*>(smem);         // QW x K approx scores
+  int* li = reinterpret_cast<int*>(ls + QW * a.K);    // QW x K corpus rows
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
   const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
   const int chunk = xcd + 8 * (slot / a.nqb);
@@ -999,18 +1007,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WA
   const int64_t c_begin = (int64_t)chunk * a.chunk_len;
   int64_t c_end = c_begin + a.chunk_len;
   if (c_end > a.N) c_end = a.N;
-  const int q0 = qb * kQW;
+  const int q0 = qb * QW;
   const int K = a.K;
   const float c1f = (float)a.c1;
-  int cntr[4] = {0, 0, 0, 0};  // pairs offered to the list of query 16b + j (same in the 4 lanes g)
+  int cntr[NB] = {};  // pairs offered to the list of query 16b + j (same in the 4 lanes g)
 
   // queries: fragments, f32 constants, list thresholds (f32, exact list values)
-  half8 qh[4], ql[4];  // query fragments: k range [8g, 8g + 8) of the hi and lo halves
-  float qA[4], qB[4], qQ[4], thl[4];
+  half8 qh[NB], ql[NB];  // query fragments: k range [8g, 8g + 8) of the hi and lo halves
+  float qA[NB], qB[NB], qQ[NB], thl[NB];
   int qsp = 0;  // bit b: query 16b + j is flagged (zero variance / f32-unsafe)
   int qvb = 0;  // bit b: query 16b + j exists
 #pragma unroll
-  for (int b = 0; b < 4; ++b) {
+  for (int b = 0; b < NB; ++b) {
     const int q = q0 + 16 * b + j;
     const bool v = q < a.Q;
     const int qq = v ? q : 0;
@@ -1027,11 +1035,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WA
     if (v && a.th0 && a.th0[q] > t0) t0 = a.th0[q];
     thl[b] = v ? lower_f32(t0) : __builtin_huge_valf();
   }
-  for (int i = lane; i < kQW * K; i += 64) {
+  for (int i = lane; i < QW * K; i += 64) {
     ls[i] = -__builtin_huge_valf();
     li[i] = -1;
   }
-  const bool myq = q0 + lane < a.Q;
+  const bool myq = lane < QW && q0 + lane < a.Q;
 
   // candidate rows are padded (kPad0, hq_seg_pack0_split): no clamping, rows past c_end are masked
   auto load_frag = [&](int64_t cs, half8* dst) {
@@ -1103,7 +1111,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WA
     const int b = qi >> 4;
     if (j == (qi & 15)) {
 #pragma unroll
-      for (int bb = 0; bb < 4; ++bb)
+      for (int bb = 0; bb < NB; ++bb)
         if (bb == b) thl[bb] = tau > thl[bb] ? tau : thl[bb];
     }
     if (lane == 0 && tau > 0.0f) atomicMax(a.gtau + q0 + qi, (unsigned long long)__double_as_longlong((double)tau));
@@ -1194,13 +1202,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WA
       }
   };
 
-  // software pipeline as in k_scan0: next step's fragment and statistics in flight
+  // Software pipeline.  NB = 4: the MFMAs of one half run while the VALU filters the other half
+  //   block A: MFMA(step i, half 1) || filter(step i, half 0)
+  //   block B: MFMA(step i+1, half 0) || filter(step i, half 1)
+  // NB = 2: MFMA(step i) then filter(step i); the other waves of the SIMD fill the gaps.
   half8 cf[2];
   flt4 cst[4];
   load_frag(c_begin, cf);
   load_stats(c_begin, cst);
   flt4 acc0[2], acc1[2];
-  mfma_half(0, cf, acc0);
+  if constexpr (NB == 4) mfma_half(0, cf, acc0);
   unsigned long long gt_bits = 0ull;
   int step = 0;
   for (int64_t cs = c_begin; cs < c_end; cs += kCS, ++step) {
@@ -1209,12 +1220,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WA
     flt4 cstn[4];
     load_frag(cs + kCS, cf1);
     load_stats(cs + kCS, cstn);
-    mfma_half(1, cf, acc1);
-    const int bits0 = filter_half(0, acc0, cst, rem);
-    if (__ballot(bits0 != 0)) insert_half(0, acc0, cst, cs, bits0);
-    mfma_half(0, cf1, acc0);
-    const int bits1 = filter_half(1, acc1, cst, rem);
-    if (__ballot(bits1 != 0)) insert_half(1, acc1, cst, cs, bits1);
+    if constexpr (NB == 4) {
+      mfma_half(1, cf, acc1);
+      const int bits0 = filter_half(0, acc0, cst, rem);
+      if (__ballot(bits0 != 0)) insert_half(0, acc0, cst, cs, bits0);
+      mfma_half(0, cf1, acc0);
+      const int bits1 = filter_half(1, acc1, cst, rem);
+      if (__ballot(bits1 != 0)) insert_half(1, acc1, cst, cs, bits1);
+    } else {
+      mfma_half(0, cf, acc0);
+      const int bits0 = filter_half(0, acc0, cst, rem);
+      if (__ballot(bits0 != 0)) insert_half(0, acc0, cst, cs, bits0);
+    }
     cf[0] = cf1[0];
     cf[1] = cf1[1];
 #pragma unroll
@@ -1223,7 +1240,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WA
       if (gt_bits != 0ull) {
         const float gf = (float)__longlong_as_double((long long)gt_bits);  // exact: list values are f32
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
+        for (int b = 0; b < NB; ++b) {
           const float v = __shfl(gf, 16 * b + j, 64);
           thl[b] = v > thl[b] ? v : thl[b];
         }
@@ -1235,13 +1252,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HQ_SCAN0F_WA
   // hand the lists (unordered is fine) to the per-query pools: one atomic per query, lane-parallel
   int nl = 0;  // entries of query `lane`
 #pragma unroll
-  for (int b = 0; b < 4; ++b) {
+  for (int b = 0; b < NB; ++b) {
     const int v = __shfl(cntr[b], lane & 15, 64);
     if ((lane >> 4) == b) nl = v < K ? v : K;
   }
   int base = 0;
   if (nl > 0 && myq) base = atomicAdd(a.pool_n + q0 + lane, nl);
-  for (int ql = 0; ql < kQW; ++ql) {
+  for (int ql = 0; ql < QW; ++ql) {
     const int n = __builtin_amdgcn_readlane(nl, ql);
     if (n == 0 || q0 + ql >= a.Q) continue;
     const int bq = __builtin_amdgcn_readlane(base, ql);
@@ -1854,10 +1871,16 @@ static void scan_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& chu
   if (chunk_len < kCB) chunk_len = kCB;
 }
 
+// 16-query blocks per wave of the split level-0 scan (HQ_SCAN_NB = 2 or 4)
+static int scan0_nb() {
+  const char* e = getenv("HQ_SCAN_NB");
+  return (e && atoi(e) == 2) ? 2 : 4;
+}
+
 // k_scan0: ~16 resident waves per CU-pair of rounds; nchunks multiple of 8 (XCD mapping), <= 512
-static void scan0_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& chunk_len) {
-  nqb = (Q + kQW - 1) / kQW;
-  int64_t target = (4096 + nqb - 1) / nqb;
+static void scan0_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& chunk_len, int qw = kQW) {
+  nqb = (Q + qw - 1) / qw;
+  int64_t target = (4096 * (kQW / qw) + nqb - 1) / nqb;
   int64_t max_chunks = (N + kCS - 1) / kCS;
   if (target > max_chunks) target = max_chunks;
   if (target > 512) target = 512;
@@ -1869,9 +1892,11 @@ static void scan0_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& ch
 }
 
 static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
-  int nqb, nchunks;
-  int64_t chunk_len;
+  int nqb, nchunks, nqb2, nchunks2;
+  int64_t chunk_len, chunk_len2;
   scan0_geometry(Q, N, nqb, nchunks, chunk_len);
+  scan0_geometry(Q, N, nqb2, nchunks2, chunk_len2, 32);
+  if (nchunks2 > nchunks) nchunks = nchunks2;
   // lists / pools + global thresholds + sample histogram + starting thresholds + pool counts
   return (size_t)nchunks * Q * k * 16 + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 8 + (size_t)Q * 4 + 256;
 }
@@ -1908,9 +1933,12 @@ static int launch_sample(const SampleArgs& a, hipStream_t s) {
 template <int KS, bool F32>
 static int launch_scan0(const Scan0Args& a, hipStream_t s) {
   if constexpr (F32) {
-    const size_t lds = (size_t)kQW * a.K * 8 + (size_t)kQW * 4;
-    HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_scan0f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_scan0f, dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
+    const int nb = scan0_nb();
+    const size_t lds = (size_t)16 * nb * a.K * 8;
+    const void* fn = nb == 2 ? (const void*)k_scan0f<2> : (const void*)k_scan0f<4>;
+    HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (nb == 2) hipLaunchKernelGGL(k_scan0f<2>, dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
+    else hipLaunchKernelGGL(k_scan0f<4>, dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
     HQ_CHECK_LAUNCH();
     return HQ_OK;
   }
@@ -1971,7 +1999,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     HQ_CHECK_HIP(hipMemsetAsync(dbg, 0, 64, s));
   }
   b.dbg = dbg;
-  scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len);
+  scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len, f32 ? 16 * scan0_nb() : kQW);
   uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
   b.ws_score = reinterpret_cast<double*>(ws);
   b.ws_id = reinterpret_cast<int64_t*>(ws + (size_t)b.nchunks * Q * k * 8);

@@ -9,7 +9,7 @@ P2="SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_IN
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  SCAN_EXPT_ONLY=default timeout -k 10 300 rocprofv3 --pmc $P -d $OUT/p$i -o p$i --output-format csv -- python tools/scan_expt.py > $OUT/p$i.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --pmc $P -d $OUT/p$i -o p$i --output-format csv -- python ${SCAN_SCRIPT:-tools/scan_debug.py} > $OUT/p$i.log 2>&1 || exit 1
 done
 python3 - <<'PY'
 import csv, glob

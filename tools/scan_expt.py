@@ -14,7 +14,12 @@ from hq_mi355x.core.search_engine import IndexCorpus  # noqa: E402
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 Q = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
 g = torch.Generator(device="cuda").manual_seed(5)
-C = torch.randn((N, 64), generator=g, device="cuda", dtype=torch.float64).cumsum(1) * 0.1
+if os.environ.get("SCAN_DATA", "bench") == "bench":  # the bench corpus: streaming indexes of N(0,1) embeddings
+    X = torch.randn((N, 1536), generator=g, device="cuda", dtype=torch.float32)
+    _, C, _ = K.map_index_quantize(X, 64, 64)
+    del X
+else:  # random walks
+    C = torch.randn((N, 64), generator=g, device="cuda", dtype=torch.float64).cumsum(1) * 0.1
 corpus = IndexCorpus(C)
 qp = corpus.prepare_queries(C[:Q] + 0.01 * torch.randn((Q, 64), generator=g, device="cuda", dtype=torch.float64))
 VARIANTS = [("count", {"HQ_SCAN_EXPT": "3"}), ("default", {}),
