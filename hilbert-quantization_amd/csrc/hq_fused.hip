@@ -37,6 +37,12 @@ __device__ __forceinline__ double quad_bcast(double v) {
   return __hiloint2double(hi, lo);
 }
 
+__device__ __forceinline__ double quad_bcast_xor1(double v) {  // value of lane ^ 1 (quad_perm 1,0,3,2)
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
 // wave64 all-reduce through DPP (xor 1, xor 2, half-row mirror, row mirror) and four readlanes: no
 // LDS round trips on the per-embedding critical path
 template <int CTRL>
@@ -59,6 +65,16 @@ __device__ __forceinline__ float wmax64(float v) {
   v = fmaxf(v, dppf<0x141>(v));
   v = fmaxf(v, dppf<0x140>(v));
   return fmaxf(fmaxf(lanef(v, 0), lanef(v, 16)), fmaxf(lanef(v, 32), lanef(v, 48)));
+}
+// index row store with 16-byte lanes: even lanes write (slot 2k, slot 2k+1) — 8-byte stores leave
+// L2 at a much lower byte rate (MI355X_MICROARCH.md, store flavours); L even and 16-B aligned rows
+__device__ __forceinline__ void store_index(double* __restrict__ row, double val, int lane, int L) {
+  const double nb = quad_bcast_xor1(val);
+  if ((L & 1) == 0 && (reinterpret_cast<uintptr_t>(row) & 15) == 0) {
+    if ((lane & 1) == 0 && lane < L) *reinterpret_cast<double2*>(row + lane) = make_double2(val, nb);
+  } else if (lane < L) {
+    row[lane] = val;
+  }
 }
 __device__ __forceinline__ uint32_t qz(float x, float mn, float rng) {
   float t = (x - mn) / rng;  // IEEE f32 division (no fast-math), then * 255 and truncate
@@ -150,6 +166,26 @@ __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int
                                             float* __restrict__ mm_out) {
   using Geo = FastGeo<NS>;
   constexpr int NLEV = Geo::levels();
+  // memory-only probes (HQ_FUSED_V = 8 / 12: the kernel's full traffic with no arithmetic; + 16: no frame
+  // stores, + 32: no index / min-max stores) bound what the arithmetic costs: V 8 runs within ~4 % of V 4
+  if constexpr ((V & 8) != 0) {
+    float acc = 0.f;
+#pragma unroll
+    for (int t = 0; t < ND; ++t) acc += (b.g[t].x + b.g[t].y) + (b.g[t].z + b.g[t].w);
+    if constexpr ((V & 32) == 0) {
+      store_index(idx_out + e * (int64_t)L, (double)acc, lane, L);
+      if (mm_out && lane == 0) mm_out[2 * e] = acc;
+    } else {
+      if (acc == 1234.5f) idx_out[0] = 0.0;  // keep the loads
+    }
+    if constexpr ((V & 16) == 0) {
+      uint8_t* dst = frame_out + e * (int64_t)Geo::FB;
+#pragma unroll
+      for (int c = lane; c < Geo::FB / 16; c += 64)
+        reinterpret_cast<uint4*>(dst)[c] = reinterpret_cast<const uint4*>(frame)[c];
+    }
+    return;
+  }
   // ---- min / max over the real elements --------------------------------------------------------
   float lmin = __builtin_huge_valf(), lmax = -__builtin_huge_valf();
 #pragma unroll
@@ -199,7 +235,7 @@ __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int
   } else if (slev >= 2) {
     val = tree[Geo::off(slev) + spos];
   }
-  if (lane < L) idx_out[e * (int64_t)L + lane] = val;
+  store_index(idx_out + e * (int64_t)L, val, lane, L);
   const float rv = (float)val;
 
   // ---- quantize into the LDS frame, stream out --------------------------------------------------
@@ -359,6 +395,11 @@ static int pick_nd(int variant, int nd, const float* in, int64_t N, int64_t stri
           case 5: return launch_ff<NS, ND, 5>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 6: return launch_ff<NS, ND, 6>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 7: return launch_ff<NS, ND, 7>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 8: return launch_ff<NS, ND, 8>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 12: return launch_ff<NS, ND, 12>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 24: return launch_ff<NS, ND, 24>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 40: return launch_ff<NS, ND, 40>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 56: return launch_ff<NS, ND, 56>(in, N, stride, d, L, plan, frame, idx, mm, s);
           default: break;
         }
       }
