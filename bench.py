@@ -153,7 +153,7 @@ def main():
     value = N * world * args.steps / wall
     bytes_per_emb = 4 * d + (n + 1) * n + 8 * L + 8
     achieved = bytes_per_emb * N / kern / 1e9
-    traffic = load_traffic("k_fused64")
+    traffic = load_traffic("k_fused_np64")
     rec = {
         "metric": "embeddings/sec Hilbert map+quantize (1536D)", "value": value, "unit": "embeddings/sec",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,

@@ -44,7 +44,7 @@ int persistent_grid(const void* kernel, int block, size_t dyn_lds, int64_t work_
 // ------------------------------------------------------------------------------------------------
 // Hilbert curve (reference core/hilbert_mapper.py)
 // ------------------------------------------------------------------------------------------------
-__host__ __device__ inline void d2xy(uint32_t n, uint32_t idx, uint32_t& x_out, uint32_t& y_out) {
+__host__ __device__ constexpr inline void d2xy(uint32_t n, uint32_t idx, uint32_t& x_out, uint32_t& y_out) {
   // _hilbert_index_to_xy (:42-66) with _rotate (:92-113)
   uint32_t x = 0, y = 0, t = idx;
   for (uint32_t s = 1; s < n; s <<= 1) {

@@ -161,9 +161,9 @@ __device__ __forceinline__ void load_emb(const float* __restrict__ src, int d, i
 
 template <int NS, int ND, int V>
 __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int d, int L, int lane, int slev,
-                                            int spos, bool pad0, double* tree, const uint32_t* lut, uint8_t* frame,
+                                            int spos, bool pad0, double* tree, const uint32_t (&lut_r)[ND], uint8_t* frame,
                                             uint8_t* __restrict__ frame_out, double* __restrict__ idx_out,
-                                            float* __restrict__ mm_out) {
+                                            float* __restrict__ mm_out, bool live = true) {
   using Geo = FastGeo<NS>;
   constexpr int NLEV = Geo::levels();
   // memory-only probes (HQ_FUSED_V = 8 / 12: the kernel's full traffic with no arithmetic; + 16: no frame
@@ -235,7 +235,7 @@ __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int
   } else if (slev >= 2) {
     val = tree[Geo::off(slev) + spos];
   }
-  store_index(idx_out + e * (int64_t)L, val, lane, L);
+  if (live) store_index(idx_out + e * (int64_t)L, val, lane, L);
   const float rv = (float)val;
 
   // ---- quantize into the LDS frame, stream out --------------------------------------------------
@@ -278,7 +278,7 @@ __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int
           e2 = (4 * j + 2 < d) ? qz(x.z, mn, rng) : q0;
           e3 = (4 * j + 3 < d) ? qz(x.w, mn, rng) : q0;
         }
-        const uint32_t ent = lut[j];
+        const uint32_t ent = lut_r[t];
         const uint32_t code = ent >> 16;
         const uint32_t w = (e0 << (8 * (code & 3))) | (e1 << (8 * ((code >> 2) & 3))) |
                            (e2 << (8 * ((code >> 4) & 3))) | (e3 << (8 * ((code >> 6) & 3)));
@@ -291,14 +291,13 @@ __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int
   if (lane < NS) frame[NS * NS + lane] = flat ? (uint8_t)128 : (uint8_t)qz(rv, mn, rng);
   __syncthreads();
   uint8_t* dst = frame_out + e * (int64_t)Geo::FB;
+  if (live) {
 #pragma unroll
-  for (int c = lane; c < Geo::FB / 16; c += 64)
-    reinterpret_cast<uint4*>(dst)[c] = reinterpret_cast<const uint4*>(frame)[c];
-  if (mm_out && lane == 0) {
-    mm_out[2 * e] = mn;
-    mm_out[2 * e + 1] = mx;
+    for (int c = lane; c < Geo::FB / 16; c += 64)
+      reinterpret_cast<uint4*>(dst)[c] = reinterpret_cast<const uint4*>(frame)[c];
+    if (mm_out && lane == 0) *reinterpret_cast<float2*>(mm_out + 2 * e) = make_float2(mn, mx);
   }
-  __syncthreads();
+  if constexpr ((V & 64) == 0) __syncthreads();  // persistent: the frame is reused by the next embedding
 }
 
 template <int NS, int ND, int V>
@@ -328,6 +327,9 @@ __global__ __launch_bounds__(64) void k_fused_fast(const float* __restrict__ in,
   const int slev = lane < L ? (int)plan.lev[lane] : -1;
   const int spos = lane < L ? plan.pos[lane] : 0;
   const bool pad0 = (d < NS * NS) || plan.zero_row;
+  uint32_t lut_r[ND];  // loop-invariant: this lane's groups lane + 64 t
+#pragma unroll
+  for (int t = 0; t < ND; ++t) lut_r[t] = lut[lane + 64 * t];
   // V & 4: three register buffers — while embedding e is processed, e+G and e+2G are in flight (HBM
   // latency under full load is several microseconds; one embedding of prefetch left waves ~70%
   // stalled); otherwise two buffers.
@@ -339,15 +341,15 @@ __global__ __launch_bounds__(64) void k_fused_fast(const float* __restrict__ in,
     if (e + G < N) load_emb<NS, ND, V>(in + (e + G) * stride, d, lane, slev, spos, B);
     while (e < N) {
       if (e + 2 * G < N) load_emb<NS, ND, V>(in + (e + 2 * G) * stride, d, lane, slev, spos, C);
-      process_emb<NS, ND, V>(e, A, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
+      process_emb<NS, ND, V>(e, A, d, L, lane, slev, spos, pad0, tree, lut_r, frame, frame_out, idx_out, mm_out);
       e += G;
       if (e >= N) break;
       if (e + 2 * G < N) load_emb<NS, ND, V>(in + (e + 2 * G) * stride, d, lane, slev, spos, A);
-      process_emb<NS, ND, V>(e, B, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
+      process_emb<NS, ND, V>(e, B, d, L, lane, slev, spos, pad0, tree, lut_r, frame, frame_out, idx_out, mm_out);
       e += G;
       if (e >= N) break;
       if (e + 2 * G < N) load_emb<NS, ND, V>(in + (e + 2 * G) * stride, d, lane, slev, spos, B);
-      process_emb<NS, ND, V>(e, C, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
+      process_emb<NS, ND, V>(e, C, d, L, lane, slev, spos, pad0, tree, lut_r, frame, frame_out, idx_out, mm_out);
       e += G;
     }
   } else {
@@ -355,14 +357,92 @@ __global__ __launch_bounds__(64) void k_fused_fast(const float* __restrict__ in,
     if (e < N) load_emb<NS, ND, V>(in + e * stride, d, lane, slev, spos, A);
     while (e < N) {
       if (e + G < N) load_emb<NS, ND, V>(in + (e + G) * stride, d, lane, slev, spos, B);
-      process_emb<NS, ND, V>(e, A, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
+      process_emb<NS, ND, V>(e, A, d, L, lane, slev, spos, pad0, tree, lut_r, frame, frame_out, idx_out, mm_out);
       e += G;
       if (e >= N) break;
       if (e + G < N) load_emb<NS, ND, V>(in + (e + G) * stride, d, lane, slev, spos, A);
-      process_emb<NS, ND, V>(e, B, d, L, lane, slev, spos, pad0, tree, lut, frame, frame_out, idx_out, mm_out);
+      process_emb<NS, ND, V>(e, B, d, L, lane, slev, spos, pad0, tree, lut_r, frame, frame_out, idx_out, mm_out);
       e += G;
     }
   }
+}
+
+// Group LUT (offset of the 2x2 block of float4 group j in the row-major frame | element order << 16),
+// evaluated at compile time so a non-persistent wave reads its six entries from L2 instead of building
+// the table per workgroup.
+template <int NS>
+struct GroupLut {
+  uint32_t v[NS * NS / 4];
+};
+template <int NS>
+constexpr GroupLut<NS> make_group_lut() {
+  GroupLut<NS> t{};
+  for (uint32_t j = 0; j < (uint32_t)(NS * NS / 4); ++j) {
+    uint32_t code = 0, off = 0;
+    for (uint32_t m = 0; m < 4; ++m) {
+      uint32_t x = 0, y = 0;
+      d2xy(NS, 4 * j + m, x, y);
+      if (m == 0) off = (y & ~1u) * NS + (x & ~1u);
+      code |= ((x & 1u) + 2u * (y & 1u)) << (2 * m);
+    }
+    t.v[j] = off | (code << 16);
+  }
+  return t;
+}
+__device__ constexpr GroupLut<16> kLut16 = make_group_lut<16>();
+__device__ constexpr GroupLut<32> kLut32 = make_group_lut<32>();
+__device__ constexpr GroupLut<64> kLut64 = make_group_lut<64>();
+template <int NS>
+__device__ __forceinline__ const uint32_t* group_lut() {
+  if constexpr (NS == 16) return kLut16.v;
+  else if constexpr (NS == 32) return kLut32.v;
+  else return kLut64.v;
+}
+
+// Non-persistent form (V & 64): one embedding per wave, WPB waves per workgroup, grid = N / WPB.  The
+// hardware dispatcher interleaves the waves' streams; measured on the fused kernel's exact traffic
+// shape (tools/ubench/hbm_shapes.hip) this moves 5.3 TB/s against 4.8-4.95 TB/s for every persistent
+// grid-stride form.  Each wave owns a tree + frame slice of LDS; the per-lane LUT entries come from
+// the compile-time table (L2 resident).
+template <int NS>
+struct NpGeo {
+  static constexpr int tree_bytes = FastGeo<NS>::tree_len() * 8;
+  static constexpr int frame_off = (tree_bytes + 15) & ~15;
+  static constexpr int wave_bytes = frame_off + ((FastGeo<NS>::FB + 15) & ~15);
+};
+
+template <int NS, int ND, int V, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_fused_np(const float* __restrict__ in, int64_t N, int64_t stride, int d,
+                                                       int L, FastPlan plan, uint8_t* __restrict__ frame_out,
+                                                       double* __restrict__ idx_out, float* __restrict__ mm_out) {
+  using Geo = FastGeo<NS>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  uint8_t* base = smem + wv * NpGeo<NS>::wave_bytes;
+  double* tree = reinterpret_cast<double*>(base);
+  uint8_t* frame = base + NpGeo<NS>::frame_off;
+  const int64_t e = (int64_t)blockIdx.x * WPB + wv;
+  const bool live = e < N;
+  const int slev = lane < L ? (int)plan.lev[lane] : -1;
+  const int spos = lane < L ? plan.pos[lane] : 0;
+  const bool pad0 = (d < NS * NS) || plan.zero_row;
+  Buf<NS, ND> A;
+  if (live) {
+    load_emb<NS, ND, V>(in + e * stride, d, lane, slev, spos, A);
+  } else {
+#pragma unroll
+    for (int t = 0; t < ND; ++t) A.g[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    A.slot = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // this lane's LUT entries (groups lane + 64 t), loaded alongside the embedding
+  uint32_t lut_r[ND];
+  const uint32_t* glut = group_lut<NS>();
+#pragma unroll
+  for (int t = 0; t < ND; ++t) lut_r[t] = glut[lane + 64 * t];
+  // level-2 nodes of the all-padding groups t >= ND stay 0.0
+  for (int k = 16 * ND + lane; k < Geo::G / 4; k += 64) tree[Geo::off(2) + k] = 0.0;
+  process_emb<NS, ND, V>(e, A, d, L, lane, slev, spos, pad0, tree, lut_r, frame, frame_out, idx_out, mm_out, live);
 }
 
 template <int NS, int ND, int V>
@@ -377,7 +457,29 @@ static int launch_ff(const float* in, int64_t N, int64_t stride, int d, int L, c
   return HQ_OK;
 }
 
-constexpr int kDefaultV = 4;  // triple buffering, plain loads, exact quantize
+template <int NS, int ND, int V>
+static int launch_np(const float* in, int64_t N, int64_t stride, int d, int L, const FastPlan& plan, uint8_t* frame,
+                     double* idx, float* mm, hipStream_t s) {
+  constexpr int WPB = 1 << ((V >> 7) & 3);
+  const size_t lds = (size_t)WPB * NpGeo<NS>::wave_bytes;
+  const int64_t grid = (N + WPB - 1) / WPB;
+  if (grid > 0x7FFFFFFF) return HQ_E_UNSUPPORTED;
+  hipLaunchKernelGGL((k_fused_np<NS, ND, V, WPB>), dim3((unsigned)grid), dim3(64 * WPB), lds, s, in, N, stride, d, L,
+                     plan, frame, idx, mm);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+template <int NS, int ND, int V>
+static int launch_any(const float* in, int64_t N, int64_t stride, int d, int L, const FastPlan& plan, uint8_t* frame,
+                      double* idx, float* mm, hipStream_t s) {
+  if constexpr ((V & 64) != 0) return launch_np<NS, ND, V>(in, N, stride, d, L, plan, frame, idx, mm, s);
+  else return launch_ff<NS, ND, V>(in, N, stride, d, L, plan, frame, idx, mm, s);
+}
+
+// Variant bits (HQ_FUSED_V): 1 nt loads, 2 reciprocal quantize, 4 triple buffering (persistent), 8 / 16 / 32
+// memory-only probes, 64 non-persistent (one embedding per wave), bits 7-8: log2 waves per workgroup.
+constexpr int kDefaultV = 64 | (1 << 7);  // non-persistent, 2 waves per workgroup, plain loads, exact quantize
 
 template <int NS, int ND>
 static int pick_nd(int variant, int nd, const float* in, int64_t N, int64_t stride, int d, int L, const FastPlan& plan,
@@ -400,10 +502,18 @@ static int pick_nd(int variant, int nd, const float* in, int64_t N, int64_t stri
           case 24: return launch_ff<NS, ND, 24>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 40: return launch_ff<NS, ND, 40>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 56: return launch_ff<NS, ND, 56>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 64: return launch_any<NS, ND, 64>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 192: return launch_any<NS, ND, 192>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 320: return launch_any<NS, ND, 320>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 448: return launch_any<NS, ND, 448>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 321: return launch_any<NS, ND, 321>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 322: return launch_any<NS, ND, 322>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 328: return launch_any<NS, ND, 328>(in, N, stride, d, L, plan, frame, idx, mm, s);
           default: break;
         }
       }
-      return launch_ff<NS, ND, kDefaultV>(in, N, stride, d, L, plan, frame, idx, mm, s);
+      if (variant == 4) return launch_ff<NS, ND, 4>(in, N, stride, d, L, plan, frame, idx, mm, s);
+      return launch_any<NS, ND, kDefaultV>(in, N, stride, d, L, plan, frame, idx, mm, s);
     }
     return pick_nd<NS, ND + 1>(variant, nd, in, N, stride, d, L, plan, frame, idx, mm, s);
   }
@@ -414,7 +524,8 @@ int fused_fast(const float* in, int64_t N, int64_t stride, int d, int n, int L, 
                float* mm, hipStream_t s) {
   if (!(n == 16 || n == 32 || n == 64)) return HQ_E_UNSUPPORTED;
   if (L < 1 || L > 64 || !idx || d < 1) return HQ_E_UNSUPPORTED;
-  if ((reinterpret_cast<uintptr_t>(in) & 15) || (stride % 4) || (reinterpret_cast<uintptr_t>(frame) & 15))
+  if ((reinterpret_cast<uintptr_t>(in) & 15) || (stride % 4) || (reinterpret_cast<uintptr_t>(frame) & 15) ||
+      (reinterpret_cast<uintptr_t>(mm) & 7))
     return HQ_E_UNSUPPORTED;
   StreamSchedule sched;
   stream_schedule((int64_t)n * n, L, sched);

@@ -200,6 +200,24 @@ def test_fused_kernel_vs_oracle(hq_lib, n, d, L):
     assert np.array_equal(got[:, 0], mn) and np.array_equal(got[:, 1], mx)
 
 
+@pytest.mark.parametrize("variant", [4, 0, 64, 192, 320, 448, 322])
+@pytest.mark.parametrize("n,d,L", [(64, 1536, 64), (32, 999, 20), (16, 200, 16)])
+def test_fused_launch_forms_vs_oracle(hq_lib, n, d, L, variant, monkeypatch):
+    """Every launch form of the fast kernel (persistent triple/double buffered, non-persistent with 1-8
+    waves per workgroup and a ragged last workgroup, reciprocal quantize) is bit-exact."""
+    from hq_mi355x import kernels as K
+    monkeypatch.setenv("HQ_FUSED_V", str(variant))
+    rng = np.random.default_rng(variant + d)
+    P = (rng.standard_normal((45, d)) * 3).astype(np.float32)
+    P[7] = 0.0
+    fr, idx, mm = K.map_index_quantize(_t(P), n, L)
+    u8, ridx, mn, mx = _oracle_fused(P, n, L)
+    assert _np(fr).tobytes() == u8.tobytes()
+    assert _np(idx).tobytes() == ridx.tobytes()
+    got = _np(mm)
+    assert np.array_equal(got[:, 0], mn) and np.array_equal(got[:, 1], mx)
+
+
 @pytest.mark.parametrize("n,d,L", [(32, 1000, 32), (64, 1536, 64), (64, 4096, 30), (16, 256, 16)])
 def test_fused_generic_path_vs_oracle(hq_lib, n, d, L, monkeypatch):
     """The non-pipelined kernel (n outside {16,32,64}, L > 64, unaligned rows) stays bit-exact too."""
