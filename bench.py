@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--queries", type=int, default=1000)
     ap.add_argument("--search-steps", type=int, default=5)
     ap.add_argument("--no-search", action="store_true")
+    ap.add_argument("--no-stream", action="store_true")
+    ap.add_argument("--stream-values", type=int, default=7_000_000_000)
+    ap.add_argument("--stream-steps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     return ap.parse_args()
@@ -129,6 +132,68 @@ def cpu_baseline_search(C, Q, seconds):
                       f"in {dt:.1f}s, linear in corpus size"}
 
 
+STREAM_CHUNK = 1024
+STREAM_BYTES_PER_CHUNK = 2 * STREAM_CHUNK + 33 * 32 + 4 * 32 + 8  # f16 in; u8 33x32 frame, f32[32] index, min/max out
+
+
+def bench_stream(args, world, rank, dev):
+    """Config 5: a 7e9-value f16 parameter stream cut into 1024-value chunks (core/streaming_processor.py:
+    539-582), each chunk Hilbert-mapped to 32x32, traditional index (L = 32) embedded, uint8 quantized
+    (:877-913; hq_chunk_encode_f16).  The chunk range is split into contiguous per-rank shards (strong
+    scaling, no collective); the 512-value tail chunk goes to the last rank."""
+    from hq_mi355x import kernels as K
+    total = args.stream_values
+    nch_all = (total + STREAM_CHUNK - 1) // STREAM_CHUNK
+    c0, c1 = rank * nch_all // world, (rank + 1) * nch_all // world
+    vals = min(c1 * STREAM_CHUNK, total) - c0 * STREAM_CHUNK
+    nch = c1 - c0
+    g = torch.Generator(device=dev).manual_seed(5 + 1000 * rank)
+    x = torch.randn((vals,), generator=g, device=dev, dtype=torch.float16).mul_(0.02)
+    out = (torch.zeros((nch, 33, 32), dtype=torch.uint8, device=dev),
+           torch.zeros((nch, 32), dtype=torch.float32, device=dev),
+           torch.zeros((nch, 2), dtype=torch.float32, device=dev))
+
+    def step():
+        K.chunk_encode_f16(x, STREAM_CHUNK, out=out)
+
+    wall, kern = timed(step, args.stream_steps, 1, world)
+    alg_bytes = 2 * total + nch_all * (STREAM_BYTES_PER_CHUNK - 2 * STREAM_CHUNK)
+    rank_bytes = 2 * vals + nch * (STREAM_BYTES_PER_CHUNK - 2 * STREAM_CHUNK)
+    achieved = rank_bytes / kern / 1e9
+    res = {
+        "metric": "GB/s streaming Hilbert quantize of a 7e9-value f16 parameter stream (algorithmic bytes)",
+        "value": alg_bytes * args.stream_steps / wall / 1e9, "unit": "GB/s",
+        "params_per_sec": total * args.stream_steps / wall, "values_total": total, "chunks_total": nch_all,
+        "values_per_rank": vals, "steps": args.stream_steps, "ms_per_step": wall / args.stream_steps * 1e3,
+        "scaling": "strong", "dtype": "f16 in, f32 arithmetic, u8 frames",
+        "config": "cfg5: 1024-value chunks -> 32x32 Hilbert image + traditional index (L=32, f32) + u8 33x32 frame, "
+                  f"contiguous chunk shards over {world} GPU(s)",
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("k_chunk_np32"),
+                     "algorithmic_bytes_per_chunk": STREAM_BYTES_PER_CHUNK, "kernel_ms": kern * 1e3},
+    }
+    del x, out
+    return res
+
+
+def cpu_baseline_stream(seconds):
+    """Oracle chunk encoder (map + traditional index + embed + u8 normalise per 1024-value chunk)."""
+    from oracle import hq_oracle as O
+    rng = np.random.default_rng(5)
+    x = (rng.standard_normal(STREAM_CHUNK * 256) * 0.02).astype(np.float16)
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for c in range(256):
+            img = O.map_to_2d(x[c * STREAM_CHUNK:(c + 1) * STREAM_CHUNK].astype(np.float32), 32)
+            O.normalize_u8(O.embed_index_row(img, O.traditional_index(img, 32)))
+        done += 256
+    dt = time.perf_counter() - t0
+    return {"value": done * STREAM_BYTES_PER_CHUNK / dt / 1e9, "unit": "GB/s (algorithmic bytes)",
+            "params_per_sec": done * STREAM_CHUNK / dt, "cores": 1, "kind": "port",
+            "sample": f"{done} chunks of 1024 f16 values through the oracle chunk encoder (NumPy, single thread) "
+                      f"in {dt:.1f}s"}
+
+
 def main():
     args = parse()
     world, rank = dist_setup(args)
@@ -211,6 +276,10 @@ def main():
             "self_match_rate": float((ids[:, 0].cpu() == torch.arange(Qn)).float().mean()),
         }
 
+    if not args.no_stream:
+        del X, frames, idx, mm, out
+        rec["stream"] = bench_stream(args, world, rank, dev)
+
     if rank == 0 and world == 1 and not args.no_cpu:
         rec["cpu_baseline"] = cpu_baseline_quantize(d, args.cpu_seconds)
         rec["cpu_baseline"]["threads_available"] = os.cpu_count()
@@ -219,6 +288,8 @@ def main():
             C = to_np(corpus_idx[:100_000])
             Qh = to_np(queries[:50])
             rec["search"]["cpu_baseline"] = cpu_baseline_search(C, Qh, args.cpu_seconds / 2)
+        if "stream" in rec:
+            rec["stream"]["cpu_baseline"] = cpu_baseline_stream(args.cpu_seconds / 2)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -61,6 +61,32 @@ __host__ __device__ constexpr inline void d2xy(uint32_t n, uint32_t idx, uint32_
   x_out = x; y_out = y;
 }
 
+// Group LUT: float4 group j (Hilbert elements 4j..4j+3) is the 2x2 block at row-major offset
+// `off` of an NS x NS image (layout invariant).  Entry = off | code << 16 where code
+// holds, per element m, its slot b = (x & 1) + 2 (y & 1) inside the block (INV = false), or per
+// slot b the element m it holds (INV = true).  Evaluated at compile time: a wave reads its entries
+// from L2 instead of building the table per workgroup.
+template <int NS>
+struct GroupLut {
+  uint32_t v[NS * NS / 4];
+};
+template <int NS, bool INV>
+constexpr GroupLut<NS> make_group_lut() {
+  GroupLut<NS> t{};
+  for (uint32_t j = 0; j < (uint32_t)(NS * NS / 4); ++j) {
+    uint32_t code = 0, off = 0;
+    for (uint32_t m = 0; m < 4; ++m) {
+      uint32_t x = 0, y = 0;
+      d2xy(NS, 4 * j + m, x, y);
+      if (m == 0) off = (y & ~1u) * NS + (x & ~1u);
+      const uint32_t b = (x & 1u) + 2u * (y & 1u);
+      code |= INV ? (m << (2 * b)) : (b << (2 * m));
+    }
+    t.v[j] = off | (code << 16);
+  }
+  return t;
+}
+
 __host__ __device__ inline uint32_t xy2d(uint32_t n, uint32_t x, uint32_t y) {
   // _xy_to_hilbert_index (:68-90); the rotate uses the loop's s, values wrap in uint32 which only
   // disturbs bits at or above s — never looked at again (SURVEY.md §8a note).
@@ -257,6 +283,41 @@ inline int dtype_size(int dt) {
     case HQ_F64: case HQ_I64: return 8;
     default: return 0;
   }
+}
+
+// wave64 all-reduce through DPP (xor 1, xor 2, half-row mirror, row mirror) and four readlanes: no
+// LDS round trips on the per-embedding critical path
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lanef(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float wmin64(float v) {
+  v = fminf(v, dppf<0xB1>(v));
+  v = fminf(v, dppf<0x4E>(v));
+  v = fminf(v, dppf<0x141>(v));
+  v = fminf(v, dppf<0x140>(v));
+  return fminf(fminf(lanef(v, 0), lanef(v, 16)), fminf(lanef(v, 32), lanef(v, 48)));
+}
+__device__ __forceinline__ float wmax64(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  v = fmaxf(v, dppf<0x140>(v));
+  return fmaxf(fmaxf(lanef(v, 0), lanef(v, 16)), fmaxf(lanef(v, 32), lanef(v, 48)));
+}
+// Fast form of qz: y' = ((x - mn) * fl(1/rng)) * 255 differs from the reference's
+// fl(fl((x - mn) / rng) * 255) by < 1e-4 (two roundings of relative 2^-24 on a value <= 255), so
+// trunc(y') == trunc(y) whenever y' is more than 1e-3 away from an integer; otherwise `slow` is set
+// and the caller recomputes that element with the exact division.
+__device__ __forceinline__ uint32_t qfast(float x, float mn, float rcp, bool& slow) {
+  const float y = ((x - mn) * rcp) * 255.0f;
+  const float fl = floorf(y);
+  const float f = y - fl;
+  slow |= (f < 1e-3f) | (f > 0.999f);
+  return (uint32_t)fl;
 }
 
 }  // namespace hq

@@ -43,29 +43,6 @@ __device__ __forceinline__ double quad_bcast_xor1(double v) {  // value of lane 
   return __hiloint2double(hi, lo);
 }
 
-// wave64 all-reduce through DPP (xor 1, xor 2, half-row mirror, row mirror) and four readlanes: no
-// LDS round trips on the per-embedding critical path
-template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float lanef(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-__device__ __forceinline__ float wmin64(float v) {
-  v = fminf(v, dppf<0xB1>(v));
-  v = fminf(v, dppf<0x4E>(v));
-  v = fminf(v, dppf<0x141>(v));
-  v = fminf(v, dppf<0x140>(v));
-  return fminf(fminf(lanef(v, 0), lanef(v, 16)), fminf(lanef(v, 32), lanef(v, 48)));
-}
-__device__ __forceinline__ float wmax64(float v) {
-  v = fmaxf(v, dppf<0xB1>(v));
-  v = fmaxf(v, dppf<0x4E>(v));
-  v = fmaxf(v, dppf<0x141>(v));
-  v = fmaxf(v, dppf<0x140>(v));
-  return fmaxf(fmaxf(lanef(v, 0), lanef(v, 16)), fmaxf(lanef(v, 32), lanef(v, 48)));
-}
 // index row store with 16-byte lanes: even lanes write (slot 2k, slot 2k+1) — 8-byte stores leave
 // L2 at a much lower byte rate (MI355X_MICROARCH.md, store flavours); L even and 16-B aligned rows
 __device__ __forceinline__ void store_index(double* __restrict__ row, double val, int lane, int L) {
@@ -81,18 +58,6 @@ __device__ __forceinline__ uint32_t qz(float x, float mn, float rng) {
   t = t * 255.0f;
   return (uint32_t)t;
 }
-// Fast form of qz: y' = ((x - mn) * fl(1/rng)) * 255 differs from the reference's
-// fl(fl((x - mn) / rng) * 255) by < 1e-4 (two roundings of relative 2^-24 on a value <= 255), so
-// trunc(y') == trunc(y) whenever y' is more than 1e-3 away from an integer; otherwise `slow` is set
-// and the caller recomputes that element with the exact division.
-__device__ __forceinline__ uint32_t qfast(float x, float mn, float rcp, bool& slow) {
-  const float y = ((x - mn) * rcp) * 255.0f;
-  const float fl = floorf(y);
-  const float f = y - fl;
-  slow |= (f < 1e-3f) | (f > 0.999f);
-  return (uint32_t)fl;
-}
-
 typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld_stream(const float* p) {  // read-once stream: non-temporal
   const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
@@ -367,31 +332,9 @@ __global__ __launch_bounds__(64) void k_fused_fast(const float* __restrict__ in,
   }
 }
 
-// Group LUT (offset of the 2x2 block of float4 group j in the row-major frame | element order << 16),
-// evaluated at compile time so a non-persistent wave reads its six entries from L2 instead of building
-// the table per workgroup.
-template <int NS>
-struct GroupLut {
-  uint32_t v[NS * NS / 4];
-};
-template <int NS>
-constexpr GroupLut<NS> make_group_lut() {
-  GroupLut<NS> t{};
-  for (uint32_t j = 0; j < (uint32_t)(NS * NS / 4); ++j) {
-    uint32_t code = 0, off = 0;
-    for (uint32_t m = 0; m < 4; ++m) {
-      uint32_t x = 0, y = 0;
-      d2xy(NS, 4 * j + m, x, y);
-      if (m == 0) off = (y & ~1u) * NS + (x & ~1u);
-      code |= ((x & 1u) + 2u * (y & 1u)) << (2 * m);
-    }
-    t.v[j] = off | (code << 16);
-  }
-  return t;
-}
-__device__ constexpr GroupLut<16> kLut16 = make_group_lut<16>();
-__device__ constexpr GroupLut<32> kLut32 = make_group_lut<32>();
-__device__ constexpr GroupLut<64> kLut64 = make_group_lut<64>();
+__device__ constexpr GroupLut<16> kLut16 = make_group_lut<16, false>();
+__device__ constexpr GroupLut<32> kLut32 = make_group_lut<32, false>();
+__device__ constexpr GroupLut<64> kLut64 = make_group_lut<64, false>();
 template <int NS>
 __device__ __forceinline__ const uint32_t* group_lut() {
   if constexpr (NS == 16) return kLut16.v;

@@ -14,6 +14,8 @@
 // exactly below so the index values are bit-identical.
 #include "hq_common.h"
 
+#include <stdlib.h>
+
 namespace hq {
 
 // np.mean over a (h x w) block with leading dimension ld, NumPy order (hq_common.h np_sum):
@@ -144,6 +146,39 @@ __global__ __launch_bounds__(64) void k_trad_image(const float* __restrict__ img
   }
 }
 
+// Host: image cell (row-major offset in an n x n image) that output slot i samples, -1 for a zero
+// slot, -2 for a block-mean slot (same case analysis as trad_slot).
+static int trad_cell(int n, const TradPlan& p, int i) {
+  if (i >= p.produced) return -1;
+  for (int e = 0; e < p.cnt; ++e) {
+    if (i >= p.first[e] + p.count[e]) continue;
+    const int k = i - p.first[e], g = p.grid[e];
+    if (!p.sampling[e]) return -2;
+    int sec = n / g;
+    if (sec < 1) sec = 1;
+    const int sy = n / sec;
+    if (sy == 0) {
+      const int h = n, w = n;
+      const int cells[5] = {0, w - 1, (h - 1) * n, (h - 1) * n + w - 1, (h / 2) * n + w / 2};
+      return cells[k < 4 ? k : 4];
+    }
+    const int sidx = k / 5, which = k % 5;
+    const int r = sidx / sy, c = sidx % sy;
+    const int r0 = r * sec, r1 = r0 + sec, c0 = c * sec, c1 = c0 + sec;
+    const int cells[5] = {r0 * n + c0, r0 * n + c1 - 1, (r1 - 1) * n + c0, (r1 - 1) * n + c1 - 1,
+                          ((r0 + r1) / 2) * n + (c0 + c1) / 2};
+    return cells[which];
+  }
+  return -1;
+}
+
+// Slot plan of the fast chunk kernel: slots [0, fm) are 8 x 8 block means on a gm x gm block grid,
+// slots [fm, n) read cell[i] (or 0.0 when cell[i] < 0).
+struct ChunkPlan {
+  int16_t cell[64];
+  int fm, gm;
+};
+
 // ---------------------------------------------------------------------------------------------
 // config 5: chunked f16 stream -> map -> traditional index -> embed -> uint8 frame
 // one wave per chunk; image staged in LDS (f32, row-major)
@@ -243,6 +278,136 @@ __global__ __launch_bounds__(64) void k_chunk(const __half* __restrict__ src, in
   }
 }
 
+// Fast form for whole chunks of exactly NS x NS values (cfg5: 1024 -> 32 x 32): one chunk per wave,
+// WPB waves per workgroup, no persistent loop (the non-persistent shape streams ~10% faster on this
+// chip, tools/ubench/hbm_shapes.hip).  Each lane loads 16-byte runs of the f16 stream (two float4
+// groups = two 2x2 image blocks) and scatters them into the wave's LDS image with the compile-time
+// group LUT; the traditional index and the 16-byte frame stores follow k_chunk.
+__device__ constexpr GroupLut<32> kLut32 = make_group_lut<32, false>();
+__device__ constexpr GroupLut<64> kLut64 = make_group_lut<64, false>();
+
+__device__ __forceinline__ float2 h2f(uint32_t w) {
+  return make_float2(__half2float(__ushort_as_half((unsigned short)(w & 0xFFFFu))),
+                     __half2float(__ushort_as_half((unsigned short)(w >> 16))));
+}
+
+template <int NS, int WPB, bool FQ>
+__global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restrict__ src, int64_t nchunks,
+                                                       ChunkPlan plan, uint8_t* __restrict__ frame_out,
+                                                       float* __restrict__ idx_out, float* __restrict__ mm_out) {
+  constexpr int CELLS = NS * NS;
+  constexpr int NU = CELLS / 512;  // 16-byte loads per lane (8 values = two groups)
+  constexpr int FB = (NS + 1) * NS;
+  __shared__ __attribute__((aligned(16))) float img_all[WPB][CELLS];
+  __shared__ float rowv_all[WPB][NS];
+  __shared__ __attribute__((aligned(16))) uint8_t rowq_all[WPB][NS];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  float* img = img_all[wv];
+  float* rowv = rowv_all[wv];
+  const int64_t c = (int64_t)blockIdx.x * WPB + wv;
+  const bool live = c < nchunks;
+  const uint32_t* lut = NS == 32 ? kLut32.v : kLut64.v;
+  uint4 raw[NU];
+  uint32_t ent[2 * NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    raw[u] = live ? reinterpret_cast<const uint4*>(src + c * CELLS)[lane + 64 * u] : make_uint4(0, 0, 0, 0);
+    ent[2 * u] = lut[2 * (lane + 64 * u)];
+    ent[2 * u + 1] = lut[2 * (lane + 64 * u) + 1];
+  }
+  float lmin = __builtin_huge_valf(), lmax = -__builtin_huge_valf();
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float2 a = h2f(h ? raw[u].z : raw[u].x), b = h2f(h ? raw[u].w : raw[u].y);
+      lmin = fminf(lmin, fminf(fminf(a.x, a.y), fminf(b.x, b.y)));
+      lmax = fmaxf(lmax, fmaxf(fmaxf(a.x, a.y), fmaxf(b.x, b.y)));
+      // element m -> slot b = (code >> 2m) & 3 of the 2x2 block (forward LUT): four b32 LDS stores,
+      // no data-dependent selects
+      const uint32_t e = ent[2 * u + h], off = e & 0xFFFFu, code = e >> 16;
+      auto at = [&](uint32_t b) { return img + off + (b & 1u) + (b >> 1) * NS; };
+      *at(code & 3u) = a.x;
+      *at((code >> 2) & 3u) = a.y;
+      *at((code >> 4) & 3u) = b.x;
+      *at((code >> 6) & 3u) = b.y;
+    }
+  }
+  __syncthreads();
+  // first-level block means (slots < fm, 8 x 8 blocks in row-major block order): np.mean's pairwise
+  // order for 64 values is eight column accumulators r_j (rows in order), then
+  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)); four lanes per block hold two columns each and combine by
+  // xor-1 / xor-2 exchanges (IEEE addition is commutative, so both partners get the same bits).
+  const int gm = plan.gm, fm = plan.fm;
+  for (int r = 0; r < (fm + 15) / 16; ++r) {
+    const int b = (lane >> 2) + 16 * r, q = lane & 3;
+    const int bb = b < fm ? b : 0;
+    const float* blk = img + ((bb / gm) * 8) * NS + (bb % gm) * 8 + 2 * q;
+    float2 acc = *reinterpret_cast<const float2*>(blk);
+#pragma unroll
+    for (int row = 1; row < 8; ++row) {
+      const float2 v = *reinterpret_cast<const float2*>(blk + row * NS);
+      acc.x = acc.x + v.x;
+      acc.y = acc.y + v.y;
+    }
+    float t = acc.x + acc.y;
+    t = t + __shfl_xor(t, 1, 64);
+    t = t + __shfl_xor(t, 2, 64);
+    t = 0.0f + t;
+    if (q == 0 && b < fm) rowv[b] = (float)((double)t / 64.0);
+  }
+  if (lane >= fm && lane < NS) {
+    const int cell = plan.cell[lane];
+    rowv[lane] = cell >= 0 ? img[cell] : 0.0f;
+  }
+  __syncthreads();
+  if (lane < NS) {
+    const float iv = rowv[lane];
+    lmin = fminf(lmin, iv);
+    lmax = fmaxf(lmax, iv);
+    if (live) idx_out[c * NS + lane] = iv;
+  }
+  const float mn = wmin64(lmin), mx = wmax64(lmax);
+  if (!live) return;
+  const bool flat = mx == mn;
+  const float rng = mx - mn;
+  const float rcp = 1.0f / rng;
+  uint8_t* dst = frame_out + c * FB;
+  // one quantized byte: reciprocal form with an exact fallback per cell position (qfast, hq_common.h)
+  // — the IEEE division runs only where some lane's value lies within 1e-3 of a level edge
+  auto qb = [&](float x) -> uint32_t {
+    if constexpr (FQ) {
+      bool slow = false;
+      uint32_t v = qfast(x, mn, rcp, slow);
+      if (__builtin_amdgcn_ballot_w64(slow))
+        if (slow) v = q8(x, mn, rng);
+      return v;
+    } else {
+      return q8(x, mn, rng);
+    }
+  };
+  // image body: 16 cells per lane, 16-byte stores
+#pragma unroll
+  for (int q = lane; q < CELLS / 16; q += 64) {
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 f = *reinterpret_cast<const float4*>(img + 16 * q + 4 * k);
+      w[k] = flat ? 0x80808080u : qb(f.x) | (qb(f.y) << 8) | (qb(f.z) << 16) | (qb(f.w) << 24);
+    }
+    *reinterpret_cast<uint4*>(dst + 16 * q) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  // index row: one value per lane, bytes packed through LDS (rowv's own slot), 16-byte stores
+  uint8_t* rowq = rowq_all[wv];
+  if (lane < NS) rowq[lane] = flat ? (uint8_t)128 : (uint8_t)qb(rowv[lane]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane < NS / 16) *reinterpret_cast<uint4*>(dst + CELLS + 16 * lane) = reinterpret_cast<const uint4*>(rowq)[lane];
+  if (lane == 0) *reinterpret_cast<float2*>(mm_out + 2 * c) = make_float2(mn, mx);
+}
+
 // ---------------------------------------------------------------------------------------------
 // I4: RAG multi-row index
 // ---------------------------------------------------------------------------------------------
@@ -311,6 +476,40 @@ static int launch_chunk(const uint16_t* in, int64_t total, int chunk, int64_t c0
   int L = NS;  // min(1024, n) (core/streaming_processor.py:897-899)
   TradPlan plan;
   trad_plan(NS, L, plan);
+  if constexpr (NS == 32 || NS == 64) {
+    const bool aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(frame)) & 15) == 0 &&
+                         (reinterpret_cast<uintptr_t>(mm) & 7) == 0;
+    if (chunk == NS * NS && c0 == 0 && fstride == (int64_t)(NS + 1) * NS && istride == NS && aligned &&
+        !getenv("HQ_CHUNK_GENERIC")) {
+      constexpr int WPB = 2;
+      const int64_t grid = (c1 + WPB - 1) / WPB;
+      if (grid <= 0x7FFFFFFF) {
+        // slots [0, fm): first-level 8 x 8 block means (the only non-sampled level, index_generator.py:329-332);
+        // every later slot must be a sample or a zero, else the generic kernel runs
+        ChunkPlan cp{};
+        cp.fm = 0;
+        cp.gm = plan.cnt > 0 ? plan.grid[0] : 1;
+        if (plan.cnt > 0 && !plan.sampling[0] && plan.first[0] == 0 && plan.grid[0] > 0 && NS / plan.grid[0] == 8)
+          cp.fm = plan.count[0] < NS ? plan.count[0] : NS;
+        bool ok = true;
+        for (int i = 0; i < 64; ++i) {
+          const int cell = i < NS && i >= cp.fm ? trad_cell(NS, plan, i) : -1;
+          if (cell == -2) ok = false;
+          cp.cell[i] = (int16_t)cell;
+        }
+        if (ok) {
+          if (getenv("HQ_CHUNK_EXACTDIV"))
+            hipLaunchKernelGGL((k_chunk_np<NS, WPB, false>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in, c1, cp,
+                               frame, idx, mm);
+          else
+            hipLaunchKernelGGL((k_chunk_np<NS, WPB, true>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in, c1, cp,
+                               frame, idx, mm);
+          HQ_CHECK_LAUNCH();
+          return HQ_OK;
+        }
+      }
+    }
+  }
   int grid = persistent_grid((const void*)k_chunk<NS>, 64, 0, c1 - c0);
   hipLaunchKernelGGL(k_chunk<NS>, dim3(grid), dim3(64), 0, s, (const __half*)in, total, chunk, c0, c1, L, plan,
                      frame, fstride, idx, istride, mm);

@@ -183,10 +183,11 @@ def map_index_quantize(x, n: int, L: Optional[int] = None, want_idx: bool = True
     return frames, idx, mm
 
 
-def chunk_encode_f16(x, chunk: int = 1024, exc=None):
+def chunk_encode_f16(x, chunk: int = 1024, exc=None, out=None):
     """Config 5: flat f16 stream -> per-chunk (u8 frame, f32 traditional index, minmax)
     (core/streaming_processor.py:539-582, 877-913).  The last (shorter) chunk uses its own
-    geometry inside its slot; unused slot bytes are zero."""
+    geometry inside its slot; unused slot bytes are zero (when `out` is given, the caller's
+    buffers are written in place and unused tail-slot bytes are left as they are)."""
     t = torch()
     x1 = _contig(x.reshape(-1))
     if x1.dtype != t.float16:
@@ -195,9 +196,17 @@ def chunk_encode_f16(x, chunk: int = 1024, exc=None):
     from .core.dimension_calculator import _optimal_side
     ns = _optimal_side(chunk)
     nch = (total + chunk - 1) // chunk
-    frames = t.zeros((nch, ns + 1, ns), dtype=t.uint8, device=x1.device)
-    idx = t.zeros((nch, ns), dtype=t.float32, device=x1.device)
-    mm = t.zeros((nch, 2), dtype=t.float32, device=x1.device)
+    if out is not None:
+        frames, idx, mm = out
+        if (tuple(frames.shape) != (nch, ns + 1, ns) or tuple(idx.shape) != (nch, ns) or tuple(mm.shape) != (nch, 2)
+                or frames.dtype != t.uint8 or idx.dtype != t.float32 or mm.dtype != t.float32
+                or not (frames.is_contiguous() and idx.is_contiguous() and mm.is_contiguous())):
+            raise ValueError(f"out buffers must be contiguous u8 [{nch}, {ns + 1}, {ns}], f32 [{nch}, {ns}], "
+                             f"f32 [{nch}, 2]")
+    else:
+        frames = t.zeros((nch, ns + 1, ns), dtype=t.uint8, device=x1.device)
+        idx = t.zeros((nch, ns), dtype=t.float32, device=x1.device)
+        mm = t.zeros((nch, 2), dtype=t.float32, device=x1.device)
     _chk(_L().hq_chunk_encode_f16(ptr(x1), total, chunk, ptr(frames), ptr(idx), ptr(mm), stream()), exc)
     return frames, idx, mm
 

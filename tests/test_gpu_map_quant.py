@@ -284,6 +284,40 @@ def test_chunk_encoder_vs_oracle(hq_lib):
         assert mm[c, 0] == mn and mm[c, 1] == mx
 
 
+@pytest.mark.parametrize("chunk,nfull,tail", [(1024, 41, 512), (4096, 9, 2500), (1024, 8, 0)])
+@pytest.mark.parametrize("mode", ["fast", "exactdiv", "generic"])
+def test_chunk_encoder_shapes_vs_oracle(hq_lib, chunk, nfull, tail, mode, monkeypatch):
+    """Fast (one chunk per wave) and generic chunk kernels: odd chunk counts (a dead wave in the last
+    workgroup), 64 x 64 chunks, the cfg5 512-value tail, constant chunks, caller-provided buffers."""
+    from hq_mi355x import kernels as K
+    import torch
+    if mode == "generic":
+        monkeypatch.setenv("HQ_CHUNK_GENERIC", "1")
+    if mode == "exactdiv":
+        monkeypatch.setenv("HQ_CHUNK_EXACTDIV", "1")
+    rng = np.random.default_rng(chunk + nfull)
+    total = chunk * nfull + tail
+    x = (rng.standard_normal(total) * 0.02).astype(np.float16)
+    x[chunk:2 * chunk] = np.float16(0.5)          # constant chunk -> all 128
+    x[2 * chunk + 7] = np.float16(-65504.0)       # extreme value
+    n = O.optimal_dimensions(chunk)[0]
+    nch = nfull + (1 if tail else 0)
+    out = (torch.full((nch, n + 1, n), 7, dtype=torch.uint8, device="cuda"),
+           torch.zeros((nch, n), dtype=torch.float32, device="cuda"),
+           torch.zeros((nch, 2), dtype=torch.float32, device="cuda"))
+    fr, idx, mm = K.chunk_encode_f16(_t(x), chunk, out=out)
+    fr, idx, mm = _np(fr), _np(idx), _np(mm)
+    for c in range(nch):
+        ch = x[c * chunk:(c + 1) * chunk].astype(np.float32)
+        m = O.optimal_dimensions(len(ch))[0]
+        img = O.map_to_2d(ch, m)
+        ridx = O.traditional_index(img, m)
+        u8, mn, mx = O.normalize_u8(O.embed_index_row(img, ridx))
+        assert fr[c][: m + 1, :m].tobytes() == u8.tobytes(), c
+        assert idx[c][:m].tobytes() == ridx.tobytes(), c
+        assert mm[c, 0] == mn and mm[c, 1] == mx
+
+
 def test_pipeline_dropin_roundtrip(hq_lib):
     from hq_mi355x.api import HilbertQuantizer
     from hq_mi355x.exceptions import QuantizationError

@@ -11,11 +11,13 @@ from collections import defaultdict
 
 
 def short(name):
-    for key in ("k_fused_np", "k_fused_fast", "k_fused", "k_scan0", "k_sample_hist", "k_hist_tau", "k_scan", "k_seg_prepare", "k_refine", "k_merge", "k_chunk",
+    for key in ("k_fused_np", "k_fused_fast", "k_fused", "k_scan0", "k_sample_hist", "k_hist_tau", "k_scan", "k_seg_prepare", "k_refine", "k_merge", "k_chunk_np", "k_chunk",
                 "k_progressive_final", "k_rescore", "k_level_scores"):
         if key in name:
             if key == "k_fused_fast":
                 return "k_fused" + name.split("k_fused_fast<")[1].split(",")[0]
+            if key == "k_chunk_np":
+                return "k_chunk_np" + name.split("k_chunk_np<")[1].split(",")[0]
             if key == "k_fused_np":
                 return "k_fused_np" + name.split("k_fused_np<")[1].split(",")[0]
             return key
