@@ -308,15 +308,17 @@ __device__ __forceinline__ float wmax64(float v) {
   v = fmaxf(v, dppf<0x140>(v));
   return fmaxf(fmaxf(lanef(v, 0), lanef(v, 16)), fmaxf(lanef(v, 32), lanef(v, 48)));
 }
-// Fast form of qz: y' = ((x - mn) * fl(1/rng)) * 255 differs from the reference's
-// fl(fl((x - mn) / rng) * 255) by < 1e-4 (two roundings of relative 2^-24 on a value <= 255), so
-// trunc(y') == trunc(y) whenever y' is more than 1e-3 away from an integer; otherwise `slow` is set
-// and the caller recomputes that element with the exact division.
+// Fast form of qz: with d = fl(x - mn) >= 0 (shared by both forms), the reference's
+// y = fl(fl(d / rng) * 255) = Y (1+e1)(1+e2) and y' = fl(fl(d * fl(1/rng)) * 255) = Y (1+e3)(1+e4)(1+e5)
+// with Y = 255 d / rng <= 255 and |ei| <= 2^-24, so |y - y'| <= 255 * 5 * 2^-24 < 7.7e-5.  Hence
+// trunc(y') == trunc(y) whenever frac(y') lies in [1e-4, 1 - 1e-4] (frac is exact: y' - floor(y')
+// for y' < 2^23); otherwise `slow` is set and the caller recomputes that element with the exact
+// division.
 __device__ __forceinline__ uint32_t qfast(float x, float mn, float rcp, bool& slow) {
   const float y = ((x - mn) * rcp) * 255.0f;
   const float fl = floorf(y);
   const float f = y - fl;
-  slow |= (f < 1e-3f) | (f > 0.999f);
+  slow |= (f < 1e-4f) | (f > 0.9999f);
   return (uint32_t)fl;
 }
 

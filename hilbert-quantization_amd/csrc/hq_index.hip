@@ -291,7 +291,7 @@ __device__ __forceinline__ float2 h2f(uint32_t w) {
                      __half2float(__ushort_as_half((unsigned short)(w >> 16))));
 }
 
-template <int NS, int WPB, bool FQ>
+template <int NS, int WPB, bool FQ, int CPW>
 __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restrict__ src, int64_t nchunks,
                                                        ChunkPlan plan, uint8_t* __restrict__ frame_out,
                                                        float* __restrict__ idx_out, float* __restrict__ mm_out) {
@@ -305,17 +305,28 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
   const int wv = threadIdx.x >> 6;
   float* img = img_all[wv];
   float* rowv = rowv_all[wv];
-  const int64_t c = (int64_t)blockIdx.x * WPB + wv;
-  const bool live = c < nchunks;
+  const int64_t c0 = ((int64_t)blockIdx.x * WPB + wv) * CPW;
   const uint32_t* lut = NS == 32 ? kLut32.v : kLut64.v;
-  uint4 raw[NU];
+  // CPW chunks per wave, all loaded up front (more bytes in flight per wave)
+  uint4 raw_all[CPW][NU];
   uint32_t ent[2 * NU];
 #pragma unroll
+  for (int k = 0; k < CPW; ++k)
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+      raw_all[k][u] = c0 + k < nchunks ? reinterpret_cast<const uint4*>(src + (c0 + k) * CELLS)[lane + 64 * u]
+                                       : make_uint4(0, 0, 0, 0);
+#pragma unroll
   for (int u = 0; u < NU; ++u) {
-    raw[u] = live ? reinterpret_cast<const uint4*>(src + c * CELLS)[lane + 64 * u] : make_uint4(0, 0, 0, 0);
     ent[2 * u] = lut[2 * (lane + 64 * u)];
     ent[2 * u + 1] = lut[2 * (lane + 64 * u) + 1];
   }
+#pragma unroll
+  for (int k = 0; k < CPW; ++k) {
+  const int64_t c = c0 + k;
+  const bool live = c < nchunks;
+  if (WPB == 1 && !live) break;
+  const uint4* raw = raw_all[k];
   float lmin = __builtin_huge_valf(), lmax = -__builtin_huge_valf();
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
@@ -352,8 +363,8 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
       acc.y = acc.y + v.y;
     }
     float t = acc.x + acc.y;
-    t = t + __shfl_xor(t, 1, 64);
-    t = t + __shfl_xor(t, 2, 64);
+    t = t + dppf<0xB1>(t);  // quad_perm xor 1
+    t = t + dppf<0x4E>(t);  // quad_perm xor 2
     t = 0.0f + t;
     if (q == 0 && b < fm) rowv[b] = (float)((double)t / 64.0);
   }
@@ -369,7 +380,7 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
     if (live) idx_out[c * NS + lane] = iv;
   }
   const float mn = wmin64(lmin), mx = wmax64(lmax);
-  if (!live) return;
+  if (live) {
   const bool flat = mx == mn;
   const float rng = mx - mn;
   const float rcp = 1.0f / rng;
@@ -406,6 +417,9 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (lane < NS / 16) *reinterpret_cast<uint4*>(dst + CELLS + 16 * lane) = reinterpret_cast<const uint4*>(rowq)[lane];
   if (lane == 0) *reinterpret_cast<float2*>(mm_out + 2 * c) = make_float2(mn, mx);
+  }
+  if constexpr (CPW > 1) __syncthreads();  // the next chunk reuses the LDS image
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -470,6 +484,34 @@ static int optimal_side(int64_t count) {
   return (int)s;
 }
 
+// fast chunk kernel launch; HQ_E_UNSUPPORTED (nothing launched) when the slot plan does not fit it
+template <int NS, int WPB, int CPW = 1>
+static int launch_chunk_np(const uint16_t* in, int64_t nchunks, const TradPlan& plan, uint8_t* frame, float* idx,
+                           float* mm, hipStream_t s) {
+  const int64_t grid = (nchunks + WPB * CPW - 1) / (WPB * CPW);
+  if (grid > 0x7FFFFFFF) return HQ_E_UNSUPPORTED;
+  // slots [0, fm): first-level 8 x 8 block means (the only non-sampled level, index_generator.py:329-332);
+  // every later slot must be a sample or a zero, else the generic kernel runs
+  ChunkPlan cp{};
+  cp.fm = 0;
+  cp.gm = plan.cnt > 0 ? plan.grid[0] : 1;
+  if (plan.cnt > 0 && !plan.sampling[0] && plan.first[0] == 0 && plan.grid[0] > 0 && NS / plan.grid[0] == 8)
+    cp.fm = plan.count[0] < NS ? plan.count[0] : NS;
+  for (int i = 0; i < 64; ++i) {
+    const int cell = i < NS && i >= cp.fm ? trad_cell(NS, plan, i) : -1;
+    if (cell == -2) return HQ_E_UNSUPPORTED;
+    cp.cell[i] = (int16_t)cell;
+  }
+  if (getenv("HQ_CHUNK_EXACTDIV"))
+    hipLaunchKernelGGL((k_chunk_np<NS, WPB, false, CPW>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in, nchunks,
+                       cp, frame, idx, mm);
+  else
+    hipLaunchKernelGGL((k_chunk_np<NS, WPB, true, CPW>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in, nchunks,
+                       cp, frame, idx, mm);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
 template <int NS>
 static int launch_chunk(const uint16_t* in, int64_t total, int chunk, int64_t c0, int64_t c1, uint8_t* frame,
                         int64_t fstride, float* idx, int64_t istride, float* mm, hipStream_t s) {
@@ -481,33 +523,17 @@ static int launch_chunk(const uint16_t* in, int64_t total, int chunk, int64_t c0
                          (reinterpret_cast<uintptr_t>(mm) & 7) == 0;
     if (chunk == NS * NS && c0 == 0 && fstride == (int64_t)(NS + 1) * NS && istride == NS && aligned &&
         !getenv("HQ_CHUNK_GENERIC")) {
-      constexpr int WPB = 2;
-      const int64_t grid = (c1 + WPB - 1) / WPB;
-      if (grid <= 0x7FFFFFFF) {
-        // slots [0, fm): first-level 8 x 8 block means (the only non-sampled level, index_generator.py:329-332);
-        // every later slot must be a sample or a zero, else the generic kernel runs
-        ChunkPlan cp{};
-        cp.fm = 0;
-        cp.gm = plan.cnt > 0 ? plan.grid[0] : 1;
-        if (plan.cnt > 0 && !plan.sampling[0] && plan.first[0] == 0 && plan.grid[0] > 0 && NS / plan.grid[0] == 8)
-          cp.fm = plan.count[0] < NS ? plan.count[0] : NS;
-        bool ok = true;
-        for (int i = 0; i < 64; ++i) {
-          const int cell = i < NS && i >= cp.fm ? trad_cell(NS, plan, i) : -1;
-          if (cell == -2) ok = false;
-          cp.cell[i] = (int16_t)cell;
-        }
-        if (ok) {
-          if (getenv("HQ_CHUNK_EXACTDIV"))
-            hipLaunchKernelGGL((k_chunk_np<NS, WPB, false>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in, c1, cp,
-                               frame, idx, mm);
-          else
-            hipLaunchKernelGGL((k_chunk_np<NS, WPB, true>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in, c1, cp,
-                               frame, idx, mm);
-          HQ_CHECK_LAUNCH();
-          return HQ_OK;
-        }
-      }
+      // launch form (A/B: HQ_CHUNK_WPB waves per workgroup, HQ_CHUNK_CPW chunks per wave)
+      const char* wev = getenv("HQ_CHUNK_WPB");
+      const char* cev = getenv("HQ_CHUNK_CPW");
+      const int wpb = wev ? atoi(wev) : 1, cpw = cev ? atoi(cev) : 2;
+      int rc;
+      if (wpb == 2) rc = launch_chunk_np<NS, 2>(in, c1, plan, frame, idx, mm, s);
+      else if (wpb == 4) rc = launch_chunk_np<NS, 4>(in, c1, plan, frame, idx, mm, s);
+      else if (cpw == 4) rc = launch_chunk_np<NS, 1, 4>(in, c1, plan, frame, idx, mm, s);
+      else if (cpw == 2) rc = launch_chunk_np<NS, 1, 2>(in, c1, plan, frame, idx, mm, s);
+      else rc = launch_chunk_np<NS, 1, 1>(in, c1, plan, frame, idx, mm, s);
+      if (rc != HQ_E_UNSUPPORTED) return rc;
     }
   }
   int grid = persistent_grid((const void*)k_chunk<NS>, 64, 0, c1 - c0);

@@ -285,7 +285,7 @@ def test_chunk_encoder_vs_oracle(hq_lib):
 
 
 @pytest.mark.parametrize("chunk,nfull,tail", [(1024, 41, 512), (4096, 9, 2500), (1024, 8, 0)])
-@pytest.mark.parametrize("mode", ["fast", "exactdiv", "generic"])
+@pytest.mark.parametrize("mode", ["fast", "exactdiv", "generic", "cpw1", "cpw4", "wpb2"])
 def test_chunk_encoder_shapes_vs_oracle(hq_lib, chunk, nfull, tail, mode, monkeypatch):
     """Fast (one chunk per wave) and generic chunk kernels: odd chunk counts (a dead wave in the last
     workgroup), 64 x 64 chunks, the cfg5 512-value tail, constant chunks, caller-provided buffers."""
@@ -295,6 +295,10 @@ def test_chunk_encoder_shapes_vs_oracle(hq_lib, chunk, nfull, tail, mode, monkey
         monkeypatch.setenv("HQ_CHUNK_GENERIC", "1")
     if mode == "exactdiv":
         monkeypatch.setenv("HQ_CHUNK_EXACTDIV", "1")
+    if mode in ("cpw1", "cpw4"):
+        monkeypatch.setenv("HQ_CHUNK_CPW", mode[-1])
+    if mode == "wpb2":
+        monkeypatch.setenv("HQ_CHUNK_WPB", "2")
     rng = np.random.default_rng(chunk + nfull)
     total = chunk * nfull + tail
     x = (rng.standard_normal(total) * 0.02).astype(np.float16)
