@@ -1906,7 +1906,8 @@ static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
 // cost: histogram init and flush)
 static void sample_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, int& nqb, int& nchunks,
                             int64_t& chunk_len) {
-  stride = N >= 16 * 4096 ? 16 : (N / 4096 > 1 ? N / 4096 : 1);
+  const int64_t sd = getenv("HQ_SAMPLE_STRIDE") ? atoi(getenv("HQ_SAMPLE_STRIDE")) : 16;  // A/B knob
+  stride = N >= sd * 4096 ? sd : (N / 4096 > 1 ? N / 4096 : 1);
   S = (N + stride - 1) / stride;
   nqb = (Q + kQW - 1) / kQW;
   const int waves = getenv("HQ_SAMPLE_WAVES") ? atoi(getenv("HQ_SAMPLE_WAVES")) : 1024;

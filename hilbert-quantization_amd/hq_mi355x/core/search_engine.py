@@ -138,12 +138,39 @@ class IndexCorpus:
             ids, ov, lv = self.brute_force(queries, min(K_out, max(self.N, 1)))
             cnt = (ids >= 0).sum(dim=1).to(t.int32)
             return ids, ov, lv, cnt
-        s0, ids, cnt, best, bid = self.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)
+        # Whole pipeline queued first (scan, exact re-rank, re-score, final ranking); the one host sync
+        # comes last and checks whether any query needs the dense exact path (list not proven complete,
+        # or nothing passed the threshold -> first arg-max).  Those rows are recomputed and replaced.
+        if M + self.SLACK > MAX_FUSED_K:
+            s0, ids, cnt, best, bid = self.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)
+            oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
+            return oid, odet[..., 0], odet[..., 1:], ocnt
+        s0, ids, cnt, res = self._scan_refine(qp, 0, M, float(threshold), 1)
+        best = t.full((Q,), -float("inf"), dtype=t.float64, device=qp.Z.device)
+        bid = t.full((Q,), -1, dtype=t.int64, device=qp.Z.device)
+        oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
+        redo = (res == 0) | (cnt == 0)
+        if bool(redo.any()):
+            sel = t.nonzero(redo).view(-1)
+            s2, i2, b2, bi2 = self._dense(qp, sel, 0, M, float(threshold), 1)
+            sub = qp.rows(sel)
+            o2, d2, c2 = self._final(sub, s2, i2, b2, bi2, K_out)
+            oid[sel], odet[sel], ocnt[sel] = o2, d2, c2
+        return oid, odet[..., 0], odet[..., 1:], ocnt
+
+    def _scan_refine(self, qp, mode: int, k: int, thr: float, thr_mode: int):
+        """Fused scan (SLACK extra list entries) + exact re-rank; resolved[q] == 0 marks an unproven list."""
+        lo_mode = 0 if thr_mode == 0 else 1
+        asc, aid, _, _ = K.scan_topk(qp, self.prep, mode, k + self.SLACK, thr - self.EPS, lo_mode, self.id_base)
+        return K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, thr_mode, self.EPS, self.id_base)
+
+    def _final(self, qp, s0, ids, best, bid, K_out: int):
+        """Exact overall + per-level re-score of the survivors and of the arg-max, then the final ranking."""
+        Q = qp.N
         det = K.rescore(qp, self.prep, ids, self.id_base)
         bdet = K.rescore(qp, self.prep, bid.view(Q, 1), self.id_base).view(Q, -1)
-        oid, odet, ocnt = K.progressive_final(s0.unsqueeze(0), ids.unsqueeze(0), det.unsqueeze(0),
-                                              best.unsqueeze(0), bid.unsqueeze(0), bdet.unsqueeze(0), K_out)
-        return oid, odet[..., 0], odet[..., 1:], ocnt
+        return K.progressive_final(s0.unsqueeze(0), ids.unsqueeze(0), det.unsqueeze(0),
+                                   best.unsqueeze(0), bid.unsqueeze(0), bdet.unsqueeze(0), K_out)
 
     def frame_search(self, queries, max_results: int, threshold: float = 0.1):
         """core/video_search.py:215-264: level-0 sim > threshold (strict), stable sort, top-k."""
