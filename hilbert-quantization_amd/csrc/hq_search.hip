@@ -571,6 +571,7 @@ __device__ __forceinline__ double const0(bool zq, bool zc, double qm, double cm)
 }
 
 typedef float flt4 __attribute__((ext_vector_type(4)));
+typedef float flt2 __attribute__((ext_vector_type(2)));
 
 // Z operand type of the f64 contraction (v_mfma_f64_16x16x4f64, C/D row (lane>>4) + 4r).
 template <bool F32> struct ZOps;
@@ -1063,26 +1064,52 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
 #pragma unroll
     for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[1], qh[2 * h + u], acc[u], 0, 0, 0);
   };
-  // branch-free f32 filter of one half; bit 4u + r = pass of pair (query 16(2h+u)+j, row 4g+r)
-  auto filter_half = [&](const int h, const flt4* acc, const flt4* cst, const int rem) -> int {
-    int bits = 0;
+  // f32 filter of one half; bit 4u + r = pass of pair (query 16(2h+u)+j, row 4g+r).
+  // pass <=> th - base <= 0 or num >= (th - base) den  <=>  max(-R, num - R den) >= 0 with
+  // R = (th - margin) - base, where num - R den is one fma (its sign is exact).  The two queries of
+  // a half share the candidate statistics, so the arithmetic runs as packed f32 (v_pk_fma/mul/add)
+  // over the query pair.  Flagged queries get th = -inf (always pass), absent ones +inf (never);
+  // flagged candidates, absent queries and rows past the chunk end are applied as bit masks, only
+  // when some lane of the wave has a candidate pass (the common step ends after one ballot).
+  auto filter_half = [&](const int h, const flt4* acc, const flt4* cst, const int rem, const int fcm) -> int {
+    const int b0 = 2 * h, b1 = 2 * h + 1;
+    auto tq = [&](int b) {
+      return ((qvb >> b) & 1) == 0 ? __builtin_huge_valf()
+                                   : (((qsp >> b) & 1) != 0 ? -__builtin_huge_valf() : thl[b] - kMarginF);
+    };
+    const flt2 T2 = {tq(b0), tq(b1)};
+    const flt2 A2 = {qA[b0], qA[b1]}, B2 = {qB[b0], qB[b1]}, Q2 = {qQ[b0], qQ[b1]};
+    const flt2 c1v = {c1f, c1f}, k35 = {0.35f, 0.35f};
+    flt2 m[4];
+    float mx = -__builtin_huge_valf();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const bool inval = 4 * g + r >= rem;
-      const bool fc = __float_as_int(cst[r].w) != 0;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int b = 2 * h + u;
-        const float G = acc[u][r];
-        const float R = (thl[b] - kMarginF) - fmaf(G, c1f, 0.35f);
-        const float num = fmaf(G, qA[b] * cst[r].x, qB[b] * cst[r].y);
-        const float den = qQ[b] + cst[r].z;
-        const bool spec = fc | (((qsp >> b) & 1) != 0);
-        const bool p = ((R <= 0.0f) | (num >= R * den) | spec) & !inval & (((qvb >> b) & 1) != 0);
-        bits |= (int)p << (4 * u + r);
-      }
+      const flt2 G2 = {acc[0][r], acc[1][r]};
+      const flt2 X2 = A2 * cst[r].x;
+      const flt2 Y2 = B2 * cst[r].y;
+      const flt2 num = __builtin_elementwise_fma(G2, X2, Y2);
+      const flt2 den = Q2 + cst[r].z;
+      const flt2 R = T2 - __builtin_elementwise_fma(G2, c1v, k35);
+      const flt2 d = __builtin_elementwise_fma(-R, den, num);
+      m[r] = flt2{fmaxf(-R.x, d.x), fmaxf(-R.y, d.y)};
+      mx = fmaxf(mx, fmaxf(m[r].x, m[r].y));
     }
-    return bits;
+    if (!__ballot((mx >= 0.0f) | (fcm != 0))) return 0;
+    int bits = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bits |= ((int)(m[r].x >= 0.0f) << r) | ((int)(m[r].y >= 0.0f) << (4 + r));
+    bits |= fcm * 0x11;
+    const int nv = rem - 4 * g;  // rows of this lane group inside the chunk
+    const int rowm = nv >= 4 ? 0xF : (nv <= 0 ? 0 : (1 << nv) - 1);
+    const int qm = (((qvb >> b0) & 1) ? 0x0F : 0) | (((qvb >> b1) & 1) ? 0xF0 : 0);
+    return bits & (rowm * 0x11) & qm;
+  };
+  // bit r: candidate row 4g + r is flagged (zero variance / f32-unsafe / pad)
+  auto flag_mask = [&](const flt4* cst) {
+    int f = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f |= (int)(__float_as_int(cst[r].w) != 0) << r;
+    return f;
   };
   // List maintenance.  A query's list starts in APPEND mode: passing pairs are appended in parallel
   // (LDS atomic slot, no ordering) while the list has room; the pair that fills it sorts it (rank
@@ -1220,16 +1247,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
     flt4 cstn[4];
     load_frag(cs + kCS, cf1);
     load_stats(cs + kCS, cstn);
+    const int fcm = flag_mask(cst);
     if constexpr (NB == 4) {
       mfma_half(1, cf, acc1);
-      const int bits0 = filter_half(0, acc0, cst, rem);
+      const int bits0 = filter_half(0, acc0, cst, rem, fcm);
       if (__ballot(bits0 != 0)) insert_half(0, acc0, cst, cs, bits0);
       mfma_half(0, cf1, acc0);
-      const int bits1 = filter_half(1, acc1, cst, rem);
+      const int bits1 = filter_half(1, acc1, cst, rem, fcm);
       if (__ballot(bits1 != 0)) insert_half(1, acc1, cst, cs, bits1);
     } else {
       mfma_half(0, cf, acc0);
-      const int bits0 = filter_half(0, acc0, cst, rem);
+      const int bits0 = filter_half(0, acc0, cst, rem, fcm);
       if (__ballot(bits0 != 0)) insert_half(0, acc0, cst, cs, bits0);
     }
     cf[0] = cf1[0];
