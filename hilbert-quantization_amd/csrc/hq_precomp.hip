@@ -1,0 +1,440 @@
+// hq_precomp.hip — pre-computed overlapping-square Hilbert index.
+//
+// Reference: core/precomputed_hilbert_index.py
+//   :121-149 _calculate_granularity_levels  (square 2, 4, ... <= n/2, at most 6 levels, then (1, n))
+//   :151-212 _precompute_level_averages     (grid squares row-major, then the (g-1)^2 squares offset
+//                                            by half a square; float(np.mean(square)) -> float32)
+//   :411-466 _compare_precomputed_levels    (float32 correlation + distance similarity)
+//   :358-409 _calculate_precomputed_similarity (normalised level weights 0.4, 0.3, 0.2, 0.1, ...)
+// HilbertQuantizer.quantize builds this index for every model (api.py:162-173).
+//
+// np.mean over a square is NumPy's pairwise sum over the C-order-flattened square (hq_common.h
+// np_sum), so every average is bit-identical.  Squares of <= 128 values are one pairwise leaf (one
+// thread); larger squares (16 x 16 and up: powers of two) split into 128-value leaves whose partial
+// sums combine in a balanced binary tree — exactly NumPy's recursion for power-of-two lengths.
+//
+// One 256-thread workgroup per image: the image (or the Hilbert scatter of a 1-D parameter stream)
+// is staged in LDS, leaf sums and averages stay in LDS, and the T averages leave with coalesced
+// stores.
+#include "hq_common.h"
+
+namespace hq {
+
+constexpr int kPreMaxLevels = 8;
+constexpr int kPreThreads = 256;
+
+struct PreLevel {
+  int g, s, count, off;  // grid side, square side, squares, first output
+  int lsh;               // log2(s)
+  int leaf0;             // first leaf task of this level (levels with s*s > 128)
+};
+struct PrePlan {
+  int nlev, total, n_small, nleaves, lsh_n;
+  PreLevel lv[kPreMaxLevels];
+};
+
+// host: levels of _calculate_granularity_levels (max_levels, min_square_size as the reference's
+// defaults 6 and 2), outputs and leaf tasks
+static int pre_plan(int n, int max_levels, int min_sq, PrePlan& p) {
+  p.nlev = 0;
+  p.total = 0;
+  p.n_small = 0;
+  p.nleaves = 0;
+  p.lsh_n = ilog2(n);
+  int s = min_sq;
+  int lv_g[16], lv_s[16], c = 0;
+  while (s <= n / 2 && c < max_levels) {
+    const int g = n / s;
+    if (g >= 2) { lv_g[c] = g; lv_s[c] = s; ++c; }
+    s *= 2;
+  }
+  if (c == 0 || lv_s[c - 1] < n) { lv_g[c] = 1; lv_s[c] = n; ++c; }
+  if (c > kPreMaxLevels) return HQ_E_UNSUPPORTED;
+  for (int i = 0; i < c; ++i) {
+    PreLevel& L = p.lv[i];
+    L.g = lv_g[i];
+    L.s = lv_s[i];
+    L.lsh = ilog2(L.s);
+    if ((1 << L.lsh) != L.s) return HQ_E_UNSUPPORTED;
+    L.count = L.g * L.g + (L.s / 2 > 0 ? (L.g - 1) * (L.g - 1) : 0);
+    L.off = p.total;
+    p.total += L.count;
+    L.leaf0 = -1;
+    if (L.s * L.s <= 128) {
+      if (L.off != p.n_small) return HQ_E_UNSUPPORTED;  // small squares form a prefix (finest first)
+      p.n_small += L.count;
+    } else {
+      L.leaf0 = p.nleaves;
+      p.nleaves += L.count * (L.s * L.s / 128);
+    }
+  }
+  p.nlev = c;
+  return HQ_OK;
+}
+
+// top-left corner of square k of a level (grid squares row-major, then offset squares)
+__device__ __forceinline__ void pre_square(const PreLevel& L, int k, int& x0, int& y0) {
+  const int gg = L.g * L.g;
+  if (k < gg) {
+    y0 = (k / L.g) * L.s;
+    x0 = (k % L.g) * L.s;
+  } else {
+    k -= gg;
+    const int h = L.g - 1;
+    y0 = (k / h) * L.s + L.s / 2;
+    x0 = (k % h) * L.s + L.s / 2;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ float pre_mean(T s, int cnt) {
+  if constexpr (sizeof(T) == 4) return (float)((double)s / (double)cnt);  // np.mean f32 (_methods._mean)
+  else return (float)(s / (double)cnt);                                 // f64 mean, stored as float32
+}
+
+// kind 0: images (n x n row-major, image stride `stride` elements); kind 1: 1-D Hilbert-ordered
+// parameter streams of d values (row stride `stride`), zero-padded to n*n and mapped to 2-D
+// (core/pipeline.py:298-319 _get_2d_representation).
+template <typename T>
+__global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ in, int kind, int64_t N, int64_t stride,
+                                                         int d, int n, PrePlan plan, float* __restrict__ out,
+                                                         int64_t out_stride) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ PreLevel lv[kPreMaxLevels];  // per-thread level lookups index LDS, not the kernarg block
+  T* img = reinterpret_cast<T*>(smem);
+  T* part = img + n * n;
+  float* res = reinterpret_cast<float*>(part + plan.nleaves);
+  const int tid = threadIdx.x;
+  const int lsh_n = plan.lsh_n;
+  if (tid < plan.nlev) lv[tid] = plan.lv[tid];
+  for (int64_t e = blockIdx.x; e < N; e += gridDim.x) {
+    const T* src = in + e * stride;
+    if (kind == 0) {
+      for (int i = tid; i < n * n; i += kPreThreads) img[i] = src[i];
+    } else {
+      for (int i = tid; i < n * n; i += kPreThreads) {
+        uint32_t x, y;
+        d2xy((uint32_t)n, (uint32_t)i, x, y);
+        img[(y << lsh_n) + x] = i < d ? src[i] : T(0);
+      }
+    }
+    __syncthreads();
+    // squares of <= 128 values: one thread each
+    for (int a = tid; a < plan.n_small; a += kPreThreads) {
+      int l = 0;
+      while (a >= lv[l].off + lv[l].count) ++l;
+      const int s = lv[l].s, lsh = lv[l].lsh, msk = s - 1;
+      int x0, y0;
+      pre_square(lv[l], a - lv[l].off, x0, y0);
+      const T* b = img + (y0 << lsh_n) + x0;
+      auto f = [&](int k) -> T { return b[((k >> lsh) << lsh_n) + (k & msk)]; };
+      res[a] = pre_mean<T>(T(0) + pw_leaf<T>(f, 0, s * s), s * s);  // np_sum for <= 128 values
+    }
+    // 128-value leaves of the larger squares
+    for (int t = tid; t < plan.nleaves; t += kPreThreads) {
+      int l = plan.nlev - 1;
+      while (lv[l].leaf0 < 0 || t < lv[l].leaf0) --l;
+      const int s = lv[l].s, lsh = lv[l].lsh, msk = s - 1;
+      const int per = (s * s) >> 7;
+      const int k = (t - lv[l].leaf0) / per, leaf = (t - lv[l].leaf0) % per;
+      int x0, y0;
+      pre_square(lv[l], k, x0, y0);
+      const T* b = img + (y0 << lsh_n) + x0;
+      auto f = [&](int q) -> T { return b[((q >> lsh) << lsh_n) + (q & msk)]; };
+      part[t] = pw_leaf<T>(f, leaf << 7, 128);
+    }
+    // balanced binary tree over each large square's leaves, adjacent pairs first (NumPy's split at
+    // n/2 for n = 128 * 2^k is exactly this tree)
+    for (int w = 1; w < 128; w <<= 1) {
+      __syncthreads();
+      for (int t = tid; t < plan.nleaves; t += kPreThreads) {
+        int l = plan.nlev - 1;
+        while (lv[l].leaf0 < 0 || t < lv[l].leaf0) --l;
+        const int per = (lv[l].s * lv[l].s) >> 7;
+        const int i = (t - lv[l].leaf0) % per;
+        if (w < per && (i & (2 * w - 1)) == 0) part[t] = part[t] + part[t + w];
+      }
+    }
+    __syncthreads();
+    for (int a = plan.n_small + tid; a < plan.total; a += kPreThreads) {
+      int l = 0;
+      while (a >= lv[l].off + lv[l].count) ++l;
+      const int per = (lv[l].s * lv[l].s) >> 7;
+      res[a] = pre_mean<T>(T(0) + part[lv[l].leaf0 + (a - lv[l].off) * per], lv[l].s * lv[l].s);
+    }
+    __syncthreads();
+    float* o = out + e * out_stride;
+    for (int a = tid; a < plan.total; a += kPreThreads) o[a] = res[a];
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Similarity (_compare_precomputed_levels / _calculate_precomputed_similarity) in the reference's
+// float32 NumPy arithmetic.  Per vector and level (first m averages): mean, std (np.std: mean, then
+// pairwise sum of squared deviations), mean of squares, and the normalised array (a - mean) / std.
+// Per pair: corr = np.mean(qn * cn), mse = np.mean((q - c) ** 2), each a pairwise f32 sum divided as
+// f32(f64(sum) / m).  Result types follow Python: the general branch yields float32, the constant
+// branches (1.0 / 0.0 / 0.1) and the clamps Python floats; the weighted sum is float32 as soon as one
+// float32 term enters it (a Python float operand is cast to float32), else float64.
+// ------------------------------------------------------------------------------------------------
+struct SimLevels {
+  int nlev;
+  int off_q[kPreMaxLevels], off_c[kPreMaxLevels], m[kPreMaxLevels];
+  double w[kPreMaxLevels];  // normalised weights (Python floats)
+};
+
+template <class F>
+__device__ __forceinline__ float np_mean32(const F& f, int m) {
+  return (float)((double)np_sum<float>(f, m) / (double)m);
+}
+
+// stats [N, nlev, 3] = (mean, std, mean of squares); norm [N, T]: normalised averages (std != 0)
+__global__ __launch_bounds__(256) void k_pre_stats(const float* __restrict__ A, int64_t N, int64_t stride, int nlev,
+                                                   SimLevels L, int side, float* __restrict__ stats,
+                                                   float* __restrict__ norm) {
+  const int64_t total = N * nlev;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = t / nlev;
+    const int l = (int)(t % nlev);
+    const int m = L.m[l];
+    const int off = side == 0 ? L.off_q[l] : L.off_c[l];
+    const float* a = A + v * stride + off;
+    float* st = stats + t * 3;
+    if (m <= 0) {
+      st[0] = st[1] = st[2] = 0.0f;
+      continue;
+    }
+    const float mean = np_mean32([&](int k) { return a[k]; }, m);
+    const float var = np_mean32([&](int k) { const float dd = a[k] - mean; return dd * dd; }, m);
+    const float sd = sqrtf(var);
+    const float msq = np_mean32([&](int k) { return a[k] * a[k]; }, m);
+    st[0] = mean;
+    st[1] = sd;
+    st[2] = msq;
+    float* o = norm + v * stride + off;
+    if (sd != 0.0f)
+      for (int k = 0; k < m; ++k) o[k] = (a[k] - mean) / sd;
+  }
+}
+
+// out_overall [Q, N] f64 value, out_type [Q, N] (0: float32, 1: Python float), out_levels
+// [Q, N, nlev] f64 (may be null)
+__global__ __launch_bounds__(256) void k_pre_pairs(const float* __restrict__ Qa, const float* __restrict__ Qn,
+                                                   const float* __restrict__ Qs, int Qc, int64_t qstride,
+                                                   const float* __restrict__ Ca, const float* __restrict__ Cn,
+                                                   const float* __restrict__ Cs, int64_t N, int64_t cstride,
+                                                   SimLevels L, double* __restrict__ out_overall,
+                                                   uint8_t* __restrict__ out_type, double* __restrict__ out_levels) {
+  const int64_t total = (int64_t)Qc * N;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t qi = t / N, ci = t % N;
+    double acc = 0.0;
+    int acc_t = -1;  // -1: int 0 (nothing added yet), 0: float32, 1: Python float
+    for (int l = 0; l < L.nlev; ++l) {
+      const int m = L.m[l];
+      const float* qs = Qs + (qi * L.nlev + l) * 3;
+      const float* cs = Cs + (ci * L.nlev + l) * 3;
+      double sim;
+      int st;  // type of the level similarity
+      if (m <= 0) {
+        sim = 0.0;
+        st = 1;
+      } else if (qs[1] == 0.0f && cs[1] == 0.0f) {
+        sim = fabsf(qs[0] - cs[0]) < 1e-6f ? 1.0 : 0.0;  // Python float compared in float32 (NEP 50)
+        st = 1;
+      } else if (qs[1] == 0.0f || cs[1] == 0.0f) {
+        sim = 0.1;
+        st = 1;
+      } else {
+        const float* qa = Qa + qi * qstride + L.off_q[l];
+        const float* ca = Ca + ci * cstride + L.off_c[l];
+        const float* qn = Qn + qi * qstride + L.off_q[l];
+        const float* cn = Cn + ci * cstride + L.off_c[l];
+        const float corr = np_mean32([&](int k) { return qn[k] * cn[k]; }, m);
+        const float corr_sim = (corr + 1.0f) / 2.0f;
+        const float mse = np_mean32([&](int k) { const float dd = qa[k] - ca[k]; return dd * dd; }, m);
+        const float maxm = qs[2] + cs[2];
+        float ds;
+        if (maxm > 0.0f) {
+          ds = 1.0f - mse / maxm;
+          ds = ds > 0.0f ? ds : 0.0f;
+        } else {
+          ds = 1.0f;
+        }
+        const float comb = 0.7f * corr_sim + 0.3f * ds;
+        if (comb < 1.0f && comb > 0.0f) {
+          sim = comb;
+          st = 0;
+        } else {
+          sim = comb < 1.0f ? 0.0 : 1.0;
+          st = 1;
+        }
+      }
+      if (out_levels) out_levels[t * L.nlev + l] = sim;
+      // term = sim * w (float32 if sim is float32), then acc + term with Python/NEP 50 typing
+      const double term = st == 0 ? (double)((float)sim * (float)L.w[l]) : sim * L.w[l];
+      if (acc_t < 0) {
+        acc = term;
+        acc_t = st;
+      } else if (acc_t == 1 && st == 1) {
+        acc = acc + term;
+      } else {
+        acc = (double)((float)acc + (float)term);
+        acc_t = 0;
+      }
+    }
+    if (acc_t < 0) acc_t = 1;
+    double v = acc < 1.0 ? acc : 1.0;
+    if (!(acc < 1.0)) acc_t = 1;
+    if (!(v > 0.0)) { v = 0.0; acc_t = 1; }
+    out_overall[t] = v;
+    out_type[t] = (uint8_t)acc_t;
+  }
+}
+
+// Legacy compare_indices_at_level of the pre-computed engine (:468-496): np.std branches, np.allclose
+// for two constant vectors, else (np.corrcoef(q, c)[0, 1] + 1) / 2 (0.0 when NaN).  corrcoef goes
+// through np.cov's BLAS dot, whose summation order is not NumPy's pairwise order: the centred dot
+// products here are sequential fma chains (agreement ~1e-15 relative, not bit-exact).
+__global__ __launch_bounds__(256) void k_pearson(const double* __restrict__ q, const double* __restrict__ C, int64_t N,
+                                                 int m, double* __restrict__ out) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x) {
+    const double* x = C + c * m;
+    const double qm = np_sum<double>([=](int k) { return q[k]; }, m) / (double)m;
+    const double cm = np_sum<double>([=](int k) { return x[k]; }, m) / (double)m;
+    const double qs = sqrt(np_sum<double>([=](int k) { const double d = q[k] - qm; return d * d; }, m) / (double)m);
+    const double cs = sqrt(np_sum<double>([=](int k) { const double d = x[k] - cm; return d * d; }, m) / (double)m);
+    double r;
+    if (qs == 0.0 && cs == 0.0) {
+      bool close = true;  // np.allclose(q, c): |q - c| <= 1e-8 + 1e-5 |c|
+      for (int k = 0; k < m; ++k) close &= fabs(q[k] - x[k]) <= 1e-8 + 1e-5 * fabs(x[k]);
+      r = close ? 1.0 : 0.0;
+    } else if (qs == 0.0 || cs == 0.0) {
+      r = 0.1;
+    } else {
+      double c00 = 0.0, c11 = 0.0, c01 = 0.0;
+      for (int k = 0; k < m; ++k) {
+        const double a = q[k] - qm, b = x[k] - cm;
+        c00 = fma(a, a, c00);
+        c11 = fma(b, b, c11);
+        c01 = fma(a, b, c01);
+      }
+      const double f = 1.0 / (double)(m - 1);
+      double corr = (c01 * f) / sqrt(c00 * f) / sqrt(c11 * f);
+      corr = corr > 1.0 ? 1.0 : (corr < -1.0 ? -1.0 : corr);
+      r = corr == corr ? (corr + 1.0) / 2.0 : 0.0;
+    }
+    out[c] = r;
+  }
+}
+
+}  // namespace hq
+
+using namespace hq;
+
+extern "C" {
+
+int hq_precomputed_layout(int n, int max_levels, int min_square_size, int32_t* levels_out, int max_out) {
+  if (n <= 0 || !is_pow2(n) || max_levels <= 0 || min_square_size <= 0)
+    return fail(HQ_E_INVALID, "bad layout request n=%d", n);
+  PrePlan p;
+  if (pre_plan(n, max_levels, min_square_size, p) != HQ_OK) return fail(HQ_E_UNSUPPORTED, "layout n=%d", n);
+  for (int i = 0; i < p.nlev && i < max_out; ++i) {
+    levels_out[4 * i + 0] = p.lv[i].g;
+    levels_out[4 * i + 1] = p.lv[i].s;
+    levels_out[4 * i + 2] = p.lv[i].count;
+    levels_out[4 * i + 3] = p.lv[i].off;
+  }
+  return p.nlev;
+}
+
+int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t in_stride, int d, int n,
+                         int max_levels, int min_square_size, float* out, int64_t out_stride, hq_stream_t stream) {
+  if (N < 0 || n <= 0 || in_stride < 0) return fail(HQ_E_INVALID, "bad shape");
+  if (!is_pow2(n)) return fail(HQ_E_NOT_POW2, "Dimension must be a power of 2, got %d", n);
+  if (n > 128) return fail(HQ_E_UNSUPPORTED, "pre-computed index of a %dx%d image (n <= 128)", n, n);
+  if (kind != 0 && kind != 1) return fail(HQ_E_INVALID, "kind %d", kind);
+  if (kind == 1 && (d < 0 || d > n * n)) return fail(HQ_E_TOO_MANY, "%d values for a %dx%d image", d, n, n);
+  if (N == 0) return HQ_OK;
+  if (!in || !out) return fail(HQ_E_INVALID, "null buffer");
+  PrePlan p;
+  if (max_levels <= 0 || min_square_size <= 0) return fail(HQ_E_INVALID, "max_levels / min_square_size");
+  if (pre_plan(n, max_levels, min_square_size, p) != HQ_OK)
+    return fail(HQ_E_UNSUPPORTED, "layout n=%d max_levels=%d min_square_size=%d (power-of-two squares, <= 8 levels)",
+                n, max_levels, min_square_size);
+  if (out_stride < p.total) return fail(HQ_E_INVALID, "out_stride %lld < %d averages", (long long)out_stride, p.total);
+  const int64_t grid64 = N < 65536 * 4 ? N : 65536 * 4;
+  const int esz = dtype == HQ_F64 ? 8 : 4;
+  const size_t lds = (size_t)esz * (n * n + p.nleaves) + 4 * (size_t)p.total;
+  if (lds > 160 * 1024) return fail(HQ_E_UNSUPPORTED, "pre-computed index n=%d dtype %d needs %zu B of LDS", n, dtype, lds);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == HQ_F32) {
+    HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_precomp<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_precomp<float>, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const float*)in, kind, N,
+                       in_stride, d, n, p, out, out_stride);
+  } else if (dtype == HQ_F64) {
+    HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_precomp<double>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_precomp<double>, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const double*)in, kind,
+                       N, in_stride, d, n, p, out, out_stride);
+  } else {
+    return fail(HQ_E_UNSUPPORTED, "pre-computed index dtype %d (f32/f64)", dtype);
+  }
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+int hq_pearson_f64(const double* q, const double* C, int64_t N, int m, double* out, hq_stream_t stream) {
+  if (N < 0 || m <= 0) return fail(HQ_E_INVALID, "bad shape");
+  if (N == 0) return HQ_OK;
+  if (!q || !C || !out) return fail(HQ_E_INVALID, "null buffer");
+  int64_t blocks = (N + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_pearson, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, q, C, N, m, out);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+int hq_precomputed_stats(const float* avgs, int64_t N, int64_t stride, int nlev, const int32_t* offsets,
+                         const int32_t* counts, float* stats, float* norm, hq_stream_t stream) {
+  if (N < 0 || nlev <= 0 || nlev > kPreMaxLevels || !offsets || !counts) return fail(HQ_E_INVALID, "bad levels");
+  if (N == 0) return HQ_OK;
+  if (!avgs || !stats || !norm) return fail(HQ_E_INVALID, "null buffer");
+  SimLevels L{};
+  L.nlev = nlev;
+  for (int l = 0; l < nlev; ++l) { L.off_q[l] = offsets[l]; L.off_c[l] = offsets[l]; L.m[l] = counts[l]; }
+  int64_t blocks = (N * nlev + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(k_pre_stats, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, avgs, N, stride, nlev, L,
+                     0, stats, norm);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+int hq_precomputed_similarity(const float* q_avgs, const float* q_norm, const float* q_stats, int Q, int64_t q_stride,
+                              const float* c_avgs, const float* c_norm, const float* c_stats, int64_t N,
+                              int64_t c_stride, int nlev, const int32_t* q_offsets, const int32_t* c_offsets,
+                              const int32_t* counts, const double* weights, double* out_overall, uint8_t* out_type,
+                              double* out_levels, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || nlev <= 0 || nlev > kPreMaxLevels) return fail(HQ_E_INVALID, "bad shape");
+  if (!q_offsets || !c_offsets || !counts || !weights) return fail(HQ_E_INVALID, "null level table");
+  if (Q == 0 || N == 0) return HQ_OK;
+  if (!q_avgs || !q_norm || !q_stats || !c_avgs || !c_norm || !c_stats || !out_overall || !out_type)
+    return fail(HQ_E_INVALID, "null buffer");
+  SimLevels L{};
+  L.nlev = nlev;
+  for (int l = 0; l < nlev; ++l) {
+    L.off_q[l] = q_offsets[l];
+    L.off_c[l] = c_offsets[l];
+    L.m[l] = counts[l];
+    L.w[l] = weights[l];
+  }
+  int64_t blocks = ((int64_t)Q * N + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(k_pre_pairs, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, q_avgs, q_norm, q_stats,
+                     Q, q_stride, c_avgs, c_norm, c_stats, N, c_stride, L, out_overall, out_type, out_levels);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+}  // extern "C"

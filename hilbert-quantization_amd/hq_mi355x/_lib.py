@@ -62,6 +62,12 @@ SIGNATURES = {
     "hq_cosine_scores": (_i, [_p, _i, _p, _i64, _i, _p, _p]),
     "hq_select_topk": (_i, [_p, _i, _i64, _i, _d, _i, _i64, _p, _p, _p, _p, _p]),
     "hq_pair_scores_raw": (_i, [_p, _p, _i64, _i, _p, _p]),
+    "hq_precomputed_layout": (_i, [_i, _i, _i, _p, _i]),
+    "hq_precomputed_index": (_i, [_i, _i, _p, _i64, _i64, _i, _i, _i, _i, _p, _i64, _p]),
+    "hq_precomputed_stats": (_i, [_p, _i64, _i64, _i, _p, _p, _p, _p, _p]),
+    "hq_precomputed_similarity": (_i, [_p, _p, _p, _i, _i64, _p, _p, _p, _i64, _i64, _i, _p, _p, _p, _p, _p, _p,
+                                       _p, _p]),
+    "hq_pearson_f64": (_i, [_p, _p, _i64, _i, _p, _p]),
 }
 
 _lock = threading.Lock()

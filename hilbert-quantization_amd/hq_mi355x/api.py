@@ -8,12 +8,15 @@ BatchQuantizer adds the batched device path (one fused kernel for N embeddings).
 """
 from __future__ import annotations
 
+import logging
 import time
 from typing import List, Optional, Union
 
 import numpy as np
 
+from .config import SystemConfig, create_default_config
 from .core.dimension_calculator import PowerOf4DimensionCalculator
+from .core.precomputed_hilbert_index import PrecomputedHilbertIndexer, PrecomputedSimilaritySearchEngine
 from .core.pipeline import QuantizationPipeline, quantize_batch
 from .core.search_engine import IndexCorpus, ProgressiveSimilaritySearchEngine
 from .exceptions import QuantizationError, ReconstructionError, SearchError, ValidationError
@@ -21,21 +24,54 @@ from .models import QuantizedModel, SearchResult
 
 
 class HilbertQuantizer:
-    def __init__(self, similarity_threshold: float = 0.1, max_results: int = 10, compression_quality: float = 0.8,
-                 min_efficiency_ratio: float = 0.5):
-        self.similarity_threshold = similarity_threshold
-        self.max_results = max_results
-        self.compression_quality = compression_quality
-        self.min_efficiency_ratio = min_efficiency_ratio
+    """api.py:27-565 drop-in: HilbertQuantizer(config=None, use_precomputed_indexing=True).
+
+    The keyword-only arguments override single config fields (similarity_threshold, max_results,
+    compression_quality, min_efficiency_ratio) without building a SystemConfig."""
+
+    def __init__(self, config: Optional[SystemConfig] = None, use_precomputed_indexing: bool = True, *,
+                 similarity_threshold: Optional[float] = None, max_results: Optional[int] = None,
+                 compression_quality: Optional[float] = None, min_efficiency_ratio: Optional[float] = None):
+        self.config = config or create_default_config()
+        if similarity_threshold is not None:
+            self.config.search.similarity_threshold = similarity_threshold
+        if max_results is not None:
+            self.config.search.max_results = max_results
+        if compression_quality is not None:
+            self.config.compression.quality = compression_quality
+        if min_efficiency_ratio is not None:
+            self.config.quantization.min_efficiency_ratio = min_efficiency_ratio
+        self.use_precomputed_indexing = use_precomputed_indexing
         self._pipeline: Optional[QuantizationPipeline] = None
         self._engine: Optional[ProgressiveSimilaritySearchEngine] = None
+        self._precomputed_indexer: Optional[PrecomputedHilbertIndexer] = None
+        self._precomputed_search_engine: Optional[PrecomputedSimilaritySearchEngine] = None
         self._model_registry: List[QuantizedModel] = []
+        self.logger = logging.getLogger(__name__)
+
+    # reference-era attribute names
+    @property
+    def similarity_threshold(self) -> float:
+        return self.config.search.similarity_threshold
+
+    @property
+    def max_results(self) -> int:
+        return self.config.search.max_results
+
+    @property
+    def compression_quality(self) -> float:
+        return self.config.compression.quality
+
+    @property
+    def min_efficiency_ratio(self) -> float:
+        return self.config.quantization.min_efficiency_ratio
 
     @property
     def quantization_pipeline(self) -> QuantizationPipeline:
         if self._pipeline is None:
             self._pipeline = QuantizationPipeline(
-                dimension_calculator=PowerOf4DimensionCalculator(self.min_efficiency_ratio))
+                dimension_calculator=PowerOf4DimensionCalculator(self.min_efficiency_ratio),
+                compression_config=self.config.compression)
         return self._pipeline
 
     @property
@@ -43,6 +79,19 @@ class HilbertQuantizer:
         if self._engine is None:
             self._engine = ProgressiveSimilaritySearchEngine(self.similarity_threshold, self.max_results * 2)
         return self._engine
+
+    @property
+    def precomputed_indexer(self) -> PrecomputedHilbertIndexer:
+        if self._precomputed_indexer is None:
+            self._precomputed_indexer = PrecomputedHilbertIndexer()
+        return self._precomputed_indexer
+
+    @property
+    def precomputed_search_engine(self) -> PrecomputedSimilaritySearchEngine:
+        if self._precomputed_search_engine is None:
+            self._precomputed_search_engine = PrecomputedSimilaritySearchEngine(
+                self.precomputed_indexer, similarity_threshold=self.similarity_threshold)
+        return self._precomputed_search_engine
 
     @staticmethod
     def _validate_parameters(p):
@@ -65,6 +114,13 @@ class HilbertQuantizer:
             qm = self.quantization_pipeline.quantize_model(parameters, model_id or f"model_{int(time.time())}",
                                                            compression_quality=self.compression_quality,
                                                            model_architecture=description)
+            if self.use_precomputed_indexing:  # api.py:162-173
+                try:
+                    image_2d = self.quantization_pipeline._get_2d_representation(parameters)
+                    pre = self.precomputed_indexer.create_precomputed_index(image_2d, qm.metadata.model_name)
+                    self.logger.info(f"Pre-computed index created: {pre.total_storage_bytes / 1024:.1f}KB")
+                except Exception as e:  # the reference continues without the index
+                    self.logger.warning(f"Failed to create pre-computed index: {e}")
             self._model_registry.append(qm)
             return qm
         except (QuantizationError, ValidationError):

@@ -93,6 +93,15 @@ class QuantizationPipeline:
         except Exception as e:
             raise HilbertQuantizationError(f"Failed to quantize model '{model_name}': {e}")
 
+    def _get_2d_representation(self, parameters):
+        """core/pipeline.py:298-323: pad + Hilbert map (the image the pre-computed index is built on)."""
+        try:
+            dims = self.dimension_calculator.calculate_optimal_dimensions(len(parameters))
+            pc = self.dimension_calculator.calculate_padding_strategy(len(parameters), dims)
+            return self.hilbert_mapper.map_to_2d(self._pad_parameters(parameters, dims, pc), dims)
+        except Exception as e:
+            raise HilbertQuantizationError(f"Failed to get 2D representation: {e}")
+
     def reconstruct_parameters(self, quantized_model: QuantizedModel):
         try:
             enhanced = self.compressor.decompress(quantized_model.compressed_data)

@@ -392,3 +392,83 @@ def pair_scores_raw(q, C, exc=None):
     out = t.empty(N, dtype=t.float64, device=C2.device)
     _chk(_L().hq_pair_scores_raw(ptr(q1), ptr(C2), N, m, ptr(out), stream()), exc)
     return out
+
+
+# ------------------------------------------------------------------- §8f row 3: pre-computed index
+
+
+def precomputed_layout(n: int, max_levels: int = 6, min_square_size: int = 2, exc=None):
+    """[(grid, square, count, first_output)] of core/precomputed_hilbert_index.py:121-212 (library)."""
+    buf = (ctypes.c_int32 * 64)()
+    k = _L().hq_precomputed_layout(int(n), int(max_levels), int(min_square_size), buf, 16)
+    if k < 0:
+        _chk(k, exc)
+    return [(buf[4 * i], buf[4 * i + 1], buf[4 * i + 2], buf[4 * i + 3]) for i in range(min(k, 16))]
+
+
+def precomputed_index(x, n: int, kind: int = 0, d: Optional[int] = None, max_levels: int = 6,
+                      min_square_size: int = 2, exc=None):
+    """Overlapping-square averages f32 [N, T] (core/precomputed_hilbert_index.py:65-212).
+    kind 0: x = images [N, n, n] (f32/f64); kind 1: x = 1-D Hilbert-ordered parameters [N, d] (f32/f64),
+    zero-padded to n*n and mapped to 2-D first (core/pipeline.py:298-319)."""
+    t = torch()
+    if kind == 0:
+        x2 = _contig(x.view(-1, n * n) if x.dim() != 2 or x.shape[1] != n * n else x)
+        dd = n * n
+    else:
+        x2 = x.view(1, -1) if x.dim() == 1 else x
+        if x2.stride(-1) != 1:
+            x2 = x2.contiguous()
+        dd = int(x2.shape[1]) if d is None else int(d)
+    N = int(x2.shape[0])
+    lay = precomputed_layout(n, max_levels, min_square_size, exc)
+    T = sum(c for (_, _, c, _) in lay)
+    out = t.empty((N, T), dtype=t.float32, device=x2.device)
+    stride = x2.stride(0) if N > 1 else x2.shape[1]
+    _chk(_L().hq_precomputed_index(dtype_code(x2.dtype), int(kind), ptr(x2), N, stride, dd, int(n), int(max_levels),
+                                   int(min_square_size), ptr(out), T, stream()), exc)
+    return out
+
+
+def precomputed_stats(avgs, offsets, counts, exc=None):
+    """Per row and level: stats f32 [N, nlev, 3] (np.mean, np.std, np.mean(a**2)) and the normalised
+    averages [N, T] ((a - mean) / std where std != 0) for the first counts[l] values of each level."""
+    t = torch()
+    a = _contig(avgs)
+    N, T = a.shape
+    nlev = len(offsets)
+    off = (ctypes.c_int32 * nlev)(*offsets)
+    cnt = (ctypes.c_int32 * nlev)(*counts)
+    st = t.empty((N, nlev, 3), dtype=t.float32, device=a.device)
+    nrm = t.zeros_like(a)
+    _chk(_L().hq_precomputed_stats(ptr(a), N, T, nlev, off, cnt, ptr(st), ptr(nrm), stream()), exc)
+    return st, nrm
+
+
+def precomputed_similarity(qa, qn, qs, ca, cn, cs, q_offsets, c_offsets, counts, weights, levels: bool = False,
+                           exc=None):
+    """_calculate_precomputed_similarity for Q x N pairs -> (overall f64 [Q, N], type u8 [Q, N]
+    (0 numpy float32, 1 Python float), level sims f64 [Q, N, nlev] or None)."""
+    t = torch()
+    Q, N = int(qa.shape[0]), int(ca.shape[0])
+    nlev = len(counts)
+    ov = t.empty((Q, N), dtype=t.float64, device=qa.device)
+    ty = t.empty((Q, N), dtype=t.uint8, device=qa.device)
+    lv = t.empty((Q, N, nlev), dtype=t.float64, device=qa.device) if levels else None
+    _chk(_L().hq_precomputed_similarity(ptr(qa), ptr(qn), ptr(qs), Q, qa.shape[1], ptr(ca), ptr(cn), ptr(cs), N,
+                                        ca.shape[1], nlev, (ctypes.c_int32 * nlev)(*q_offsets),
+                                        (ctypes.c_int32 * nlev)(*c_offsets), (ctypes.c_int32 * nlev)(*counts),
+                                        (ctypes.c_double * nlev)(*weights), ptr(ov), ptr(ty),
+                                        ptr(lv) if lv is not None else None, stream()), exc)
+    return ov, ty, lv
+
+
+def pearson_f64(q, C, exc=None):
+    """Legacy compare_indices_at_level of the pre-computed engine (:468-496) for q [m] vs C [N, m]."""
+    t = torch()
+    q1 = _contig(q.reshape(-1))
+    C2 = _contig(C)
+    N, m = C2.shape
+    out = t.empty(N, dtype=t.float64, device=C2.device)
+    _chk(_L().hq_pearson_f64(ptr(q1), ptr(C2), N, m, ptr(out), stream()), exc)
+    return out

@@ -235,6 +235,42 @@ int hq_pair_scores_raw(const double* q, const double* C, int64_t N, int m, doubl
 int hq_cosine_scores(const float* a, int Q, const float* b, int64_t N, int K, double* out,
                      hq_stream_t stream);
 
+/* ---- §8f row 3: pre-computed overlapping-square index ---------------------------------------
+ * replaces core/precomputed_hilbert_index.py:65-212 PrecomputedHilbertIndexer.
+ * create_precomputed_index (built for every model by HilbertQuantizer.quantize, api.py:162-173).
+ * hq_precomputed_layout: levels of _calculate_granularity_levels (:121-149) as int32 quadruples
+ *   (grid, square, count, first output) into levels_out[4*max_out]; returns the level count.
+ * hq_precomputed_index: N inputs -> float32 averages [N, T] (row stride out_stride >= T), levels
+ *   finest first, each level = grid squares row-major then the half-offset squares; every value is
+ *   float32(np.mean(square)) bit for bit.  kind 0: n x n images (dtype HQ_F32 / HQ_F64, image
+ *   stride in_stride elements); kind 1: 1-D Hilbert-ordered streams of d <= n*n values, zero
+ *   padded (core/pipeline.py:298-319 _get_2d_representation).  n: power of two <= 128 (f64: <= 64);
+ *   max_levels / min_square_size as PrecomputedHilbertIndexer's constructor (defaults 6, 2).        */
+int hq_precomputed_layout(int n, int max_levels, int min_square_size, int32_t* levels_out, int max_out);
+int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t in_stride, int d, int n,
+                         int max_levels, int min_square_size, float* out, int64_t out_stride, hq_stream_t stream);
+/* hq_precomputed_stats: per vector and level l (averages [offsets[l], offsets[l] + counts[l]) of
+ *   each row of avgs, row stride `stride`): stats [N, nlev, 3] float32 = (np.mean, np.std,
+ *   np.mean(a**2)) in NumPy's order, and norm (same layout as avgs) = (a - mean) / std where std != 0.
+ *   Call it with counts = min(query count, candidate count) per level (the reference truncates,
+ *   :427-431).
+ * hq_precomputed_similarity: replaces :358-466 (_calculate_precomputed_similarity over
+ *   _compare_precomputed_levels) for Q x N pairs: out_overall [Q, N] (float64 holding the exact
+ *   value), out_type [Q, N] (0: the reference returns a numpy float32, 1: a Python float — decides
+ *   the `>= similarity_threshold` comparison, :342), out_levels [Q, N, nlev] (nullable).  weights:
+ *   the normalised level weights (Python floats, :390-404).                                      */
+/* hq_pearson_f64: replaces :468-496 (PrecomputedSimilaritySearchEngine.compare_indices_at_level, the
+ *   legacy np.corrcoef comparison) for one query q[m] against N rows of C [N, m] -> out [N] f64;
+ *   np.std branches and np.allclose exact, the correlation within ~1e-15 (BLAS order in np.cov). */
+int hq_pearson_f64(const double* q, const double* C, int64_t N, int m, double* out, hq_stream_t stream);
+int hq_precomputed_stats(const float* avgs, int64_t N, int64_t stride, int nlev, const int32_t* offsets,
+                         const int32_t* counts, float* stats, float* norm, hq_stream_t stream);
+int hq_precomputed_similarity(const float* q_avgs, const float* q_norm, const float* q_stats, int Q, int64_t q_stride,
+                              const float* c_avgs, const float* c_norm, const float* c_stats, int64_t N,
+                              int64_t c_stride, int nlev, const int32_t* q_offsets, const int32_t* c_offsets,
+                              const int32_t* counts, const double* weights, double* out_overall, uint8_t* out_type,
+                              double* out_levels, hq_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

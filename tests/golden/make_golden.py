@@ -275,13 +275,76 @@ def rag_score_fixtures(hq):
     return out
 
 
+def precomputed_fixtures(hq):
+    """core/precomputed_hilbert_index.py: overlapping-square averages and the f32 level similarity."""
+    import contextlib
+    import io
+    from hilbert_quantization.core.precomputed_hilbert_index import (
+        PrecomputedHilbertIndexer, PrecomputedSimilaritySearchEngine)
+    from hilbert_quantization.core.hilbert_mapper import HilbertCurveMapper
+    rng = np.random.default_rng(77)
+    out = {}
+    ix = PrecomputedHilbertIndexer()
+    imgs = {}
+    for n in [2, 4, 8, 16, 32, 64, 128]:
+        imgs[f"n{n}"] = (rng.standard_normal((n, n)) * rng.uniform(0.1, 3)).astype(np.float32)
+    p = rng.standard_normal(1536).astype(np.float32)
+    padded = np.zeros(4096, dtype=np.float32)
+    padded[:1536] = p
+    imgs["pad1536"] = HilbertCurveMapper().map_to_2d(padded, (64, 64))
+    imgs["const32"] = np.full((32, 32), 0.25, dtype=np.float32)
+    imgs["f64_16"] = rng.standard_normal((16, 16))
+    for name, img in imgs.items():
+        with contextlib.redirect_stdout(io.StringIO()):
+            idx = ix.create_precomputed_index(img, name)
+        out[f"img_{name}"] = img
+        out[f"avg_{name}"] = np.concatenate([lv.averages for lv in idx.levels])
+        out[f"meta_{name}"] = np.array([[lv.grid_size, lv.square_size, lv.num_squares] for lv in idx.levels],
+                                       dtype=np.int64)
+        out[f"xy_{name}"] = np.array([xy for lv in idx.levels for xy in lv.square_coordinates], dtype=np.int64)
+        out[f"bytes_{name}"] = np.array(idx.total_storage_bytes, dtype=np.int64)
+    # similarity: query 64x64 image against noisy copies, a constant image, a negated image
+    eng = PrecomputedSimilaritySearchEngine(ix)
+    base = imgs["pad1536"]
+    cands = [base, base + rng.normal(0, 0.05, base.shape).astype(np.float32),
+             base + rng.normal(0, 0.5, base.shape).astype(np.float32), -base,
+             np.full((64, 64), 0.1, dtype=np.float32), rng.standard_normal((64, 64)).astype(np.float32),
+             base * 2.0 + 1.0, np.zeros((64, 64), dtype=np.float32)]
+    with contextlib.redirect_stdout(io.StringIO()):
+        qi = ix.create_precomputed_index(base, "q")
+        cis = [ix.create_precomputed_index(c.astype(np.float32), f"c{i}") for i, c in enumerate(cands)]
+    out["sim_cands"] = np.stack([c.astype(np.float32) for c in cands])
+    sims, types, lev = [], [], []
+    for ci in cis:
+        v = eng._calculate_precomputed_similarity(qi, ci)
+        sims.append(float(v))
+        types.append(0 if isinstance(v, np.floating) and v.dtype == np.float32 else 1)
+        lev.append([float(eng._compare_precomputed_levels(a, b)) for a, b in zip(qi.levels, ci.levels)])
+    out["sim_overall"] = np.array(sims)
+    out["sim_type"] = np.array(types, dtype=np.int64)
+    out["sim_levels"] = np.array(lev)
+    # constant-vs-constant level branch within 1e-6 (float32 comparison) and the 0.1 branch
+    a = np.full(5, 0.5, dtype=np.float32)
+    out["lvl_const_pairs"] = np.array([0.5, 0.5000005, 0.500001, 0.6], dtype=np.float32)
+    from hilbert_quantization.core.precomputed_hilbert_index import PrecomputedLevel
+    lv = lambda arr: PrecomputedLevel(2, 2, len(arr), arr, [])  # noqa: E731
+    out["lvl_const_vals"] = np.array([float(eng._compare_precomputed_levels(lv(a), lv(np.full(5, v, dtype=np.float32))))
+                                      for v in out["lvl_const_pairs"]])
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default="", help="comma-separated fixture names to (re)generate")
     a = ap.parse_args()
     hq = _import_reference(a.ref)
+    only = set(filter(None, a.only.split(",")))
     for name, fn in [("mapper", mapper_fixtures), ("index", index_fixtures), ("quant", quant_fixtures),
-                     ("search", search_fixtures), ("rag_score", rag_score_fixtures)]:
+                     ("search", search_fixtures), ("rag_score", rag_score_fixtures),
+                     ("precomputed", precomputed_fixtures)]:
+        if only and name not in only:
+            continue
         d = fn(hq)
         path = os.path.join(HERE, f"{name}.npz")
         np.savez_compressed(path, **d)

@@ -213,3 +213,38 @@ def test_rag_scoring_golden(golden):
     np.testing.assert_allclose(O.rag_granularity_weights(5), g["ml_w5"], atol=1e-15)
     got = O.rag_multi_level_similarity(g["ml_Q"], g["ml_C"])
     np.testing.assert_allclose(got, g["ml"], atol=1e-12)
+
+
+# ---------------------------------------------------------------- §8f row 3: pre-computed index
+
+PRE_NAMES = ["n2", "n4", "n8", "n16", "n32", "n64", "n128", "pad1536", "const32", "f64_16"]
+
+
+@pytest.mark.parametrize("name", PRE_NAMES)
+def test_precomputed_index_golden(golden, name):
+    g = golden("precomputed")
+    img = g[f"img_{name}"]
+    avg, meta = O.precomputed_index(img)
+    assert avg[0].tobytes() == g[f"avg_{name}"].tobytes()
+    assert [(a, b, c) for (a, b, c, _) in meta] == [tuple(r) for r in g[f"meta_{name}"]]
+    n = img.shape[0]
+    xy = [xy for (gg, s, _, _) in meta for xy in O.precomputed_squares(n, gg, s)]
+    assert np.array_equal(np.array(xy, dtype=np.int64).reshape(-1, 2), g[f"xy_{name}"].reshape(-1, 2))
+    # storage accounting (:98): averages bytes + 16 per coordinate pair
+    assert int(g[f"bytes_{name}"]) == sum(4 * c + 16 * c for (_, _, c, _) in meta)
+
+
+def test_precomputed_similarity_golden(golden):
+    g = golden("precomputed")
+    q, _ = O.precomputed_index(g["img_pad1536"])
+    C, meta = O.precomputed_index(g["sim_cands"])
+    ql = [q[0, o:o + c] for (_, _, c, o) in meta]
+    for i in range(len(C)):
+        cl = [C[i, o:o + c] for (_, _, c, o) in meta]
+        ov, sims = O.precomputed_similarity(ql, cl)
+        assert float(ov) == g["sim_overall"][i], i
+        assert (0 if isinstance(ov, np.float32) else 1) == g["sim_type"][i], i
+        assert [float(s) for s in sims] == list(g["sim_levels"][i]), i
+    a = np.full(5, 0.5, dtype=np.float32)
+    for v, want in zip(g["lvl_const_pairs"], g["lvl_const_vals"]):
+        assert float(O.precomputed_level_similarity(a, np.full(5, v, dtype=np.float32))) == want
