@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--search-steps", type=int, default=5)
     ap.add_argument("--no-search", action="store_true")
     ap.add_argument("--no-stream", action="store_true")
+    ap.add_argument("--no-precomputed", action="store_true")
     ap.add_argument("--stream-values", type=int, default=7_000_000_000)
     ap.add_argument("--stream-steps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
@@ -130,6 +131,36 @@ def cpu_baseline_search(C, Q, seconds):
             "cores": 1, "kind": "port",
             "sample": f"{done} queries x {len(C)} candidates, oracle progressive_search (NumPy, single thread) "
                       f"in {dt:.1f}s, linear in corpus size"}
+
+
+def bench_precomputed(args, X, world):
+    """the pre-computed overlapping-square index HilbertQuantizer.quantize builds per
+    model (api.py:162-173, core/precomputed_hilbert_index.py:65-212), batched over the cfg2 embeddings:
+    pad + Hilbert map in LDS, 2,610 float32 square averages per 64x64 image (hq_precomputed_index)."""
+    from hq_mi355x import kernels as K
+    N, d = X.shape
+    n = 64
+    lay = K.precomputed_layout(n)
+    T = sum(c for (_, _, c, _) in lay)
+    out = torch.empty((N, T), dtype=torch.float32, device=X.device)
+    stride = X.stride(0)
+
+    def step():
+        from hq_mi355x import _lib
+        from hq_mi355x._dev import ptr, stream
+        _lib.check(_lib.lib().hq_precomputed_index(0, 1, ptr(X), N, stride, d, n, 6, 2, ptr(out), T, stream()))
+
+    wall, kern = timed(step, max(2, args.steps // 4), 1, world)
+    steps = max(2, args.steps // 4)
+    per = 4 * d + 4 * T
+    achieved = per * N / kern / 1e9
+    del out
+    return {"metric": "embeddings/sec pre-computed square-average index (1536D -> 64x64, 2,610 averages)",
+            "value": N * world * steps / wall, "unit": "embeddings/sec", "steps": steps,
+            "ms_per_step": wall / steps * 1e3, "scaling": "weak",
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("k_precomp"),
+                         "algorithmic_bytes_per_embedding": per, "kernel_ms": kern * 1e3}}
 
 
 STREAM_CHUNK = 1024
@@ -275,6 +306,9 @@ def main():
                                  "time; the scan is bound by the per-pair f32 filter on the VALUs (DESIGN.md)"},
             "self_match_rate": float((ids[:, 0].cpu() == torch.arange(Qn)).float().mean()),
         }
+
+    if not args.no_precomputed:
+        rec["precomputed"] = bench_precomputed(args, X, world)
 
     if not args.no_stream:
         del X, frames, idx, mm, out

@@ -21,6 +21,10 @@
 namespace hq {
 
 constexpr int kPreMaxLevels = 8;
+
+__device__ constexpr GroupLut<16> kPreLut16 = make_group_lut<16, false>();
+__device__ constexpr GroupLut<32> kPreLut32 = make_group_lut<32, false>();
+__device__ constexpr GroupLut<64> kPreLut64 = make_group_lut<64, false>();
 constexpr int kPreThreads = 256;
 
 struct PreLevel {
@@ -92,13 +96,72 @@ __device__ __forceinline__ float pre_mean(T s, int cnt) {
   else return (float)(s / (double)cnt);                                 // f64 mean, stored as float32
 }
 
+// eight consecutive values from a 16-byte aligned LDS address
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, T (&v)[8]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const double2 a = *reinterpret_cast<const double2*>(p + 2 * h);
+      v[2 * h] = a.x;
+      v[2 * h + 1] = a.y;
+    }
+  }
+}
+
+// np.add.reduce over an S x S square (S = 4 or 8: 16 / 64 values, one pairwise leaf) whose rows start
+// at b, b + ld, ...: eight accumulators over the C-order flattening, then
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), identity added first.  Rows are read as S/2-wide vectors.
+template <typename T, int S>
+__device__ __forceinline__ T sq_sum(const T* b, int ld) {
+  T x[S * S];
+#pragma unroll
+  for (int r = 0; r < S; ++r)
+#pragma unroll
+    for (int c = 0; c < S; c += S / 2) {
+      if constexpr (S == 8 && sizeof(T) == 4) {
+        const float4 v = *reinterpret_cast<const float4*>(b + r * ld + c);
+        x[r * S + c] = v.x; x[r * S + c + 1] = v.y; x[r * S + c + 2] = v.z; x[r * S + c + 3] = v.w;
+      } else if constexpr (sizeof(T) == 4 || S == 4) {
+        // 4x4 (two 8-byte halves per row) or 8x8 f64 (two 16-byte quarters per half row)
+#pragma unroll
+        for (int h = 0; h < S / 2; h += 2) {
+          if constexpr (sizeof(T) == 4) {
+            const float2 v = *reinterpret_cast<const float2*>(b + r * ld + c + h);
+            x[r * S + c + h] = v.x; x[r * S + c + h + 1] = v.y;
+          } else {
+            const double2 v = *reinterpret_cast<const double2*>(b + r * ld + c + h);
+            x[r * S + c + h] = v.x; x[r * S + c + h + 1] = v.y;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < S / 2; h += 2) {
+          const double2 v = *reinterpret_cast<const double2*>(b + r * ld + c + h);
+          x[r * S + c + h] = v.x; x[r * S + c + h + 1] = v.y;
+        }
+      }
+    }
+  T r8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r8[j] = x[j];
+#pragma unroll
+  for (int i = 8; i < S * S; i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r8[j] = r8[j] + x[i + j];
+  return T(0) + (((r8[0] + r8[1]) + (r8[2] + r8[3])) + ((r8[4] + r8[5]) + (r8[6] + r8[7])));
+}
+
 // kind 0: images (n x n row-major, image stride `stride` elements); kind 1: 1-D Hilbert-ordered
 // parameter streams of d values (row stride `stride`), zero-padded to n*n and mapped to 2-D
 // (core/pipeline.py:298-319 _get_2d_representation).
 template <typename T>
 __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ in, int kind, int64_t N, int64_t stride,
                                                          int d, int n, PrePlan plan, float* __restrict__ out,
-                                                         int64_t out_stride) {
+                                                         int64_t out_stride, int use_lut) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ PreLevel lv[kPreMaxLevels];  // per-thread level lookups index LDS, not the kernarg block
   T* img = reinterpret_cast<T*>(smem);
@@ -109,8 +172,34 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
   if (tid < plan.nlev) lv[tid] = plan.lv[tid];
   for (int64_t e = blockIdx.x; e < N; e += gridDim.x) {
     const T* src = in + e * stride;
+    const bool vec_ok = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
     if (kind == 0) {
       for (int i = tid; i < n * n; i += kPreThreads) img[i] = src[i];
+    } else if (use_lut) {
+      const uint32_t* glut = n == 16 ? kPreLut16.v : (n == 32 ? kPreLut32.v : kPreLut64.v);
+      // float4 groups = 2x2 blocks (Hilbert layout invariant): compile-time group LUT
+      for (int j = tid; j < (n * n) >> 2; j += kPreThreads) {
+        const uint32_t ent = glut[j], off = ent & 0xFFFFu, code = ent >> 16;
+        T v[4];
+        if (vec_ok && 4 * j + 3 < d) {
+          if constexpr (sizeof(T) == 4) {
+            const float4 q4 = *reinterpret_cast<const float4*>(src + 4 * j);
+            v[0] = q4.x; v[1] = q4.y; v[2] = q4.z; v[3] = q4.w;
+          } else {
+            const double2 a2 = *reinterpret_cast<const double2*>(src + 4 * j);
+            const double2 b2 = *reinterpret_cast<const double2*>(src + 4 * j + 2);
+            v[0] = a2.x; v[1] = a2.y; v[2] = b2.x; v[3] = b2.y;
+          }
+        } else {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) v[m] = 4 * j + m < d ? src[4 * j + m] : T(0);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const uint32_t b = (code >> (2 * m)) & 3u;
+          img[off + (b & 1u) + (b >> 1) * n] = v[m];
+        }
+      }
     } else {
       for (int i = tid; i < n * n; i += kPreThreads) {
         uint32_t x, y;
@@ -119,18 +208,28 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
       }
     }
     __syncthreads();
-    // squares of <= 128 values: one thread each
-    for (int a = tid; a < plan.n_small; a += kPreThreads) {
-      int l = 0;
-      while (a >= lv[l].off + lv[l].count) ++l;
-      const int s = lv[l].s, lsh = lv[l].lsh, msk = s - 1;
-      int x0, y0;
-      pre_square(lv[l], a - lv[l].off, x0, y0);
-      const T* b = img + (y0 << lsh_n) + x0;
-      auto f = [&](int k) -> T { return b[((k >> lsh) << lsh_n) + (k & msk)]; };
-      res[a] = pre_mean<T>(T(0) + pw_leaf<T>(f, 0, s * s), s * s);  // np_sum for <= 128 values
+    // squares of <= 128 values: one thread each, level by level (uniform geometry per loop); 4x4 and
+    // 8x8 squares read whole row segments (their x0 is a multiple of s/2) and sum in registers
+    for (int l = 0; l < plan.nlev; ++l) {
+      const PreLevel& L = plan.lv[l];
+      if (L.leaf0 >= 0) continue;
+      const int s = L.s, lsh = L.lsh, msk = s - 1;
+      for (int k = tid; k < L.count; k += kPreThreads) {
+        int x0, y0;
+        pre_square(L, k, x0, y0);
+        const T* b = img + (y0 << lsh_n) + x0;
+        T sum;
+        if (s == 8) sum = sq_sum<T, 8>(b, n);
+        else if (s == 4) sum = sq_sum<T, 4>(b, n);
+        else {
+          auto f = [&](int q) -> T { return b[((q >> lsh) << lsh_n) + (q & msk)]; };
+          sum = T(0) + pw_leaf<T>(f, 0, s * s);  // np_sum for <= 128 values
+        }
+        res[L.off + k] = pre_mean<T>(sum, s * s);
+      }
     }
-    // 128-value leaves of the larger squares
+    // 128-value leaves of the larger squares: 16 steps of 8 consecutive values (one row segment,
+    // 8-aligned because x0 is a multiple of s/2 >= 8), eight accumulators as NumPy's pairwise leaf
     for (int t = tid; t < plan.nleaves; t += kPreThreads) {
       int l = plan.nlev - 1;
       while (lv[l].leaf0 < 0 || t < lv[l].leaf0) --l;
@@ -140,27 +239,28 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
       int x0, y0;
       pre_square(lv[l], k, x0, y0);
       const T* b = img + (y0 << lsh_n) + x0;
-      auto f = [&](int q) -> T { return b[((q >> lsh) << lsh_n) + (q & msk)]; };
-      part[t] = pw_leaf<T>(f, leaf << 7, 128);
-    }
-    // balanced binary tree over each large square's leaves, adjacent pairs first (NumPy's split at
-    // n/2 for n = 128 * 2^k is exactly this tree)
-    for (int w = 1; w < 128; w <<= 1) {
-      __syncthreads();
-      for (int t = tid; t < plan.nleaves; t += kPreThreads) {
-        int l = plan.nlev - 1;
-        while (lv[l].leaf0 < 0 || t < lv[l].leaf0) --l;
-        const int per = (lv[l].s * lv[l].s) >> 7;
-        const int i = (t - lv[l].leaf0) % per;
-        if (w < per && (i & (2 * w - 1)) == 0) part[t] = part[t] + part[t + w];
+      T r[8];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int q = (leaf << 7) + 8 * i;
+        T v[8];
+        load8<T>(b + ((q >> lsh) << lsh_n) + (q & msk), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = i == 0 ? v[j] : r[j] + v[j];
       }
+      part[t] = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
     }
     __syncthreads();
+    // balanced binary tree over each large square's leaves, adjacent pairs first (NumPy's split at
+    // n/2 for n = 128 * 2^k is exactly this tree), one thread per square
     for (int a = plan.n_small + tid; a < plan.total; a += kPreThreads) {
       int l = 0;
       while (a >= lv[l].off + lv[l].count) ++l;
       const int per = (lv[l].s * lv[l].s) >> 7;
-      res[a] = pre_mean<T>(T(0) + part[lv[l].leaf0 + (a - lv[l].off) * per], lv[l].s * lv[l].s);
+      T* pp = part + lv[l].leaf0 + (a - lv[l].off) * per;
+      for (int w = 1; w < per; w <<= 1)
+        for (int i = 0; i < per; i += 2 * w) pp[i] = pp[i] + pp[i + w];
+      res[a] = pre_mean<T>(T(0) + pp[0], lv[l].s * lv[l].s);
     }
     __syncthreads();
     float* o = out + e * out_stride;
@@ -369,14 +469,15 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   const size_t lds = (size_t)esz * (n * n + p.nleaves) + 4 * (size_t)p.total;
   if (lds > 160 * 1024) return fail(HQ_E_UNSUPPORTED, "pre-computed index n=%d dtype %d needs %zu B of LDS", n, dtype, lds);
   hipStream_t s = (hipStream_t)stream;
+  const int use_lut = kind == 1 && n >= 16 && n <= 64;  // compile-time group LUT exists for this n
   if (dtype == HQ_F32) {
     HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_precomp<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(k_precomp<float>, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const float*)in, kind, N,
-                       in_stride, d, n, p, out, out_stride);
+                       in_stride, d, n, p, out, out_stride, use_lut);
   } else if (dtype == HQ_F64) {
     HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_precomp<double>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(k_precomp<double>, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const double*)in, kind,
-                       N, in_stride, d, n, p, out, out_stride);
+                       N, in_stride, d, n, p, out, out_stride, use_lut);
   } else {
     return fail(HQ_E_UNSUPPORTED, "pre-computed index dtype %d (f32/f64)", dtype);
   }
