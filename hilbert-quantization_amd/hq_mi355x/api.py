@@ -4,7 +4,8 @@ HilbertQuantizer keeps quantize / reconstruct / search and the model registry wi
 exception wrapping (QuantizationError / ReconstructionError / SearchError / ValidationError).  The
 search uses ProgressiveSimilaritySearchEngine(threshold, max_candidates_per_level = 2 * max_results)
 as the reference does (api.py:93-101) and filters results >= threshold (:284-287).
-BatchQuantizer adds the batched device path (one fused kernel for N embeddings).
+BatchQuantizer keeps the reference surface (quantize_batch / search_batch) on the batched device path:
+one fused launch per vector length, one resident corpus per search batch.
 """
 from __future__ import annotations
 
@@ -19,8 +20,9 @@ from .core.dimension_calculator import PowerOf4DimensionCalculator
 from .core.precomputed_hilbert_index import PrecomputedHilbertIndexer, PrecomputedSimilaritySearchEngine
 from .core.pipeline import QuantizationPipeline, quantize_batch
 from .core.search_engine import IndexCorpus, ProgressiveSimilaritySearchEngine
-from .exceptions import QuantizationError, ReconstructionError, SearchError, ValidationError
-from .models import QuantizedModel, SearchResult
+from .exceptions import (HilbertQuantizationError, QuantizationError, ReconstructionError, SearchError,
+                         ValidationError)
+from .models import ModelMetadata, QuantizedModel, SearchResult
 
 
 class HilbertQuantizer:
@@ -128,6 +130,11 @@ class HilbertQuantizer:
         except Exception as e:
             raise QuantizationError(f"Unexpected error during quantization: {e}") from e
 
+    def quantize_many(self, parameter_sets, model_ids: Optional[List[str]] = None,
+                      descriptions: Optional[List[str]] = None, validate: bool = True) -> List[QuantizedModel]:
+        """quantize() for many vectors in one batched device pass (same models, registry, indices)."""
+        return _ingest(self, parameter_sets, model_ids, descriptions, True, validate)
+
     def reconstruct(self, quantized_model: QuantizedModel, validate: bool = True) -> np.ndarray:
         try:
             return self.quantization_pipeline.reconstruct_parameters(quantized_model)
@@ -163,15 +170,154 @@ class HilbertQuantizer:
         self._model_registry.clear()
 
 
+def _ingest(hq: "HilbertQuantizer", parameter_sets, model_ids=None, descriptions=None, parallel: bool = True,
+            validate: bool = True, verbose: bool = False) -> List[QuantizedModel]:
+    """Batched HilbertQuantizer.quantize: the same QuantizedModels, registry entries,
+    pre-computed indices and compressor state as calling quantize() model by model, in order.
+
+    float32 vectors of one length go through ONE fused launch (hq_map_index_quantize: frames, f64
+    indices, min/max) and one pre-computed-index launch; the frames come back in one copy and the host
+    JPEG stage (same call as core/compressor.py:71-80, byte-identical output) runs on a thread pool.
+    Validation and efficiency failures surface at the same model, with the same exception, as the
+    sequential path (models before it are quantized and registered first).  Other dtypes take the
+    per-model path.  `verbose` = the reference's per-model pre-computed-index prints."""
+    import concurrent.futures as cf
+    import os as _os
+    from .core.compressor import encode_jpeg
+    from .core.precomputed_hilbert_index import PrecomputedIndex, _square_coordinates, PrecomputedLevel
+    from ._dev import to_dev, to_np
+    from . import kernels as K
+
+    sets = [np.array(p, dtype=np.float32) if isinstance(p, list) else p for p in parameter_sets]
+    names = [model_ids[i] if model_ids else f"model_{i}" for i in range(len(sets))]
+    descs = [descriptions[i] if descriptions else None for i in range(len(sets))]
+    # first failure in sequence order (validation, then dimension / efficiency check)
+    stop, stop_exc = len(sets), None
+    for i, p in enumerate(sets):
+        try:
+            if validate:
+                hq._validate_parameters(p)
+            if p.dtype == np.float32:
+                calc = PowerOf4DimensionCalculator(hq.min_efficiency_ratio)
+                calc.calculate_padding_strategy(len(p), calc.calculate_optimal_dimensions(len(p)))
+        except Exception as e:
+            stop = i
+            stop_exc = e if isinstance(e, (QuantizationError, ValidationError)) else \
+                QuantizationError(f"Unexpected error during quantization: "
+                                  f"{HilbertQuantizationError(f'Failed to quantize model {names[i]!r}: {e}')}")
+            break
+    out: List[Optional[QuantizedModel]] = [None] * stop
+    groups = {}
+    for i in range(stop):
+        if sets[i].dtype == np.float32 and sets[i].ndim == 1:
+            groups.setdefault(len(sets[i]), []).append(i)
+        else:
+            out[i] = None  # per-model path below
+    pipe = hq.quantization_pipeline
+    quality = hq.compression_quality
+    last_state = None  # (position, min, max) of the last non-constant frame: the compressor's state
+    workers = min(32, _os.cpu_count() or 1) if parallel else 1
+    with cf.ThreadPoolExecutor(max_workers=workers) as pool:
+        for d, members in groups.items():
+            X = to_dev(np.stack([sets[i] for i in members]))
+            frames, idx, mm = quantize_batch(X, hq.min_efficiency_ratio)
+            n = int(frames.shape[2])
+            pre = K.precomputed_index(X, n, 1) if hq.use_precomputed_indexing else None
+            fr_h, idx_h, mm_h = to_np(frames), to_np(idx), to_np(mm)
+            jpegs = list(pool.map(lambda k: encode_jpeg(fr_h[k], quality), range(len(members))))
+            pre_h = to_np(pre) if pre is not None else None
+            layout = K.precomputed_layout(n) if pre is not None else None
+            for k, i in enumerate(members):
+                data = jpegs[k]
+                size = sets[i].nbytes
+                md = ModelMetadata(model_name=names[i], original_size_bytes=size, compressed_size_bytes=len(data),
+                                   compression_ratio=size / len(data) if data else 0.0,
+                                   quantization_timestamp=time.strftime("%Y-%m-%d %H:%M:%S"),
+                                   model_architecture=descs[i], additional_info={})
+                out[i] = QuantizedModel(compressed_data=data, original_dimensions=(n, n), parameter_count=d,
+                                        compression_quality=quality, hierarchical_indices=idx_h[k].copy(), metadata=md)
+                if mm_h[k, 1] != mm_h[k, 0] and (last_state is None or i > last_state[0]):
+                    last_state = (i, mm_h[k, 0], mm_h[k, 1])
+                if pre_h is not None:
+                    levels = [PrecomputedLevel(g, s_, c, pre_h[k, o:o + c].copy(), _square_coordinates(n, g, s_))
+                              for (g, s_, c, o) in layout]
+                    tot = sum(lv.averages.nbytes + len(lv.square_coordinates) * 16 for lv in levels)
+                    hq.precomputed_indexer._index_cache[names[i]] = PrecomputedIndex(names[i], (n, n), levels, 0.0,
+                                                                                     tot)
+                    if verbose:
+                        print(f"Pre-computing {len(levels)} granularity levels for {names[i]}...")
+    for i in range(stop):
+        if out[i] is None:  # non-float32 vectors: the per-model drop-in path (registers itself)
+            out[i] = hq.quantize(sets[i], names[i], descs[i], validate=False)
+            continue
+        hq._model_registry.append(out[i])
+    if last_state is not None:
+        pipe.compressor._norm_min = np.float32(last_state[1])
+        pipe.compressor._norm_max = np.float32(last_state[2])
+    if stop_exc is not None:
+        raise stop_exc
+    return out
+
+
 class BatchQuantizer:
-    """Batched device path: one fused launch per batch, indices kept resident for search."""
+    """api.py:567-650 drop-in: BatchQuantizer(config).quantize_batch / search_batch, batched on the GPU
+    (one fused launch per vector length, one resident corpus per search batch)."""
 
-    def __init__(self, min_efficiency_ratio: float = 0.5):
-        self.min_efficiency_ratio = min_efficiency_ratio
+    def __init__(self, config: Optional[SystemConfig] = None):
+        self.quantizer = HilbertQuantizer(config)
+        self.logger = logging.getLogger(__name__)
 
-    def quantize_batch(self, parameters, index_space_size: Optional[int] = None):
+    def quantize_batch(self, parameter_sets, model_ids: Optional[List[str]] = None,
+                       descriptions: Optional[List[str]] = None, parallel: bool = True) -> List[QuantizedModel]:
+        if model_ids and len(model_ids) != len(parameter_sets):
+            raise ValueError("Number of model IDs must match number of parameter sets")
+        if descriptions and len(descriptions) != len(parameter_sets):
+            raise ValueError("Number of descriptions must match number of parameter sets")
+        return _ingest(self.quantizer, parameter_sets, model_ids, descriptions, parallel)
+
+    def search_batch(self, query_sets, candidate_models: List[QuantizedModel],
+                     max_results: int = 10) -> List[List[SearchResult]]:
+        """api.py:621-650: quantizer.search per query (a failing query yields []).  With an explicit
+        candidate pool the queries are quantized in one batch (registered in order, as search() does)
+        and answered by one batched progressive scan; without one, the pool is the growing registry
+        and the queries run one by one, exactly as the reference."""
+        hq = self.quantizer
+        if not candidate_models:
+            out = []
+            for q in query_sets:
+                try:
+                    out.append(hq.search(q, candidate_models, max_results))
+                except Exception as e:
+                    self.logger.error(f"Failed search: {e}")
+                    out.append([])
+            return out
+        ok, models = [], []
+        for i, q in enumerate(query_sets):
+            q = np.array(q, dtype=np.float32) if isinstance(q, list) else q
+            try:
+                hq._validate_parameters(q)
+                ok.append((i, q))
+            except Exception as e:
+                self.logger.error(f"Failed search {i + 1}: {e}")
+        results: List[List[SearchResult]] = [[] for _ in query_sets]
+        if not ok:
+            return results
+        try:
+            models = _ingest(hq, [q for _, q in ok], [f"model_{int(time.time())}" for _ in ok], None, True,
+                             validate=False)
+        except Exception as e:  # the sequential path would fail each of these queries the same way
+            self.logger.error(f"Failed search batch: {e}")
+            return results
+        found = hq.search_engine.progressive_search_batch([m.hierarchical_indices for m in models],
+                                                          candidate_models, max_results)
+        thr = hq.similarity_threshold
+        for (i, _), res in zip(ok, found):
+            results[i] = [r for r in res if r.similarity_score >= thr]
+        return results
+
+    def quantize_device(self, parameters, index_space_size: Optional[int] = None):
         """f32 [N, d] -> (frames u8 [N, n+1, n], indices f64 [N, L], minmax f32 [N, 2]) on the GPU."""
-        return quantize_batch(parameters, self.min_efficiency_ratio, index_space_size)
+        return quantize_batch(parameters, self.quantizer.min_efficiency_ratio, index_space_size)
 
     @staticmethod
     def build_corpus(indices, id_base: int = 0) -> IndexCorpus:

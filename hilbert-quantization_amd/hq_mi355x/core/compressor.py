@@ -19,6 +19,16 @@ from .._dev import to_dev, to_np
 from ..exceptions import CompressionError
 
 
+def encode_jpeg(u8: np.ndarray, quality: float) -> bytes:
+    """The reference's JPEG stage for an already normalised uint8 frame (core/compressor.py:71-80):
+    PIL 'L' image, quality max(1, min(95, int(q * 95))), optimize=True.  Host codec (SURVEY §8f row 2);
+    the same frame bytes give the same JPEG bytes as the per-model path."""
+    from PIL import Image
+    buf = io.BytesIO()
+    Image.fromarray(u8, "L").save(buf, format="JPEG", quality=max(1, min(95, int(quality * 95))), optimize=True)
+    return buf.getvalue()
+
+
 class MPEGAICompressorImpl:
     def __init__(self, config: Optional[object] = None):
         self.config = config
@@ -44,16 +54,17 @@ class MPEGAICompressorImpl:
         return to_np(K.dequantize_u8(to_dev(u8), to_dev(mm), CompressionError))
 
     def compress(self, image, quality: float) -> bytes:
+        """core/compressor.py:43-103: validation, GPU normalise, then the host JPEG codec."""
+        if not isinstance(image, np.ndarray):
+            raise ValueError("Image must be a numpy array")
+        if image.ndim != 2:
+            raise ValueError("Image must be 2-dimensional")
         if not 0.0 <= quality <= 1.0:
-            raise CompressionError(f"Quality must be between 0.0 and 1.0, got {quality}")
+            raise ValueError("Quality must be between 0.0 and 1.0")
         try:
-            from PIL import Image
-        except ImportError as e:  # codec is optional, the normalise stage is not
-            raise CompressionError(f"JPEG codec unavailable: {e}")
-        u8 = self._normalize_for_compression(image)
-        buf = io.BytesIO()
-        Image.fromarray(u8, mode="L").save(buf, format="JPEG", quality=int(quality * 95), optimize=True)
-        return buf.getvalue()
+            return encode_jpeg(self._normalize_for_compression(image), quality)
+        except Exception as e:
+            raise RuntimeError(f"Failed to compress image: {e}")
 
     def decompress(self, compressed_data: bytes):
         from PIL import Image

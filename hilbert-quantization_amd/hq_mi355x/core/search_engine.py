@@ -307,6 +307,23 @@ class ProgressiveSimilaritySearchEngine:
             return self._results(candidate_pool, to_np(ids)[0], to_np(ov)[0], to_np(lv)[0], int(to_np(cnt)[0]))
         return self._progressive_mixed(q, candidate_pool, max_results)
 
+    def progressive_search_batch(self, queries: Sequence, candidate_pool: List[QuantizedModel],
+                                 max_results: int) -> List[List[SearchResult]]:
+        """progressive_search for many queries against one pool: one resident corpus and one batched
+        scan when every index has the same length (else query by query)."""
+        if not candidate_pool:
+            return [[] for _ in queries]
+        qs = [np.asarray(q, dtype=np.float64) for q in queries]
+        L = len(qs[0]) if qs else 0
+        if not qs or any(len(q) != L for q in qs) or L == 0 or not self._parse_index_structure(qs[0], L) \
+                or not self._uniform(qs[0], candidate_pool):
+            return [self.progressive_search(q, candidate_pool, max_results) for q in qs]
+        corpus = IndexCorpus(np.stack([np.asarray(c.hierarchical_indices, dtype=np.float64) for c in candidate_pool]))
+        ids, ov, lv, cnt = corpus.progressive(np.stack(qs), max_results, self.similarity_threshold,
+                                              self.max_candidates_per_level)
+        ids, ov, lv, cnt = to_np(ids), to_np(ov), to_np(lv), to_np(cnt)
+        return [self._results(candidate_pool, ids[i], ov[i], lv[i], int(cnt[i])) for i in range(len(qs))]
+
     def _progressive_mixed(self, q, pool, max_results):
         """Candidate pools of mixed index length: scores from the GPU, the reference's level loop
         (:254-300) applied to them."""
