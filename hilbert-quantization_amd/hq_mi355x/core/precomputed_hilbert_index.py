@@ -17,6 +17,7 @@ Index files are written with numpy's .npz (no pickle) instead of the reference's
 """
 from __future__ import annotations
 
+import functools
 import logging
 import time
 from dataclasses import dataclass
@@ -50,8 +51,10 @@ class PrecomputedIndex:
     total_storage_bytes: int
 
 
+@functools.lru_cache(maxsize=64)
 def _square_coordinates(n: int, g: int, s: int) -> List[Tuple[int, int]]:
-    """(start_x, start_y) of each square in output order (:169-204): integer geometry only."""
+    """(start_x, start_y) of each square in output order (:169-204): integer geometry only.  Cached:
+    indices of one geometry share the (read-only) list."""
     out = [(c * s, r * s) for r in range(g) for c in range(g)]
     off = s // 2
     if off > 0:
