@@ -13,7 +13,7 @@ timeout -k 10 600 python bench.py "$@" > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG
 cat $OUT/bench_$TAG.json; tail -3 $OUT/bench_$TAG.err
 [ $rc -eq 0 ] || { echo "bench rc=$rc: stopping"; exit $rc; }
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu > $OUT/prof_$TAG.log 2>&1; rc=$?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu --no-ingest > $OUT/prof_$TAG.log 2>&1; rc=$?
 echo "rocprof rc=$rc"
 find $OUT/prof_$TAG -name "*stats*" | head
 exit 0
