@@ -18,6 +18,8 @@
 // stores.
 #include "hq_common.h"
 
+#include <stdlib.h>
+
 namespace hq {
 
 constexpr int kPreMaxLevels = 8;
@@ -76,17 +78,22 @@ static int pre_plan(int n, int max_levels, int min_sq, PrePlan& p) {
   return HQ_OK;
 }
 
-// top-left corner of square k of a level (grid squares row-major, then offset squares)
+// top-left corner of square k of a level (grid squares row-major, then offset squares).  g is a power
+// of two (shifts); the offset grid's side g - 1 is not: its row is floor((k + 0.5) / (g - 1)) in f32,
+// exact for n <= 128: k < 63^2 and g - 1 <= 63 put (k + 0.5) / (g - 1) (<= 63) at least 1/126 away
+// from an integer, while v_rcp_f32 + the product err by < 63 * 2^-21.
 __device__ __forceinline__ void pre_square(const PreLevel& L, int k, int& x0, int& y0) {
+  const int lg = __builtin_ctz((unsigned)L.g);
   const int gg = L.g * L.g;
   if (k < gg) {
-    y0 = (k / L.g) * L.s;
-    x0 = (k % L.g) * L.s;
+    y0 = (k >> lg) << L.lsh;
+    x0 = (k & (L.g - 1)) << L.lsh;
   } else {
     k -= gg;
     const int h = L.g - 1;
-    y0 = (k / h) * L.s + L.s / 2;
-    x0 = (k % h) * L.s + L.s / 2;
+    const int r = (int)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)h));
+    y0 = (r << L.lsh) + L.s / 2;
+    x0 = ((k - r * h) << L.lsh) + L.s / 2;
   }
 }
 
@@ -161,11 +168,11 @@ __device__ __forceinline__ T sq_sum(const T* b, int ld) {
 template <typename T>
 __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ in, int kind, int64_t N, int64_t stride,
                                                          int d, int n, PrePlan plan, float* __restrict__ out,
-                                                         int64_t out_stride, int use_lut) {
+                                                         int64_t out_stride, int use_lut, int ld) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ PreLevel lv[kPreMaxLevels];  // per-thread level lookups index LDS, not the kernarg block
   T* img = reinterpret_cast<T*>(smem);
-  T* part = img + n * n;
+  T* part = img + ld * n;  // row stride ld = n + pad (16-B aligned rows spread the bank pattern)
   float* res = reinterpret_cast<float*>(part + plan.nleaves);
   const int tid = threadIdx.x;
   const int lsh_n = plan.lsh_n;
@@ -174,12 +181,13 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
     const T* src = in + e * stride;
     const bool vec_ok = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
     if (kind == 0) {
-      for (int i = tid; i < n * n; i += kPreThreads) img[i] = src[i];
+      for (int i = tid; i < n * n; i += kPreThreads) img[(i >> lsh_n) * ld + (i & (n - 1))] = src[i];
     } else if (use_lut) {
       const uint32_t* glut = n == 16 ? kPreLut16.v : (n == 32 ? kPreLut32.v : kPreLut64.v);
       // float4 groups = 2x2 blocks (Hilbert layout invariant): compile-time group LUT
       for (int j = tid; j < (n * n) >> 2; j += kPreThreads) {
-        const uint32_t ent = glut[j], off = ent & 0xFFFFu, code = ent >> 16;
+        const uint32_t ent = glut[j], off0 = ent & 0xFFFFu, code = ent >> 16;
+        const uint32_t off = (off0 >> lsh_n) * ld + (off0 & (n - 1));
         T v[4];
         if (vec_ok && 4 * j + 3 < d) {
           if constexpr (sizeof(T) == 4) {
@@ -197,14 +205,14 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const uint32_t b = (code >> (2 * m)) & 3u;
-          img[off + (b & 1u) + (b >> 1) * n] = v[m];
+          img[off + (b & 1u) + (b >> 1) * ld] = v[m];
         }
       }
     } else {
       for (int i = tid; i < n * n; i += kPreThreads) {
         uint32_t x, y;
         d2xy((uint32_t)n, (uint32_t)i, x, y);
-        img[(y << lsh_n) + x] = i < d ? src[i] : T(0);
+        img[y * ld + x] = i < d ? src[i] : T(0);
       }
     }
     __syncthreads();
@@ -217,12 +225,13 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
       for (int k = tid; k < L.count; k += kPreThreads) {
         int x0, y0;
         pre_square(L, k, x0, y0);
-        const T* b = img + (y0 << lsh_n) + x0;
+        const T* b = img + y0 * ld + x0;
         T sum;
-        if (s == 8) sum = sq_sum<T, 8>(b, n);
-        else if (s == 4) sum = sq_sum<T, 4>(b, n);
+        if (s == 8) sum = sq_sum<T, 8>(b, ld);
+        else if (s == 4) sum = sq_sum<T, 4>(b, ld);
+        else if (s == 2) sum = T(0) + ((((T(-0.0) + b[0]) + b[1]) + b[ld]) + b[ld + 1]);  // NumPy n < 8 branch
         else {
-          auto f = [&](int q) -> T { return b[((q >> lsh) << lsh_n) + (q & msk)]; };
+          auto f = [&](int q) -> T { return b[(q >> lsh) * ld + (q & msk)]; };
           sum = T(0) + pw_leaf<T>(f, 0, s * s);  // np_sum for <= 128 values
         }
         res[L.off + k] = pre_mean<T>(sum, s * s);
@@ -234,17 +243,17 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
       int l = plan.nlev - 1;
       while (lv[l].leaf0 < 0 || t < lv[l].leaf0) --l;
       const int s = lv[l].s, lsh = lv[l].lsh, msk = s - 1;
-      const int per = (s * s) >> 7;
-      const int k = (t - lv[l].leaf0) / per, leaf = (t - lv[l].leaf0) % per;
+      const int lper = 2 * lsh - 7;  // log2 of the leaves per square
+      const int k = (t - lv[l].leaf0) >> lper, leaf = (t - lv[l].leaf0) & ((1 << lper) - 1);
       int x0, y0;
       pre_square(lv[l], k, x0, y0);
-      const T* b = img + (y0 << lsh_n) + x0;
+      const T* b = img + y0 * ld + x0;
       T r[8];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int q = (leaf << 7) + 8 * i;
         T v[8];
-        load8<T>(b + ((q >> lsh) << lsh_n) + (q & msk), v);
+        load8<T>(b + (q >> lsh) * ld + (q & msk), v);
 #pragma unroll
         for (int j = 0; j < 8; ++j) r[j] = i == 0 ? v[j] : r[j] + v[j];
       }
@@ -466,18 +475,22 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   if (out_stride < p.total) return fail(HQ_E_INVALID, "out_stride %lld < %d averages", (long long)out_stride, p.total);
   const int64_t grid64 = N < 65536 * 4 ? N : 65536 * 4;
   const int esz = dtype == HQ_F64 ? 8 : 4;
-  const size_t lds = (size_t)esz * (n * n + p.nleaves) + 4 * (size_t)p.total;
+  const char* pev = getenv("HQ_PRECOMP_PAD");
+  const int pad = pev ? atoi(pev) : 4;
+  if (pad < 0 || (pad & 3)) return fail(HQ_E_INVALID, "HQ_PRECOMP_PAD must be a multiple of 4");
+  const int ld = n + pad;
+  const size_t lds = (size_t)esz * ((size_t)ld * n + p.nleaves) + 4 * (size_t)p.total;
   if (lds > 160 * 1024) return fail(HQ_E_UNSUPPORTED, "pre-computed index n=%d dtype %d needs %zu B of LDS", n, dtype, lds);
   hipStream_t s = (hipStream_t)stream;
   const int use_lut = kind == 1 && n >= 16 && n <= 64;  // compile-time group LUT exists for this n
   if (dtype == HQ_F32) {
     HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_precomp<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(k_precomp<float>, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const float*)in, kind, N,
-                       in_stride, d, n, p, out, out_stride, use_lut);
+                       in_stride, d, n, p, out, out_stride, use_lut, ld);
   } else if (dtype == HQ_F64) {
     HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_precomp<double>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(k_precomp<double>, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const double*)in, kind,
-                       N, in_stride, d, n, p, out, out_stride, use_lut);
+                       N, in_stride, d, n, p, out, out_stride, use_lut, ld);
   } else {
     return fail(HQ_E_UNSUPPORTED, "pre-computed index dtype %d (f32/f64)", dtype);
   }
