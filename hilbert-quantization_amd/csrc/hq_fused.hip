@@ -202,6 +202,7 @@ __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int
   }
   if (live) store_index(idx_out + e * (int64_t)L, val, lane, L);
   const float rv = (float)val;
+  if constexpr ((V & 512) != 0) __syncthreads();  // frame overlays the tree: every slot read first
 
   // ---- quantize into the LDS frame, stream out --------------------------------------------------
   const bool flat = mx == mn;
@@ -351,7 +352,11 @@ template <int NS>
 struct NpGeo {
   static constexpr int tree_bytes = FastGeo<NS>::tree_len() * 8;
   static constexpr int frame_off = (tree_bytes + 15) & ~15;
-  static constexpr int wave_bytes = frame_off + ((FastGeo<NS>::FB + 15) & ~15);
+  static constexpr int frame_bytes = (FastGeo<NS>::FB + 15) & ~15;
+  static constexpr int wave_bytes = frame_off + frame_bytes;
+  // V & 512: the frame overlays the tree (the tree is dead once the index slots are read), so a wave
+  // needs max(tree, frame) bytes of LDS and more waves fit on a CU
+  static constexpr int alias_bytes = frame_off > frame_bytes ? frame_off : frame_bytes;
 };
 
 template <int NS, int ND, int V, int WPB>
@@ -362,9 +367,10 @@ __global__ __launch_bounds__(64 * WPB) void k_fused_np(const float* __restrict__
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  uint8_t* base = smem + wv * NpGeo<NS>::wave_bytes;
+  constexpr bool kAlias = (V & 512) != 0;
+  uint8_t* base = smem + wv * (kAlias ? NpGeo<NS>::alias_bytes : NpGeo<NS>::wave_bytes);
   double* tree = reinterpret_cast<double*>(base);
-  uint8_t* frame = base + NpGeo<NS>::frame_off;
+  uint8_t* frame = base + (kAlias ? 0 : NpGeo<NS>::frame_off);
   const int64_t e = (int64_t)blockIdx.x * WPB + wv;
   const bool live = e < N;
   const int slev = lane < L ? (int)plan.lev[lane] : -1;
@@ -404,7 +410,7 @@ template <int NS, int ND, int V>
 static int launch_np(const float* in, int64_t N, int64_t stride, int d, int L, const FastPlan& plan, uint8_t* frame,
                      double* idx, float* mm, hipStream_t s) {
   constexpr int WPB = 1 << ((V >> 7) & 3);
-  const size_t lds = (size_t)WPB * NpGeo<NS>::wave_bytes;
+  const size_t lds = (size_t)WPB * ((V & 512) ? NpGeo<NS>::alias_bytes : NpGeo<NS>::wave_bytes);
   const int64_t grid = (N + WPB - 1) / WPB;
   if (grid > 0x7FFFFFFF) return HQ_E_UNSUPPORTED;
   hipLaunchKernelGGL((k_fused_np<NS, ND, V, WPB>), dim3((unsigned)grid), dim3(64 * WPB), lds, s, in, N, stride, d, L,
@@ -421,8 +427,9 @@ static int launch_any(const float* in, int64_t N, int64_t stride, int d, int L, 
 }
 
 // Variant bits (HQ_FUSED_V): 1 nt loads, 2 reciprocal quantize, 4 triple buffering (persistent), 8 / 16 / 32
-// memory-only probes, 64 non-persistent (one embedding per wave), bits 7-8: log2 waves per workgroup.
-constexpr int kDefaultV = 64 | (1 << 7);  // non-persistent, 2 waves per workgroup, plain loads, exact quantize
+// memory-only probes, 64 non-persistent (one embedding per wave), bits 7-8: log2 waves per workgroup,
+// 512 frame overlays the tree in LDS (non-persistent form).
+constexpr int kDefaultV = 64 | (1 << 7) | 512;  // non-persistent, 2 waves per workgroup, frame over tree, exact quantize
 
 template <int NS, int ND>
 static int pick_nd(int variant, int nd, const float* in, int64_t N, int64_t stride, int d, int L, const FastPlan& plan,
@@ -452,6 +459,11 @@ static int pick_nd(int variant, int nd, const float* in, int64_t N, int64_t stri
           case 321: return launch_any<NS, ND, 321>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 322: return launch_any<NS, ND, 322>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 328: return launch_any<NS, ND, 328>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 576: return launch_any<NS, ND, 576>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 704: return launch_any<NS, ND, 704>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 832: return launch_any<NS, ND, 832>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 960: return launch_any<NS, ND, 960>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 840: return launch_any<NS, ND, 840>(in, N, stride, d, L, plan, frame, idx, mm, s);
           default: break;
         }
       }
