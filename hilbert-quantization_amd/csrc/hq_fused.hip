@@ -217,37 +217,52 @@ __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int
   }
   if (!flat) {
     const float rcp = 1.0f / rng;
-    (void)rcp;
+    const float c255 = rcp * 255.0f;
+    (void)c255;
 #pragma unroll
     for (int t = 0; t < ND; ++t) {
       const int j = lane + 64 * t;
       if (j < groups_data) {
         const float4 x = b.g[t];
-        uint32_t e0, e1, e2, e3;
-        if constexpr ((V & 2) != 0) {
-          bool slow = false;
-          e0 = qfast(x.x, mn, rcp, slow);
-          e1 = (4 * j + 1 < d) ? qfast(x.y, mn, rcp, slow) : q0;
-          e2 = (4 * j + 2 < d) ? qfast(x.z, mn, rcp, slow) : q0;
-          e3 = (4 * j + 3 < d) ? qfast(x.w, mn, rcp, slow) : q0;
-          if (__builtin_amdgcn_ballot_w64(slow)) {  // rare: some lane is within 1e-3 of a level edge
-            if (slow) {
-              e0 = qz(x.x, mn, rng);
-              e1 = (4 * j + 1 < d) ? qz(x.y, mn, rng) : q0;
-              e2 = (4 * j + 2 < d) ? qz(x.z, mn, rng) : q0;
-              e3 = (4 * j + 3 < d) ? qz(x.w, mn, rng) : q0;
-            }
-          }
-        } else {
-          e0 = qz(x.x, mn, rng);
-          e1 = (4 * j + 1 < d) ? qz(x.y, mn, rng) : q0;
-          e2 = (4 * j + 2 < d) ? qz(x.z, mn, rng) : q0;
-          e3 = (4 * j + 3 < d) ? qz(x.w, mn, rng) : q0;
-        }
         const uint32_t ent = lut_r[t];
         const uint32_t code = ent >> 16;
-        const uint32_t w = (e0 << (8 * (code & 3))) | (e1 << (8 * ((code >> 2) & 3))) |
-                           (e2 << (8 * ((code >> 4) & 3))) | (e3 << (8 * ((code >> 6) & 3)));
+        uint32_t w;
+        if constexpr ((V & 2) != 0) {
+          // packed f32 pairs: y = (x - mn) * fl(fl(1/rng) * 255) (qfast's < 7.7e-5 bound), floor(y)
+          // placed straight into its 2x2-block byte by v_cvt_pk_u8_f32; the exact division only at an
+          // element position where some lane's y lies within 1e-4 of an integer
+          typedef float f2v __attribute__((ext_vector_type(2)));
+          const f2v mn2 = {mn, mn}, c2 = {c255, c255}, h2 = {0.5f, 0.5f};
+          const f2v ya = (f2v{x.x, x.y} - mn2) * c2, yb = (f2v{x.z, x.w} - mn2) * c2;
+          f2v fa = {floorf(ya.x), floorf(ya.y)}, fb = {floorf(yb.x), floorf(yb.y)};
+          const f2v ta = (ya - fa) - h2, tb = (yb - fb) - h2;
+          const float q0f = (float)q0;
+          if (4 * j + 3 >= d) {  // the group that straddles d: padding elements quantize 0.0
+            if (4 * j + 1 >= d) fa.y = q0f;
+            if (4 * j + 2 >= d) fb.x = q0f;
+            fb.y = q0f;
+          }
+          const float xs[4] = {x.x, x.y, x.z, x.w};
+          const bool sl[4] = {fabsf(ta.x) > 0.4999f, fabsf(ta.y) > 0.4999f && 4 * j + 1 < d,
+                              fabsf(tb.x) > 0.4999f && 4 * j + 2 < d, fabsf(tb.y) > 0.4999f && 4 * j + 3 < d};
+          const uint32_t p0 = code & 3u, p1 = (code >> 2) & 3u, p2 = (code >> 4) & 3u, p3 = (code >> 6) & 3u;
+          w = __builtin_amdgcn_cvt_pk_u8_f32(fa.x, p0, 0u);
+          w = __builtin_amdgcn_cvt_pk_u8_f32(fa.y, p1, w);
+          w = __builtin_amdgcn_cvt_pk_u8_f32(fb.x, p2, w);
+          w = __builtin_amdgcn_cvt_pk_u8_f32(fb.y, p3, w);
+          const uint32_t ps[4] = {p0, p1, p2, p3};
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            if (__builtin_amdgcn_ballot_w64(sl[m]))
+              if (sl[m]) w = (w & ~(0xFFu << (8 * ps[m]))) | (qz(xs[m], mn, rng) << (8 * ps[m]));
+        } else {
+          const uint32_t e0 = qz(x.x, mn, rng);
+          const uint32_t e1 = (4 * j + 1 < d) ? qz(x.y, mn, rng) : q0;
+          const uint32_t e2 = (4 * j + 2 < d) ? qz(x.z, mn, rng) : q0;
+          const uint32_t e3 = (4 * j + 3 < d) ? qz(x.w, mn, rng) : q0;
+          w = (e0 << (8 * (code & 3))) | (e1 << (8 * ((code >> 2) & 3))) | (e2 << (8 * ((code >> 4) & 3))) |
+              (e3 << (8 * ((code >> 6) & 3)));
+        }
         const uint32_t off = ent & 0xFFFFu;
         *reinterpret_cast<uint16_t*>(frame + off) = (uint16_t)(w & 0xFFFFu);
         *reinterpret_cast<uint16_t*>(frame + off + NS) = (uint16_t)(w >> 16);
@@ -463,6 +478,7 @@ static int pick_nd(int variant, int nd, const float* in, int64_t N, int64_t stri
           case 704: return launch_any<NS, ND, 704>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 832: return launch_any<NS, ND, 832>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 960: return launch_any<NS, ND, 960>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 706: return launch_any<NS, ND, 706>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 840: return launch_any<NS, ND, 840>(in, N, stride, d, L, plan, frame, idx, mm, s);
           default: break;
         }
