@@ -57,24 +57,57 @@ class ShardedIndexCorpus:
         self.n_total = int(n_total)
         self.group = group
 
-    def progressive(self, queries, max_results: int, threshold: float = 0.1, max_candidates_per_level: int = 100):
-        """Global progressive search; every rank returns the same (ids, overall, levels, count)."""
+    def local_records(self, qp, M: int, threshold: float):
+        """This shard's exact contribution [Q, M + 1, 2 + W]: the level-0 top-M >= threshold by (score
+        desc, global id asc) with exact overall / level re-scores, plus the shard's first arg-max slot
+        (used only when no shard has a passing candidate).  The scan, re-rank, re-scores and packing
+        are queued before the one host sync, which only checks for rows that need the dense exact path
+        (list not proven complete, or nothing passed -> arg-max)."""
         t = torch()
         c = self.local
-        qp = c.prepare_queries(queries)
         Q = qp.N
-        M = int(max_candidates_per_level)
-        if self.n_total <= M:
-            return self.brute_force(queries, max_results)
-        s0, ids, _, best, bid = c.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)
-        det = K.rescore(qp, c.prep, ids, c.id_base)
-        bdet = K.rescore(qp, c.prep, bid.view(Q, 1), c.id_base)
-        rec = t.cat([pack(s0, ids, det), pack(best.view(Q, 1), bid.view(Q, 1), bdet)], dim=1)  # [Q, M+1, 2+W]
-        g = all_gather(rec, self.group)  # [R, Q, M+1, 2+W]
+        s0, ids, cnt, res = c._scan_refine(qp, 0, M, float(threshold), 1)
+        best = t.full((Q,), -float("inf"), dtype=t.float64, device=qp.Z.device)
+        bid = t.full((Q,), -1, dtype=t.int64, device=qp.Z.device)
+
+        def records(q, s0_, ids_, best_, bid_):
+            det = K.rescore(q, c.prep, ids_, c.id_base)
+            bdet = K.rescore(q, c.prep, bid_.view(-1, 1), c.id_base)
+            return t.cat([pack(s0_, ids_, det), pack(best_.view(-1, 1), bid_.view(-1, 1), bdet)], dim=1)
+
+        rec = records(qp, s0, ids, best, bid)
+        redo = (res == 0) | (cnt == 0)
+        if bool(redo.any()):
+            sel = t.nonzero(redo).view(-1)
+            s2, i2, b2, bi2 = c._dense(qp, sel, 0, M, float(threshold), 1)
+            rec[sel] = records(qp.rows(sel), s2, i2, b2, bi2)
+        return rec
+
+    @staticmethod
+    def merge(g, M: int, max_results: int):
+        """Merge gathered records [R, Q, M + 1, 2 + W] exactly as the single-GPU ranking."""
         gs, gi, gd = unpack(g[:, :, :M])
         bs, bi, bd = unpack(g[:, :, M])
         oid, odet, cnt = K.progressive_final(gs, gi, gd, bs, bi, bd, int(max_results))
         return oid, odet[..., 0], odet[..., 1:], cnt
+
+    def progressive(self, queries, max_results: int, threshold: float = 0.1, max_candidates_per_level: int = 100):
+        """Global progressive search; every rank returns the same (ids, overall, levels, count)."""
+        c = self.local
+        M = int(max_candidates_per_level)
+        if self.n_total <= M:
+            return self.brute_force(queries, max_results)
+        qp = c.prepare_queries(queries)
+        if M + c.SLACK > 64:  # beyond the fused scan's list length: the dense exact path per shard
+            t = torch()
+            Q = qp.N
+            s0, ids, _, best, bid = c.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)
+            det = K.rescore(qp, c.prep, ids, c.id_base)
+            bdet = K.rescore(qp, c.prep, bid.view(Q, 1), c.id_base)
+            rec = t.cat([pack(s0, ids, det), pack(best.view(Q, 1), bid.view(Q, 1), bdet)], dim=1)
+        else:
+            rec = self.local_records(qp, M, threshold)
+        return self.merge(all_gather(rec, self.group), M, max_results)
 
     def brute_force(self, queries, max_results: int):
         """Global top-k by the overall score: local top-k, all-gather, R-way merge."""

@@ -172,6 +172,31 @@ def test_sharded_merge_equals_single(hq_lib):
     np.testing.assert_array_equal(_np(odet)[..., 0], ref[1])
 
 
+def test_sharded_corpus_records_equal_single(hq_lib):
+    """ShardedIndexCorpus.local_records (sync-late path, dense fix-ups) of 3 shards merged == unsharded;
+    a shard where nothing passes contributes its exact arg-max slot; world size 1 without a process
+    group gathers its own records."""
+    import torch
+    from hq_mi355x.core.search_engine import IndexCorpus
+    from hq_mi355x.distributed import ShardedIndexCorpus, shard_range
+    C = _corpus(3000, 64, 41)
+    C[2500:2504] = C[10]
+    Q = np.concatenate([C[[10, 20, 2999]], C[[5, 6]] + 0.01])
+    full = IndexCorpus(C)
+    for thr in (0.1, 0.97):
+        ref = [_np(x) for x in full.progressive(Q, 10, thr, 20)]
+        recs = []
+        for r in range(3):
+            a, b = shard_range(len(C), r, 3)
+            sh = ShardedIndexCorpus(C[a:b], id_base=a, n_total=len(C))
+            recs.append(sh.local_records(sh.local.prepare_queries(Q), 20, thr))
+        oid, ov, lv, cnt = ShardedIndexCorpus.merge(torch.stack(recs, 0), 20, 10)
+        assert np.array_equal(_np(oid), ref[0]) and np.array_equal(_np(cnt), ref[3]), thr
+        np.testing.assert_array_equal(_np(ov), ref[1])
+        one = ShardedIndexCorpus(C, id_base=0, n_total=len(C)).progressive(Q, 10, thr, 20)
+        assert np.array_equal(_np(one[0]), ref[0])
+
+
 def test_rag_scores(hq_lib, golden):
     from hq_mi355x.rag import similarity as S
     g = golden("rag_score")
