@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--no-stream", action="store_true")
     ap.add_argument("--no-precomputed", action="store_true")
     ap.add_argument("--no-ingest", action="store_true")
+    ap.add_argument("--no-frames", action="store_true")
+    ap.add_argument("--frames", type=int, default=250_000)
     ap.add_argument("--ingest-models", type=int, default=20000)
     ap.add_argument("--stream-values", type=int, default=7_000_000_000)
     ap.add_argument("--stream-steps", type=int, default=5)
@@ -163,6 +165,52 @@ def bench_precomputed(args, X, world):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("k_precomp"),
                          "algorithmic_bytes_per_embedding": per, "kernel_ms": kern * 1e3}}
+
+
+def bench_frames(args, world, rank, dev):
+    """S7 / north star "frame similarity as a batched dot over N x (side x side) images": 1000 query
+    frames against a resident corpus of 64x64 frames (K = 4096) per GPU, (cos + 1) / 2 for every pair
+    (rag/search/engine.py:622-660), split-f16 MFMA contraction (hq_cos_scores_mfma).  A step =
+    prepare the query batch + score it against the whole corpus (f64 [Q, N] out)."""
+    from hq_mi355x import kernels as K
+    Nf, Qn, Kd = args.frames, args.queries, 4096
+    g = torch.Generator(device=dev).manual_seed(7 + 1000 * rank)
+    F = torch.randn((Nf, Kd), generator=g, device=dev, dtype=torch.float32)
+    Qf = F[:Qn] + 0.1 * torch.randn((Qn, Kd), generator=g, device=dev, dtype=torch.float32)
+    corpus = K.cos_prepare(F)
+    del F
+    torch.cuda.synchronize()
+
+    def step():
+        K.cosine_scores_mfma(K.cos_prepare(Qf), corpus)
+
+    steps = max(2, args.search_steps)
+    wall, kern = timed(step, steps, 1, world)
+    flops = 2.0 * Qn * Nf * Kd
+    peak = FP16_MATRIX_PEAK_TFS / 3.0
+    res = {"metric": "frame-pair cosine scores/sec (1000 queries x 64x64 frames)",
+           "value": Qn * Nf * world * steps / wall, "unit": "pairs/sec", "queries": Qn, "frames_per_gpu": Nf,
+           "K": Kd, "steps": steps, "ms_per_step": wall / steps * 1e3, "scaling": "weak",
+           "roofline": {"bound": "mfma", "achieved": flops / kern / 1e12, "peak": peak, "unit": "TFLOP/s",
+                        "frac": flops / kern / 1e12 / peak,
+                        "note": "algorithmic 2*Q*N*K f32 dot flops per step; peak = dense f16 MFMA / 3 (split-f16: "
+                                "hi.hi + hi.lo + lo.hi)"}}
+    del corpus, Qf
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle import hq_oracle as O
+        rng = np.random.default_rng(7)
+        B = rng.standard_normal((20000, Kd)).astype(np.float32)
+        A = rng.standard_normal((4, Kd)).astype(np.float32)
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < args.cpu_seconds / 4:
+            O.rag_cosine(A[n % 4], B)
+            n += 1
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": n * len(B) / dt, "unit": "pairs/sec", "cores": 1, "kind": "port",
+                               "sample": f"{n} queries x {len(B)} 4096-d frames, oracle rag_cosine (NumPy) in "
+                                         f"{dt:.1f}s"}
+    return res
 
 
 def bench_ingest(args):
@@ -347,6 +395,9 @@ def main():
 
     if not args.no_precomputed:
         rec["precomputed"] = bench_precomputed(args, X, world)
+
+    if not args.no_frames:
+        rec["frames"] = bench_frames(args, world, rank, dev)
 
     if rank == 0 and world == 1 and not args.no_ingest:
         rec["ingest"] = bench_ingest(args)

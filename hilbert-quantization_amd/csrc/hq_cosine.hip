@@ -1,0 +1,231 @@
+// hq_cosine.hip — dense frame similarity on the matrix cores (north star: "the
+// frame similarity as a batched L2/dot over N x (side x side) images — MFMA for the dense
+// query x corpus contraction").
+//
+// Reference: rag/search/engine.py:622-660 _calculate_embedding_cosine_similarity — flatten, truncate
+// to the common length, dot / (|a| |b|), (cos + 1) / 2, 0.0 when a norm is 0 — applied to every
+// (query, stored frame) pair by the RAG search loops (:503-507, :1025-1051).  The reference computes
+// in float32 through BLAS (sdot / snrm2 order), so scores agree within the north star's 1e-5, not bit
+// for bit (DESIGN.md §4.5 has the error budget).
+//
+// Layout (hq_cos_prepare, once per corpus / query batch): every row x is scaled by a power of two s
+// (max |s x| in [0.5, 1)) and split as hi = f16(s x), lo = f16(s x - hi) into a row of Kp = K rounded
+// up to 32 halves each: X16 [rows, 2, Kp] (hi row then lo row), plus inv[row] = 1 / (s |x|) (f64 norm
+// of the original values; 0 for a zero row).  dot(a, b) = (hi_a.hi_b + hi_a.lo_b + lo_a.hi_b) / (s_a
+// s_b) + O(2^-22 |a||b|).
+//
+// GEMM (k_cos_mfma): workgroup = 4 waves, tile 128 queries x 128 frames, K steps of 32 staged through
+// LDS (double buffered, rows padded to 80 B so the sixteen rows of a fragment read fall in distinct
+// banks); each wave owns 64 x 64 = 4 x 4 tiles of v_mfma_f32_16x16x32_f16 x 3 (hi.hi, hi.lo, lo.hi).
+// XCD-aware block order: the query tiles of one frame tile run back to back on one XCD, so the frame
+// tile is read from HBM once per XCD L2.  Epilogue: (acc * inv_q * inv_c + 1) / 2, f64 stores.
+#include "hq_common.h"
+
+namespace hq {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCosT = 128;                 // tile rows (queries) = tile cols (frames)
+constexpr int kCosK = 32;                  // K per step
+constexpr int kCosRow = 40;                // LDS halves per tile row (32 + 8 pad: 80 B)
+constexpr int kCosPlane = kCosT * kCosRow;  // halves per (tile, hi|lo) plane
+
+// ---- prepare: scale, split, inverse norm ------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_cos_prepare(const float* __restrict__ X, int64_t N, int64_t ld, int K,
+                                                     int Kp, int64_t rows_out, _Float16* __restrict__ X16,
+                                                     double* __restrict__ inv) {
+  // one wave per row
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = w0; r < rows_out; r += nw) {
+    _Float16* hi = X16 + r * 2 * Kp;
+    _Float16* lo = hi + Kp;
+    if (r >= N) {  // pad rows: zeros, inv 0
+      for (int k = lane; k < Kp; k += 64) hi[k] = lo[k] = (_Float16)0.0f;
+      if (lane == 0) inv[r] = 0.0;
+      continue;
+    }
+    const float* x = X + r * ld;
+    float amax = 0.0f;
+    double ss = 0.0;
+    for (int k = lane; k < K; k += 64) {
+      const float v = x[k];
+      amax = fmaxf(amax, fabsf(v));
+      ss = fma((double)v, (double)v, ss);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+      ss += __shfl_xor(ss, o, 64);
+    }
+    int e = 0;
+    if (amax > 0.0f) frexpf(amax, &e);  // amax = m 2^e, m in [0.5, 1)
+    const float s = ldexpf(1.0f, -e);   // s x in (-1, 1)
+    for (int k = lane; k < Kp; k += 64) {
+      const float v = k < K ? x[k] * s : 0.0f;
+      const _Float16 h = (_Float16)v;
+      hi[k] = h;
+      lo[k] = (_Float16)(v - (float)h);
+    }
+    if (lane == 0) inv[r] = ss > 0.0 ? 1.0 / ((double)s * sqrt(ss)) : 0.0;
+  }
+}
+
+// ---- GEMM + epilogue ---------------------------------------------------------------------------------
+struct CosArgs {
+  const _Float16* A;  // queries [Qp, 2, Kp]
+  const _Float16* B;  // frames  [Np, 2, Kp]
+  const double* ia;   // [Qp]
+  const double* ib;   // [Np]
+  int Q;
+  int64_t N;
+  int Kp;
+  int qtiles;
+  int64_t ntiles;
+  double* out;  // [Q, N]
+};
+
+__global__ __launch_bounds__(256) void k_cos_mfma(CosArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t cos_smem[];
+  // [buf][A hi, A lo, B hi, B lo][kCosPlane]: 80 KiB, dynamic (above the 64 KiB static limit)
+  auto lds = reinterpret_cast<_Float16 (*)[4][kCosPlane]>(cos_smem);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // XCD-aware order: blocks with equal (blockIdx % 8) share an XCD; the query tiles of a frame tile
+  // are consecutive within one XCD's sequence
+  const int64_t blk = blockIdx.x;
+  const int64_t xcd = blk & 7, slot = blk >> 3;
+  const int qt = (int)(slot % a.qtiles);
+  const int64_t nt = xcd + 8 * (slot / a.qtiles);
+  if (nt >= a.ntiles) return;
+  const int64_t q0 = (int64_t)qt * kCosT, n0 = nt * kCosT;
+  const int Kp = a.Kp;
+  // global -> register staging: plane p (0..3), 128 rows x 4 chunks of 16 B = 512 chunks, 2 per thread
+  h8 stage[4][2];
+  auto load_step = [&](int k0) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const _Float16* base = p < 2 ? a.A + (q0 * 2 + p) * (int64_t)Kp : a.B + (n0 * 2 + (p - 2)) * (int64_t)Kp;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = tid + 256 * i, row = c >> 2, seg = c & 3;
+        stage[p][i] = *reinterpret_cast<const h8*>(base + (int64_t)row * 2 * Kp + k0 + 8 * seg);
+      }
+    }
+  };
+  auto store_step = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = tid + 256 * i, row = c >> 2, seg = c & 3;
+        *reinterpret_cast<h8*>(&lds[buf][p][row * kCosRow + 8 * seg]) = stage[p][i];
+      }
+  };
+  // wave tile: rows 64 * (wv >> 1) .. +64 (queries), cols 64 * (wv & 1) .. +64 (frames)
+  const int wr = 64 * (wv >> 1), wc = 64 * (wv & 1);
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int steps = Kp / kCosK;
+  load_step(0);
+  store_step(0);
+  __syncthreads();
+  for (int s = 0; s < steps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < steps) load_step((s + 1) * kCosK);
+    h8 bh[4], bl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bh[j] = *reinterpret_cast<const h8*>(&lds[buf][2][(wc + 16 * j + fr) * kCosRow + fk]);
+      bl[j] = *reinterpret_cast<const h8*>(&lds[buf][3][(wc + 16 * j + fr) * kCosRow + fk]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const h8 ah = *reinterpret_cast<const h8*>(&lds[buf][0][(wr + 16 * i + fr) * kCosRow + fk]);
+      const h8 al = *reinterpret_cast<const h8*>(&lds[buf][1][(wr + 16 * i + fr) * kCosRow + fk]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // D[query row][frame col]: A operand = queries, B operand = frames, so each output row's 16
+        // frames are 16 consecutive lanes (128-byte stores)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (s + 1 < steps) store_step(buf ^ 1);
+    __syncthreads();
+  }
+  // epilogue: lane holds queries 4 (lane >> 4) + r of each 16-query tile, frame lane & 15
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t q = q0 + wr + 16 * i + 4 * (lane >> 4) + r;
+      if (q >= a.Q) continue;
+      const double iq = a.ia[q];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t n = n0 + wc + 16 * j + fr;
+        if (n >= a.N) continue;
+        const double ic = a.ib[n];
+        const double cs = (double)acc[i][j][r] * iq * ic;
+        a.out[q * a.N + n] = (iq != 0.0 && ic != 0.0) ? (cs + 1.0) / 2.0 : 0.0;
+      }
+    }
+}
+
+}  // namespace hq
+
+using namespace hq;
+
+extern "C" {
+
+int hq_cos_padded_k(int K) { return K <= 0 ? 0 : ((K + kCosK - 1) / kCosK) * kCosK; }
+int64_t hq_cos_padded_rows(int64_t N) { return N <= 0 ? 0 : ((N + kCosT - 1) / kCosT) * kCosT; }
+
+int hq_cos_prepare(const float* X, int64_t N, int64_t ld, int K, void* X16, double* inv, hq_stream_t stream) {
+  if (N < 0 || K <= 0 || ld < K) return fail(HQ_E_INVALID, "bad shape N=%lld K=%d ld=%lld", (long long)N, K, (long long)ld);
+  if (N == 0) return HQ_OK;
+  if (!X || !X16 || !inv) return fail(HQ_E_INVALID, "null buffer");
+  const int Kp = hq_cos_padded_k(K);
+  const int64_t rows = hq_cos_padded_rows(N);
+  int64_t blocks = (rows + 3) / 4;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(k_cos_prepare, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, X, N, ld, K, Kp, rows,
+                     reinterpret_cast<_Float16*>(X16), inv);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* B16, const double* inv_b, int64_t N,
+                       int K, double* out, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || K <= 0) return fail(HQ_E_INVALID, "bad shape");
+  if (Q == 0 || N == 0) return HQ_OK;
+  if (!A16 || !inv_a || !B16 || !inv_b || !out) return fail(HQ_E_INVALID, "null buffer");
+  CosArgs a;
+  a.A = reinterpret_cast<const _Float16*>(A16);
+  a.B = reinterpret_cast<const _Float16*>(B16);
+  a.ia = inv_a;
+  a.ib = inv_b;
+  a.Q = Q;
+  a.N = N;
+  a.Kp = hq_cos_padded_k(K);
+  a.qtiles = (int)(hq_cos_padded_rows(Q) / kCosT);
+  a.ntiles = hq_cos_padded_rows(N) / kCosT;
+  a.out = out;
+  const int64_t nt8 = ((a.ntiles + 7) / 8) * 8;
+  const int64_t blocks = nt8 * a.qtiles;
+  if (blocks > 0x7FFFFFFF) return fail(HQ_E_UNSUPPORTED, "too many tiles");
+  const size_t lds = sizeof(_Float16) * 2 * 4 * kCosPlane;
+  HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_cos_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_cos_mfma, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+}  // extern "C"

@@ -68,6 +68,10 @@ SIGNATURES = {
     "hq_precomputed_similarity": (_i, [_p, _p, _p, _i, _i64, _p, _p, _p, _i64, _i64, _i, _p, _p, _p, _p, _p, _p,
                                        _p, _p]),
     "hq_pearson_f64": (_i, [_p, _p, _i64, _i, _p, _p]),
+    "hq_cos_padded_k": (_i, [_i]),
+    "hq_cos_padded_rows": (_i64, [_i64]),
+    "hq_cos_prepare": (_i, [_p, _i64, _i64, _i, _p, _p, _p]),
+    "hq_cos_scores_mfma": (_i, [_p, _p, _i, _p, _p, _i64, _i, _p, _p]),
 }
 
 _lock = threading.Lock()

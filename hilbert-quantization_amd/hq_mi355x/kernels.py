@@ -353,7 +353,7 @@ def progressive_final(s0, ids, det, best, best_id, best_det, K: int, exc=None):
     return oid, odet, cnt
 
 
-def cosine_scores(a, b, exc=None):
+def cosine_scores_f64(a, b, exc=None):
     """(cos + 1) / 2 of rows of a [Q, K] against rows of b [N, K] (rag/search/engine.py:622-660)."""
     t = torch()
     a2 = _contig(a.reshape(a.shape[0], -1).to(t.float32))
@@ -472,3 +472,59 @@ def pearson_f64(q, C, exc=None):
     out = t.empty(N, dtype=t.float64, device=C2.device)
     _chk(_L().hq_pearson_f64(ptr(q1), ptr(C2), N, m, ptr(out), stream()), exc)
     return out
+
+
+# --------------------------------------------------------------------- S7 on the matrix cores
+
+
+class CosRows:
+    """Split-f16 rows for the MFMA cosine (hq_cos_prepare): X16 [Np, 2, Kp] f16, inv [Np] f64."""
+
+    __slots__ = ("X16", "inv", "N", "K")
+
+    def __init__(self, X16, inv, N, K):
+        self.X16, self.inv, self.N, self.K = X16, inv, int(N), int(K)
+
+
+def cos_prepare(x, exc=None) -> CosRows:
+    t = torch()
+    x2 = x.view(1, -1) if x.dim() == 1 else x.reshape(x.shape[0], -1)
+    if x2.dtype != t.float32:
+        x2 = x2.to(t.float32)
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    N, K = int(x2.shape[0]), int(x2.shape[1])
+    Kp = int(_L().hq_cos_padded_k(K))
+    Np = int(_L().hq_cos_padded_rows(N))
+    X16 = t.empty((max(Np, 1), 2, max(Kp, 1)), dtype=t.float16, device=x2.device)
+    inv = t.empty(max(Np, 1), dtype=t.float64, device=x2.device)
+    if N:
+        _chk(_L().hq_cos_prepare(ptr(x2), N, x2.stride(0) if N > 1 else K, K, ptr(X16), ptr(inv), stream()), exc)
+    return CosRows(X16, inv, N, K)
+
+
+def cosine_scores_mfma(q: CosRows, c: CosRows, exc=None):
+    """(cos + 1) / 2 of every prepared query row against every prepared frame row -> f64 [Q, N]."""
+    t = torch()
+    if q.K != c.K:
+        raise ValueError(f"query length {q.K} != frame length {c.K}")
+    out = t.empty((q.N, c.N), dtype=t.float64, device=q.X16.device)
+    _chk(_L().hq_cos_scores_mfma(ptr(q.X16), ptr(q.inv), q.N, ptr(c.X16), ptr(c.inv), c.N, q.K, ptr(out),
+                                 stream()), exc)
+    return out
+
+
+MFMA_COS_MIN_WORK = 1 << 22
+
+
+def cosine_scores(a, b, exc=None):
+    """(cos + 1) / 2 of every row of a [Q, K] against every row of b [N, K] (rag/search/engine.py:622-660)
+    -> f64 [Q, N].  Large problems run on the matrix cores (split-f16 MFMA, within 1e-5 of the
+    reference's float32 BLAS result); small ones in the f64 kernel."""
+    a2 = a.reshape(a.shape[0], -1)
+    b2 = b.reshape(b.shape[0], -1)
+    Q, N = int(a2.shape[0]), int(b2.shape[0])
+    K = min(int(a2.shape[1]), int(b2.shape[1]))  # the reference truncates to the common length
+    if Q * N * max(K, 1) >= MFMA_COS_MIN_WORK and K > 0 and not os.environ.get("HQ_COS_F64"):
+        return cosine_scores_mfma(cos_prepare(a2[:, :K], exc), cos_prepare(b2[:, :K], exc), exc)
+    return cosine_scores_f64(a, b, exc)

@@ -271,6 +271,20 @@ int hq_precomputed_similarity(const float* q_avgs, const float* q_norm, const fl
                               const int32_t* counts, const double* weights, double* out_overall, uint8_t* out_type,
                               double* out_levels, hq_stream_t stream);
 
+/* ---- S7 dense frame similarity on the matrix cores ------------------------------------------
+ * replaces rag/search/engine.py:622-660 (_calculate_embedding_cosine_similarity) for Q query x N
+ * frame pairs of K values (e.g. 64 x 64 images, K = 4096).
+ * hq_cos_prepare: f32 rows X [N, K] (row stride ld) -> split-f16 rows X16 [hq_cos_padded_rows(N), 2,
+ *   hq_cos_padded_k(K)] (power-of-two scaled hi / lo halves) and inv [padded rows] = 1 / (scale |x|)
+ *   (0 for a zero row).  Prepare a corpus once, each query batch per call.
+ * hq_cos_scores_mfma: out [Q, N] f64 = (cos + 1) / 2 (0 when a norm is 0), split-f16 MFMA contraction
+ *   (v_mfma_f32_16x16x32_f16 x 3), within 1e-5 of the reference's float32 BLAS result.          */
+int hq_cos_padded_k(int K);
+int64_t hq_cos_padded_rows(int64_t N);
+int hq_cos_prepare(const float* X, int64_t N, int64_t ld, int K, void* X16, double* inv, hq_stream_t stream);
+int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* B16, const double* inv_b, int64_t N,
+                       int K, double* out, hq_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -249,3 +249,38 @@ def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, monkeypatch):
         pos = np.nonzero(s >= 0.1)[0]
         ref = pos[np.argsort(-s[pos], kind="stable")][:20]
         assert list(s_ids[a][: s_cnt[a]]) == list(ref), a
+
+
+@pytest.mark.parametrize("Q,N,K", [(3, 5, 4096), (130, 300, 1024), (257, 129, 1000), (64, 2000, 4096)])
+def test_cosine_mfma_vs_f64(hq_lib, Q, N, K):
+    """S7 on the matrix cores (split-f16 MFMA) == exact f64 cosine within 2e-6 on (cos + 1) / 2; zero rows
+    give 0.0, mixed magnitudes and ragged tiles (Q, N not multiples of 128, K not of 32) included."""
+    import torch
+    from hq_mi355x import kernels as K_
+    rng = np.random.default_rng(Q + N + K)
+    A = (rng.standard_normal((Q, K)) * 10 ** rng.uniform(-3, 3, (Q, 1))).astype(np.float32)
+    B = (rng.standard_normal((N, K)) * 10 ** rng.uniform(-3, 3, (N, 1))).astype(np.float32)
+    B[: min(N, 4)] = A[0] * 2.0          # exact matches -> cos = 1
+    A[-1] = 0.0                          # zero query row
+    B[-1] = 0.0                          # zero frame row
+    got = _np(K_.cosine_scores_mfma(K_.cos_prepare(torch.from_numpy(A).cuda()),
+                                    K_.cos_prepare(torch.from_numpy(B).cuda())))
+    a64, b64 = A.astype(np.float64), B.astype(np.float64)
+    na, nb = np.linalg.norm(a64, axis=1), np.linalg.norm(b64, axis=1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        want = ((a64 @ b64.T) / np.outer(na, nb) + 1.0) / 2.0
+    want[na == 0, :] = 0.0
+    want[:, nb == 0] = 0.0
+    assert np.max(np.abs(got - want)) < 2e-6
+    assert np.all(got[-1] == 0.0) and np.all(got[:, -1] == 0.0)
+
+
+def test_cosine_mfma_vs_reference_golden(hq_lib, golden):
+    """The reference's own float32 cosine values (rag/search/engine.py:622-660) within the north star's 1e-5."""
+    import torch
+    from hq_mi355x import kernels as K_
+    g = golden("rag_score")
+    A = g["cos_A"].reshape(len(g["cos_A"]), -1)
+    B = g["cos_B"].reshape(1, -1)
+    got = _np(K_.cosine_scores_mfma(K_.cos_prepare(torch.from_numpy(B).cuda()), K_.cos_prepare(torch.from_numpy(A).cuda())))[0]
+    assert np.max(np.abs(got - g["cos"])) < 1e-5

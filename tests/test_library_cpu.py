@@ -14,7 +14,7 @@ HEADER = os.path.join(ROOT, "include", "hq_mi355x.h")
 
 def declared_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|size_t|const char\*)\s+(hq_[a-z0-9_]+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|size_t|const char\*)\s+(hq_[a-z0-9_]+)\(", txt, re.M)))
 
 
 @pytest.fixture(scope="module")
