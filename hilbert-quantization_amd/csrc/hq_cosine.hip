@@ -21,6 +21,8 @@
 // tile is read from HBM once per XCD L2.  Epilogue: (acc * inv_q * inv_c + 1) / 2, f64 stores.
 #include "hq_common.h"
 
+#include <stdlib.h>
+
 namespace hq {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -29,7 +31,6 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int kCosT = 128;                 // tile rows (queries) = tile cols (frames)
 constexpr int kCosK = 32;                  // K per step
 constexpr int kCosRow = 40;                // LDS halves per tile row (32 + 8 pad: 80 B)
-constexpr int kCosPlane = kCosT * kCosRow;  // halves per (tile, hi|lo) plane
 
 // ---- prepare: scale, split, inverse norm ------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_cos_prepare(const float* __restrict__ X, int64_t N, int64_t ld, int K,
@@ -86,10 +87,17 @@ struct CosArgs {
   double* out;  // [Q, N]
 };
 
+// TQ = query rows per workgroup tile (128 or 256); frames per tile kCosT = 128.  LDS per buffer:
+// (2 TQ + 2 * 128) rows of 80 B.
+template <int TQ>
 __global__ __launch_bounds__(256) void k_cos_mfma(CosArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t cos_smem[];
-  // [buf][A hi, A lo, B hi, B lo][kCosPlane]: 80 KiB, dynamic (above the 64 KiB static limit)
-  auto lds = reinterpret_cast<_Float16 (*)[4][kCosPlane]>(cos_smem);
+  constexpr int kBuf = (2 * TQ + 2 * kCosT) * kCosRow;  // halves per buffer
+  _Float16* lds0 = reinterpret_cast<_Float16*>(cos_smem);
+  // plane p of buffer b: A hi / A lo (TQ rows), B hi / B lo (128 rows)
+  auto plane = [&](int b, int p) -> _Float16* {
+    return lds0 + b * kBuf + (p < 2 ? p * TQ * kCosRow : 2 * TQ * kCosRow + (p - 2) * kCosT * kCosRow);
+  };
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // XCD-aware order: blocks with equal (blockIdx % 8) share an XCD; the query tiles of a frame tile
   // are consecutive within one XCD's sequence
@@ -98,36 +106,48 @@ __global__ __launch_bounds__(256) void k_cos_mfma(CosArgs a) {
   const int qt = (int)(slot % a.qtiles);
   const int64_t nt = xcd + 8 * (slot / a.qtiles);
   if (nt >= a.ntiles) return;
-  const int64_t q0 = (int64_t)qt * kCosT, n0 = nt * kCosT;
+  const int64_t q0 = (int64_t)qt * TQ, n0 = nt * kCosT;
   const int Kp = a.Kp;
-  // global -> register staging: plane p (0..3), 128 rows x 4 chunks of 16 B = 512 chunks, 2 per thread
-  h8 stage[4][2];
+  // global -> register staging: A planes TQ rows, B planes 128 rows, 4 chunks of 16 B per row
+  constexpr int CA = TQ * 4 / 256, CB = kCosT * 4 / 256;  // chunks per thread per plane
+  h8 sa[2][CA], sb[2][CB];
   auto load_step = [&](int k0) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const _Float16* base = p < 2 ? a.A + (q0 * 2 + p) * (int64_t)Kp : a.B + (n0 * 2 + (p - 2)) * (int64_t)Kp;
+    for (int p = 0; p < 2; ++p) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < CA; ++i) {
         const int c = tid + 256 * i, row = c >> 2, seg = c & 3;
-        stage[p][i] = *reinterpret_cast<const h8*>(base + (int64_t)row * 2 * Kp + k0 + 8 * seg);
+        sa[p][i] = *reinterpret_cast<const h8*>(a.A + ((q0 + row) * 2 + p) * (int64_t)Kp + k0 + 8 * seg);
+      }
+#pragma unroll
+      for (int i = 0; i < CB; ++i) {
+        const int c = tid + 256 * i, row = c >> 2, seg = c & 3;
+        sb[p][i] = *reinterpret_cast<const h8*>(a.B + ((n0 + row) * 2 + p) * (int64_t)Kp + k0 + 8 * seg);
       }
     }
   };
   auto store_step = [&](int buf) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+    for (int p = 0; p < 2; ++p) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < CA; ++i) {
         const int c = tid + 256 * i, row = c >> 2, seg = c & 3;
-        *reinterpret_cast<h8*>(&lds[buf][p][row * kCosRow + 8 * seg]) = stage[p][i];
+        *reinterpret_cast<h8*>(plane(buf, p) + row * kCosRow + 8 * seg) = sa[p][i];
       }
-  };
-  // wave tile: rows 64 * (wv >> 1) .. +64 (queries), cols 64 * (wv & 1) .. +64 (frames)
-  const int wr = 64 * (wv >> 1), wc = 64 * (wv & 1);
-  const int fr = lane & 15, fk = 8 * (lane >> 4);
-  f4 acc[4][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < CB; ++i) {
+        const int c = tid + 256 * i, row = c >> 2, seg = c & 3;
+        *reinterpret_cast<h8*>(plane(buf, 2 + p) + row * kCosRow + 8 * seg) = sb[p][i];
+      }
+    }
+  };
+  // wave tile: queries (TQ/2) * (wv >> 1) .. + TQ/2, frames 64 * (wv & 1) .. +64
+  constexpr int MI = TQ / 32;  // 16-row query tiles per wave
+  const int wr = (TQ / 2) * (wv >> 1), wc = 64 * (wv & 1);
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  f4 acc[MI][4];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
@@ -141,13 +161,13 @@ __global__ __launch_bounds__(256) void k_cos_mfma(CosArgs a) {
     h8 bh[4], bl[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      bh[j] = *reinterpret_cast<const h8*>(&lds[buf][2][(wc + 16 * j + fr) * kCosRow + fk]);
-      bl[j] = *reinterpret_cast<const h8*>(&lds[buf][3][(wc + 16 * j + fr) * kCosRow + fk]);
+      bh[j] = *reinterpret_cast<const h8*>(plane(buf, 2) + (wc + 16 * j + fr) * kCosRow + fk);
+      bl[j] = *reinterpret_cast<const h8*>(plane(buf, 3) + (wc + 16 * j + fr) * kCosRow + fk);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const h8 ah = *reinterpret_cast<const h8*>(&lds[buf][0][(wr + 16 * i + fr) * kCosRow + fk]);
-      const h8 al = *reinterpret_cast<const h8*>(&lds[buf][1][(wr + 16 * i + fr) * kCosRow + fk]);
+    for (int i = 0; i < MI; ++i) {
+      const h8 ah = *reinterpret_cast<const h8*>(plane(buf, 0) + (wr + 16 * i + fr) * kCosRow + fk);
+      const h8 al = *reinterpret_cast<const h8*>(plane(buf, 1) + (wr + 16 * i + fr) * kCosRow + fk);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         // D[query row][frame col]: A operand = queries, B operand = frames, so each output row's 16
@@ -162,7 +182,7 @@ __global__ __launch_bounds__(256) void k_cos_mfma(CosArgs a) {
   }
   // epilogue: lane holds queries 4 (lane >> 4) + r of each 16-query tile, frame lane & 15
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t q = q0 + wr + 16 * i + 4 * (lane >> 4) + r;
@@ -177,6 +197,19 @@ __global__ __launch_bounds__(256) void k_cos_mfma(CosArgs a) {
         a.out[q * a.N + n] = (iq != 0.0 && ic != 0.0) ? (cs + 1.0) / 2.0 : 0.0;
       }
     }
+}
+
+template <int TQ>
+static int launch_cos(CosArgs a, hipStream_t s) {
+  a.qtiles = (int)((hq_cos_padded_rows(a.Q) + TQ - 1) / TQ);
+  const int64_t nt8 = ((a.ntiles + 7) / 8) * 8;
+  const int64_t blocks = nt8 * a.qtiles;
+  if (blocks > 0x7FFFFFFF) return fail(HQ_E_UNSUPPORTED, "too many tiles");
+  const size_t lds = sizeof(_Float16) * 2 * (2 * TQ + 2 * kCosT) * kCosRow;
+  HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_cos_mfma<TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_cos_mfma<TQ>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
 }
 
 }  // namespace hq
@@ -215,17 +248,14 @@ int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* 
   a.Q = Q;
   a.N = N;
   a.Kp = hq_cos_padded_k(K);
-  a.qtiles = (int)(hq_cos_padded_rows(Q) / kCosT);
   a.ntiles = hq_cos_padded_rows(N) / kCosT;
   a.out = out;
-  const int64_t nt8 = ((a.ntiles + 7) / 8) * 8;
-  const int64_t blocks = nt8 * a.qtiles;
-  if (blocks > 0x7FFFFFFF) return fail(HQ_E_UNSUPPORTED, "too many tiles");
-  const size_t lds = sizeof(_Float16) * 2 * 4 * kCosPlane;
-  HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_cos_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k_cos_mfma, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
-  HQ_CHECK_LAUNCH();
-  return HQ_OK;
+  // 256-query tiles need the query rows padded to 256 (hq_cos_padded_rows pads to 128): use them only
+  // when the padded query count is a multiple of 256
+  const char* ev = getenv("HQ_COS_TQ");
+  const int tq = ev ? atoi(ev) : 128;  // A/B: 256-query tiles run at 1 wave per SIMD and measured 7% slower
+  if (tq == 256 && hq_cos_padded_rows(Q) % 256 == 0) return launch_cos<256>(a, (hipStream_t)stream);
+  return launch_cos<128>(a, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -1,0 +1,7 @@
+#!/bin/bash
+# A/B the S7 MFMA cosine: each argument is an env assignment list ("-" = defaults)
+for v in "$@"; do
+  [ "$v" = "-" ] && v="HQ_NONE=1"
+  r=$(env $v timeout -k 10 120 python bench.py --no-search --no-stream --no-precomputed --no-ingest --no-cpu --steps 2 | python3 -c "import json,sys; d=json.loads(sys.stdin.read())['frames']; print(round(d['value']/1e9,2), round(d['roofline']['achieved'],1), round(d['roofline']['frac'],3), round(d['ms_per_step'],3))") || exit 1
+  echo "$v: $r"
+done
