@@ -14,13 +14,15 @@
 // of the original values; 0 for a zero row).  dot(a, b) = (hi_a.hi_b + hi_a.lo_b + lo_a.hi_b) / (s_a
 // s_b) + O(2^-22 |a||b|).
 //
-// GEMM (default k_cos_g3<256>): workgroup = 8 waves, tile 128 queries x 256 frames, each wave 64 x 64 =
-// 4 x 4 tiles of v_mfma_f32_16x16x32_f16 x 3 (hi.hi, hi.lo, lo.hi), K steps of 32.  Operands go HBM ->
+// GEMM (default k_cos_g3<256, 1>): workgroup = 8 waves, tile 128 queries x 256 frames, each wave 64 x 64
+// = 4 x 4 tiles of v_mfma_f32_16x16x32_f16 x 3 (hi.hi, hi.lo, lo.hi), K steps of 32.  Operands go HBM ->
 // LDS by global_load_lds_dwordx4 (LDS-DMA, no staging registers) into three stages, two steps ahead,
-// XOR-swizzled on the source address so the fragment reads are bank-conflict free.  XCD-aware block
-// order: the query tiles of one frame tile run back to back on one XCD, so the frame tile is read from
-// HBM once per XCD L2.  Epilogue: (acc * inv_q * inv_c + 1) / 2, f64 stores.  k_cos_mfma (register
-// staged, two buffers, 128 x 128) stays as the A/B baseline (HQ_COS_KERNEL=regstage).
+// XOR-swizzled on the source address so the fragment reads are bank-conflict free.  Ping-pong: the two
+// waves of every SIMD run one barrier phase apart, one issuing its reads + DMA while the other runs
+// its MFMAs.  XCD-aware block order: the query tiles of one frame tile run back to back on one XCD, so
+// the frame tile is read from HBM once per XCD L2.  Epilogue: (acc * inv_q * inv_c + 1) / 2, f64
+// stores.  A/B baselines: k_cos_g3<256, 0> (same staging, waves in lockstep) and k_cos_mfma (register
+// staged, two buffers, 128 x 128).
 #include "hq_common.h"
 
 #include <stdlib.h>
@@ -213,9 +215,10 @@ __device__ __forceinline__ int cos_sw(int g) { return (0x78 >> (2 * g)) & 3; }  
 // Three-stage LDS-DMA pipeline: tile 128 queries x TN frames, TN / 32 waves (each 64 x 64), K steps of
 // 32, three LDS stages so the DMA of step s + 2 is in flight while step s computes (two steps of MFMA
 // cover the HBM latency of the streamed frame rows).  The DMAs are inline asm (hipcc would otherwise
-// drain them with vmcnt(0) at every barrier); each wave retires its own pieces of stage s with a
-// counted vmcnt (the PW pieces of stage s + 1 stay in flight) and one s_barrier publishes the stage.
-template <int TN>
+// drain them with vmcnt(0) at every barrier); each wave retires its own pieces of a stage with a
+// counted vmcnt (the PW pieces of the next stage stay in flight) and an s_barrier publishes it.
+// PP = 0: all waves in lockstep, one barrier per K step; PP = 1: ping-pong (below).
+template <int TN, int PP>
 __global__ __launch_bounds__(TN * 2) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_cos_g3(CosArgs a, int64_t np_rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t cos_smem[];
   constexpr int TQ = 128, NW = TN / 32, kRow = kCosK, ST = 3;
@@ -253,15 +256,16 @@ __global__ __launch_bounds__(TN * 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
     const int off = (p < 2 ? p * TQ * kRow : 2 * TQ * kRow + (p - 2) * TN * kRow) + slab * 16 * kRow;
     dst[t] = __builtin_amdgcn_readfirstlane(lbase + 2 * off);
   }
+  auto piece = [&](int t, int k0, int stage) {
+    uint32_t keep;
+    const _Float16* g = src[t] + k0;
+    const uint32_t d = dst[t] + stage * (2 * kBuf);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(d) : "memory");
+  };
   auto issue = [&](int k0, int stage) {
 #pragma unroll
-    for (int t = 0; t < PW; ++t) {
-      uint32_t keep;
-      const _Float16* g = src[t] + k0;
-      const uint32_t d = dst[t] + stage * (2 * kBuf);
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(g), "s"(d) : "memory");
-    }
+    for (int t = 0; t < PW; ++t) piece(t, k0, stage);
   };
   const int wr = 64 * (wv & 1), wc = 64 * (wv >> 1);
   const int fr = lane & 15;
@@ -276,6 +280,62 @@ __global__ __launch_bounds__(TN * 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
   issue(0, 0);
   if (steps > 1) issue(kCosK, 1);
   int stage = 0;
+  if constexpr (PP) {
+    // Ping-pong: waves w and w + 4 share a SIMD; group 1 (waves 4-7) runs one barrier phase behind
+    // group 0, so on every SIMD one wave issues its fragment reads + DMA while the other runs MFMAs.
+    // Phases per K step: memory (DMA of step s + 2, 16 ds_read_b128, lgkmcnt(0)) then compute (48
+    // MFMA), each closed by one block barrier.  Stage s + 1 is published at barrier 2s + 2: group 0
+    // reaches it after computing step s, group 1 after its memory phase of step s; both retire it
+    // with vmcnt(PW) (only the just-issued stage s + 2 stays in flight).  The lgkmcnt(0) before each
+    // memory-phase barrier retires the reads of a stage before the other group's DMA may overwrite it.
+    const int grp = __builtin_amdgcn_readfirstlane(wv >> 2);
+    if (steps > 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (grp) asm volatile("s_barrier" ::: "memory");
+    for (int s = 0; s < steps; ++s) {
+      if (s + 2 < steps) issue((s + 2) * kCosK, stage == 0 ? 2 : stage - 1);
+      const _Float16* pA = lds0 + stage * kBuf;
+      const _Float16* pB = pA + 2 * TQ * kRow;
+      h8 bh[4], bl[4], ah[4], al[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bh[j] = *reinterpret_cast<const h8*>(pB + (wc + 16 * j + fr) * kRow + rseg);
+        bl[j] = *reinterpret_cast<const h8*>(pB + TN * kRow + (wc + 16 * j + fr) * kRow + rseg);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ah[i] = *reinterpret_cast<const h8*>(pA + (wr + 16 * i + fr) * kRow + rseg);
+        al[i] = *reinterpret_cast<const h8*>(pA + TQ * kRow + (wr + 16 * i + fr) * kRow + rseg);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (grp) {
+        if (s + 2 < steps) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (!grp) {
+        if (s + 2 < steps) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      } else {
+        asm volatile("s_barrier" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      stage = stage == ST - 1 ? 0 : stage + 1;
+    }
+    if (!grp) asm volatile("s_barrier" ::: "memory");  // group 1's extra barrier: equal counts per wave
+  } else
   for (int s = 0; s < steps; ++s) {
     // retire this wave's pieces of stage s (those of s + 1 may stay in flight), then publish
     if (s + 1 < steps) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PW) : "memory");
@@ -328,7 +388,7 @@ __global__ __launch_bounds__(TN * 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
     }
 }
 
-template <int TN>
+template <int TN, int PP>
 static int launch_g3(CosArgs a, hipStream_t s) {
   const int64_t np_rows = a.ntiles * kCosT;
   a.qtiles = (int)(hq_cos_padded_rows(a.Q) / 128);
@@ -337,7 +397,7 @@ static int launch_g3(CosArgs a, hipStream_t s) {
   const int64_t blocks = nt8 * a.qtiles;
   if (blocks > 0x7FFFFFFF) return fail(HQ_E_UNSUPPORTED, "too many tiles");
   const size_t lds = sizeof(_Float16) * 3 * (2 * 128 + 2 * TN) * kCosK;
-  auto kern = k_cos_g3<TN>;
+  auto kern = k_cos_g3<TN, PP>;
   HQ_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(TN * 2), lds, s, a, np_rows);
   HQ_CHECK_LAUNCH();
@@ -395,10 +455,12 @@ int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* 
   a.Kp = hq_cos_padded_k(K);
   a.ntiles = hq_cos_padded_rows(N) / kCosT;
   a.out = out;
-  // A/B: HQ_COS_KERNEL=regstage runs the register-staged two-buffer kernel (DESIGN.md §4.5 has both)
+  // A/B: HQ_COS_KERNEL=regstage (register-staged two-buffer kernel) or lockstep (the DMA kernel without
+  // the ping-pong stagger); DESIGN.md §4.5 has the measurements
   const char* ek = getenv("HQ_COS_KERNEL");
   if (ek && strcmp(ek, "regstage") == 0) return launch_cos<128>(a, (hipStream_t)stream);
-  return launch_g3<256>(a, (hipStream_t)stream);
+  if (ek && strcmp(ek, "lockstep") == 0) return launch_g3<256, 0>(a, (hipStream_t)stream);
+  return launch_g3<256, 1>(a, (hipStream_t)stream);
 }
 
 }  // extern "C"

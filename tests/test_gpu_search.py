@@ -286,11 +286,12 @@ def test_cosine_mfma_vs_reference_golden(hq_lib, golden):
     assert np.max(np.abs(got - g["cos"])) < 1e-5
 
 
-@pytest.mark.parametrize("Q,N,K", [(130, 300, 1024), (257, 700, 4096), (1, 257, 32)])
-def test_cosine_dma_kernel_matches_regstage(hq_lib, Q, N, K, monkeypatch):
-    """The default LDS-DMA three-stage kernel (k_cos_g3, 256-frame tiles, swizzled LDS) and the
-    register-staged baseline (k_cos_mfma, 128-frame tiles) run the same MFMA sequence per output, so
-    their scores are bit-identical, ragged last frame tile (N not a multiple of 256) included."""
+@pytest.mark.parametrize("Q,N,K", [(130, 300, 1024), (257, 700, 4096), (1, 257, 32), (5, 40, 64)])
+def test_cosine_dma_kernels_match_regstage(hq_lib, Q, N, K, monkeypatch):
+    """The default LDS-DMA ping-pong kernel (k_cos_g3<256, 1>: 256-frame tiles, swizzled LDS, staggered
+    wave groups), its lockstep form and the register-staged baseline (k_cos_mfma, 128-frame tiles) run
+    the same MFMA sequence per output, so their scores are bit-identical; ragged last frame tile (N not
+    a multiple of 256) and 1- and 2-step K loops (K = 32, 64: the prologue / drain paths) included."""
     import torch
     from hq_mi355x import kernels as K_
     rng = np.random.default_rng(11 + Q + N)
@@ -298,6 +299,6 @@ def test_cosine_dma_kernel_matches_regstage(hq_lib, Q, N, K, monkeypatch):
     B = rng.standard_normal((N, K)).astype(np.float32)
     pa, pb = K_.cos_prepare(torch.from_numpy(A).cuda()), K_.cos_prepare(torch.from_numpy(B).cuda())
     got = _np(K_.cosine_scores_mfma(pa, pb))
-    monkeypatch.setenv("HQ_COS_KERNEL", "regstage")
-    base = _np(K_.cosine_scores_mfma(pa, pb))
-    np.testing.assert_array_equal(got, base)
+    for kern in ("lockstep", "regstage"):
+        monkeypatch.setenv("HQ_COS_KERNEL", kern)
+        np.testing.assert_array_equal(got, _np(K_.cosine_scores_mfma(pa, pb)), err_msg=kern)
