@@ -19,6 +19,7 @@
 #include "hq_common.h"
 
 #include <stdlib.h>
+#include <string.h>
 
 namespace hq {
 
@@ -36,6 +37,9 @@ struct PreLevel {
 };
 struct PrePlan {
   int nlev, total, n_small, nleaves, lsh_n;
+  int maxper;    // most 128-value leaves in one square
+  int tree_lds;  // 1: combine the leaves through LDS (squares of > 64 leaves, or HQ_PRECOMP_TREE=lds)
+  int diag;      // A/B diagnostics only (wrong averages): bit 0 skip small squares, 1 leaves, 2 load, 3 store
   PreLevel lv[kPreMaxLevels];
 };
 
@@ -46,6 +50,9 @@ static int pre_plan(int n, int max_levels, int min_sq, PrePlan& p) {
   p.total = 0;
   p.n_small = 0;
   p.nleaves = 0;
+  p.maxper = 0;
+  p.tree_lds = 0;
+  p.diag = 0;
   p.lsh_n = ilog2(n);
   int s = min_sq;
   int lv_g[16], lv_s[16], c = 0;
@@ -70,11 +77,15 @@ static int pre_plan(int n, int max_levels, int min_sq, PrePlan& p) {
       if (L.off != p.n_small) return HQ_E_UNSUPPORTED;  // small squares form a prefix (finest first)
       p.n_small += L.count;
     } else {
+      const int per = L.s * L.s / 128;
+      p.nleaves = (p.nleaves + per - 1) / per * per;  // a square's leaves start on a multiple of per
       L.leaf0 = p.nleaves;
-      p.nleaves += L.count * (L.s * L.s / 128);
+      p.nleaves += L.count * per;
+      if (per > p.maxper) p.maxper = per;
     }
   }
   p.nlev = c;
+  if (2 * p.maxper > 64) p.tree_lds = 1;  // a square's leaf lanes would span waves
   return HQ_OK;
 }
 
@@ -97,10 +108,13 @@ __device__ __forceinline__ void pre_square(const PreLevel& L, int k, int& x0, in
   }
 }
 
+// np.mean's f64 division by the count (_methods._mean; f32 input: f32(f64(sum) / cnt)).  Every count
+// here is a power of two (s * s squares), so the division is the exact product with 1 / cnt: one
+// rounding either way, and none at all before the final cast unless the result is subnormal.
 template <typename T>
-__device__ __forceinline__ float pre_mean(T s, int cnt) {
-  if constexpr (sizeof(T) == 4) return (float)((double)s / (double)cnt);  // np.mean f32 (_methods._mean)
-  else return (float)(s / (double)cnt);                                 // f64 mean, stored as float32
+__device__ __forceinline__ float pre_mean(T s, int lcnt) {
+  const double inv = __builtin_amdgcn_ldexp(1.0, -lcnt);  // 2^-lcnt, cnt = 2^lcnt
+  return (float)((double)s * inv);
 }
 
 // eight consecutive values from a 16-byte aligned LDS address
@@ -116,6 +130,18 @@ __device__ __forceinline__ void load8(const T* p, T (&v)[8]) {
       v[2 * h] = a.x;
       v[2 * h + 1] = a.y;
     }
+  }
+}
+
+// four consecutive values from a 16-byte aligned LDS address
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, T (&v)[4]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  } else {
+    const double2 a = *reinterpret_cast<const double2*>(p), b = *reinterpret_cast<const double2*>(p + 2);
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
   }
 }
 
@@ -162,10 +188,26 @@ __device__ __forceinline__ T sq_sum(const T* b, int ld) {
   return T(0) + (((r8[0] + r8[1]) + (r8[2] + r8[3])) + ((r8[4] + r8[5]) + (r8[6] + r8[7])));
 }
 
+// all squares of one level with S x S <= 128 values (S = 1, 2, 4, 8): one NumPy pairwise leaf per thread
+template <typename T, int S>
+__device__ __forceinline__ void pre_small(const PreLevel& L, const T* img, int ld, float* res, int tid) {
+  for (int k = tid; k < L.count; k += kPreThreads) {
+    int x0, y0;
+    pre_square(L, k, x0, y0);
+    const T* b = img + y0 * ld + x0;
+    T sum;
+    if constexpr (S == 8) sum = sq_sum<T, 8>(b, ld);
+    else if constexpr (S == 4) sum = sq_sum<T, 4>(b, ld);
+    else if constexpr (S == 2) sum = T(0) + ((((T(-0.0) + b[0]) + b[1]) + b[ld]) + b[ld + 1]);  // NumPy n < 8 branch
+    else sum = T(0) + (T(-0.0) + b[0]);  // one value
+    res[L.off + k] = pre_mean<T>(sum, 2 * L.lsh);
+  }
+}
+
 // kind 0: images (n x n row-major, image stride `stride` elements); kind 1: 1-D Hilbert-ordered
 // parameter streams of d values (row stride `stride`), zero-padded to n*n and mapped to 2-D
 // (core/pipeline.py:298-319 _get_2d_representation).
-template <typename T>
+template <typename T, int PF>
 __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ in, int kind, int64_t N, int64_t stride,
                                                          int d, int n, PrePlan plan, float* __restrict__ out,
                                                          int64_t out_stride, int use_lut, int ld) {
@@ -177,35 +219,60 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
   const int tid = threadIdx.x;
   const int lsh_n = plan.lsh_n;
   if (tid < plan.nlev) lv[tid] = plan.lv[tid];
-  for (int64_t e = blockIdx.x; e < N; e += gridDim.x) {
+  // The barriers below order LDS only: s_waitcnt lgkmcnt(0) + s_barrier, so the prefetch of the next
+  // image (plain global loads into registers) stays in flight through this image's reductions
+  // (__syncthreads' release fence would wait for it with vmcnt(0)).
+  auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  // 1-D streams with the compile-time group LUT (n = 16 / 32 / 64): each thread owns float4 groups
+  // j = tid + 256 i (2x2 blocks, Hilbert layout invariant); their LUT entries live in registers and
+  // the next image's values are fetched while the current one is reduced
+  constexpr int kPreG = 4;  // groups per thread at n = 64
+  const int G = (n * n) >> 2;
+  uint32_t lut[kPreG];
+  T pf[kPreG][4];
+  if (use_lut) {
+    const uint32_t* glut = n == 16 ? kPreLut16.v : (n == 32 ? kPreLut32.v : kPreLut64.v);
+#pragma unroll
+    for (int i = 0; i < kPreG; ++i) lut[i] = tid + kPreThreads * i < G ? glut[tid + kPreThreads * i] : 0u;
+  }
+  auto fetch = [&](int64_t e) {
     const T* src = in + e * stride;
     const bool vec_ok = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
-    if (kind == 0) {
+#pragma unroll
+    for (int i = 0; i < kPreG; ++i) {
+      const int j = tid + kPreThreads * i;
+      if (vec_ok && 4 * j + 3 < d) {
+        if constexpr (sizeof(T) == 4) {
+          const float4 q4 = *reinterpret_cast<const float4*>(src + 4 * j);
+          pf[i][0] = q4.x; pf[i][1] = q4.y; pf[i][2] = q4.z; pf[i][3] = q4.w;
+        } else {
+          const double2 a2 = *reinterpret_cast<const double2*>(src + 4 * j);
+          const double2 b2 = *reinterpret_cast<const double2*>(src + 4 * j + 2);
+          pf[i][0] = a2.x; pf[i][1] = a2.y; pf[i][2] = b2.x; pf[i][3] = b2.y;
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) pf[i][m] = 4 * j + m < d ? src[4 * j + m] : T(0);  // zero padding
+      }
+    }
+  };
+  if (PF && use_lut && (int64_t)blockIdx.x < N) fetch(blockIdx.x);
+  for (int64_t e = blockIdx.x; e < N; e += gridDim.x) {
+    const T* src = in + e * stride;
+    if (plan.diag & 4) {
+    } else if (kind == 0) {
       for (int i = tid; i < n * n; i += kPreThreads) img[(i >> lsh_n) * ld + (i & (n - 1))] = src[i];
     } else if (use_lut) {
-      const uint32_t* glut = n == 16 ? kPreLut16.v : (n == 32 ? kPreLut32.v : kPreLut64.v);
-      // float4 groups = 2x2 blocks (Hilbert layout invariant): compile-time group LUT
-      for (int j = tid; j < (n * n) >> 2; j += kPreThreads) {
-        const uint32_t ent = glut[j], off0 = ent & 0xFFFFu, code = ent >> 16;
-        const uint32_t off = (off0 >> lsh_n) * ld + (off0 & (n - 1));
-        T v[4];
-        if (vec_ok && 4 * j + 3 < d) {
-          if constexpr (sizeof(T) == 4) {
-            const float4 q4 = *reinterpret_cast<const float4*>(src + 4 * j);
-            v[0] = q4.x; v[1] = q4.y; v[2] = q4.z; v[3] = q4.w;
-          } else {
-            const double2 a2 = *reinterpret_cast<const double2*>(src + 4 * j);
-            const double2 b2 = *reinterpret_cast<const double2*>(src + 4 * j + 2);
-            v[0] = a2.x; v[1] = a2.y; v[2] = b2.x; v[3] = b2.y;
-          }
-        } else {
+      if (!PF) fetch(e);
 #pragma unroll
-          for (int m = 0; m < 4; ++m) v[m] = 4 * j + m < d ? src[4 * j + m] : T(0);
-        }
+      for (int i = 0; i < kPreG; ++i) {
+        if (tid + kPreThreads * i >= G) continue;
+        const uint32_t off0 = lut[i] & 0xFFFFu, code = lut[i] >> 16;
+        const uint32_t off = (off0 >> lsh_n) * ld + (off0 & (n - 1));
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const uint32_t b = (code >> (2 * m)) & 3u;
-          img[off + (b & 1u) + (b >> 1) * ld] = v[m];
+          img[off + (b & 1u) + (b >> 1) * ld] = pf[i][m];
         }
       }
     } else {
@@ -215,36 +282,29 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
         img[y * ld + x] = i < d ? src[i] : T(0);
       }
     }
-    __syncthreads();
+    lds_barrier();
+    if (PF && use_lut && e + gridDim.x < N) fetch(e + gridDim.x);
     // squares of <= 128 values: one thread each, level by level (uniform geometry per loop); 4x4 and
     // 8x8 squares read whole row segments (their x0 is a multiple of s/2) and sum in registers
-    for (int l = 0; l < plan.nlev; ++l) {
+    for (int l = 0; l < plan.nlev && !(plan.diag & 1); ++l) {
       const PreLevel& L = plan.lv[l];
       if (L.leaf0 >= 0) continue;
-      const int s = L.s, lsh = L.lsh, msk = s - 1;
-      for (int k = tid; k < L.count; k += kPreThreads) {
-        int x0, y0;
-        pre_square(L, k, x0, y0);
-        const T* b = img + y0 * ld + x0;
-        T sum;
-        if (s == 8) sum = sq_sum<T, 8>(b, ld);
-        else if (s == 4) sum = sq_sum<T, 4>(b, ld);
-        else if (s == 2) sum = T(0) + ((((T(-0.0) + b[0]) + b[1]) + b[ld]) + b[ld + 1]);  // NumPy n < 8 branch
-        else {
-          auto f = [&](int q) -> T { return b[(q >> lsh) * ld + (q & msk)]; };
-          sum = T(0) + pw_leaf<T>(f, 0, s * s);  // np_sum for <= 128 values
-        }
-        res[L.off + k] = pre_mean<T>(sum, s * s);
-      }
+      // one straight-line loop per square size (the size is uniform per level)
+      if (L.s == 2) pre_small<T, 2>(L, img, ld, res, tid);
+      else if (L.s == 4) pre_small<T, 4>(L, img, ld, res, tid);
+      else if (L.s == 8) pre_small<T, 8>(L, img, ld, res, tid);
+      else pre_small<T, 1>(L, img, ld, res, tid);
     }
     // 128-value leaves of the larger squares: 16 steps of 8 consecutive values (one row segment,
     // 8-aligned because x0 is a multiple of s/2 >= 8), eight accumulators as NumPy's pairwise leaf
-    for (int t = tid; t < plan.nleaves; t += kPreThreads) {
-      int l = plan.nlev - 1;
+    auto leaf_sum = [&](int t, int& l, int& k, int& leaf) -> T {
+      l = plan.nlev - 1;
       while (lv[l].leaf0 < 0 || t < lv[l].leaf0) --l;
       const int s = lv[l].s, lsh = lv[l].lsh, msk = s - 1;
       const int lper = 2 * lsh - 7;  // log2 of the leaves per square
-      const int k = (t - lv[l].leaf0) >> lper, leaf = (t - lv[l].leaf0) & ((1 << lper) - 1);
+      k = (t - lv[l].leaf0) >> lper;
+      leaf = (t - lv[l].leaf0) & ((1 << lper) - 1);
+      if (k >= lv[l].count) return T(0);  // alignment gap before the next level
       int x0, y0;
       pre_square(lv[l], k, x0, y0);
       const T* b = img + y0 * ld + x0;
@@ -257,9 +317,63 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
 #pragma unroll
         for (int j = 0; j < 8; ++j) r[j] = i == 0 ? v[j] : r[j] + v[j];
       }
-      part[t] = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    }
-    __syncthreads();
+      return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    };
+    if (plan.diag & 2) {
+    } else if (!plan.tree_lds) {
+      // Two lanes per leaf: lane h = 0 / 1 keeps accumulators r0-r3 / r4-r7 (columns 4h..4h+3 of each
+      // 8-value step), so ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7)) is one shuffle — NumPy's leaf order
+      // exactly.  A square's <= 32 leaves then sit on 2 * per consecutive lanes of one wave (leaf0 is
+      // aligned to per): the balanced tree over them (adjacent pairs first) by shuffles, and the first
+      // lane stores the mean.
+      for (int u0 = 0; u0 < 2 * plan.nleaves; u0 += kPreThreads) {
+        const int u = u0 + tid, t = u >> 1, h = u & 1;
+        int l = 0, k = 0, leaf = 0;
+        T v = T(0);
+        bool live = false;
+        if (t < plan.nleaves) {
+          l = plan.nlev - 1;
+          while (lv[l].leaf0 < 0 || t < lv[l].leaf0) --l;
+          const int s = lv[l].s, lsh = lv[l].lsh, msk = s - 1;
+          const int lper = 2 * lsh - 7;
+          k = (t - lv[l].leaf0) >> lper;
+          leaf = (t - lv[l].leaf0) & ((1 << lper) - 1);
+          live = k < lv[l].count;  // else an alignment gap before the next level
+          if (live) {
+            int x0, y0;
+            pre_square(lv[l], k, x0, y0);
+            const T* b = img + y0 * ld + x0 + 4 * h;
+            T r[4];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int q = (leaf << 7) + 8 * i;
+              T w4[4];
+              load4<T>(b + (q >> lsh) * ld + (q & msk), w4);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) r[j] = i == 0 ? w4[j] : r[j] + w4[j];
+            }
+            v = (r[0] + r[1]) + (r[2] + r[3]);
+          }
+        }
+        const int per = live ? (lv[l].s * lv[l].s) >> 7 : 0;
+        {
+          const T o = __shfl_down(v, 1, 64);
+          if (h == 0) v = v + o;
+        }
+        for (int w = 1; w < plan.maxper; w <<= 1) {
+          const T o = __shfl_down(v, 2 * w, 64);
+          if (w < per && h == 0 && (leaf & (2 * w - 1)) == 0) v = v + o;
+        }
+        if (live && h == 0 && leaf == 0) res[lv[l].off + k] = pre_mean<T>(T(0) + v, 2 * lv[l].lsh);
+      }
+      lds_barrier();
+    } else {
+      for (int t = tid; t < plan.nleaves; t += kPreThreads) {
+        int l, k, leaf;
+        const T v = leaf_sum(t, l, k, leaf);
+        if (k < lv[l].count) part[t] = v;
+      }
+      lds_barrier();
     // balanced binary tree over each large square's leaves, adjacent pairs first (NumPy's split at
     // n/2 for n = 128 * 2^k is exactly this tree), one thread per square
     for (int a = plan.n_small + tid; a < plan.total; a += kPreThreads) {
@@ -269,12 +383,23 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
       T* pp = part + lv[l].leaf0 + (a - lv[l].off) * per;
       for (int w = 1; w < per; w <<= 1)
         for (int i = 0; i < per; i += 2 * w) pp[i] = pp[i] + pp[i + w];
-      res[a] = pre_mean<T>(T(0) + pp[0], lv[l].s * lv[l].s);
+      res[a] = pre_mean<T>(T(0) + pp[0], 2 * lv[l].lsh);
     }
-    __syncthreads();
+    lds_barrier();
+    }
     float* o = out + e * out_stride;
-    for (int a = tid; a < plan.total; a += kPreThreads) o[a] = res[a];
-    __syncthreads();
+    if (!(plan.diag & 8)) {
+      // float4 stores from the first 16-byte boundary of the row; scalar head and tail
+      const int head = min((int)((4 - ((reinterpret_cast<uintptr_t>(o) >> 2) & 3)) & 3), plan.total);
+      const int nv = (plan.total - head) >> 2;
+      if (tid < head) o[tid] = res[tid];
+      for (int i = tid; i < nv; i += kPreThreads) {
+        const int a = head + 4 * i;
+        *reinterpret_cast<float4*>(o + a) = make_float4(res[a], res[a + 1], res[a + 2], res[a + 3]);
+      }
+      for (int a = head + 4 * nv + tid; a < plan.total; a += kPreThreads) o[a] = res[a];
+    }
+    lds_barrier();
   }
 }
 
@@ -473,6 +598,10 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
     return fail(HQ_E_UNSUPPORTED, "layout n=%d max_levels=%d min_square_size=%d (power-of-two squares, <= 8 levels)",
                 n, max_levels, min_square_size);
   if (out_stride < p.total) return fail(HQ_E_INVALID, "out_stride %lld < %d averages", (long long)out_stride, p.total);
+  const char* tev = getenv("HQ_PRECOMP_TREE");  // A/B: "lds" = combine leaves through LDS
+  if (tev && strcmp(tev, "lds") == 0) p.tree_lds = 1;
+  const char* dev = getenv("HQ_PRECOMP_DIAG");
+  if (dev) p.diag = atoi(dev);
   const int64_t grid64 = N < 65536 * 4 ? N : 65536 * 4;
   const int esz = dtype == HQ_F64 ? 8 : 4;
   const char* pev = getenv("HQ_PRECOMP_PAD");
@@ -483,13 +612,17 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   if (lds > 160 * 1024) return fail(HQ_E_UNSUPPORTED, "pre-computed index n=%d dtype %d needs %zu B of LDS", n, dtype, lds);
   hipStream_t s = (hipStream_t)stream;
   const int use_lut = kind == 1 && n >= 16 && n <= 64;  // compile-time group LUT exists for this n
+  const char* fev = getenv("HQ_PRECOMP_PF");           // A/B: 1 = prefetch the next image into registers
+  const int pf = fev ? atoi(fev) : 0;
   if (dtype == HQ_F32) {
-    HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_precomp<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_precomp<float>, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const float*)in, kind, N,
+    auto kern = pf ? k_precomp<float, 1> : k_precomp<float, 0>;
+    HQ_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const float*)in, kind, N,
                        in_stride, d, n, p, out, out_stride, use_lut, ld);
   } else if (dtype == HQ_F64) {
-    HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_precomp<double>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_precomp<double>, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const double*)in, kind,
+    auto kern = k_precomp<double, 0>;
+    HQ_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const double*)in, kind,
                        N, in_stride, d, n, p, out, out_stride, use_lut, ld);
   } else {
     return fail(HQ_E_UNSUPPORTED, "pre-computed index dtype %d (f32/f64)", dtype);
