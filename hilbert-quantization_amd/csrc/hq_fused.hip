@@ -462,24 +462,26 @@ static int pick_nd(int variant, int nd, const float* in, int64_t N, int64_t stri
           case 5: return launch_ff<NS, ND, 5>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 6: return launch_ff<NS, ND, 6>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 7: return launch_ff<NS, ND, 7>(in, N, stride, d, L, plan, frame, idx, mm, s);
-          case 8: return launch_ff<NS, ND, 8>(in, N, stride, d, L, plan, frame, idx, mm, s);
-          case 12: return launch_ff<NS, ND, 12>(in, N, stride, d, L, plan, frame, idx, mm, s);
-          case 24: return launch_ff<NS, ND, 24>(in, N, stride, d, L, plan, frame, idx, mm, s);
-          case 40: return launch_ff<NS, ND, 40>(in, N, stride, d, L, plan, frame, idx, mm, s);
-          case 56: return launch_ff<NS, ND, 56>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 64: return launch_any<NS, ND, 64>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 192: return launch_any<NS, ND, 192>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 320: return launch_any<NS, ND, 320>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 448: return launch_any<NS, ND, 448>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 321: return launch_any<NS, ND, 321>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 322: return launch_any<NS, ND, 322>(in, N, stride, d, L, plan, frame, idx, mm, s);
-          case 328: return launch_any<NS, ND, 328>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 576: return launch_any<NS, ND, 576>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 704: return launch_any<NS, ND, 704>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 832: return launch_any<NS, ND, 832>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 960: return launch_any<NS, ND, 960>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 706: return launch_any<NS, ND, 706>(in, N, stride, d, L, plan, frame, idx, mm, s);
+#ifdef HQ_DIAG  // memory-only probes (bits 8 / 16 / 32): wrong outputs, A/B builds only (make DIAG=1)
+          case 8: return launch_ff<NS, ND, 8>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 12: return launch_ff<NS, ND, 12>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 24: return launch_ff<NS, ND, 24>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 40: return launch_ff<NS, ND, 40>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 56: return launch_ff<NS, ND, 56>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 328: return launch_any<NS, ND, 328>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 840: return launch_any<NS, ND, 840>(in, N, stride, d, L, plan, frame, idx, mm, s);
+#endif
           default: break;
         }
       }

@@ -600,8 +600,10 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   if (out_stride < p.total) return fail(HQ_E_INVALID, "out_stride %lld < %d averages", (long long)out_stride, p.total);
   const char* tev = getenv("HQ_PRECOMP_TREE");  // A/B: "lds" = combine leaves through LDS
   if (tev && strcmp(tev, "lds") == 0) p.tree_lds = 1;
+#ifdef HQ_DIAG  // phase-skipping diagnostics (wrong averages): A/B builds only (make DIAG=1)
   const char* dev = getenv("HQ_PRECOMP_DIAG");
   if (dev) p.diag = atoi(dev);
+#endif
   const int64_t grid64 = N < 65536 * 4 ? N : 65536 * 4;
   const int esz = dtype == HQ_F64 ? 8 : 4;
   const char* pev = getenv("HQ_PRECOMP_PAD");
