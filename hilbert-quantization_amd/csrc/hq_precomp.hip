@@ -150,6 +150,19 @@ __device__ __forceinline__ void load4(const T* p, T (&v)[4]) {
 // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), identity added first.  Rows are read as S/2-wide vectors.
 template <typename T, int S>
 __device__ __forceinline__ T sq_sum(const T* b, int ld) {
+  if constexpr (S == 8) {
+    // 8x8: row r is step r of the eight accumulators; at most four rows of loads in flight (VGPRs)
+    T r8[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      T v[8];
+      load8<T>(b + r * ld, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r8[j] = r == 0 ? v[j] : r8[j] + v[j];
+      if (r == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    return T(0) + (((r8[0] + r8[1]) + (r8[2] + r8[3])) + ((r8[4] + r8[5]) + (r8[6] + r8[7])));
+  }
   T x[S * S];
 #pragma unroll
   for (int r = 0; r < S; ++r)
@@ -297,64 +310,47 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
     }
     // 128-value leaves of the larger squares: 16 steps of 8 consecutive values (one row segment,
     // 8-aligned because x0 is a multiple of s/2 >= 8), eight accumulators as NumPy's pairwise leaf
-    auto leaf_sum = [&](int t, int& l, int& k, int& leaf) -> T {
+    // Two lanes per 128-value leaf: lane h = 0 / 1 keeps NumPy's accumulators r0-r3 / r4-r7 (columns
+    // 4h..4h+3 of each 8-value step, 16 steps of one row segment, 8-aligned because x0 is a multiple of
+    // s/2 >= 8), so ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7)) is one shuffle — the leaf order exactly.
+    // Task u = 2 t + h for leaf t; every lane of the block runs the same number of rounds (shuffles).
+    auto half_leaf = [&](int u, int& l, int& k, int& leaf, bool& live) -> T {
+      const int t = u >> 1, h = u & 1;
+      l = 0; k = 0; leaf = 0; live = false;
+      if (t >= plan.nleaves) return T(0);
       l = plan.nlev - 1;
       while (lv[l].leaf0 < 0 || t < lv[l].leaf0) --l;
       const int s = lv[l].s, lsh = lv[l].lsh, msk = s - 1;
       const int lper = 2 * lsh - 7;  // log2 of the leaves per square
       k = (t - lv[l].leaf0) >> lper;
       leaf = (t - lv[l].leaf0) & ((1 << lper) - 1);
-      if (k >= lv[l].count) return T(0);  // alignment gap before the next level
+      live = k < lv[l].count;        // else an alignment gap before the next level
+      if (!live) return T(0);
       int x0, y0;
       pre_square(lv[l], k, x0, y0);
-      const T* b = img + y0 * ld + x0;
-      T r[8];
+      const T* b = img + y0 * ld + x0 + 4 * h;
+      T r[4];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int q = (leaf << 7) + 8 * i;
-        T v[8];
-        load8<T>(b + (q >> lsh) * ld + (q & msk), v);
+        T w4[4];
+        load4<T>(b + (q >> lsh) * ld + (q & msk), w4);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = i == 0 ? v[j] : r[j] + v[j];
+        for (int j = 0; j < 4; ++j) r[j] = i == 0 ? w4[j] : r[j] + w4[j];
+        if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // at most 8 steps of loads in flight
       }
-      return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+      return (r[0] + r[1]) + (r[2] + r[3]);
     };
     if (plan.diag & 2) {
     } else if (!plan.tree_lds) {
-      // Two lanes per leaf: lane h = 0 / 1 keeps accumulators r0-r3 / r4-r7 (columns 4h..4h+3 of each
-      // 8-value step), so ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7)) is one shuffle — NumPy's leaf order
-      // exactly.  A square's <= 32 leaves then sit on 2 * per consecutive lanes of one wave (leaf0 is
-      // aligned to per): the balanced tree over them (adjacent pairs first) by shuffles, and the first
-      // lane stores the mean.
+      // a square's <= 32 leaves sit on 2 * per consecutive lanes of one wave (leaf0 is aligned to
+      // per): the balanced tree over them (adjacent pairs first) by shuffles, the first lane stores
+      // the mean
       for (int u0 = 0; u0 < 2 * plan.nleaves; u0 += kPreThreads) {
-        const int u = u0 + tid, t = u >> 1, h = u & 1;
-        int l = 0, k = 0, leaf = 0;
-        T v = T(0);
-        bool live = false;
-        if (t < plan.nleaves) {
-          l = plan.nlev - 1;
-          while (lv[l].leaf0 < 0 || t < lv[l].leaf0) --l;
-          const int s = lv[l].s, lsh = lv[l].lsh, msk = s - 1;
-          const int lper = 2 * lsh - 7;
-          k = (t - lv[l].leaf0) >> lper;
-          leaf = (t - lv[l].leaf0) & ((1 << lper) - 1);
-          live = k < lv[l].count;  // else an alignment gap before the next level
-          if (live) {
-            int x0, y0;
-            pre_square(lv[l], k, x0, y0);
-            const T* b = img + y0 * ld + x0 + 4 * h;
-            T r[4];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const int q = (leaf << 7) + 8 * i;
-              T w4[4];
-              load4<T>(b + (q >> lsh) * ld + (q & msk), w4);
-#pragma unroll
-              for (int j = 0; j < 4; ++j) r[j] = i == 0 ? w4[j] : r[j] + w4[j];
-            }
-            v = (r[0] + r[1]) + (r[2] + r[3]);
-          }
-        }
+        int l, k, leaf;
+        bool live;
+        const int h = tid & 1;
+        T v = half_leaf(u0 + tid, l, k, leaf, live);
         const int per = live ? (lv[l].s * lv[l].s) >> 7 : 0;
         {
           const T o = __shfl_down(v, 1, 64);
@@ -368,10 +364,12 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
       }
       lds_barrier();
     } else {
-      for (int t = tid; t < plan.nleaves; t += kPreThreads) {
+      for (int u0 = 0; u0 < 2 * plan.nleaves; u0 += kPreThreads) {
         int l, k, leaf;
-        const T v = leaf_sum(t, l, k, leaf);
-        if (k < lv[l].count) part[t] = v;
+        bool live;
+        T v = half_leaf(u0 + tid, l, k, leaf, live);
+        const T o = __shfl_down(v, 1, 64);
+        if (live && (tid & 1) == 0) part[(u0 + tid) >> 1] = v + o;
       }
       lds_barrier();
     // balanced binary tree over each large square's leaves, adjacent pairs first (NumPy's split at
