@@ -221,7 +221,7 @@ __device__ __forceinline__ void pre_small(const PreLevel& L, const T* img, int l
 // parameter streams of d values (row stride `stride`), zero-padded to n*n and mapped to 2-D
 // (core/pipeline.py:298-319 _get_2d_representation).
 template <typename T, int PF>
-__global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ in, int kind, int64_t N, int64_t stride,
+__global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))) void k_precomp(const T* __restrict__ in, int kind, int64_t N, int64_t stride,
                                                          int d, int n, PrePlan plan, float* __restrict__ out,
                                                          int64_t out_stride, int use_lut, int ld) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -248,12 +248,18 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
 #pragma unroll
     for (int i = 0; i < kPreG; ++i) lut[i] = tid + kPreThreads * i < G ? glut[tid + kPreThreads * i] : 0u;
   }
+  // The per-thread group geometry (element masks against d, LUT scatter offsets) is loop-invariant;
+  // hoisted out of the image loop it held ~40 VGPRs and spilled SGPR masks, so it is laundered per
+  // image (empty asm) and recomputed: a few VALU ops against a wave per SIMD more.
   auto fetch = [&](int64_t e) {
     const T* src = in + e * stride;
     const bool vec_ok = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+    int dd = d;
+    asm volatile("" : "+s"(dd));
 #pragma unroll
     for (int i = 0; i < kPreG; ++i) {
       const int j = tid + kPreThreads * i;
+      const int d = dd;
       if (vec_ok && 4 * j + 3 < d) {
         if constexpr (sizeof(T) == 4) {
           const float4 q4 = *reinterpret_cast<const float4*>(src + 4 * j);
@@ -280,7 +286,9 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
 #pragma unroll
       for (int i = 0; i < kPreG; ++i) {
         if (tid + kPreThreads * i >= G) continue;
-        const uint32_t off0 = lut[i] & 0xFFFFu, code = lut[i] >> 16;
+        uint32_t ent = lut[i];
+        asm volatile("" : "+v"(ent));
+        const uint32_t off0 = ent & 0xFFFFu, code = ent >> 16;
         const uint32_t off = (off0 >> lsh_n) * ld + (off0 & (n - 1));
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
@@ -300,7 +308,15 @@ __global__ __launch_bounds__(kPreThreads) void k_precomp(const T* __restrict__ i
     // squares of <= 128 values: one thread each, level by level (uniform geometry per loop); 4x4 and
     // 8x8 squares read whole row segments (their x0 is a multiple of s/2) and sum in registers
     for (int l = 0; l < plan.nlev && !(plan.diag & 1); ++l) {
-      const PreLevel& L = plan.lv[l];
+      // this level's geometry from the LDS copy into SGPRs (indexing the kernarg plan by a loop
+      // variable keeps the whole plan live in SGPRs, which spill)
+      PreLevel L;
+      L.g = __builtin_amdgcn_readfirstlane(lv[l].g);
+      L.s = __builtin_amdgcn_readfirstlane(lv[l].s);
+      L.count = __builtin_amdgcn_readfirstlane(lv[l].count);
+      L.off = __builtin_amdgcn_readfirstlane(lv[l].off);
+      L.lsh = __builtin_amdgcn_readfirstlane(lv[l].lsh);
+      L.leaf0 = __builtin_amdgcn_readfirstlane(lv[l].leaf0);
       if (L.leaf0 >= 0) continue;
       // one straight-line loop per square size (the size is uniform per level)
       if (L.s == 2) pre_small<T, 2>(L, img, ld, res, tid);
