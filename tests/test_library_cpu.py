@@ -108,3 +108,26 @@ def test_product_has_no_cpu_fallback():
         from hq_mi355x.core import HilbertCurveMapper
         with pytest.raises(_lib.NativeLibraryError):
             HilbertCurveMapper().map_to_2d(np.arange(16, dtype=np.float32), (4, 4))
+
+
+def test_validation_paths_of_batched_entries(lib):
+    """Argument checks of the S7, pre-computed and stream entries return before any device work:
+    empty problems are no-ops (HQ_OK), bad shapes are errors with the reference's messages."""
+    from hq_mi355x import _lib
+    assert lib.hq_cos_padded_k(1) == 32 and lib.hq_cos_padded_k(4096) == 4096 and lib.hq_cos_padded_k(0) == 0
+    assert lib.hq_cos_padded_rows(1) == 128 and lib.hq_cos_padded_rows(250_000) == 250_112
+    assert lib.hq_cos_scores_mfma(None, None, 0, None, None, 5, 64, None, None) == _lib.HQ_OK
+    assert lib.hq_cos_scores_mfma(None, None, 3, None, None, 0, 64, None, None) == _lib.HQ_OK
+    assert lib.hq_cos_scores_mfma(None, None, -1, None, None, 5, 64, None, None) == _lib.HQ_E_INVALID
+    assert lib.hq_cos_scores_mfma(None, None, 3, None, None, 5, 64, None, None) == _lib.HQ_E_INVALID  # null
+    assert lib.hq_cos_prepare(None, 4, 10, 16, None, None, None) == _lib.HQ_E_INVALID                # ld < K
+    assert lib.hq_cos_prepare(None, 0, 16, 16, None, None, None) == _lib.HQ_OK
+    rc = lib.hq_precomputed_index(0, 1, None, 1, 64, 10, 3, 6, 2, None, 64, None)
+    assert rc == _lib.HQ_E_NOT_POW2 and _lib.last_error() == "Dimension must be a power of 2, got 3"
+    assert lib.hq_precomputed_index(0, 1, None, 1, 64, 10, 256, 6, 2, None, 64, None) == _lib.HQ_E_UNSUPPORTED
+    assert lib.hq_precomputed_index(0, 2, None, 1, 64, 10, 8, 6, 2, None, 64, None) == _lib.HQ_E_INVALID
+    assert lib.hq_precomputed_index(0, 1, None, 1, 100, 65, 8, 6, 2, None, 64, None) == _lib.HQ_E_TOO_MANY
+    assert lib.hq_precomputed_index(0, 1, None, 0, 64, 10, 8, 6, 2, None, 64, None) == _lib.HQ_OK
+    assert lib.hq_chunk_encode_f16(None, 0, 1024, None, None, None, None) == _lib.HQ_OK
+    assert lib.hq_chunk_encode_f16(None, 10, 0, None, None, None, None) == _lib.HQ_E_INVALID
+    assert lib.hq_chunk_encode_f16(None, 10, 1024, None, None, None, None) == _lib.HQ_E_INVALID      # null
