@@ -218,7 +218,7 @@ __device__ __forceinline__ int cos_sw(int g) { return (0x78 >> (2 * g)) & 3; }  
 // drain them with vmcnt(0) at every barrier); each wave retires its own pieces of a stage with a
 // counted vmcnt (the PW pieces of the next stage stay in flight) and an s_barrier publishes it.
 // PP = 0: all waves in lockstep, one barrier per K step; PP = 1: ping-pong (below).
-template <int TN, int PP>
+template <int TN, int PP, bool NTS = true>
 __global__ __launch_bounds__(TN * 2) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_cos_g3(CosArgs a, int64_t np_rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t cos_smem[];
   constexpr int TQ = 128, NW = TN / 32, kRow = kCosK, ST = 3;
@@ -383,12 +383,14 @@ __global__ __launch_bounds__(TN * 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
         if (n >= a.N) continue;
         const double ic = a.ib[n];
         const double cs = (double)acc[i][j][r] * iq * ic;
-        a.out[q * a.N + n] = (iq != 0.0 && ic != 0.0) ? (cs + 1.0) / 2.0 : 0.0;
+        const double v = (iq != 0.0 && ic != 0.0) ? (cs + 1.0) / 2.0 : 0.0;
+        if constexpr (NTS) __builtin_nontemporal_store(v, a.out + q * a.N + n);  // write-once scores
+        else a.out[q * a.N + n] = v;
       }
     }
 }
 
-template <int TN, int PP>
+template <int TN, int PP, bool NTS = true>
 static int launch_g3(CosArgs a, hipStream_t s) {
   const int64_t np_rows = a.ntiles * kCosT;
   a.qtiles = (int)(hq_cos_padded_rows(a.Q) / 128);
@@ -397,7 +399,7 @@ static int launch_g3(CosArgs a, hipStream_t s) {
   const int64_t blocks = nt8 * a.qtiles;
   if (blocks > 0x7FFFFFFF) return fail(HQ_E_UNSUPPORTED, "too many tiles");
   const size_t lds = sizeof(_Float16) * 3 * (2 * 128 + 2 * TN) * kCosK;
-  auto kern = k_cos_g3<TN, PP>;
+  auto kern = k_cos_g3<TN, PP, NTS>;
   HQ_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(TN * 2), lds, s, a, np_rows);
   HQ_CHECK_LAUNCH();
@@ -460,6 +462,7 @@ int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* 
   const char* ek = getenv("HQ_COS_KERNEL");
   if (ek && strcmp(ek, "regstage") == 0) return launch_cos<128>(a, (hipStream_t)stream);
   if (ek && strcmp(ek, "lockstep") == 0) return launch_g3<256, 0>(a, (hipStream_t)stream);
+  if (ek && strcmp(ek, "temporal") == 0) return launch_g3<256, 1, false>(a, (hipStream_t)stream);
   return launch_g3<256, 1>(a, (hipStream_t)stream);
 }
 

@@ -45,10 +45,18 @@ __device__ __forceinline__ double quad_bcast_xor1(double v) {  // value of lane 
 
 // index row store with 16-byte lanes: even lanes write (slot 2k, slot 2k+1) — 8-byte stores leave
 // L2 at a much lower byte rate (MI355X_MICROARCH.md, store flavours); L even and 16-B aligned rows
+template <bool NT = false>
 __device__ __forceinline__ void store_index(double* __restrict__ row, double val, int lane, int L) {
   const double nb = quad_bcast_xor1(val);
   if ((L & 1) == 0 && (reinterpret_cast<uintptr_t>(row) & 15) == 0) {
-    if ((lane & 1) == 0 && lane < L) *reinterpret_cast<double2*>(row + lane) = make_double2(val, nb);
+    if ((lane & 1) == 0 && lane < L) {
+      if constexpr (NT) {
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store(d2v{val, nb}, reinterpret_cast<d2v*>(row + lane));
+      } else {
+        *reinterpret_cast<double2*>(row + lane) = make_double2(val, nb);
+      }
+    }
   } else if (lane < L) {
     row[lane] = val;
   }
@@ -200,7 +208,7 @@ __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int
   } else if (slev >= 2) {
     val = tree[Geo::off(slev) + spos];
   }
-  if (live) store_index(idx_out + e * (int64_t)L, val, lane, L);
+  if (live) store_index<(V & 2048) != 0>(idx_out + e * (int64_t)L, val, lane, L);
   const float rv = (float)val;
   if constexpr ((V & 512) != 0) __syncthreads();  // frame overlays the tree: every slot read first
 
@@ -274,8 +282,14 @@ __device__ __forceinline__ void process_emb(int64_t e, const Buf<NS, ND>& b, int
   uint8_t* dst = frame_out + e * (int64_t)Geo::FB;
   if (live) {
 #pragma unroll
-    for (int c = lane; c < Geo::FB / 16; c += 64)
-      reinterpret_cast<uint4*>(dst)[c] = reinterpret_cast<const uint4*>(frame)[c];
+    for (int c = lane; c < Geo::FB / 16; c += 64) {
+      if constexpr ((V & 1024) != 0) {  // non-temporal frame stores (A/B)
+        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(reinterpret_cast<const u4v*>(frame)[c], reinterpret_cast<u4v*>(dst) + c);
+      } else {
+        reinterpret_cast<uint4*>(dst)[c] = reinterpret_cast<const uint4*>(frame)[c];
+      }
+    }
     if (mm_out && lane == 0) *reinterpret_cast<float2*>(mm_out + 2 * e) = make_float2(mn, mx);
   }
   if constexpr ((V & 64) == 0) __syncthreads();  // persistent: the frame is reused by the next embedding
@@ -443,8 +457,10 @@ static int launch_any(const float* in, int64_t N, int64_t stride, int d, int L, 
 
 // Variant bits (HQ_FUSED_V): 1 nt loads, 2 reciprocal quantize, 4 triple buffering (persistent), 8 / 16 / 32
 // memory-only probes, 64 non-persistent (one embedding per wave), bits 7-8: log2 waves per workgroup,
-// 512 frame overlays the tree in LDS (non-persistent form).
-constexpr int kDefaultV = 64 | (1 << 7) | 512;  // non-persistent, 2 waves per workgroup, frame over tree, exact quantize
+// 512 frame overlays the tree in LDS (non-persistent form), 1024 / 2048 non-temporal frame / index stores
+// (write-once outputs: +5% / +0.2%, tools/ab_fused.sh).
+constexpr int kDefaultV = 64 | (1 << 7) | 512 | 1024 | 2048;  // non-persistent, 2 waves per workgroup, frame
+                                                               // over tree, exact quantize, NT stores
 
 template <int NS, int ND>
 static int pick_nd(int variant, int nd, const float* in, int64_t N, int64_t stride, int d, int L, const FastPlan& plan,
@@ -473,6 +489,7 @@ static int pick_nd(int variant, int nd, const float* in, int64_t N, int64_t stri
           case 832: return launch_any<NS, ND, 832>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 960: return launch_any<NS, ND, 960>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 706: return launch_any<NS, ND, 706>(in, N, stride, d, L, plan, frame, idx, mm, s);
+          case 1728: return launch_any<NS, ND, 1728>(in, N, stride, d, L, plan, frame, idx, mm, s);
 #ifdef HQ_DIAG  // memory-only probes (bits 8 / 16 / 32): wrong outputs, A/B builds only (make DIAG=1)
           case 8: return launch_ff<NS, ND, 8>(in, N, stride, d, L, plan, frame, idx, mm, s);
           case 12: return launch_ff<NS, ND, 12>(in, N, stride, d, L, plan, frame, idx, mm, s);

@@ -291,7 +291,14 @@ __device__ __forceinline__ float2 h2f(uint32_t w) {
                      __half2float(__ushort_as_half((unsigned short)(w >> 16))));
 }
 
-template <int NS, int WPB, bool FQ, int CPW>
+// NT: non-temporal stores of the write-once outputs (frames, index rows, min/max)
+template <typename T>
+__device__ __forceinline__ void st_out(T* p, T v, bool nt) {
+  if (nt) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+template <int NS, int WPB, bool FQ, int CPW, bool NT>
 __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restrict__ src, int64_t nchunks,
                                                        ChunkPlan plan, uint8_t* __restrict__ frame_out,
                                                        float* __restrict__ idx_out, float* __restrict__ mm_out) {
@@ -377,7 +384,7 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
     const float iv = rowv[lane];
     lmin = fminf(lmin, iv);
     lmax = fmaxf(lmax, iv);
-    if (live) idx_out[c * NS + lane] = iv;
+    if (live) st_out(idx_out + c * NS + lane, iv, NT);
   }
   const float mn = wmin64(lmin), mx = wmax64(lmax);
   if (live) {
@@ -432,7 +439,8 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
         w[k] = qb(f.x) | (qb(f.y) << 8) | (qb(f.z) << 16) | (qb(f.w) << 24);
       }
     }
-    *reinterpret_cast<uint4*>(dst + 16 * q) = make_uint4(w[0], w[1], w[2], w[3]);
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    st_out(reinterpret_cast<u4v*>(dst + 16 * q), u4v{w[0], w[1], w[2], w[3]}, NT);
   }
   // index row: one value per lane, bytes packed through LDS (rowv's own slot), 16-byte stores
   uint8_t* rowq = rowq_all[wv];
@@ -440,8 +448,14 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (lane < NS / 16) *reinterpret_cast<uint4*>(dst + CELLS + 16 * lane) = reinterpret_cast<const uint4*>(rowq)[lane];
-  if (lane == 0) *reinterpret_cast<float2*>(mm_out + 2 * c) = make_float2(mn, mx);
+  if (lane < NS / 16) {
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    st_out(reinterpret_cast<u4v*>(dst + CELLS + 16 * lane), reinterpret_cast<const u4v*>(rowq)[lane], NT);
+  }
+  if (lane == 0) {
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    st_out(reinterpret_cast<f2v*>(mm_out + 2 * c), f2v{mn, mx}, NT);
+  }
   }
   if constexpr (CPW > 1) __syncthreads();  // the next chunk reuses the LDS image
   }
@@ -527,12 +541,17 @@ static int launch_chunk_np(const uint16_t* in, int64_t nchunks, const TradPlan& 
     if (cell == -2) return HQ_E_UNSUPPORTED;
     cp.cell[i] = (int16_t)cell;
   }
+  const char* nev = getenv("HQ_CHUNK_NT");  // A/B: 1 = non-temporal stores (measured equal, off)
+  const bool nt = nev ? atoi(nev) != 0 : false;
   if (getenv("HQ_CHUNK_EXACTDIV"))
-    hipLaunchKernelGGL((k_chunk_np<NS, WPB, false, CPW>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in, nchunks,
-                       cp, frame, idx, mm);
+    hipLaunchKernelGGL((k_chunk_np<NS, WPB, false, CPW, false>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in,
+                       nchunks, cp, frame, idx, mm);
+  else if (nt)
+    hipLaunchKernelGGL((k_chunk_np<NS, WPB, true, CPW, true>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in,
+                       nchunks, cp, frame, idx, mm);
   else
-    hipLaunchKernelGGL((k_chunk_np<NS, WPB, true, CPW>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in, nchunks,
-                       cp, frame, idx, mm);
+    hipLaunchKernelGGL((k_chunk_np<NS, WPB, true, CPW, false>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in,
+                       nchunks, cp, frame, idx, mm);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }

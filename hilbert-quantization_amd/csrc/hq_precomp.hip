@@ -40,6 +40,7 @@ struct PrePlan {
   int maxper;    // most 128-value leaves in one square
   int tree_lds;  // 1: combine the leaves through LDS (squares of > 64 leaves, or HQ_PRECOMP_TREE=lds)
   int diag;      // A/B diagnostics only (wrong averages): bit 0 skip small squares, 1 leaves, 2 load, 3 store
+  int nt;        // non-temporal output stores
   PreLevel lv[kPreMaxLevels];
 };
 
@@ -53,6 +54,7 @@ static int pre_plan(int n, int max_levels, int min_sq, PrePlan& p) {
   p.maxper = 0;
   p.tree_lds = 0;
   p.diag = 0;
+  p.nt = 1;
   p.lsh_n = ilog2(n);
   int s = min_sq;
   int lv_g[16], lv_s[16], c = 0;
@@ -406,10 +408,14 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
       // float4 stores from the first 16-byte boundary of the row; scalar head and tail
       const int head = min((int)((4 - ((reinterpret_cast<uintptr_t>(o) >> 2) & 3)) & 3), plan.total);
       const int nv = (plan.total - head) >> 2;
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const bool nt = plan.nt;  // non-temporal: the averages are written once (A/B HQ_PRECOMP_NT)
       if (tid < head) o[tid] = res[tid];
       for (int i = tid; i < nv; i += kPreThreads) {
         const int a = head + 4 * i;
-        *reinterpret_cast<float4*>(o + a) = make_float4(res[a], res[a + 1], res[a + 2], res[a + 3]);
+        const f4v v = {res[a], res[a + 1], res[a + 2], res[a + 3]};
+        if (nt) __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(o + a));
+        else *reinterpret_cast<f4v*>(o + a) = v;
       }
       for (int a = head + 4 * nv + tid; a < plan.total; a += kPreThreads) o[a] = res[a];
     }
@@ -612,6 +618,8 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
     return fail(HQ_E_UNSUPPORTED, "layout n=%d max_levels=%d min_square_size=%d (power-of-two squares, <= 8 levels)",
                 n, max_levels, min_square_size);
   if (out_stride < p.total) return fail(HQ_E_INVALID, "out_stride %lld < %d averages", (long long)out_stride, p.total);
+  const char* nev = getenv("HQ_PRECOMP_NT");
+  if (nev) p.nt = atoi(nev) != 0;
   const char* tev = getenv("HQ_PRECOMP_TREE");  // A/B: "lds" = combine leaves through LDS
   if (tev && strcmp(tev, "lds") == 0) p.tree_lds = 1;
 #ifdef HQ_DIAG  // phase-skipping diagnostics (wrong averages): A/B builds only (make DIAG=1)

@@ -200,7 +200,7 @@ def test_fused_kernel_vs_oracle(hq_lib, n, d, L):
     assert np.array_equal(got[:, 0], mn) and np.array_equal(got[:, 1], mx)
 
 
-@pytest.mark.parametrize("variant", [4, 0, 64, 192, 320, 448, 322, 576, 704, 832, 706])
+@pytest.mark.parametrize("variant", [4, 0, 64, 192, 320, 448, 322, 576, 704, 832, 706, 1728, 3776])
 @pytest.mark.parametrize("n,d,L", [(64, 1536, 64), (32, 999, 20), (16, 200, 16)])
 def test_fused_launch_forms_vs_oracle(hq_lib, n, d, L, variant, monkeypatch):
     """Every launch form of the fast kernel (persistent triple/double buffered, non-persistent with 1-8
