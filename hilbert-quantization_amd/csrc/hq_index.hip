@@ -298,7 +298,7 @@ __device__ __forceinline__ void st_out(T* p, T v, bool nt) {
   else *p = v;
 }
 
-template <int NS, int WPB, bool FQ, int CPW, bool NT>
+template <int NS, int WPB, bool FQ, int CPW, int NT>
 __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restrict__ src, int64_t nchunks,
                                                        ChunkPlan plan, uint8_t* __restrict__ frame_out,
                                                        float* __restrict__ idx_out, float* __restrict__ mm_out) {
@@ -321,8 +321,16 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
   for (int k = 0; k < CPW; ++k)
 #pragma unroll
     for (int u = 0; u < NU; ++u)
-      raw_all[k][u] = c0 + k < nchunks ? reinterpret_cast<const uint4*>(src + (c0 + k) * CELLS)[lane + 64 * u]
-                                       : make_uint4(0, 0, 0, 0);
+      if constexpr ((NT & 2) != 0) {  // non-temporal loads (A/B)
+        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+        const u4v r = c0 + k < nchunks
+                          ? __builtin_nontemporal_load(reinterpret_cast<const u4v*>(src + (c0 + k) * CELLS) + lane + 64 * u)
+                          : u4v{0u, 0u, 0u, 0u};
+        raw_all[k][u] = make_uint4(r.x, r.y, r.z, r.w);
+      } else {
+        raw_all[k][u] = c0 + k < nchunks ? reinterpret_cast<const uint4*>(src + (c0 + k) * CELLS)[lane + 64 * u]
+                                         : make_uint4(0, 0, 0, 0);
+      }
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     ent[2 * u] = lut[2 * (lane + 64 * u)];
@@ -384,7 +392,7 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
     const float iv = rowv[lane];
     lmin = fminf(lmin, iv);
     lmax = fmaxf(lmax, iv);
-    if (live) st_out(idx_out + c * NS + lane, iv, NT);
+    if (live) st_out(idx_out + c * NS + lane, iv, (NT & 1) != 0);
   }
   const float mn = wmin64(lmin), mx = wmax64(lmax);
   if (live) {
@@ -440,7 +448,7 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
       }
     }
     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-    st_out(reinterpret_cast<u4v*>(dst + 16 * q), u4v{w[0], w[1], w[2], w[3]}, NT);
+    st_out(reinterpret_cast<u4v*>(dst + 16 * q), u4v{w[0], w[1], w[2], w[3]}, (NT & 1) != 0);
   }
   // index row: one value per lane, bytes packed through LDS (rowv's own slot), 16-byte stores
   uint8_t* rowq = rowq_all[wv];
@@ -450,11 +458,11 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (lane < NS / 16) {
     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-    st_out(reinterpret_cast<u4v*>(dst + CELLS + 16 * lane), reinterpret_cast<const u4v*>(rowq)[lane], NT);
+    st_out(reinterpret_cast<u4v*>(dst + CELLS + 16 * lane), reinterpret_cast<const u4v*>(rowq)[lane], (NT & 1) != 0);
   }
   if (lane == 0) {
     typedef float f2v __attribute__((ext_vector_type(2)));
-    st_out(reinterpret_cast<f2v*>(mm_out + 2 * c), f2v{mn, mx}, NT);
+    st_out(reinterpret_cast<f2v*>(mm_out + 2 * c), f2v{mn, mx}, (NT & 1) != 0);
   }
   }
   if constexpr (CPW > 1) __syncthreads();  // the next chunk reuses the LDS image
@@ -541,16 +549,22 @@ static int launch_chunk_np(const uint16_t* in, int64_t nchunks, const TradPlan& 
     if (cell == -2) return HQ_E_UNSUPPORTED;
     cp.cell[i] = (int16_t)cell;
   }
-  const char* nev = getenv("HQ_CHUNK_NT");  // A/B: 1 = non-temporal stores (measured equal, off)
-  const bool nt = nev ? atoi(nev) != 0 : false;
+  const char* nev = getenv("HQ_CHUNK_NT");  // A/B bits: 1 non-temporal stores (measured equal), 2 loads
+  const int nt = nev ? atoi(nev) : 0;
   if (getenv("HQ_CHUNK_EXACTDIV"))
-    hipLaunchKernelGGL((k_chunk_np<NS, WPB, false, CPW, false>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in,
+    hipLaunchKernelGGL((k_chunk_np<NS, WPB, false, CPW, 0>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in,
                        nchunks, cp, frame, idx, mm);
-  else if (nt)
-    hipLaunchKernelGGL((k_chunk_np<NS, WPB, true, CPW, true>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in,
+  else if (nt == 1)
+    hipLaunchKernelGGL((k_chunk_np<NS, WPB, true, CPW, 1>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in,
+                       nchunks, cp, frame, idx, mm);
+  else if (nt == 2)
+    hipLaunchKernelGGL((k_chunk_np<NS, WPB, true, CPW, 2>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in,
+                       nchunks, cp, frame, idx, mm);
+  else if (nt == 3)
+    hipLaunchKernelGGL((k_chunk_np<NS, WPB, true, CPW, 3>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in,
                        nchunks, cp, frame, idx, mm);
   else
-    hipLaunchKernelGGL((k_chunk_np<NS, WPB, true, CPW, false>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in,
+    hipLaunchKernelGGL((k_chunk_np<NS, WPB, true, CPW, 0>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in,
                        nchunks, cp, frame, idx, mm);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
