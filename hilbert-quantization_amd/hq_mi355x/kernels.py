@@ -284,6 +284,21 @@ def level_scores(q: Prepared, c: Prepared, level: int, exc=None):
     return out
 
 
+_WS = {}
+
+
+def _workspace(nbytes: int, dev):
+    """Scan workspace reused across calls on the same stream (stream order makes the reuse safe: the
+    previous scan's kernels finish before the next scan's first write).  Saves an allocation between
+    the query preparation and the first scan launch of every batch."""
+    t = torch()
+    key = (str(dev), stream())
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = _WS[key] = t.empty(nbytes, dtype=t.uint8, device=dev)
+    return ws[:nbytes]
+
+
 def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.0, thr_mode: int = 0,
               id_base: int = 0, need_best: bool = False, exc=None):
     """Fused MFMA scan + per-query top-k on APPROXIMATE scores.  mode 0: level-0 score, 1: overall.
@@ -294,7 +309,7 @@ def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.
     Q, N = q.N, c.N
     dev = q.Z.device
     ws_bytes = int(_lib.load().hq_scan_workspace_size(Q, N, k))
-    ws = t.empty(ws_bytes, dtype=t.uint8, device=dev)
+    ws = _workspace(ws_bytes, dev)
     sc = t.empty((Q, k), dtype=t.float64, device=dev)
     ids = t.empty((Q, k), dtype=t.int64, device=dev)
     best = t.empty(Q, dtype=t.float64, device=dev) if need_best else None
