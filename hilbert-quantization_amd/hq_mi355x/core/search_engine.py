@@ -146,9 +146,10 @@ class IndexCorpus:
             oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
             return oid, odet[..., 0], odet[..., 1:], ocnt
         s0, ids, cnt, res = self._scan_refine(qp, 0, M, float(threshold), 1)
-        best = t.full((Q,), -float("inf"), dtype=t.float64, device=qp.Z.device)
-        bid = t.full((Q,), -1, dtype=t.int64, device=qp.Z.device)
-        oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
+        # no arg-max on this path: a query where nothing passed (count 0) is recomputed by the dense path
+        # below, so the fallback slot is a constant (-inf, id -1, zero re-scores) kept per batch size
+        best, bid, bdet = self._no_fallback(Q, qp.Z.device)
+        oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out, bdet)
         redo = (res == 0) | (cnt == 0)
         if bool(redo.any()):
             sel = t.nonzero(redo).view(-1)
@@ -158,17 +159,28 @@ class IndexCorpus:
             oid[sel], odet[sel], ocnt[sel] = o2, d2, c2
         return oid, odet[..., 0], odet[..., 1:], ocnt
 
+    def _no_fallback(self, Q: int, dev):
+        t = torch()
+        cache = self.__dict__.setdefault("_nofb", {})
+        key = (Q, str(dev))
+        if key not in cache:
+            cache[key] = (t.full((Q,), -float("inf"), dtype=t.float64, device=dev),
+                          t.full((Q,), -1, dtype=t.int64, device=dev),
+                          t.zeros((Q, 1 + self.nseg), dtype=t.float64, device=dev))
+        return cache[key]
+
     def _scan_refine(self, qp, mode: int, k: int, thr: float, thr_mode: int):
         """Fused scan (SLACK extra list entries) + exact re-rank; resolved[q] == 0 marks an unproven list."""
         lo_mode = 0 if thr_mode == 0 else 1
         asc, aid, _, _ = K.scan_topk(qp, self.prep, mode, k + self.SLACK, thr - self.EPS, lo_mode, self.id_base)
         return K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, thr_mode, self.EPS, self.id_base)
 
-    def _final(self, qp, s0, ids, best, bid, K_out: int):
+    def _final(self, qp, s0, ids, best, bid, K_out: int, bdet=None):
         """Exact overall + per-level re-score of the survivors and of the arg-max, then the final ranking."""
         Q = qp.N
         det = K.rescore(qp, self.prep, ids, self.id_base)
-        bdet = K.rescore(qp, self.prep, bid.view(Q, 1), self.id_base).view(Q, -1)
+        if bdet is None:
+            bdet = K.rescore(qp, self.prep, bid.view(Q, 1), self.id_base).view(Q, -1)
         return K.progressive_final(s0.unsqueeze(0), ids.unsqueeze(0), det.unsqueeze(0),
                                    best.unsqueeze(0), bid.unsqueeze(0), bdet.unsqueeze(0), K_out)
 
