@@ -626,7 +626,9 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   const char* dev = getenv("HQ_PRECOMP_DIAG");
   if (dev) p.diag = atoi(dev);
 #endif
-  const int64_t grid64 = N < 65536 * 4 ? N : 65536 * 4;
+  const char* gev = getenv("HQ_PRECOMP_GRID");  // A/B: workgroups (each loops over images)
+  const int64_t gcap = gev ? atoll(gev) : 65536 * 4;
+  const int64_t grid64 = N < gcap ? N : gcap;
   const int esz = dtype == HQ_F64 ? 8 : 4;
   const char* pev = getenv("HQ_PRECOMP_PAD");
   const int pad = pev ? atoi(pev) : 4;
