@@ -62,7 +62,8 @@ static void seg_info(int L, SegInfo& s) {
 // per-segment statistics + normalised vectors (reference np.mean/np.std order)
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_seg_prepare(const double* __restrict__ idx, int64_t N, SegInfo si,
-                                                     double* __restrict__ Z, double* __restrict__ stats) {
+                                                     int src_f32, double* __restrict__ Z,
+                                                     double* __restrict__ stats) {
   const int64_t total = N * si.nseg;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -76,16 +77,27 @@ __global__ __launch_bounds__(256) void k_seg_prepare(const double* __restrict__ 
     const double sd = sqrt(np_sum<double>(fd, m) / (double)m);        // np.std (_methods._var)
     auto fs = [=](int k) -> double { return x[k] * x[k]; };
     const double msq = np_sum<double>(fs, m) / (double)m;             // np.mean(q ** 2)
+    double mean_u = mean, sd_u = sd;
+    if (src_f32 && sd == 0.0) {
+      // f32 index vectors: np.std runs in f32 (_methods._var: f32 pairwise sum, f32 divide, x - mean,
+      // x * x, f32 pairwise sum, divide, sqrt).  A constant segment whose f32 sum is inexact has
+      // std32 != 0 there, and the reference takes the normalised branch (search_engine.py:153-167).
+      auto gx = [=](int k) -> float { return (float)x[k]; };
+      const float mean32 = np_sum<float>(gx, m) / (float)m;
+      auto gd = [=](int k) -> float { float d = (float)x[k] - mean32; return d * d; };
+      const float sd32 = sqrtf(np_sum<float>(gd, m) / (float)m);
+      if (sd32 != 0.0f) { mean_u = (double)mean32; sd_u = (double)sd32; }
+    }
     double* z = Z + row * si.Lp + si.poff[s];
-    if (sd == 0.0) {
+    if (sd_u == 0.0) {
       for (int i = 0; i < si.plen[s]; ++i) z[i] = 0.0;
     } else {
-      for (int i = 0; i < m; ++i) z[i] = (x[i] - mean) / sd;          // (q - mean(q)) / std (:150-151)
+      for (int i = 0; i < m; ++i) z[i] = (x[i] - mean_u) / sd_u;      // (q - mean(q)) / std (:150-151)
       for (int i = m; i < si.plen[s]; ++i) z[i] = 0.0;
     }
     double* st = stats + (row * si.nseg + s) * 4;
-    st[0] = mean;
-    st[1] = sd;
+    st[0] = mean_u;
+    st[1] = sd_u;
     st[2] = msq;
     st[3] = 0.0;
   }
@@ -2147,6 +2159,11 @@ int hq_seg_padded_len(int L) {
 }
 
 int hq_seg_prepare(const double* idx, int64_t N, int L, double* Z, double* stats, hq_stream_t stream) {
+  return hq_seg_prepare_src(idx, N, L, 0, Z, stats, stream);
+}
+
+int hq_seg_prepare_src(const double* idx, int64_t N, int L, int src_f32, double* Z, double* stats,
+                       hq_stream_t stream) {
   if (L <= 0 || N < 0) return fail(HQ_E_INVALID, "bad shape N=%lld L=%d", (long long)N, L);
   if (N == 0) return HQ_OK;
   if (!idx || !Z || !stats) return fail(HQ_E_INVALID, "null buffer");
@@ -2156,7 +2173,8 @@ int hq_seg_prepare(const double* idx, int64_t N, int L, double* Z, double* stats
   const int64_t total = N * si.nseg;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(k_seg_prepare, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, idx, N, si, Z, stats);
+  hipLaunchKernelGGL(k_seg_prepare, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, idx, N, si, src_f32 ? 1 : 0,
+                     Z, stats);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }

@@ -50,6 +50,7 @@ SIGNATURES = {
     "hq_seg_count": (_i, [_i]),
     "hq_seg_padded_len": (_i, [_i]),
     "hq_seg_prepare": (_i, [_p, _i64, _i, _p, _p, _p]),
+    "hq_seg_prepare_src": (_i, [_p, _i64, _i, _i, _p, _p, _p]),
     "hq_level_scores": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _p, _p]),
     "hq_refine_topk": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _p, _p, _i, _i, _d, _i, _d, _i64, _p, _p, _p, _p, _p]),
     "hq_scan_workspace_size": (_sz, [_i, _i64, _i]),

@@ -37,6 +37,20 @@ def _f64(x):
     return to_dev(x, t.float64)
 
 
+def _idx(x):
+    """Host index vector as f64, or kept f32 when it is f32 (IndexCorpus then applies the f32 statistics)."""
+    a = np.asarray(x)
+    return a if a.dtype == np.float32 else a.astype(np.float64, copy=False)
+
+
+def _is_f32(x) -> bool:
+    """float32 index vectors: the reference's np.std/np.mean then run in f32 (search_engine.py:153-159)."""
+    dt = getattr(x, "dtype", None)
+    if dt is None:
+        return False
+    return dt == np.float32 or str(dt) == "torch.float32"
+
+
 class IndexCorpus:
     """A corpus of equal-length hierarchical index vectors resident in HBM.
 
@@ -53,21 +67,23 @@ class IndexCorpus:
     SLACK = 8
 
     def __init__(self, indices, id_base: int = 0):
+        f32 = _is_f32(indices)
         x = _f64(indices)
         if x.dim() != 2:
             raise ValueError("IndexCorpus expects a 2-D [N, L] array of index vectors")
         self.N, self.L = int(x.shape[0]), int(x.shape[1])
         self.id_base = int(id_base)
-        self.prep = K.pack0(K.seg_prepare(x))
+        self.prep = K.pack0(K.seg_prepare(x, src_f32=f32))
         self.nseg = self.prep.nseg
 
     def prepare_queries(self, queries) -> "K.Prepared":
+        f32 = _is_f32(queries)
         q = _f64(queries)
         if q.dim() == 1:
             q = q.view(1, -1)
         if q.shape[1] != self.L:
             raise ValueError(f"query index length {q.shape[1]} != corpus index length {self.L}")
-        return K.pack0(K.seg_prepare(q))
+        return K.pack0(K.seg_prepare(q, src_f32=f32))
 
     # ---- scores ------------------------------------------------------------------------------
     def level_scores(self, queries, level: int):
@@ -222,10 +238,10 @@ class ProgressiveSimilaritySearchEngine:
         for Lc, members in groups.items():
             if Lc == 0:
                 continue
-            C = np.stack([np.asarray(cands[i], dtype=np.float64) for i in members])
+            C = np.stack([_idx(cands[i]) for i in members])
             if Lc == len(q):
                 corpus = IndexCorpus(C)
-                s = to_np(corpus.level_scores(np.asarray(q, dtype=np.float64)[None], level))[0]
+                s = to_np(corpus.level_scores(_idx(q)[None], level))[0]
             else:
                 cl = self._parse_index_structure(C[0], Lc)
                 if level >= len(cl):
@@ -235,7 +251,7 @@ class ProgressiveSimilaritySearchEngine:
                 m = min(qe - qs, ce - cs)
                 if m <= 0:
                     continue
-                qseg = np.asarray(q, dtype=np.float64)[qs:qs + m]
+                qseg = _idx(q)[qs:qs + m]
                 s = to_np(K.pair_scores_raw(_f64(qseg), _f64(np.ascontiguousarray(C[:, cs:cs + m]))))
             out[members] = s
         return out
@@ -257,8 +273,8 @@ class ProgressiveSimilaritySearchEngine:
         if not ql:
             return np.zeros(N), np.zeros((N, 0))
         if all(len(c) == len(q) for c in cands) and N:
-            corpus = IndexCorpus(np.stack([np.asarray(c, dtype=np.float64) for c in cands]))
-            qp = corpus.prepare_queries(np.asarray(q, dtype=np.float64)[None])
+            corpus = IndexCorpus(np.stack([_idx(c) for c in cands]))
+            qp = corpus.prepare_queries(_idx(q)[None])
             ids = torch().arange(N, device=qp.Z.device).view(1, N)
             det = to_np(K.rescore(qp, corpus.prep, ids))[0]
             return det[:, 0], det[:, 1:]
@@ -294,9 +310,9 @@ class ProgressiveSimilaritySearchEngine:
                            max_results: int) -> List[SearchResult]:
         if len(query_indices) == 0 or not candidate_pool:
             return []
-        q = np.asarray(query_indices, dtype=np.float64)
+        q = _idx(query_indices)
         if self._uniform(q, candidate_pool):
-            corpus = IndexCorpus(np.stack([np.asarray(c.hierarchical_indices, dtype=np.float64)
+            corpus = IndexCorpus(np.stack([_idx(c.hierarchical_indices)
                                            for c in candidate_pool]))
             ids, ov, lv = corpus.brute_force(q[None], min(max_results, len(candidate_pool)))
             return self._results(candidate_pool, to_np(ids)[0], to_np(ov)[0], to_np(lv)[0], with_error=False)
@@ -308,11 +324,11 @@ class ProgressiveSimilaritySearchEngine:
                            max_results: int) -> List[SearchResult]:
         if len(query_indices) == 0 or not candidate_pool:
             return []
-        q = np.asarray(query_indices, dtype=np.float64)
+        q = _idx(query_indices)
         if not self._parse_index_structure(q, len(q)):
             return []
         if self._uniform(q, candidate_pool):
-            corpus = IndexCorpus(np.stack([np.asarray(c.hierarchical_indices, dtype=np.float64)
+            corpus = IndexCorpus(np.stack([_idx(c.hierarchical_indices)
                                            for c in candidate_pool]))
             ids, ov, lv, cnt = corpus.progressive(q[None], max_results, self.similarity_threshold,
                                                   self.max_candidates_per_level)
@@ -325,12 +341,12 @@ class ProgressiveSimilaritySearchEngine:
         scan when every index has the same length (else query by query)."""
         if not candidate_pool:
             return [[] for _ in queries]
-        qs = [np.asarray(q, dtype=np.float64) for q in queries]
+        qs = [_idx(q) for q in queries]
         L = len(qs[0]) if qs else 0
         if not qs or any(len(q) != L for q in qs) or L == 0 or not self._parse_index_structure(qs[0], L) \
                 or not self._uniform(qs[0], candidate_pool):
             return [self.progressive_search(q, candidate_pool, max_results) for q in qs]
-        corpus = IndexCorpus(np.stack([np.asarray(c.hierarchical_indices, dtype=np.float64) for c in candidate_pool]))
+        corpus = IndexCorpus(np.stack([_idx(c.hierarchical_indices) for c in candidate_pool]))
         ids, ov, lv, cnt = corpus.progressive(np.stack(qs), max_results, self.similarity_threshold,
                                               self.max_candidates_per_level)
         ids, ov, lv, cnt = to_np(ids), to_np(ov), to_np(lv), to_np(cnt)

@@ -248,7 +248,8 @@ class Prepared:
         return pack0(p) if self.Z16 is not None else p
 
 
-def seg_prepare(idx, exc=None) -> Prepared:
+def seg_prepare(idx, exc=None, src_f32: bool = False) -> Prepared:
+    """src_f32: the rows are float32 index vectors (hq_seg_prepare_src: NumPy f32 zero-variance test)."""
     t = torch()
     i2 = _contig((idx if idx.dim() == 2 else idx.view(1, -1)).to(t.float64))
     N, L = i2.shape
@@ -256,7 +257,7 @@ def seg_prepare(idx, exc=None) -> Prepared:
     Z = t.empty((N, Lp), dtype=t.float64, device=i2.device)
     S = t.empty((N, ns, 4), dtype=t.float64, device=i2.device)
     if N:
-        _chk(_L().hq_seg_prepare(ptr(i2), N, L, ptr(Z), ptr(S), stream()), exc)
+        _chk(_L().hq_seg_prepare_src(ptr(i2), N, L, 1 if src_f32 else 0, ptr(Z), ptr(S), stream()), exc)
     return Prepared(i2, Z, S, L)
 
 

@@ -142,6 +142,12 @@ int hq_parse_structure(int L, int32_t* out, int max_levels);
 int hq_seg_count(int L);
 int hq_seg_padded_len(int L);
 int hq_seg_prepare(const double* idx, int64_t N, int L, double* Z, double* stats, hq_stream_t stream);
+/* As hq_seg_prepare; src_f32 != 0 marks rows that hold float32 index vectors (widened to f64):
+ * a segment that is constant in f64 but whose NumPy f32 std is non-zero (a constant whose f32
+ * pairwise sum is inexact, e.g. 64 x 0.1f) gets the f32 mean/std and z = (c - mean32)/std32, so
+ * the score takes the reference's normalised branch (core/search_engine.py:153-167 on f32 arrays). */
+int hq_seg_prepare_src(const double* idx, int64_t N, int L, int src_f32, double* Z, double* stats,
+                       hq_stream_t stream);
 
 /* ---- S3/S4: dense EXACT scores ---------------------------------------------------------------
  * replaces core/search_engine.py:111-189 compare_indices_at_level (level >= 0) and :191-230
