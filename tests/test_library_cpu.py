@@ -131,3 +131,18 @@ def test_validation_paths_of_batched_entries(lib):
     assert lib.hq_chunk_encode_f16(None, 0, 1024, None, None, None, None) == _lib.HQ_OK
     assert lib.hq_chunk_encode_f16(None, 10, 0, None, None, None, None) == _lib.HQ_E_INVALID
     assert lib.hq_chunk_encode_f16(None, 10, 1024, None, None, None, None) == _lib.HQ_E_INVALID      # null
+
+
+def test_search_host_keeps_f32_index_vectors():
+    """Host dtype plumbing for hq_seg_prepare_src: float32 index vectors stay float32 until the
+    corpus is prepared (the f32 flag), everything else is widened to f64 (no compute here)."""
+    import numpy as np
+    import torch
+    from hq_mi355x.core import search_engine as se
+    a32 = np.zeros(8, np.float32)
+    assert se._is_f32(a32) and se._is_f32(torch.zeros(3, dtype=torch.float32))
+    assert not se._is_f32(np.zeros(8)) and not se._is_f32([0.1, 0.2])
+    assert se._idx(a32).dtype == np.float32
+    assert se._idx([1, 2]).dtype == np.float64
+    assert se._idx(np.zeros(3, np.float16)).dtype == np.float64
+    assert np.stack([se._idx(a32), se._idx(a32)]).dtype == np.float32
