@@ -60,10 +60,29 @@ static void seg_info(int L, SegInfo& s) {
 
 // ------------------------------------------------------------------------------------------------
 // per-segment statistics + normalised vectors (reference np.mean/np.std order)
+//
+// stats[row][seg] = (mean, std, msq, aux): the model the APPROXIMATE scans evaluate (Z = normalised
+// values, score from G = sum zq zc, corr = G / m, sum q c = std_q std_c G + m mean_q mean_c).
+// f64 sources: NumPy f64 statistics, z = (x - mean) / std, aux = 0.
+// f32 sources (src_f32): the reference runs np.std / np.mean and the normalisation in float32
+// (NumPy keeps the array dtype), so z = f32((x - mean32) / std32), std = std32 (float32 pairwise
+// order) — the reference's own normalised values.  Their sum is m (mean64 - mean32) / std32, not 0,
+// so the identity for sum q c needs the exact (f64) means: mean = mean64 (the dropped product of the
+// two mean errors is ~1e-14 relative).  A segment whose float32 std is 0 (the reference's constant
+// branch) stores the float32 mean (compared in float32 there) and std 0.  aux bits (as a double):
+//   kAuxF32    float32 source: the exact path recomputes this vector's statistics, z and (when the
+//              other side is float32 too) the whole score in float32
+//   kAuxUnsafe mean of squares outside [2^-100, 2^100]: float32 squares under/overflow in the
+//              reference, which the model does not follow; callers score such vectors on the dense
+//              exact path
 // ------------------------------------------------------------------------------------------------
+constexpr int kAuxF32 = 1, kAuxUnsafe = 2;
+
+__device__ __forceinline__ int aux_bits(const double* st) { return (int)st[3]; }
+
 __global__ __launch_bounds__(256) void k_seg_prepare(const double* __restrict__ idx, int64_t N, SegInfo si,
-                                                     int src_f32, double* __restrict__ Z,
-                                                     double* __restrict__ stats) {
+                                                     int all_f32, const uint8_t* __restrict__ row_f32,
+                                                     double* __restrict__ Z, double* __restrict__ stats) {
   const int64_t total = N * si.nseg;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -77,38 +96,59 @@ __global__ __launch_bounds__(256) void k_seg_prepare(const double* __restrict__ 
     const double sd = sqrt(np_sum<double>(fd, m) / (double)m);        // np.std (_methods._var)
     auto fs = [=](int k) -> double { return x[k] * x[k]; };
     const double msq = np_sum<double>(fs, m) / (double)m;             // np.mean(q ** 2)
-    double mean_u = mean, sd_u = sd;
-    if (src_f32 && sd == 0.0) {
-      // f32 index vectors: np.std runs in f32 (_methods._var: f32 pairwise sum, f32 divide, x - mean,
-      // x * x, f32 pairwise sum, divide, sqrt).  A constant segment whose f32 sum is inexact has
-      // std32 != 0 there, and the reference takes the normalised branch (search_engine.py:153-167).
+    double* z = Z + row * si.Lp + si.poff[s];
+    double* st = stats + (row * si.nseg + s) * 4;
+    if (row_f32 ? row_f32[row] != 0 : all_f32 != 0) {
+      // _methods._var on float32: f32 pairwise sum, divide, x - mean, x * x, f32 pairwise sum, divide,
+      // sqrt (np.mean = f32(f64(sum) / m) = the f32 division: the double rounding is innocuous)
       auto gx = [=](int k) -> float { return (float)x[k]; };
       const float mean32 = np_sum<float>(gx, m) / (float)m;
       auto gd = [=](int k) -> float { float d = (float)x[k] - mean32; return d * d; };
       const float sd32 = sqrtf(np_sum<float>(gd, m) / (float)m);
-      if (sd32 != 0.0f) { mean_u = (double)mean32; sd_u = (double)sd32; }
+      int aux = kAuxF32;
+      if (!(msq >= 0x1p-100 && msq <= 0x1p100)) aux |= kAuxUnsafe;
+      if (sd32 == 0.0f) {
+        for (int i = 0; i < si.plen[s]; ++i) z[i] = 0.0;
+        st[0] = (double)mean32;
+        st[1] = 0.0;
+      } else {
+        for (int i = 0; i < m; ++i) z[i] = (double)(((float)x[i] - mean32) / sd32);  // (q - mean(q)) / std
+        for (int i = m; i < si.plen[s]; ++i) z[i] = 0.0;
+        st[0] = mean;
+        st[1] = (double)sd32;
+      }
+      st[2] = msq;
+      st[3] = (double)aux;
+      continue;
     }
-    double* z = Z + row * si.Lp + si.poff[s];
-    if (sd_u == 0.0) {
+    if (sd == 0.0) {
       for (int i = 0; i < si.plen[s]; ++i) z[i] = 0.0;
     } else {
-      for (int i = 0; i < m; ++i) z[i] = (x[i] - mean_u) / sd_u;      // (q - mean(q)) / std (:150-151)
+      for (int i = 0; i < m; ++i) z[i] = (x[i] - mean) / sd;          // (q - mean(q)) / std (:150-151)
       for (int i = m; i < si.plen[s]; ++i) z[i] = 0.0;
     }
-    double* st = stats + (row * si.nseg + s) * 4;
-    st[0] = mean_u;
-    st[1] = sd_u;
+    st[0] = mean;
+    st[1] = sd;
     st[2] = msq;
     st[3] = 0.0;
   }
 }
 
+// constant branches of compare_indices_at_level (search_engine.py:141-148); both32: both arrays are
+// float32, so the mean difference and the 1e-6 literal are float32 (NEP 50)
+__device__ __forceinline__ double const0(bool zq, bool zc, double qm, double cm, bool both32 = false) {
+  if (zq && zc) {
+    if (both32) return fabsf((float)qm - (float)cm) < 1e-6f ? 1.0 : 0.0;
+    return fabs(qm - cm) < 1e-6 ? 1.0 : 0.0;
+  }
+  return 0.1;
+}
+
 // score of one level from the contraction G and the two vectors' segment statistics
 __device__ __forceinline__ double level_sim(double G, double qm, double qs, double qq, double cm, double cs,
-                                            double cq, double m, double inv_m) {
+                                            double cq, double m, double inv_m, bool both32 = false) {
   const bool fq = qs == 0.0, fc = cs == 0.0;
-  if (fq && fc) return fabs(qm - cm) < 1e-6 ? 1.0 : 0.0;
-  if (fq || fc) return 0.1;
+  if (fq || fc) return const0(fq, fc, qm, cm, both32);
   const double corr = G * inv_m;
   const double sim = (corr + 1.0) * 0.5;
   const double t1 = (qs * cs) * G;
@@ -134,17 +174,86 @@ struct VecSet {
   const double* S;    // N x nseg x 4 (mean, std, mean of squares, 0)
 };
 
-__device__ double exact_level(const double* q, const double* zq, const double* sq, const double* c,
-                              const double* zc, const double* sc, int m) {
-  const double qs = sq[1], cs = sc[1];
-  if (qs == 0.0 && cs == 0.0) return fabs(sq[0] - sc[0]) < 1e-6 ? 1.0 : 0.0;   // :141-145
-  if (qs == 0.0 || cs == 0.0) return 0.1;                                        // :146-148
-  auto fp = [=](int k) -> double { return zq[k] * zc[k]; };
+// One side of a level comparison: the raw segment, its normalised copy (f64 sides) and statistics in
+// the side's own dtype.  f32 sides recompute np.mean / np.std / np.mean(x ** 2) in float32 NumPy order.
+struct Side {
+  const double* x;  // raw values (f32 sources hold float32 values)
+  const double* z;  // (x - mean) / std in f64 (f64 sides); null: computed on the fly
+  double mean, sd, msq;
+  bool f32;
+};
+
+__device__ __forceinline__ Side make_side(const double* x, const double* z, const double* st, int m, bool f32) {
+  Side r;
+  r.x = x;
+  r.z = z;
+  r.f32 = f32;
+  if (f32) {
+    auto gx = [=](int k) -> float { return (float)x[k]; };
+    const float mean = np_sum<float>(gx, m) / (float)m;
+    auto gd = [=](int k) -> float { const float d = (float)x[k] - mean; return d * d; };
+    const float sd = sqrtf(np_sum<float>(gd, m) / (float)m);
+    auto gs = [=](int k) -> float { const float v = (float)x[k]; return v * v; };
+    r.mean = mean;
+    r.sd = sd;
+    r.msq = np_sum<float>(gs, m) / (float)m;
+  } else if (st) {
+    r.mean = st[0];
+    r.sd = st[1];
+    r.msq = st[2];
+  } else {
+    auto fx = [=](int k) -> double { return x[k]; };
+    r.mean = np_sum<double>(fx, m) / (double)m;
+    const double mu = r.mean;
+    auto fd = [=](int k) -> double { const double d = x[k] - mu; return d * d; };
+    r.sd = sqrt(np_sum<double>(fd, m) / (double)m);
+    auto fs = [=](int k) -> double { return x[k] * x[k]; };
+    r.msq = np_sum<double>(fs, m) / (double)m;
+  }
+  return r;
+}
+
+// element k of the side's normalised array ((q - np.mean(q)) / q_std in the side's dtype)
+__device__ __forceinline__ double side_z(const Side& s, int k) {
+  if (s.f32) return (double)(((float)s.x[k] - (float)s.mean) / (float)s.sd);
+  if (s.z) return s.z[k];
+  return (s.x[k] - s.mean) / s.sd;
+}
+
+// compare_indices_at_level (search_engine.py:111-189) for one segment in the reference's operation
+// order and dtype.  *np32 = 1 when the result is a numpy float32 (both sides f32, general branch,
+// not clamped), else it is a Python float: the type decides the overall weighted sum's arithmetic.
+__device__ double exact_level_sides(const Side& q, const Side& c, int m, int* np32) {
+  *np32 = 0;
+  const bool both32 = q.f32 && c.f32;
+  if (q.sd == 0.0 || c.sd == 0.0) return const0(q.sd == 0.0, c.sd == 0.0, q.mean, c.mean, both32);  // :141-148
+  if (both32) {
+    // float32 throughout: np.mean = f32(f64(f32 pairwise sum) / m) = f32 division (exact double
+    // rounding); Python float literals are cast to float32 (NEP 50); no FMA contraction
+    auto fp = [&](int k) -> float { return (float)side_z(q, k) * (float)side_z(c, k); };
+    const float corr = np_sum<float>(fp, m) / (float)m;                          // :154
+    const float sim = (corr + 1.0f) / 2.0f;                                        // :158
+    auto fd = [&](int k) -> float { const float d = (float)q.x[k] - (float)c.x[k]; return d * d; };
+    const float mse = np_sum<float>(fd, m) / (float)m;                             // :161
+    const float maxmse = (float)q.msq + (float)c.msq;                              // :162
+    float ds = 1.0f;
+    if (maxmse > 0.0f) {
+      ds = 1.0f - mse / maxmse;
+      ds = ds > 0.0f ? ds : 0.0f;
+    }
+    const float comb = 0.7f * sim + 0.3f * ds;                                     // :171
+    if (comb < 1.0f && comb > 0.0f) {
+      *np32 = 1;
+      return comb;
+    }
+    return comb < 1.0f ? 0.0 : 1.0;                                                // :174 (Python floats)
+  }
+  auto fp = [&](int k) -> double { return side_z(q, k) * side_z(c, k); };
   const double corr = np_sum<double>(fp, m) / (double)m;                         // :154
   const double sim = (corr + 1.0) / 2.0;                                         // :158
-  auto fd = [=](int k) -> double { double d = q[k] - c[k]; return d * d; };
+  auto fd = [&](int k) -> double { double d = q.x[k] - c.x[k]; return d * d; };
   const double mse = np_sum<double>(fd, m) / (double)m;                          // :161
-  const double maxmse = sq[2] + sc[2];                                           // :162
+  const double maxmse = q.msq + c.msq;                                           // :162
   double ds = 1.0;
   if (maxmse > 0.0) {
     ds = 1.0 - (mse / maxmse);
@@ -157,6 +266,12 @@ __device__ double exact_level(const double* q, const double* zq, const double* s
   return comb > 0.0 ? comb : 0.0;
 }
 
+__device__ double exact_level(const double* q, const double* zq, const double* sq, const double* c,
+                              const double* zc, const double* sc, int m, int* np32) {
+  const bool qf = (aux_bits(sq) & kAuxF32) != 0, cf = (aux_bits(sc) & kAuxF32) != 0;
+  return exact_level_sides(make_side(q, zq, sq, m, qf), make_side(c, zc, sc, m, cf), m, np32);
+}
+
 __device__ double exact_pair(const VecSet& A, int64_t ia, const VecSet& B, int64_t ib, const SegInfo& si, int level,
                              double* lv) {
   const double* ra = A.raw + ia * si.L;
@@ -165,24 +280,40 @@ __device__ double exact_pair(const VecSet& A, int64_t ia, const VecSet& B, int64
   const double* zb = B.Z + ib * si.Lp;
   const double* sa = A.S + ia * si.nseg * 4;
   const double* sb = B.S + ib * si.nseg * 4;
+  int t32;
   if (level >= 0) {
     if (level >= si.nseg) return 0.0;
     const int s = level;
     return exact_level(ra + si.src[s], za + si.poff[s], sa + 4 * s, rb + si.src[s], zb + si.poff[s], sb + 4 * s,
-                       si.len[s]);
+                       si.len[s], &t32);
   }
-  // search_engine.py:191-230: running weighted sum in level order, divide, clamp
+  // search_engine.py:191-230: running weighted sum in level order, divide, clamp.  Python typing:
+  // the sum starts as the Python float 0.0; a float32 level score makes the term float32 (the weight
+  // is cast to float32) and from then on the sum is float32 (a Python float operand is cast to it).
   double tws = 0.0, tw = 0.0;
+  bool acc32 = false;
   for (int s = 0; s < si.nseg; ++s) {
     const double v = exact_level(ra + si.src[s], za + si.poff[s], sa + 4 * s, rb + si.src[s], zb + si.poff[s],
-                                 sb + 4 * s, si.len[s]);
+                                 sb + 4 * s, si.len[s], &t32);
     if (lv) lv[s] = v;
     const double w = 1.0 / (double)(s + 1);
-    tws = tws + v * w;
+    const double term = t32 ? (double)((float)v * (float)w) : v * w;
+    if (!acc32 && !t32) {
+      tws = tws + term;
+    } else {
+      tws = (double)((float)tws + (float)term);
+      acc32 = true;
+    }
     tw = tw + w;
   }
-  double ov = tw > 0.0 ? tws / tw : 0.0;
-  ov = ov < 1.0 ? ov : 1.0;
+  double ov;
+  if (acc32) {
+    const float o = (float)tws / (float)tw;
+    ov = o < 1.0f ? (double)o : 1.0;
+  } else {
+    ov = tw > 0.0 ? tws / tw : 0.0;
+    ov = ov < 1.0 ? ov : 1.0;
+  }
   return ov > 0.0 ? ov : 0.0;
 }
 
@@ -395,7 +526,7 @@ __global__ __launch_bounds__(256) void k_scan(ScanArgs a) {
         for (int r = 0; r < 4; ++r) {
           const double* qst = qstat + (wave * 16 + (lane >> 4) + 4 * r) * nsu * 4;
           score[r] = level_sim(acc[r], qst[0], qst[1], qst[2], cst[0], cst[1], cst[2], (double)si.len[0],
-                               si.inv_m[0]);
+                               si.inv_m[0], (aux_bits(qst) & aux_bits(cst) & kAuxF32) != 0);
         }
       } else {
         double tws[4] = {0.0, 0.0, 0.0, 0.0};
@@ -410,7 +541,7 @@ __global__ __launch_bounds__(256) void k_scan(ScanArgs a) {
           for (int r = 0; r < 4; ++r) {
             const double* qst = qstat + ((wave * 16 + (lane >> 4) + 4 * r) * nsu + s) * 4;
             double v = level_sim(acc[r], qst[0], qst[1], qst[2], cst[0], cst[1], cst[2], (double)si.len[s],
-                                 si.inv_m[s]);
+                                 si.inv_m[s], (aux_bits(qst) & aux_bits(cst) & kAuxF32) != 0);
             tws[r] = tws[r] + v * si.w[s];
           }
         }
@@ -576,12 +707,6 @@ __device__ __forceinline__ double approx0(double G, double c1, double qA, double
   return s > 0.0 ? s : 0.0;
 }
 
-// constant branches of compare_indices_at_level (search_engine.py:141-148)
-__device__ __forceinline__ double const0(bool zq, bool zc, double qm, double cm) {
-  if (zq && zc) return fabs(qm - cm) < 1e-6 ? 1.0 : 0.0;
-  return 0.1;
-}
-
 typedef float flt4 __attribute__((ext_vector_type(4)));
 typedef float flt2 __attribute__((ext_vector_type(2)));
 
@@ -596,6 +721,7 @@ template <> struct ZOps<false> {
   static __device__ __forceinline__ const T* zc(const Scan0Args& a, int64_t c) { return a.Zc + c * a.Lp; }
 };
 
+// f64 sources only (hq_seg_prepare without float32 rows): the constant branch compares means in f64
 template <int KS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_scan0(Scan0Args a) {
   typedef ZOps<false> Z;
@@ -1197,11 +1323,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
         if (__ballot(pb && flagged)) {
           if (pb && flagged) {
             const int q = q0 + 16 * b + j;
+            const int64_t c = cs + 4 * g + r;
             const double* sq = a.Sq + (int64_t)q * a.nseg * 4;
-            const double* sc = a.Sc + (cs + 4 * g + r) * a.nseg * 4;
+            const double* sc = a.Sc + c * a.nseg * 4;
             const double qm = sq[0], qs = sq[1], qq = sq[2], cm = sc[0], csd = sc[1], cq = sc[2];
             const double v = (qs == 0.0 || csd == 0.0)
-                                 ? const0(qs == 0.0, csd == 0.0, qm, cm)
+                                 ? const0(qs == 0.0, csd == 0.0, qm, cm, (aux_bits(sq) & aux_bits(sc) & kAuxF32) != 0)
                                  : approx0((double)acc[u][r], a.c1, (0.6 * a.inv_m) * qs, 0.6 * qm, qq, csd, cm, cq);
             s = (float)v;
           }
@@ -1772,27 +1899,14 @@ __global__ __launch_bounds__(64) void k_select(const double* __restrict__ sc, in
 }
 
 // compare_indices_at_level on raw equal-length segments (mixed-length candidate pools): the query
-// segment q[0..m) against each row of C (N x m), statistics computed in place in NumPy order.
+// segment q[0..m) against each row of C (N x m), statistics computed in place in NumPy order and in each
+// side's dtype (q_f32 / c_f32: float32 values).
 __global__ __launch_bounds__(256) void k_pair_raw(const double* __restrict__ q, const double* __restrict__ C, int64_t N,
-                                                  int m, double* __restrict__ out) {
+                                                  int m, int q_f32, int c_f32, double* __restrict__ out) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x) {
-    const double* x = C + c * m;
-    auto fq = [=](int k) -> double { return q[k]; };
-    auto fc = [=](int k) -> double { return x[k]; };
-    const double qm = np_sum<double>(fq, m) / (double)m;
-    const double cm = np_sum<double>(fc, m) / (double)m;
-    auto fqd = [=](int k) -> double { double d = q[k] - qm; return d * d; };
-    auto fcd = [=](int k) -> double { double d = x[k] - cm; return d * d; };
-    const double qs = sqrt(np_sum<double>(fqd, m) / (double)m);
-    const double cs = sqrt(np_sum<double>(fcd, m) / (double)m);
-    double G = 0.0;
-    if (qs != 0.0 && cs != 0.0)
-      for (int k = 0; k < m; ++k) G = fma((q[k] - qm) / qs, (x[k] - cm) / cs, G);
-    auto fqq = [=](int k) -> double { return q[k] * q[k]; };
-    auto fcc = [=](int k) -> double { return x[k] * x[k]; };
-    const double qq = np_sum<double>(fqq, m) / (double)m;
-    const double cq = np_sum<double>(fcc, m) / (double)m;
-    out[c] = level_sim(G, qm, qs, qq, cm, cs, cq, (double)m, 1.0 / (double)m);
+    int t32;
+    out[c] = exact_level_sides(make_side(q, nullptr, nullptr, m, q_f32 != 0),
+                               make_side(C + c * m, nullptr, nullptr, m, c_f32 != 0), m, &t32);
   }
 }
 
@@ -2164,6 +2278,11 @@ int hq_seg_prepare(const double* idx, int64_t N, int L, double* Z, double* stats
 
 int hq_seg_prepare_src(const double* idx, int64_t N, int L, int src_f32, double* Z, double* stats,
                        hq_stream_t stream) {
+  return hq_seg_prepare_rows(idx, N, L, src_f32, nullptr, Z, stats, stream);
+}
+
+int hq_seg_prepare_rows(const double* idx, int64_t N, int L, int src_f32, const uint8_t* row_f32, double* Z,
+                        double* stats, hq_stream_t stream) {
   if (L <= 0 || N < 0) return fail(HQ_E_INVALID, "bad shape N=%lld L=%d", (long long)N, L);
   if (N == 0) return HQ_OK;
   if (!idx || !Z || !stats) return fail(HQ_E_INVALID, "null buffer");
@@ -2174,7 +2293,7 @@ int hq_seg_prepare_src(const double* idx, int64_t N, int L, int src_f32, double*
   int64_t blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(k_seg_prepare, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, idx, N, si, src_f32 ? 1 : 0,
-                     Z, stats);
+                     row_f32, Z, stats);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
@@ -2381,12 +2500,18 @@ int hq_select_topk(const double* scores, int Q, int64_t N, int k, double thresho
 }
 
 int hq_pair_scores_raw(const double* q, const double* C, int64_t N, int m, double* out, hq_stream_t stream) {
+  return hq_pair_scores_raw_src(q, C, N, m, 0, 0, out, stream);
+}
+
+int hq_pair_scores_raw_src(const double* q, const double* C, int64_t N, int m, int q_f32, int c_f32, double* out,
+                           hq_stream_t stream) {
   if (N < 0 || m <= 0) return fail(HQ_E_INVALID, "bad shape");
   if (N == 0) return HQ_OK;
   if (!q || !C || !out) return fail(HQ_E_INVALID, "null buffer");
   int64_t blocks = (N + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(k_pair_raw, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, q, C, N, m, out);
+  hipLaunchKernelGGL(k_pair_raw, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, q, C, N, m, q_f32 ? 1 : 0,
+                     c_f32 ? 1 : 0, out);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }

@@ -51,6 +51,7 @@ SIGNATURES = {
     "hq_seg_padded_len": (_i, [_i]),
     "hq_seg_prepare": (_i, [_p, _i64, _i, _p, _p, _p]),
     "hq_seg_prepare_src": (_i, [_p, _i64, _i, _i, _p, _p, _p]),
+    "hq_seg_prepare_rows": (_i, [_p, _i64, _i, _i, _p, _p, _p, _p]),
     "hq_level_scores": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _p, _p]),
     "hq_refine_topk": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _p, _p, _i, _i, _d, _i, _d, _i64, _p, _p, _p, _p, _p]),
     "hq_scan_workspace_size": (_sz, [_i, _i64, _i]),
@@ -63,6 +64,7 @@ SIGNATURES = {
     "hq_cosine_scores": (_i, [_p, _i, _p, _i64, _i, _p, _p]),
     "hq_select_topk": (_i, [_p, _i, _i64, _i, _d, _i, _i64, _p, _p, _p, _p, _p]),
     "hq_pair_scores_raw": (_i, [_p, _p, _i64, _i, _p, _p]),
+    "hq_pair_scores_raw_src": (_i, [_p, _p, _i64, _i, _i, _i, _p, _p]),
     "hq_precomputed_layout": (_i, [_i, _i, _i, _p, _i]),
     "hq_precomputed_index": (_i, [_i, _i, _p, _i64, _i64, _i, _i, _i, _i, _p, _i64, _p]),
     "hq_precomputed_stats": (_i, [_p, _i64, _i64, _i, _p, _p, _p, _p, _p]),

@@ -51,6 +51,55 @@ def _is_f32(x) -> bool:
     return dt == np.float32 or str(dt) == "torch.float32"
 
 
+def _stack_rows(rows):
+    """Equal-length index vectors -> ([N, L] f64 array, per-row float32 flags or None).  Pools mixing
+    float32 and float64 vectors keep each row's dtype semantics (hq_seg_prepare_rows)."""
+    flags = np.array([_is_f32(r) for r in rows], dtype=bool)
+    if flags.all():
+        return np.stack([np.asarray(r) for r in rows]), None
+    if not flags.any():
+        return np.stack([np.asarray(r, dtype=np.float64) for r in rows]), None
+    return np.stack([np.asarray(r, dtype=np.float64) for r in rows]), flags
+
+
+# level scores the reference returns as Python floats (constant branches, clamps); any other value
+# of a float32 comparison is a numpy float32 (core/search_engine.py:141-174)
+_PY_LEVEL_VALUES = (0.0, 0.1, 1.0)
+
+
+def f32_threshold(t: float, thr_mode: int) -> float:
+    """Threshold that reproduces the reference's comparisons for float32 level scores.  NumPy compares
+    a float32 score with a Python float threshold in float32 (NEP 50): `s >= t` is `s >= f32(t)`.  Between
+    t and f32(t) there is no other float32 value, so only one side of the rounding changes a decision;
+    f32(t) is returned when it does and no Python-float score value (0, 0.1, 1) lies in between."""
+    t32 = float(np.float32(t))
+    if thr_mode == 1 and t32 < t:
+        return t if any(t32 <= p < t for p in _PY_LEVEL_VALUES) else t32
+    if thr_mode == 2 and t32 > t:
+        return t if any(t < p <= t32 for p in _PY_LEVEL_VALUES) else t32
+    return t
+
+
+def combine_levels(lv: np.ndarray, both32: bool) -> np.ndarray:
+    """_calculate_overall_similarity (search_engine.py:191-230) from per-level scores [N, nl]: running
+    sum of score * 1/(l+1), divide, clamp.  both32: the level scores came from float32 arrays, so a
+    value outside (0, 0.1, 1) is a numpy float32 and the sum turns float32 once one enters (NEP 50)."""
+    N, nl = lv.shape
+    tws = np.zeros(N)
+    acc32 = np.zeros(N, dtype=bool)
+    tw = 0.0
+    for l in range(nl):
+        v, w = lv[:, l], 1.0 / (l + 1)
+        t32 = (~np.isin(v, _PY_LEVEL_VALUES)) if both32 else np.zeros(N, dtype=bool)
+        term = np.where(t32, (v.astype(np.float32) * np.float32(w)).astype(np.float64), v * w)
+        f32sum = (tws.astype(np.float32) + term.astype(np.float32)).astype(np.float64)
+        tws = np.where(acc32 | t32, f32sum, tws + term)
+        acc32 = acc32 | t32
+        tw += w
+    out = np.where(acc32, (tws.astype(np.float32) / np.float32(tw)).astype(np.float64), tws / tw if tw > 0 else 0.0)
+    return np.maximum(0.0, np.minimum(1.0, out))
+
+
 class IndexCorpus:
     """A corpus of equal-length hierarchical index vectors resident in HBM.
 
@@ -66,24 +115,49 @@ class IndexCorpus:
     EPS = 2e-5
     SLACK = 8
 
-    def __init__(self, indices, id_base: int = 0):
+    def __init__(self, indices, id_base: int = 0, row_f32=None):
         f32 = _is_f32(indices)
         x = _f64(indices)
         if x.dim() != 2:
             raise ValueError("IndexCorpus expects a 2-D [N, L] array of index vectors")
         self.N, self.L = int(x.shape[0]), int(x.shape[1])
         self.id_base = int(id_base)
-        self.prep = K.pack0(K.seg_prepare(x, src_f32=f32))
+        self.prep = K.pack0(K.seg_prepare(x, src_f32=f32, row_f32=None if f32 else row_f32))
         self.nseg = self.prep.nseg
+        # float32 rows outside the scans' model (values whose squares under/overflow in float32): the
+        # whole corpus then takes the dense exact path (one host sync, at build time, f32 corpora only)
+        self.dense_only = bool(self.prep.unsafe_rows().any()) if self.prep.f32 and self.N else False
 
-    def prepare_queries(self, queries) -> "K.Prepared":
+    def prepare_queries(self, queries, row_f32=None) -> "K.Prepared":
+        """queries: [Q, L] (or [L]); a pair (array, per-row float32 flags) for mixed-dtype batches."""
+        if isinstance(queries, tuple):
+            queries, row_f32 = queries
         f32 = _is_f32(queries)
         q = _f64(queries)
         if q.dim() == 1:
             q = q.view(1, -1)
         if q.shape[1] != self.L:
             raise ValueError(f"query index length {q.shape[1]} != corpus index length {self.L}")
-        return K.pack0(K.seg_prepare(q, src_f32=f32))
+        return K.pack0(K.seg_prepare(q, src_f32=f32, row_f32=None if f32 else row_f32))
+
+    def _fused_ok(self, mode: int) -> bool:
+        """The fused scans hold the contracted columns in registers: <= 256 padded values (hq_scan_topk)."""
+        if mode == 0:
+            return int(K._L().hq_seg_level0_len(self.L)) <= 256
+        return self.prep.Lp <= 256
+
+    def _thr(self, qp, thr: float, thr_mode: int) -> float:
+        """Threshold for the float32 comparisons of an all-float32 query batch and corpus (f32_threshold)."""
+        if thr_mode and qp.all32 and self.prep.all32:
+            return f32_threshold(float(thr), thr_mode)
+        return float(thr)
+
+    def _forced(self, qp):
+        """Device bool [Q] of queries that must take the dense exact path (float32 outside the model)."""
+        t = torch()
+        if self.dense_only:
+            return t.ones(qp.N, dtype=t.bool, device=qp.Z.device)
+        return qp.unsafe_rows() if qp.f32 else None
 
     # ---- scores ------------------------------------------------------------------------------
     def level_scores(self, queries, level: int):
@@ -108,10 +182,11 @@ class IndexCorpus:
         t = torch()
         Q = qp.N
         dev = qp.Z.device
+        thr = self._thr(qp, thr, thr_mode)
         best = t.full((Q,), -float("inf"), dtype=t.float64, device=dev)
         bid = t.full((Q,), -1, dtype=t.int64, device=dev)
         kp = k + self.SLACK
-        if kp > MAX_FUSED_K:
+        if kp > MAX_FUSED_K or self.dense_only or not self._fused_ok(mode):
             sc, ids, b, bi = self._dense(qp, t.arange(Q, device=dev), mode, k, thr, thr_mode)
             cnt = (ids >= 0).sum(1).to(t.int32)
             return sc, ids, cnt, b, bi
@@ -121,6 +196,9 @@ class IndexCorpus:
         redo = (res == 0)
         if need_best:
             redo = redo | (cnt == 0)
+        forced = self._forced(qp)
+        if forced is not None:
+            redo = redo | forced
         sel = t.nonzero(redo).view(-1)
         if sel.numel():
             s2, i2, b2, bi2 = self._dense(qp, sel, mode, k, thr, thr_mode)
@@ -157,16 +235,20 @@ class IndexCorpus:
         # Whole pipeline queued first (scan, exact re-rank, re-score, final ranking); the one host sync
         # comes last and checks whether any query needs the dense exact path (list not proven complete,
         # or nothing passed the threshold -> first arg-max).  Those rows are recomputed and replaced.
-        if M + self.SLACK > MAX_FUSED_K:
+        if M + self.SLACK > MAX_FUSED_K or self.dense_only or not self._fused_ok(0):
             s0, ids, cnt, best, bid = self.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)
             oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
             return oid, odet[..., 0], odet[..., 1:], ocnt
+        threshold = self._thr(qp, threshold, 1)
         s0, ids, cnt, res = self._scan_refine(qp, 0, M, float(threshold), 1)
         # no arg-max on this path: a query where nothing passed (count 0) is recomputed by the dense path
         # below, so the fallback slot is a constant (-inf, id -1, zero re-scores) kept per batch size
         best, bid, bdet = self._no_fallback(Q, qp.Z.device)
         oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out, bdet)
         redo = (res == 0) | (cnt == 0)
+        forced = self._forced(qp)
+        if forced is not None:
+            redo = redo | forced
         if bool(redo.any()):
             sel = t.nonzero(redo).view(-1)
             s2, i2, b2, bi2 = self._dense(qp, sel, 0, M, float(threshold), 1)
@@ -223,6 +305,10 @@ class ProgressiveSimilaritySearchEngine:
         return [lv for lv in levels if lv.start_index < len(indices)]
 
     # ---- pair scores ---------------------------------------------------------------------------
+    def _corpus(self, rows) -> IndexCorpus:
+        C, flags = _stack_rows(rows)
+        return IndexCorpus(C, row_f32=flags)
+
     def _scores_at_level(self, q: np.ndarray, cands: Sequence[np.ndarray], level: int) -> np.ndarray:
         """compare_indices_at_level(q, c, level) for every candidate, on the GPU."""
         N = len(cands)
@@ -232,10 +318,10 @@ class ProgressiveSimilaritySearchEngine:
         ql = self._parse_index_structure(q, len(q))
         if level >= len(ql):
             return out
-        groups: Dict[int, List[int]] = {}
+        groups: Dict[Tuple[int, bool], List[int]] = {}
         for i, c in enumerate(cands):
-            groups.setdefault(len(c), []).append(i)
-        for Lc, members in groups.items():
+            groups.setdefault((len(c), _is_f32(c)), []).append(i)
+        for (Lc, c32), members in groups.items():
             if Lc == 0:
                 continue
             C = np.stack([_idx(cands[i]) for i in members])
@@ -252,7 +338,8 @@ class ProgressiveSimilaritySearchEngine:
                 if m <= 0:
                     continue
                 qseg = _idx(q)[qs:qs + m]
-                s = to_np(K.pair_scores_raw(_f64(qseg), _f64(np.ascontiguousarray(C[:, cs:cs + m]))))
+                s = to_np(K.pair_scores_raw(_f64(qseg), _f64(np.ascontiguousarray(C[:, cs:cs + m])),
+                                            q_f32=_is_f32(q), c_f32=c32))
             out[members] = s
         return out
 
@@ -273,19 +360,20 @@ class ProgressiveSimilaritySearchEngine:
         if not ql:
             return np.zeros(N), np.zeros((N, 0))
         if all(len(c) == len(q) for c in cands) and N:
-            corpus = IndexCorpus(np.stack([_idx(c) for c in cands]))
+            corpus = self._corpus(cands)
             qp = corpus.prepare_queries(_idx(q)[None])
             ids = torch().arange(N, device=qp.Z.device).view(1, N)
             det = to_np(K.rescore(qp, corpus.prep, ids))[0]
             return det[:, 0], det[:, 1:]
         lv = np.stack([self._scores_at_level(q, cands, l) for l in range(len(ql))], axis=1)
-        tws = np.zeros(N)
-        tw = 0.0
-        for l in range(len(ql)):
-            w = 1.0 / (l + 1)
-            tws = tws + lv[:, l] * w
-            tw += w
-        return np.clip(tws / tw, 0.0, 1.0), lv
+        # per candidate: float32 arithmetic when both arrays are float32 (mixed lengths are rare: host loop)
+        out = np.zeros(N)
+        q32 = _is_f32(q)
+        for both32 in (False, True):
+            sel = [i for i, c in enumerate(cands) if (q32 and _is_f32(c)) == both32]
+            if sel:
+                out[sel] = combine_levels(lv[sel], both32)
+        return out, lv
 
     # ---- searches ------------------------------------------------------------------------------
     @staticmethod
@@ -312,8 +400,7 @@ class ProgressiveSimilaritySearchEngine:
             return []
         q = _idx(query_indices)
         if self._uniform(q, candidate_pool):
-            corpus = IndexCorpus(np.stack([_idx(c.hierarchical_indices)
-                                           for c in candidate_pool]))
+            corpus = self._corpus([c.hierarchical_indices for c in candidate_pool])
             ids, ov, lv = corpus.brute_force(q[None], min(max_results, len(candidate_pool)))
             return self._results(candidate_pool, to_np(ids)[0], to_np(ov)[0], to_np(lv)[0], with_error=False)
         ov, lv = self._overall_many(q, [c.hierarchical_indices for c in candidate_pool])
@@ -328,8 +415,7 @@ class ProgressiveSimilaritySearchEngine:
         if not self._parse_index_structure(q, len(q)):
             return []
         if self._uniform(q, candidate_pool):
-            corpus = IndexCorpus(np.stack([_idx(c.hierarchical_indices)
-                                           for c in candidate_pool]))
+            corpus = self._corpus([c.hierarchical_indices for c in candidate_pool])
             ids, ov, lv, cnt = corpus.progressive(q[None], max_results, self.similarity_threshold,
                                                   self.max_candidates_per_level)
             return self._results(candidate_pool, to_np(ids)[0], to_np(ov)[0], to_np(lv)[0], int(to_np(cnt)[0]))
@@ -346,8 +432,10 @@ class ProgressiveSimilaritySearchEngine:
         if not qs or any(len(q) != L for q in qs) or L == 0 or not self._parse_index_structure(qs[0], L) \
                 or not self._uniform(qs[0], candidate_pool):
             return [self.progressive_search(q, candidate_pool, max_results) for q in qs]
-        corpus = IndexCorpus(np.stack([_idx(c.hierarchical_indices) for c in candidate_pool]))
-        ids, ov, lv, cnt = corpus.progressive(np.stack(qs), max_results, self.similarity_threshold,
+        corpus = self._corpus([c.hierarchical_indices for c in candidate_pool])
+        Qa, qflags = _stack_rows(qs)
+        ids, ov, lv, cnt = corpus.progressive(Qa if qflags is None else (Qa, qflags), max_results,
+                                              self.similarity_threshold,
                                               self.max_candidates_per_level)
         ids, ov, lv, cnt = to_np(ids), to_np(ov), to_np(lv), to_np(cnt)
         return [self._results(candidate_pool, ids[i], ov[i], lv[i], int(cnt[i])) for i in range(len(qs))]

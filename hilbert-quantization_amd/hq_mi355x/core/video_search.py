@@ -6,10 +6,9 @@ from __future__ import annotations
 
 from typing import List, Sequence, Tuple
 
-import numpy as np
 
 from .._dev import to_np
-from .search_engine import IndexCorpus
+from .search_engine import IndexCorpus, _idx
 
 
 class HierarchicalFrameSearch:
@@ -18,8 +17,8 @@ class HierarchicalFrameSearch:
         self.similarity_threshold = similarity_threshold
 
     def search(self, query_indices, max_results: int) -> List[Tuple[int, float]]:
-        ids, sc = self.corpus.frame_search(np.asarray(query_indices, dtype=np.float64)[None], max_results,
-                                           self.similarity_threshold)
+        # the query keeps its dtype: a float32 index is compared with float32 statistics, as in the reference
+        ids, sc = self.corpus.frame_search(_idx(query_indices)[None], max_results, self.similarity_threshold)
         ids, sc = to_np(ids)[0], to_np(sc)[0]
         return [(int(i), float(s)) for i, s in zip(ids, sc) if i >= 0]
 

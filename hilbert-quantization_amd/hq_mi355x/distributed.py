@@ -66,6 +66,7 @@ class ShardedIndexCorpus:
         t = torch()
         c = self.local
         Q = qp.N
+        threshold = c._thr(qp, threshold, 1)
         s0, ids, cnt, res = c._scan_refine(qp, 0, M, float(threshold), 1)
         best = t.full((Q,), -float("inf"), dtype=t.float64, device=qp.Z.device)
         bid = t.full((Q,), -1, dtype=t.int64, device=qp.Z.device)
@@ -77,6 +78,9 @@ class ShardedIndexCorpus:
 
         rec = records(qp, s0, ids, best, bid)
         redo = (res == 0) | (cnt == 0)
+        forced = c._forced(qp)
+        if forced is not None:
+            redo = redo | forced
         if bool(redo.any()):
             sel = t.nonzero(redo).view(-1)
             s2, i2, b2, bi2 = c._dense(qp, sel, 0, M, float(threshold), 1)
@@ -98,7 +102,7 @@ class ShardedIndexCorpus:
         if self.n_total <= M:
             return self.brute_force(queries, max_results)
         qp = c.prepare_queries(queries)
-        if M + c.SLACK > 64:  # beyond the fused scan's list length: the dense exact path per shard
+        if M + c.SLACK > 64 or c.dense_only or not c._fused_ok(0):  # the dense exact path per shard (list length / f32 model)
             t = torch()
             Q = qp.N
             s0, ids, _, best, bid = c.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)

@@ -231,34 +231,51 @@ def seg_padded_len(L: int) -> int:
 
 class Prepared:
     """Device-resident prepared index vectors: raw R [N, L] f64, Z [N, Lp] f64 (segment padded,
-    normalised) and stats S [N, nseg, 4] (mean, std, mean of squares).  Built once per corpus."""
+    normalised) and stats S [N, nseg, 4] (mean, std, mean of squares, aux).  Built once per corpus.
+    f32: some rows are float32 index vectors (aux bit 1; hq_seg_prepare_src / _rows)."""
 
-    __slots__ = ("R", "Z", "S", "L", "N", "nseg", "Lp", "Z16", "S32")
+    __slots__ = ("R", "Z", "S", "L", "N", "nseg", "Lp", "Z16", "S32", "f32", "all32")
 
-    def __init__(self, R, Z, S, L):
+    def __init__(self, R, Z, S, L, f32: bool = False, all32: bool = False):
         self.R, self.Z, self.S, self.L = R, Z, S, int(L)
         self.N = Z.shape[0]
         self.nseg = S.shape[1]
         self.Lp = Z.shape[1]
+        self.f32 = bool(f32)      # some rows are float32 sources
+        self.all32 = bool(all32)  # every row is
         self.Z16 = self.S32 = None  # split-f16 level-0 copies for the level-0 scan (pack0)
 
     def rows(self, sel):
         """Sub-set of rows (device index tensor) as a new Prepared (level-0 copies re-packed on demand)."""
-        p = Prepared(self.R.index_select(0, sel), self.Z.index_select(0, sel), self.S.index_select(0, sel), self.L)
+        p = Prepared(self.R.index_select(0, sel), self.Z.index_select(0, sel), self.S.index_select(0, sel), self.L,
+                     self.f32, self.all32)
         return pack0(p) if self.Z16 is not None else p
 
+    def unsafe_rows(self):
+        """Device bool [N]: float32 rows outside the scans' model (aux bit 2, hq_mi355x.h) -> dense exact path."""
+        return (self.S[:, :, 3] >= 2.0).any(dim=1)
 
-def seg_prepare(idx, exc=None, src_f32: bool = False) -> Prepared:
-    """src_f32: the rows are float32 index vectors (hq_seg_prepare_src: NumPy f32 zero-variance test)."""
+
+def seg_prepare(idx, exc=None, src_f32: bool = False, row_f32=None) -> Prepared:
+    """src_f32: every row is a float32 index vector; row_f32 (bool per row, host or device): some are
+    (hq_seg_prepare_rows).  The reference computes those rows' statistics and scores in float32."""
     t = torch()
     i2 = _contig((idx if idx.dim() == 2 else idx.view(1, -1)).to(t.float64))
     N, L = i2.shape
     Lp, ns = seg_padded_len(L), seg_count(L)
     Z = t.empty((N, Lp), dtype=t.float64, device=i2.device)
     S = t.empty((N, ns, 4), dtype=t.float64, device=i2.device)
+    rf = None
+    any32 = all32 = bool(src_f32)
+    if row_f32 is not None and not src_f32:
+        flags = np.asarray(row_f32, dtype=bool).reshape(-1)
+        if flags.size != N:
+            raise ValueError("row_f32 needs one flag per row")
+        any32, all32 = bool(flags.any()), bool(flags.all()) and N > 0
+        rf = _contig(t.from_numpy(flags.astype(np.uint8)).to(i2.device))
     if N:
-        _chk(_L().hq_seg_prepare_src(ptr(i2), N, L, 1 if src_f32 else 0, ptr(Z), ptr(S), stream()), exc)
-    return Prepared(i2, Z, S, L)
+        _chk(_L().hq_seg_prepare_rows(ptr(i2), N, L, 1 if src_f32 else 0, ptr(rf), ptr(Z), ptr(S), stream()), exc)
+    return Prepared(i2, Z, S, L, any32, all32)
 
 
 PAD0 = 48  # pad rows of the level-0 copies (hq_mi355x.h: hq_seg_pack0_split)
@@ -315,8 +332,9 @@ def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.
     ids = t.empty((Q, k), dtype=t.int64, device=dev)
     best = t.empty(Q, dtype=t.float64, device=dev) if need_best else None
     bid = t.empty(Q, dtype=t.int64, device=dev) if need_best else None
+    # HQ_SCAN_F64 (A/B knob): the f64 wave-level kernel, f64 sources only
     if (mode == 0 and not need_best and q.Z16 is not None and c.Z16 is not None
-            and not os.environ.get("HQ_SCAN_F64")):
+            and (not os.environ.get("HQ_SCAN_F64") or q.f32 or c.f32)):
         _chk(_L().hq_scan0_topk_split(ptr(q.Z16), ptr(q.S32), ptr(q.S), Q, ptr(c.Z16), ptr(c.S32), ptr(c.S), N, c.L,
                                       k, float(threshold), thr_mode, int(id_base), ptr(ws), ws_bytes, ptr(sc),
                                       ptr(ids), stream()), exc)
@@ -399,14 +417,16 @@ def select_topk(scores, k: int, threshold: float = 0.0, thr_mode: int = 0, id_ba
     return os_, oi, b, bi
 
 
-def pair_scores_raw(q, C, exc=None):
-    """compare_indices_at_level on raw equal-length segments: q [m] vs C [N, m] -> f64 [N]."""
+def pair_scores_raw(q, C, exc=None, q_f32: bool = False, c_f32: bool = False):
+    """compare_indices_at_level on raw equal-length segments: q [m] vs C [N, m] -> f64 [N]; q_f32 / c_f32:
+    that side holds float32 values (statistics in float32; the whole score when both are)."""
     t = torch()
     q1 = _contig(q.reshape(-1).to(t.float64))
     C2 = _contig(C.to(t.float64))
     N, m = C2.shape
     out = t.empty(N, dtype=t.float64, device=C2.device)
-    _chk(_L().hq_pair_scores_raw(ptr(q1), ptr(C2), N, m, ptr(out), stream()), exc)
+    _chk(_L().hq_pair_scores_raw_src(ptr(q1), ptr(C2), N, m, 1 if q_f32 else 0, 1 if c_f32 else 0, ptr(out),
+                                     stream()), exc)
     return out
 
 

@@ -136,18 +136,28 @@ int hq_parse_structure(int L, int32_t* out, int max_levels);
  * starts at a multiple of 4 and is zero-filled to a multiple of 4, Lp = hq_seg_padded_len(L)
  * columns, nseg = hq_seg_count(L).  For every row of idx (f64 N x L):
  *   Z[row][poff_s + j] = (c_j - mean_s) / std_s   (0 where std_s == 0)     f64 N x Lp
- *   stats[row][s]      = {mean_s, std_s, mean(c^2)_s, 0}                  f64 N x nseg x 4
+ *   stats[row][s]      = {mean_s, std_s, mean(c^2)_s, aux}                f64 N x nseg x 4
  * mean/std follow NumPy's pairwise summation order so the std == 0 branches of
- * core/search_engine.py:137-147 match bit-for-bit.                                              */
+ * core/search_engine.py:137-147 match bit-for-bit.  aux = 0 for f64 sources.                     */
 int hq_seg_count(int L);
 int hq_seg_padded_len(int L);
 int hq_seg_prepare(const double* idx, int64_t N, int L, double* Z, double* stats, hq_stream_t stream);
-/* As hq_seg_prepare; src_f32 != 0 marks rows that hold float32 index vectors (widened to f64):
- * a segment that is constant in f64 but whose NumPy f32 std is non-zero (a constant whose f32
- * pairwise sum is inexact, e.g. 64 x 0.1f) gets the f32 mean/std and z = (c - mean32)/std32, so
- * the score takes the reference's normalised branch (core/search_engine.py:153-167 on f32 arrays). */
+/* As hq_seg_prepare; src_f32 != 0 marks rows that hold float32 index vectors (widened to f64).  The
+ * reference then runs np.mean / np.std / the normalisation (and, when both sides are float32, the
+ * whole score) in float32 (core/search_engine.py:137-189 keep the array dtype).  For such rows
+ *   Z = f32((c - mean32) / std32), std = std32 (float32 NumPy order), mean = the f64 mean (the sum of
+ *   the float32 z is not 0; with the exact mean, sum q*c = std_q std_c G + m mean_q mean_c holds),
+ *   aux = 1 (float32 source; the exact scores recompute the float32 statistics), + 2 when the mean of
+ *   squares is outside [2^-100, 2^100] (float32 squares under/overflow: the scans' model does not
+ *   hold; callers score such rows on the dense exact path).
+ * A segment whose float32 std is 0 stores the float32 mean and std 0 (the reference's constant
+ * branch, whose mean comparison is float32).                                                     */
 int hq_seg_prepare_src(const double* idx, int64_t N, int L, int src_f32, double* Z, double* stats,
                        hq_stream_t stream);
+/* As hq_seg_prepare_src with a per-row flag (pools mixing float32 and float64 index vectors):
+ * row_f32 (device u8[N], may be NULL: src_f32 applies to every row) != 0 marks float32 rows.      */
+int hq_seg_prepare_rows(const double* idx, int64_t N, int L, int src_f32, const uint8_t* row_f32, double* Z,
+                        double* stats, hq_stream_t stream);
 
 /* ---- S3/S4: dense EXACT scores ---------------------------------------------------------------
  * replaces core/search_engine.py:111-189 compare_indices_at_level (level >= 0) and :191-230
@@ -167,7 +177,10 @@ int hq_level_scores(const double* Rq, const double* Zq, const double* Sq, int Q,
  * (brute_force_search :302-338).  thr_mode 0: keep all; 1: score >= threshold; 2: > threshold.
  * Also the first arg-max of the approximate score (out_best, may be NULL).  id_base is added to
  * local row ids (sharding).  out_score/out_id: Q x k (-inf / -1 in empty slots), 1 <= k <= 64.
- * The exact ranking is obtained with hq_refine_topk on a slightly larger list.
+ * The exact ranking is obtained with hq_refine_topk on a slightly larger list.  Vectors with an aux
+ * bit 2 (unsafe) segment are outside the model: callers use the dense exact path for them.  Mode 0
+ * without the arg-max and with a level-0 segment of <= 32 values runs an f64 wave-level kernel for
+ * f64 sources only (float32 rows: hq_scan0_topk_split).
  * workspace: hq_scan_workspace_size(Q, N, k) bytes of device memory.                            */
 size_t hq_scan_workspace_size(int Q, int64_t N, int k);
 int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, const double* Sc,
@@ -235,6 +248,10 @@ int hq_select_topk(const double* scores, int Q, int64_t N, int k, double thresho
  * m (search_engine.py:122-135): q f64[m] against C f64 N x m -> out f64[N].                      */
 int hq_pair_scores_raw(const double* q, const double* C, int64_t N, int m, double* out,
                        hq_stream_t stream);
+/* As hq_pair_scores_raw; q_f32 / c_f32 != 0: that side holds float32 values, whose statistics and
+ * normalised values the reference computes in float32 (the whole score when both are float32).   */
+int hq_pair_scores_raw_src(const double* q, const double* C, int64_t N, int m, int q_f32, int c_f32,
+                           double* out, hq_stream_t stream);
 
 /* ---- S7: RAG cosine scores (rag/search/engine.py:622-660, 1025-1051) --------------------------
  * a: f32 Q x K, b: f32 N x K -> out f64 Q x N of (cos + 1) / 2 (0 if a norm is 0).               */

@@ -251,6 +251,97 @@ def search_fixtures(hq):
     return out
 
 
+def _f32_rows(rng, L, N):
+    """float32 index vectors: random rows plus every case where NumPy's float32 statistics leave the
+    f64 model (SURVEY.md §8a hazard 5): inexact constants, 1-ulp near-constants, f32
+    underflow of d*d, tiny / huge magnitudes, a large mean / std ratio."""
+    C = rng.standard_normal((N, L)).astype(np.float32)
+    C[1] = np.float32(0.1)
+    C[2] = np.float32(1.7)
+    C[3] = 0.0
+    C[4] = np.float32(0.5)
+    C[5, : L // 2] = np.float32(0.1)
+    C[6] = C[1]
+    v = np.float32(1.7)
+    C[7] = v
+    C[7, [3, 9, 17]] = np.nextafter(v, np.float32(2))          # 1-ulp near-constant
+    C[8] = np.float32(0.1)
+    C[8, ::5] = np.nextafter(np.float32(0.1), np.float32(1))
+    C[9] = np.where(np.arange(L) % 2 == 0, np.float32(1e-25), np.float32(2e-25))  # d*d underflows
+    C[10] = (rng.standard_normal(L) * 1e-20).astype(np.float32)  # squares in the f32 denormal range
+    C[11] = (1000.0 + rng.standard_normal(L) * 1e-3).astype(np.float32)  # large mean / std ratio
+    C[12] = C[11] + np.float32(0.001)
+    C[13] = -C[20]
+    C[14] = C[20] * np.float32(2.0) + np.float32(1.0)
+    C[15] = C[7]
+    C[15, 0] = np.nextafter(v, np.float32(0))
+    return C
+
+
+def search_f32_fixtures(hq):
+    """compare_indices_at_level / _calculate_overall_similarity / searches on float32 index vectors,
+    run by the reference itself: NumPy keeps the array dtype, so np.std, the normalisation and (when
+    both arrays are float32) the whole score run in float32, and the score is a numpy.float32 unless a
+    constant branch or a clamp returns a Python float (core/search_engine.py:111-230).  Also a float64
+    query against float32 candidates (mixed) and a pool mixing both dtypes."""
+    from hilbert_quantization.core.search_engine import ProgressiveSimilaritySearchEngine
+    from hilbert_quantization.models import QuantizedModel, ModelMetadata
+    out = {}
+    rng = np.random.default_rng(4242)
+
+    def models_of(rows):
+        ms = []
+        for b, r in enumerate(rows):
+            md = ModelMetadata(model_name=f"m{b}", original_size_bytes=1, compressed_size_bytes=1,
+                               compression_ratio=1.0, quantization_timestamp="t")
+            ms.append(QuantizedModel(compressed_data=b"x", original_dimensions=(8, 8), parameter_count=1,
+                                     compression_quality=0.8, hierarchical_indices=r, metadata=md))
+        return ms
+
+    for tag, L, N in [("L64", 64, 72), ("L32", 32, 48), ("L256", 256, 40)]:
+        C = _f32_rows(rng, L, N)
+        Q = np.stack([C[20] + rng.normal(0, 0.01, L).astype(np.float32), C[1], C[7], C[8], C[9], C[10], C[11],
+                      C[3], rng.standard_normal(L).astype(np.float32)])
+        eng = ProgressiveSimilaritySearchEngine(similarity_threshold=0.1, max_candidates_per_level=20)
+        nl = len(eng._parse_index_structure(Q[0], L))
+        for qtag, QQ in [("q32", Q), ("q64", Q.astype(np.float64))]:
+            per = np.zeros((len(QQ), N, nl))
+            per_t = np.zeros((len(QQ), N, nl), np.int8)
+            ov = np.zeros((len(QQ), N))
+            ov_t = np.zeros((len(QQ), N), np.int8)
+            for a in range(len(QQ)):
+                for b in range(N):
+                    for lv in range(nl):
+                        v = eng.compare_indices_at_level(QQ[a], C[b], lv)
+                        per[a, b, lv] = float(v)
+                        per_t[a, b, lv] = isinstance(v, np.float32)
+                    v = eng._calculate_overall_similarity(QQ[a], C[b])[0]
+                    ov[a, b] = float(v)
+                    ov_t[a, b] = isinstance(v, np.float32)
+            out[f"{tag}_{qtag}_per_level"] = per
+            out[f"{tag}_{qtag}_per_level_f32"] = per_t
+            out[f"{tag}_{qtag}_overall"] = ov
+            out[f"{tag}_{qtag}_overall_f32"] = ov_t
+        # searches: float32 pool, and a pool mixing float32 / float64 rows (odd rows widened)
+        pools = {"pool32": [C[b] for b in range(N)],
+                 "poolmix": [C[b] if b % 2 == 0 else C[b].astype(np.float64) for b in range(N)]}
+        K = 10
+        for ptag, rows in pools.items():
+            models = models_of(rows)
+            for stag, fn in [("bf", eng.brute_force_search), ("pg", eng.progressive_search)]:
+                ids = np.full((len(Q), K), -1, np.int64)
+                sc = np.zeros((len(Q), K))
+                for a in range(len(Q)):
+                    for j, x in enumerate(fn(Q[a], models, K)):
+                        ids[a, j] = int(x.model.model_id[1:])
+                        sc[a, j] = float(x.similarity_score)
+                out[f"{tag}_{ptag}_{stag}_ids"] = ids
+                out[f"{tag}_{ptag}_{stag}_sc"] = sc
+        out[f"{tag}_C"] = C
+        out[f"{tag}_Q"] = Q
+    return out
+
+
 def rag_score_fixtures(hq):
     from hilbert_quantization.rag.search import engine as E
     cls = E.RAGSearchEngineImpl if hasattr(E, "RAGSearchEngineImpl") else None
@@ -341,7 +432,8 @@ def main():
     hq = _import_reference(a.ref)
     only = set(filter(None, a.only.split(",")))
     for name, fn in [("mapper", mapper_fixtures), ("index", index_fixtures), ("quant", quant_fixtures),
-                     ("search", search_fixtures), ("rag_score", rag_score_fixtures),
+                     ("search", search_fixtures), ("search_f32", search_f32_fixtures),
+                     ("rag_score", rag_score_fixtures),
                      ("precomputed", precomputed_fixtures)]:
         if only and name not in only:
             continue

@@ -205,6 +205,76 @@ def test_search_orders_golden(golden, tag):
     np.testing.assert_allclose(sc, g[f"{tag}_fallback_sc"], atol=1e-12)
 
 
+@pytest.mark.parametrize("tag", ["L64", "L32", "L256"])
+def test_scores_f32_golden(golden, tag):
+    """float32 index vectors (and a float64 query against them): every level score, its Python type
+    and the overall score bit-identical to the reference (tests/golden/search_f32.npz), including
+    inexact constants, 1-ulp near-constants, f32 underflow and a large mean / std ratio."""
+    g = golden("search_f32")
+    C, Q = g[f"{tag}_C"], g[f"{tag}_Q"]
+    assert C.dtype == np.float32
+    for qtag, QQ in [("q32", Q), ("q64", Q.astype(np.float64))]:
+        per, ov = g[f"{tag}_{qtag}_per_level"], g[f"{tag}_{qtag}_overall"]
+        for a in range(len(QQ)):
+            o, p = O.overall_similarity(QQ[a], C)
+            np.testing.assert_array_equal(p, per[a], err_msg=f"{tag} {qtag} q{a}")
+            np.testing.assert_array_equal(O.level_types(p, QQ.dtype == np.float32),
+                                          g[f"{tag}_{qtag}_per_level_f32"][a].astype(bool))
+            np.testing.assert_array_equal(o, ov[a], err_msg=f"{tag} {qtag} q{a} overall")
+
+
+@pytest.mark.parametrize("tag", ["L64", "L32", "L256"])
+def test_search_orders_f32_golden(golden, tag):
+    g = golden("search_f32")
+    C, Q = g[f"{tag}_C"], g[f"{tag}_Q"]
+    for a in range(len(Q)):
+        ids, sc, _ = O.brute_force_search(Q[a], C, 10)
+        np.testing.assert_array_equal(ids, g[f"{tag}_pool32_bf_ids"][a][: len(ids)])
+        np.testing.assert_array_equal(sc, g[f"{tag}_pool32_bf_sc"][a][: len(ids)])
+        ids, sc, _, _ = O.progressive_search(Q[a], C, 10, 0.1, 20)
+        ref = g[f"{tag}_pool32_pg_ids"][a]
+        np.testing.assert_array_equal(ids, ref[ref >= 0])
+        np.testing.assert_array_equal(sc, g[f"{tag}_pool32_pg_sc"][a][: len(ids)])
+
+
+def test_f32_threshold_and_typed_overall_host_logic():
+    """Host logic of the float32 search path (hq_mi355x.core.search_engine): the threshold that
+    reproduces NumPy's float32 comparison, and the typed weighted sum, against NumPy itself."""
+    from hq_mi355x.core.search_engine import combine_levels, f32_threshold
+    for t in (0.1, 0.3, 0.7, 0.123456789, 0.5, 1e-46, 0.95):
+        t32 = np.float32(t)
+        for mode in (1, 2):
+            te = f32_threshold(t, mode)
+            # every float32 value next to t and every Python-float score value decides as in NumPy
+            cands = [np.nextafter(t32, np.float32(-1)), t32, np.nextafter(t32, np.float32(2))]
+            for v in cands:
+                if float(v) in (0.0, 1.0):  # never a numpy float32 score (those lie in (0, 1))
+                    continue
+                want = (v >= t) if mode == 1 else (v > t)   # numpy float32 vs Python float (NEP 50)
+                got = (float(v) >= te) if mode == 1 else (float(v) > te)
+                assert bool(want) == got, (t, mode, v)
+            for p in (0.0, 0.1, 1.0):
+                want = (p >= t) if mode == 1 else (p > t)
+                got = (p >= te) if mode == 1 else (p > te)
+                assert want == got, (t, mode, p)
+    rng = np.random.default_rng(3)
+    lv = rng.uniform(0, 1, (50, 5)).astype(np.float32).astype(np.float64)
+    lv[:5] = 0.1
+    lv[5:10, 0] = 1.0
+    lv[10:15, 2] = 0.0
+    got = combine_levels(lv, True)
+    for i in range(len(lv)):
+        tws, tw = 0.0, 0.0
+        for l in range(5):
+            v = lv[i, l]
+            v = float(v) if v in (0.0, 0.1, 1.0) else np.float32(v)
+            w = 1.0 / (l + 1)
+            tws += v * w
+            tw += w
+        want = max(0.0, min(1.0, tws / tw))
+        assert got[i] == float(want), i
+
+
 def test_rag_scoring_golden(golden):
     g = golden("rag_score")
     got = O.rag_cosine(g["cos_B"], g["cos_A"])
