@@ -255,6 +255,7 @@ def _ingest(hq: "HilbertQuantizer", parameter_sets, model_ids=None, descriptions
         pipe.compressor._norm_min = np.float32(last_state[1])
         pipe.compressor._norm_max = np.float32(last_state[2])
     if stop_exc is not None:
+        stop_exc.hq_quantized = out  # models quantized and registered before the failing one
         raise stop_exc
     return out
 
@@ -300,18 +301,35 @@ class BatchQuantizer:
             except Exception as e:
                 self.logger.error(f"Failed search {i + 1}: {e}")
         results: List[List[SearchResult]] = [[] for _ in query_sets]
-        if not ok:
+        # quantize the valid queries in batches; a query whose quantize fails (dimension / efficiency
+        # check) yields [] and the queries after it continue, as the reference's per-query loop does
+        done = []  # (query position, QuantizedModel)
+        pending = ok
+        while pending:
+            try:
+                models = _ingest(hq, [q for _, q in pending], [f"model_{int(time.time())}" for _ in pending], None,
+                                 True, validate=False)
+                done.extend((i, m) for (i, _), m in zip(pending, models))
+                pending = []
+            except Exception as e:
+                part = getattr(e, "hq_quantized", None)
+                if part is None:  # not a per-query failure: answer the rest one query at a time
+                    for i, q in pending:
+                        try:
+                            results[i] = hq.search(q, candidate_models, max_results)
+                        except Exception as e2:
+                            self.logger.error(f"Failed search {i + 1}: {e2}")
+                    pending = []
+                    break
+                done.extend((i, m) for (i, _), m in zip(pending, part))
+                self.logger.error(f"Failed search {pending[len(part)][0] + 1}: {e}")
+                pending = pending[len(part) + 1:]
+        if not done:
             return results
-        try:
-            models = _ingest(hq, [q for _, q in ok], [f"model_{int(time.time())}" for _ in ok], None, True,
-                             validate=False)
-        except Exception as e:  # the sequential path would fail each of these queries the same way
-            self.logger.error(f"Failed search batch: {e}")
-            return results
-        found = hq.search_engine.progressive_search_batch([m.hierarchical_indices for m in models],
+        found = hq.search_engine.progressive_search_batch([m.hierarchical_indices for _, m in done],
                                                           candidate_models, max_results)
         thr = hq.similarity_threshold
-        for (i, _), res in zip(ok, found):
+        for (i, _), res in zip(done, found):
             results[i] = [r for r in res if r.similarity_score >= thr]
         return results
 

@@ -90,3 +90,26 @@ def test_search_batch_matches_sequential(hq_lib):
         assert [r.matching_indices for r in res] == [r.matching_indices for r in want]
     # the queries were registered, as search() does
     assert len(bq.quantizer._model_registry) == 40 + 3
+
+
+def test_search_batch_failing_query_only_blanks_itself(hq_lib):
+    """a query failing the efficiency check (api.py:621-650 catches per query) yields []
+    while the queries before AND after it are quantized, registered and answered."""
+    pytest.importorskip("PIL")
+    from hq_mi355x.api import BatchQuantizer, HilbertQuantizer
+    rng = np.random.default_rng(8)
+    base = [rng.standard_normal(1024).astype(np.float32) for _ in range(30)]
+    bq = BatchQuantizer()
+    cands = bq.quantize_batch(base)
+    bad = rng.standard_normal(1500).astype(np.float32)  # 1500 / 4096 < 0.5: QuantizationError
+    queries = [base[2] + np.float32(0.01), bad, base[9] + np.float32(0.02), bad, base[17] + np.float32(0.03)]
+    got = bq.search_batch(queries, cands, max_results=5)
+    assert got[1] == [] and got[3] == []
+    seq = HilbertQuantizer()
+    for i in (0, 2, 4):
+        with contextlib.redirect_stdout(io.StringIO()):
+            want = seq.search(queries[i], cands, max_results=5)
+        assert got[i], i
+        assert [r.model.metadata.model_name for r in got[i]] == [r.model.metadata.model_name for r in want]
+        assert [r.similarity_score for r in got[i]] == [r.similarity_score for r in want]
+    assert len(bq.quantizer._model_registry) == 30 + 3
