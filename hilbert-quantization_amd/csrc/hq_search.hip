@@ -1110,7 +1110,7 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
 constexpr float kMarginF = 6e-5f;
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 constexpr int kZ16Row = 64;  // halfs per split row: hi[32] then lo[32]
-constexpr int kPad0 = 3 * kCS;  // pad rows of the f32 copies (hq_seg_pack0_f32); reads reach cs + 31
+constexpr int kPad0 = 3 * kCS;  // pad rows of the f32 copies (hq_seg_pack0_split); reads reach cs + 31
 
 __device__ __forceinline__ float lower_f32(double x) {  // largest float <= x (x finite or +-inf)
   float f = (float)x;
@@ -1122,18 +1122,19 @@ __device__ __forceinline__ float lower_f32(double x) {  // largest float <= x (x
 }
 __device__ __forceinline__ int shr1_f32i(float v) { return shr1_i32(__float_as_int(v)); }
 
-// NB = 16-query blocks per wave: 4 (64 queries, two pipelined halves, 2 waves/SIMD) or 2 (32
-// queries, one half, smaller register file: more waves per SIMD)
-template <int NB> struct Scan0fOcc;
-template <> struct Scan0fOcc<4> { static constexpr int waves = 2; };
-#ifndef HQ_NB2_WAVES
-#define HQ_NB2_WAVES 4
-#endif
-template <> struct Scan0fOcc<2> { static constexpr int waves = HQ_NB2_WAVES; };
-
-template <int NB>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB>::waves))) void k_scan0f(
-    Scan0Args a) {
+// One wave = 64 queries (4 blocks b of 16: lane (g, j) owns queries 16b + j) x one corpus chunk,
+// 16 candidates per step (lane group g owns rows 4g + r, r < 4, of the step: the MFMA D layout).
+// Candidate statistics come in the SoA-per-4-rows layout of hq_seg_pack0_split (std[4], mean[4],
+// msq[4], flag bits[4] per group of 4 rows), so the filter's packed f32 arithmetic runs over PAIRS OF
+// ROWS (r, r+1) of one query: G2 = acc.xy / acc.zw and the statistics pairs are register pairs, the
+// query constants are splats — no operand moves.  Per pair:
+//   E = base - T = fma(G, c1, 0.35 - T),  num = fma(G, qA cs, qB cm),  d = fma(E, den, num)
+//   pass <=> max(E, d) >= 0   (den = msq_q + msq_c >= 0; see filter_half)
+// T = thl - kMarginF; 0.35 - T is kept per query (k0) and refreshed only when a threshold moves.
+// The step loop is unrolled by two (ping-pong registers for the next step's fragments/statistics),
+// candidate pointers advance by a constant per step.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_scan0f(Scan0Args a) {
+  constexpr int NB = 4;
   constexpr int QW = 16 * NB;  // queries per wave
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   float* ls = reinterpret_cast<float*>(smem);         // QW x K approx scores
@@ -1153,7 +1154,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
 
   // queries: fragments, f32 constants, list thresholds (f32, exact list values)
   half8 qh[NB], ql[NB];  // query fragments: k range [8g, 8g + 8) of the hi and lo halves
-  float qA[NB], qB[NB], qQ[NB], thl[NB];
+  float qA[NB], qB[NB], qQ[NB], thl[NB], k0[NB];
   int qsp = 0;  // bit b: query 16b + j is flagged (zero variance / f32-unsafe)
   int qvb = 0;  // bit b: query 16b + j exists
 #pragma unroll
@@ -1164,16 +1165,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
     const _Float16* zr = a.Zq16 + (int64_t)qq * kZ16Row + 8 * g;
     qh[b] = *reinterpret_cast<const half8*>(zr);
     ql[b] = *reinterpret_cast<const half8*>(zr + 32);
-    const flt4 st = *reinterpret_cast<const flt4*>(a.Sq32 + (int64_t)qq * 4);
-    qA[b] = (float)(0.6 * a.inv_m) * st.x;
-    qB[b] = 0.6f * st.y;
-    qQ[b] = st.z;
-    if (v && __float_as_int(st.w) != 0) qsp |= 1 << b;
+    const int64_t gq = (int64_t)(qq >> 2) * 16 + (qq & 3);  // SoA-per-4 statistics
+    const float sd = a.Sq32[gq], mn = a.Sq32[gq + 4], ms = a.Sq32[gq + 8];
+    const int fl = __float_as_int(a.Sq32[gq + 12]);
+    qA[b] = (float)(0.6 * a.inv_m) * sd;
+    qB[b] = 0.6f * mn;
+    qQ[b] = ms;
+    if (v && fl != 0) qsp |= 1 << b;
     if (v) qvb |= 1 << b;
     double t0 = a.thr0;
     if (v && a.th0 && a.th0[q] > t0) t0 = a.th0[q];
     thl[b] = v ? lower_f32(t0) : __builtin_huge_valf();
   }
+  // k0 = 0.35 - (thl - margin); flagged queries always pass (+inf), absent ones never (-inf)
+  auto refresh_k0 = [&](const int b) {
+    k0[b] = ((qvb >> b) & 1) == 0 ? -__builtin_huge_valf()
+                                  : (((qsp >> b) & 1) != 0 ? __builtin_huge_valf() : 0.35f - (thl[b] - kMarginF));
+  };
+#pragma unroll
+  for (int b = 0; b < NB; ++b) refresh_k0(b);
   for (int i = lane; i < QW * K; i += 64) {
     ls[i] = -__builtin_huge_valf();
     li[i] = -1;
@@ -1181,15 +1191,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
   const bool myq = lane < QW && q0 + lane < a.Q;
 
   // candidate rows are padded (kPad0, hq_seg_pack0_split): no clamping, rows past c_end are masked
-  auto load_frag = [&](int64_t cs, half8* dst) {
-    const _Float16* p = a.Zc16 + (cs + j) * kZ16Row + 8 * g;
-    dst[0] = *reinterpret_cast<const half8*>(p);
-    dst[1] = *reinterpret_cast<const half8*>(p + 32);
+  struct CStep {
+    half8 f[2];   // fragment: hi, lo of row cs + j, k range [8g, 8g + 8)
+    flt4 sd, mn, ms;  // statistics of rows 4g .. 4g + 3
+    int fm;       // bit r: row 4g + r flagged (zero variance / f32-unsafe / pad)
   };
-  auto load_stats = [&](int64_t cs, flt4* dst) {
-    const flt4* p = reinterpret_cast<const flt4*>(a.Sc32) + cs + 4 * g;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dst[r] = p[r];
+  const _Float16* pz = a.Zc16 + (c_begin + j) * kZ16Row + 8 * g;
+  const float* pst = a.Sc32 + (c_begin / 4 + g) * 16;
+  auto load_step = [&](CStep& c) {
+    c.f[0] = *reinterpret_cast<const half8*>(pz);
+    c.f[1] = *reinterpret_cast<const half8*>(pz + 32);
+    c.sd = *reinterpret_cast<const flt4*>(pst);
+    c.mn = *reinterpret_cast<const flt4*>(pst + 4);
+    c.ms = *reinterpret_cast<const flt4*>(pst + 8);
+    const flt4 fl = *reinterpret_cast<const flt4*>(pst + 12);
+    c.fm = (int)(__float_as_int(fl.x) != 0) | ((int)(__float_as_int(fl.y) != 0) << 1) |
+           ((int)(__float_as_int(fl.z) != 0) << 2) | ((int)(__float_as_int(fl.w) != 0) << 3);
+    pz += kCS * kZ16Row;
+    pst += kCS * 4;
   };
   // G of two 16-query blocks: hi.hi + hi.lo + lo.hi, two accumulation chains interleaved
   auto mfma_half = [&](const int h, const half8* f, flt4* acc) {
@@ -1203,54 +1222,48 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
     for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[1], qh[2 * h + u], acc[u], 0, 0, 0);
   };
   // f32 filter of one half; bit 4u + r = pass of pair (query 16(2h+u)+j, row 4g+r).
-  // pass <=> th - base <= 0 or num >= (th - base) den  <=>  max(-R, num - R den) >= 0 with
-  // R = (th - margin) - base, where num - R den is one fma (its sign is exact).  The two queries of
-  // a half share the candidate statistics, so the arithmetic runs as packed f32 (v_pk_fma/mul/add)
-  // over the query pair.  Flagged queries get th = -inf (always pass), absent ones +inf (never);
-  // flagged candidates, absent queries and rows past the chunk end are applied as bit masks, only
-  // when some lane of the wave has a candidate pass (the common step ends after one ballot).
-  auto filter_half = [&](const int h, const flt4* acc, const flt4* cst, const int rem, const int fcm) -> int {
-    const int b0 = 2 * h, b1 = 2 * h + 1;
-    auto tq = [&](int b) {
-      return ((qvb >> b) & 1) == 0 ? __builtin_huge_valf()
-                                   : (((qsp >> b) & 1) != 0 ? -__builtin_huge_valf() : thl[b] - kMarginF);
-    };
-    const flt2 T2 = {tq(b0), tq(b1)};
-    const flt2 A2 = {qA[b0], qA[b1]}, B2 = {qB[b0], qB[b1]}, Q2 = {qQ[b0], qQ[b1]};
-    const flt2 c1v = {c1f, c1f}, k35 = {0.35f, 0.35f};
-    flt2 m[4];
+  // pass <=> base >= T or base + num / den >= T  <=>  max(E, E den + num) >= 0 with E = base - T
+  // (den > 0; E den + num is one fma, its sign exact).  Flagged candidates, absent queries and rows
+  // past the chunk end are bit masks, applied only when some lane of the wave has a candidate pass
+  // (the common half-step ends after one ballot).
+  auto filter_half = [&](const int h, const flt4* acc, const CStep& c, const int rem) -> int {
+    const flt2 c1v = {c1f, c1f};
+    flt2 m[4];  // [2u + p]: rows (2p, 2p + 1) of query block 2h + u
     float mx = -__builtin_huge_valf();
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const flt2 G2 = {acc[0][r], acc[1][r]};
-      const flt2 X2 = A2 * cst[r].x;
-      const flt2 Y2 = B2 * cst[r].y;
-      const flt2 num = __builtin_elementwise_fma(G2, X2, Y2);
-      const flt2 den = Q2 + cst[r].z;
-      const flt2 R = T2 - __builtin_elementwise_fma(G2, c1v, k35);
-      const flt2 d = __builtin_elementwise_fma(-R, den, num);
-      m[r] = flt2{fmaxf(-R.x, d.x), fmaxf(-R.y, d.y)};
-      mx = fmaxf(mx, fmaxf(m[r].x, m[r].y));
+    for (int u = 0; u < 2; ++u) {
+      const int b = 2 * h + u;
+      const flt2 K0 = {k0[b], k0[b]}, A2 = {qA[b], qA[b]}, B2 = {qB[b], qB[b]}, Q2 = {qQ[b], qQ[b]};
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const flt2 G2 = p == 0 ? acc[u].xy : acc[u].zw;
+        const flt2 sd2 = p == 0 ? c.sd.xy : c.sd.zw;
+        const flt2 mn2 = p == 0 ? c.mn.xy : c.mn.zw;
+        const flt2 ms2 = p == 0 ? c.ms.xy : c.ms.zw;
+        const flt2 E = __builtin_elementwise_fma(G2, c1v, K0);
+        const flt2 num = __builtin_elementwise_fma(G2, A2 * sd2, B2 * mn2);
+        const flt2 d = __builtin_elementwise_fma(E, Q2 + ms2, num);
+        const flt2 mm = {fmaxf(E.x, d.x), fmaxf(E.y, d.y)};
+        m[2 * u + p] = mm;
+        mx = fmaxf(mx, fmaxf(mm.x, mm.y));
+      }
     }
-    if (!__ballot((mx >= 0.0f) | (fcm != 0))) return 0;
+    if (!__ballot((mx >= 0.0f) | (c.fm != 0))) return 0;
     int bits = 0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bits |= ((int)(m[r].x >= 0.0f) << r) | ((int)(m[r].y >= 0.0f) << (4 + r));
-    bits |= fcm * 0x11;
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        bits |= ((int)(m[2 * u + p].x >= 0.0f) << (4 * u + 2 * p)) | ((int)(m[2 * u + p].y >= 0.0f) << (4 * u + 2 * p + 1));
+    bits |= c.fm * 0x11;
     const int nv = rem - 4 * g;  // rows of this lane group inside the chunk
     const int rowm = nv >= 4 ? 0xF : (nv <= 0 ? 0 : (1 << nv) - 1);
+    const int b0 = 2 * h, b1 = 2 * h + 1;
     const int qm = (((qvb >> b0) & 1) ? 0x0F : 0) | (((qvb >> b1) & 1) ? 0xF0 : 0);
     return bits & (rowm * 0x11) & qm;
   };
-  // bit r: candidate row 4g + r is flagged (zero variance / f32-unsafe / pad)
-  auto flag_mask = [&](const flt4* cst) {
-    int f = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) f |= (int)(__float_as_int(cst[r].w) != 0) << r;
-    return f;
-  };
   // List maintenance.  A query's list starts in APPEND mode: passing pairs are appended in parallel
-  // (LDS atomic slot, no ordering) while the list has room; the pair that fills it sorts it (rank
+  // (slot from the ballot, no ordering) while the list has room; the pair that fills it sorts it (rank
   // sort), sets the query's threshold to its K-th score and switches it to SORTED mode, where later
   // pairs are merged one at a time.  With the sampled starting thresholds most queries never leave
   // append mode within a chunk.  cntr[b] counts the pairs ever offered (>= K: sorted mode); the slots
@@ -1277,7 +1290,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
     if (j == (qi & 15)) {
 #pragma unroll
       for (int bb = 0; bb < NB; ++bb)
-        if (bb == b) thl[bb] = tau > thl[bb] ? tau : thl[bb];
+        if (bb == b && tau > thl[bb]) {
+          thl[bb] = tau;
+          refresh_k0(bb);
+        }
     }
     if (lane == 0 && tau > 0.0f) atomicMax(a.gtau + q0 + qi, (unsigned long long)__double_as_longlong((double)tau));
   };
@@ -1300,7 +1316,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
   };
   // score, test and file the passing pairs of one half: f32 for plain pairs (the filter's expression
   // with the division), f64 statistics for flagged pairs
-  auto insert_half = [&](const int h, const flt4* acc, const flt4* cst, const int64_t cs, const int bits) {
+  auto insert_half = [&](const int h, const flt4* acc, const CStep& c, const int64_t cs, const int bits) {
     if (a.expt == 3 && lane == 0) atomicAdd(a.dbg, 1ull);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -1308,13 +1324,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
       for (int r = 0; r < 4; ++r) {
         const int b = 2 * h + u;
         const bool pb = (bits >> (4 * u + r)) & 1;
-        if (!__ballot(pb)) continue;
+        const unsigned long long mpb = __ballot(pb);
+        if (!mpb) continue;
+        if (a.expt == 3 && lane == 0) {
+          atomicAdd(a.dbg + 3, (unsigned long long)__popcll(mpb));
+          atomicAdd(a.dbg + 4, 1ull);
+        }
         float s = -__builtin_huge_valf();
-        const bool flagged = (((qsp >> b) & 1) != 0) | (__float_as_int(cst[r].w) != 0);
+        const bool flagged = (((qsp >> b) & 1) != 0) | (((c.fm >> r) & 1) != 0);
         if (pb && !flagged) {
           const float G = acc[u][r];
-          const float num = fmaf(G, qA[b] * cst[r].x, qB[b] * cst[r].y);
-          float t = num * __builtin_amdgcn_rcpf(qQ[b] + cst[r].z);  // 1 ulp
+          const float num = fmaf(G, qA[b] * c.sd[r], qB[b] * c.mn[r]);
+          float t = num * __builtin_amdgcn_rcpf(qQ[b] + c.ms[r]);  // 1 ulp
           t = t > 0.0f ? t : 0.0f;
           s = fmaf(G, c1f, 0.35f) + t;
           s = s < 1.0f ? s : 1.0f;
@@ -1323,9 +1344,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
         if (__ballot(pb && flagged)) {
           if (pb && flagged) {
             const int q = q0 + 16 * b + j;
-            const int64_t c = cs + 4 * g + r;
             const double* sq = a.Sq + (int64_t)q * a.nseg * 4;
-            const double* sc = a.Sc + c * a.nseg * 4;
+            const double* sc = a.Sc + (cs + 4 * g + r) * a.nseg * 4;
             const double qm = sq[0], qs = sq[1], qq = sq[2], cm = sc[0], csd = sc[1], cq = sc[2];
             const double v = (qs == 0.0 || csd == 0.0)
                                  ? const0(qs == 0.0, csd == 0.0, qm, cm, (aux_bits(sq) & aux_bits(sc) & kAuxF32) != 0)
@@ -1334,10 +1354,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
           }
         }
         const bool ok = pb && s >= thl[b];
-        if (a.expt == 3 && lane == 0) atomicAdd(a.dbg + 1, (unsigned long long)__popcll(__ballot(ok)));
         const int qi = 16 * b + j;
         const int id = (int)(cs + 4 * g + r);
         const unsigned long long mok = __ballot(ok);
+        if (a.expt == 3 && lane == 0) atomicAdd(a.dbg + 1, (unsigned long long)__popcll(mok));
         const unsigned long long mine = (mok >> j) & 0x0001000100010001ull;  // query j's pairs, bit 16g
         const int pos = cntr[b] + __popcll(mine & ((1ull << (16 * g)) - 1ull));
         cntr[b] += __popcll(mine);
@@ -1368,53 +1388,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Scan0fOcc<NB
       }
   };
 
-  // Software pipeline.  NB = 4: the MFMAs of one half run while the VALU filters the other half
-  //   block A: MFMA(step i, half 1) || filter(step i, half 0)
+  // Software pipeline: the MFMAs of one half run while the VALU filters the other half
+  //   block A: MFMA(step i, half 1)   || filter(step i, half 0)
   //   block B: MFMA(step i+1, half 0) || filter(step i, half 1)
-  // NB = 2: MFMA(step i) then filter(step i); the other waves of the SIMD fill the gaps.
-  half8 cf[2];
-  flt4 cst[4];
-  load_frag(c_begin, cf);
-  load_stats(c_begin, cst);
+  CStep cA, cB;
+  load_step(cA);
   flt4 acc0[2], acc1[2];
-  if constexpr (NB == 4) mfma_half(0, cf, acc0);
+  mfma_half(0, cA.f, acc0);
   unsigned long long gt_bits = 0ull;
   int step = 0;
-  for (int64_t cs = c_begin; cs < c_end; cs += kCS, ++step) {
+  auto body = [&](const int64_t cs, const CStep& cur, CStep& nxt) {
+    load_step(nxt);  // rows past the chunk (padded array): harmless, masked
     const int rem = (int)(c_end - cs);
-    half8 cf1[2];
-    flt4 cstn[4];
-    load_frag(cs + kCS, cf1);
-    load_stats(cs + kCS, cstn);
-    const int fcm = flag_mask(cst);
-    if constexpr (NB == 4) {
-      mfma_half(1, cf, acc1);
-      const int bits0 = filter_half(0, acc0, cst, rem, fcm);
-      if (__ballot(bits0 != 0)) insert_half(0, acc0, cst, cs, bits0);
-      mfma_half(0, cf1, acc0);
-      const int bits1 = filter_half(1, acc1, cst, rem, fcm);
-      if (__ballot(bits1 != 0)) insert_half(1, acc1, cst, cs, bits1);
-    } else {
-      mfma_half(0, cf, acc0);
-      const int bits0 = filter_half(0, acc0, cst, rem, fcm);
-      if (__ballot(bits0 != 0)) insert_half(0, acc0, cst, cs, bits0);
-    }
-    cf[0] = cf1[0];
-    cf[1] = cf1[1];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) cst[r] = cstn[r];
+    mfma_half(1, cur.f, acc1);
+    const int bits0 = filter_half(0, acc0, cur, rem);
+    if (__ballot(bits0 != 0)) insert_half(0, acc0, cur, cs, bits0);
+    mfma_half(0, nxt.f, acc0);
+    const int bits1 = filter_half(1, acc1, cur, rem);
+    if (__ballot(bits1 != 0)) insert_half(1, acc1, cur, cs, bits1);
     if ((step & 3) == 0) {
       if (gt_bits != 0ull) {
         const float gf = (float)__longlong_as_double((long long)gt_bits);  // exact: list values are f32
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
           const float v = __shfl(gf, 16 * b + j, 64);
-          thl[b] = v > thl[b] ? v : thl[b];
+          if (v > thl[b]) {
+            thl[b] = v;
+            refresh_k0(b);
+          }
         }
       }
       if (myq) gt_bits = __atomic_load_n(a.gtau + q0 + lane, __ATOMIC_RELAXED);
     }
+    ++step;
+  };
+  int64_t cs = c_begin;
+  for (; cs + kCS < c_end; cs += 2 * kCS) {
+    body(cs, cA, cB);
+    body(cs + kCS, cB, cA);
   }
+  if (cs < c_end) body(cs, cA, cB);
 
   // hand the lists (unordered is fine) to the per-query pools: one atomic per query, lane-parallel
   int nl = 0;  // entries of query `lane`
@@ -1571,11 +1584,11 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
     const _Float16* zr = a.Zq16 + (int64_t)qq * kZ16Row + 8 * g;
     qh[b] = *reinterpret_cast<const half8*>(zr);
     ql[b] = *reinterpret_cast<const half8*>(zr + 32);
-    const flt4 st = *reinterpret_cast<const flt4*>(a.Sq32 + (int64_t)qq * 4);
-    qA[b] = (float)(0.6 * a.inv_m) * st.x;
-    qB[b] = 0.6f * st.y;
-    qQ[b] = st.z;
-    if (v && __float_as_int(st.w) == 0) qok |= 1 << b;
+    const int64_t gq = (int64_t)(qq >> 2) * 16 + (qq & 3);  // SoA-per-4 statistics
+    qA[b] = (float)(0.6 * a.inv_m) * a.Sq32[gq];
+    qB[b] = 0.6f * a.Sq32[gq + 4];
+    qQ[b] = a.Sq32[gq + 8];
+    if (v && __float_as_int(a.Sq32[gq + 12]) == 0) qok |= 1 << b;
   }
   __syncthreads();
   auto row_of = [&](int64_t i) -> int64_t { return (i < a.S ? i : a.S - 1) * a.stride; };
@@ -1589,9 +1602,13 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
   float cut[4] = {-1.0f, -1.0f, -1.0f, -1.0f};  // per query: scores below need no counting
   int step = 0;
   for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
-    flt4 cst[4];
+    flt4 cst[4];  // (std, mean, msq, flags) of rows 4g + r
 #pragma unroll
-    for (int r = 0; r < 4; ++r) cst[r] = reinterpret_cast<const flt4*>(a.Sc32)[row_of(cs + 4 * g + r)];
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = row_of(cs + 4 * g + r);
+      const float* p = a.Sc32 + (row >> 2) * 16 + (row & 3);
+      cst[r] = flt4{p[0], p[4], p[8], p[12]};
+    }
     half8 cfn[2];
     load_frag(cs + kCS, cfn);
     flt4 acc[4];
@@ -1762,7 +1779,17 @@ __global__ __launch_bounds__(64) void k_progressive_final(int R, int Q, int M, i
     };
     load_head();
     int n = 0;
-    for (; n < M; ++n) {
+    if (R == 1) {
+      // one list: it is already the (score desc, id asc) order; its valid entries come first
+      for (int i = lane; i < M; i += 64) {
+        const bool v = ids[(int64_t)q * M + i] >= 0;
+        const unsigned long long m = __ballot(v);
+        n += __popcll(m);
+        if (v) sel[i] = i;
+      }
+      n = __builtin_amdgcn_readfirstlane(n);
+    }
+    for (; R > 1 && n < M; ++n) {
       double bs = hs;
       int64_t bid = hid;
       int bl = lane;
@@ -1815,13 +1842,24 @@ __global__ __launch_bounds__(64) void k_progressive_final(int R, int Q, int M, i
       const int64_t rq = (int64_t)(v >> 16) * Q + q;
       return fb_id >= 0 ? rq : rq * M + (v & 0xFFFF);
     };
+    // stable rank of survivor i: ranks from register copies of the overall scores (n <= 64 here:
+    // M <= 64 on the fused path; larger n re-reads the rows)
+    double ovl = -__builtin_huge_val();
+    if (lane < n) ovl = rowbase[row_of(sel[lane]) * W];
     for (int i = lane; i < n; i += 64) {
       const int64_t oi = row_of(sel[i]);
       const double ovi = rowbase[oi * W];
       int rank = 0;
-      for (int jj = 0; jj < n; ++jj) {
-        const double ovj = rowbase[row_of(sel[jj]) * W];
-        rank += (ovj > ovi || (ovj == ovi && jj < i)) ? 1 : 0;
+      if (n <= 64) {
+        for (int jj = 0; jj < n; ++jj) {
+          const double ovj = rl_f64(ovl, jj);
+          rank += (ovj > ovi || (ovj == ovi && jj < i)) ? 1 : 0;
+        }
+      } else {
+        for (int jj = 0; jj < n; ++jj) {
+          const double ovj = rowbase[row_of(sel[jj]) * W];
+          rank += (ovj > ovi || (ovj == ovi && jj < i)) ? 1 : 0;
+        }
       }
       if (rank < K) {
         out_id[(int64_t)q * K + rank] = fb_id >= 0 ? fb_id : ids[oi];
@@ -1920,7 +1958,8 @@ __global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int6
                                                const double* __restrict__ cs, const int64_t* __restrict__ cid, int kp,
                                                int k, double thr, int thr_mode, double eps, int64_t id_base,
                                                double* __restrict__ os, int64_t* __restrict__ oid,
-                                               int* __restrict__ ocnt, int* __restrict__ ores) {
+                                               int* __restrict__ ocnt, int* __restrict__ ores, int count_empty,
+                                               int* __restrict__ oredo) {
   __shared__ double es[kMaxTopK];
   __shared__ int64_t ei[kMaxTopK];
   const int lane = threadIdx.x;
@@ -1941,36 +1980,41 @@ __global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int6
       ei[lane] = id;
     }
     __syncthreads();
+    // rank of each valid entry by (score desc, id asc) among the valid ones (kp <= 64: one lane each)
+    const double e = lane < kp ? es[lane] : -__builtin_huge_val();
+    const int64_t id = lane < kp ? ei[lane] : -1;
+    const bool valid = id >= 0;
+    const int n = __popcll(__ballot(valid));
+    int rank = 0;
+    for (int o = 0; o < kp; ++o) {
+      const double so = rl_f64(e, o);
+      const long long io = __double_as_longlong(rl_f64(__longlong_as_double((long long)id), o));
+      rank += (io >= 0 && (so > e || (so == e && io < id))) ? 1 : 0;
+    }
+    const int cnt = n < k ? n : k;
+    if (valid && rank < k) {
+      os[(int64_t)q * k + rank] = e;
+      oid[(int64_t)q * k + rank] = id;
+    }
+    for (int j = cnt + lane; j < k; j += 64) {
+      os[(int64_t)q * k + j] = -__builtin_huge_val();
+      oid[(int64_t)q * k + j] = -1;
+    }
+    // k-th exact score (the entry of rank k - 1)
+    const unsigned long long mk = __ballot(valid && rank == k - 1);
+    const double kth = mk ? rl_f64(e, __builtin_ctzll(mk)) : -__builtin_huge_val();
     if (lane == 0) {
-      int n = 0;
-      for (int j = 0; j < kp; ++j) {  // compact valid entries, then insertion sort
-        if (ei[j] < 0) continue;
-        double s = es[j];
-        int64_t id = ei[j];
-        int p = n++;
-        while (p > 0 && better(s, id, es[p - 1], ei[p - 1])) {
-          es[p] = es[p - 1];
-          ei[p] = ei[p - 1];
-          --p;
-        }
-        es[p] = s;
-        ei[p] = id;
-      }
-      const int cnt = n < k ? n : k;
-      for (int j = 0; j < k; ++j) {
-        os[(int64_t)q * k + j] = j < cnt ? es[j] : -__builtin_huge_val();
-        oid[(int64_t)q * k + j] = j < cnt ? ei[j] : -1;
-      }
       ocnt[q] = cnt;
       const bool full = cid[base + kp - 1] >= 0;
       int res = 1;
       if (full) {
         const double bound = cs[base + kp - 1] + eps;
-        if (n >= k) res = bound < es[k - 1];
+        if (n >= k) res = bound < kth;
         else if (thr_mode == 0) res = 0;
         else res = thr_mode == 1 ? (bound < thr) : (bound <= thr);
       }
       ores[q] = res;
+      if (oredo && (res == 0 || (count_empty && cnt == 0))) atomicAdd(oredo, 1);
     }
     __syncthreads();
   }
@@ -2023,12 +2067,6 @@ static void scan_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& chu
   chunk_len = (N + nchunks - 1) / nchunks;
   chunk_len = ((chunk_len + kCB - 1) / kCB) * kCB;
   if (chunk_len < kCB) chunk_len = kCB;
-}
-
-// 16-query blocks per wave of the split level-0 scan (HQ_SCAN_NB = 2 or 4)
-static int scan0_nb() {
-  const char* e = getenv("HQ_SCAN_NB");
-  return (e && atoi(e) == 2) ? 2 : 4;
 }
 
 // k_scan0: ~16 resident waves per CU-pair of rounds; nchunks multiple of 8 (XCD mapping), <= 512
@@ -2088,12 +2126,9 @@ static int launch_sample(const SampleArgs& a, hipStream_t s) {
 template <int KS, bool F32>
 static int launch_scan0(const Scan0Args& a, hipStream_t s) {
   if constexpr (F32) {
-    const int nb = scan0_nb();
-    const size_t lds = (size_t)16 * nb * a.K * 8;
-    const void* fn = nb == 2 ? (const void*)k_scan0f<2> : (const void*)k_scan0f<4>;
-    HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    if (nb == 2) hipLaunchKernelGGL(k_scan0f<2>, dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
-    else hipLaunchKernelGGL(k_scan0f<4>, dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
+    const size_t lds = (size_t)kQW * a.K * 8;
+    HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_scan0f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_scan0f, dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
     HQ_CHECK_LAUNCH();
     return HQ_OK;
   }
@@ -2154,23 +2189,26 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     HQ_CHECK_HIP(hipMemsetAsync(dbg, 0, 64, s));
   }
   b.dbg = dbg;
-  scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len, f32 ? 16 * scan0_nb() : kQW);
+  scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len);
   uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
   b.ws_score = reinterpret_cast<double*>(ws);
   b.ws_id = reinterpret_cast<int64_t*>(ws + (size_t)b.nchunks * Q * k * 8);
-  b.gtau = reinterpret_cast<unsigned long long*>(ws + (size_t)b.nchunks * Q * k * 16);
-  HQ_CHECK_HIP(hipMemsetAsync(b.gtau, 0, sizeof(unsigned long long) * Q, s));
-  unsigned int* hist = reinterpret_cast<unsigned int*>(ws + (size_t)b.nchunks * Q * k * 16 + (size_t)Q * 8);
-  double* th0 = reinterpret_cast<double*>(ws + (size_t)b.nchunks * Q * k * 16 + (size_t)Q * 8 +
-                                          (size_t)Q * kBins * 4);
+  // [lists / pools][gtau Q x 8][hist Q x kBins x 4][pool_n Q x 4][th0 Q x 8]: the three zeroed
+  // regions are adjacent, so one memset clears them
+  const size_t lists = (size_t)b.nchunks * Q * k * 16;
+  b.gtau = reinterpret_cast<unsigned long long*>(ws + lists);
+  unsigned int* hist = reinterpret_cast<unsigned int*>(ws + lists + (size_t)Q * 8);
+  b.pool_n = reinterpret_cast<int*>(ws + lists + (size_t)Q * 8 + (size_t)Q * kBins * 4);
+  double* th0 = reinterpret_cast<double*>(ws + lists + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 4);
   b.th0 = nullptr;
   // f32 path: per-query pools in the list area (cap = nchunks * k entries, never overflows)
   b.pool_cap = b.nchunks * k;
   b.pool_s = reinterpret_cast<float*>(ws);
   b.pool_i = reinterpret_cast<int*>(ws + (size_t)Q * b.pool_cap * 4);
-  b.pool_n = reinterpret_cast<int*>(ws + (size_t)b.nchunks * Q * k * 16 + (size_t)Q * 8 + (size_t)Q * kBins * 4 +
-                                    (size_t)Q * 8);
-  if (f32) HQ_CHECK_HIP(hipMemsetAsync(b.pool_n, 0, sizeof(int) * Q, s));
+  const bool sample = getenv("HQ_SCAN_NOSAMPLE") == nullptr;
+  HQ_CHECK_HIP(hipMemsetAsync(b.gtau, 0, (size_t)Q * 8 + (sample ? (size_t)Q * kBins * 4 : 0) + (f32 ? (size_t)Q * 4 : 0),
+                              s));
+  if (f32 && !sample) HQ_CHECK_HIP(hipMemsetAsync(b.pool_n, 0, sizeof(int) * Q, s));
   int rc;
   if (getenv("HQ_SCAN_NOSAMPLE") == nullptr) {
     SampleArgs sa;
@@ -2180,7 +2218,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     sample_geometry(Q, N, sa.stride, sa.S, sa.nqb, sa.nchunks, sa.chunk_len);
     sa.hist = hist;
     sa.K = k;
-    HQ_CHECK_HIP(hipMemsetAsync(hist, 0, sizeof(unsigned int) * kBins * Q, s));
+
     rc = f32 ? scan0_dispatch<true>(ks, b, &sa, s) : scan0_dispatch<false>(ks, b, &sa, s);
     if (rc) return rc;
     hipLaunchKernelGGL(k_hist_tau, dim3((Q + 255) / 256), dim3(256), 0, s, (const unsigned int*)hist, Q, k,
@@ -2197,11 +2235,11 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     HQ_CHECK_LAUNCH();
   }
   if (b.expt == 3) {
-    unsigned long long h[3];
+    unsigned long long h[5];
     HQ_CHECK_HIP(hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, s));
     HQ_CHECK_HIP(hipStreamSynchronize(s));
-    fprintf(stderr, "k_scan0f: waves %d, insert entries %llu, passing pairs %llu, list inserts %llu\n",
-            b.nqb * b.nchunks, h[0], h[1], h[2]);
+    fprintf(stderr, "k_scan0f: waves %d, insert entries %llu, passing pairs %llu, list inserts %llu, filter passes "
+            "%llu in %llu (u, r) iterations\n", b.nqb * b.nchunks, h[0], h[1], h[2], h[3], h[4]);
   }
   if (!f32) {
     int mg = Q < 4096 ? Q : 4096;
@@ -2214,30 +2252,36 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
 }
 
 // Split-f16 level-0 copies for the default scan: Z16 [N + kPad0, 64] = (hi[32], lo[32]) of the
-// level-0 segment zero-padded to 32, and S32 [N + kPad0, 4] = (std, mean, msq, flag bits: 1 zero
-// variance, 2 msq outside [2^-60, 2^60], 4 pad row).  k_scan0f reads up to 31 rows past a step start.
+// level-0 segment zero-padded to 32, and S32 = per-row (std, mean, msq, flag bits: 1 zero variance,
+// 2 msq outside [2^-60, 2^60], 4 pad row) in SoA groups of 4 rows: group G = rows 4G .. 4G + 3 holds
+// std[4], mean[4], msq[4], flags[4] (16 floats), for the rows [0, round_up(N, 4) + kPad0).  k_scan0f
+// reads up to 31 rows past a step start.
+__host__ __device__ __forceinline__ int64_t pack0_rows(int64_t N) { return ((N + 3) & ~int64_t(3)) + kPad0; }
+
 __global__ void k_pack0(const double* __restrict__ Z, const double* __restrict__ S, int64_t N, int Lp, int P0,
                         int nseg, _Float16* __restrict__ Z16, float* __restrict__ S32) {
-  const int64_t rows = N + kPad0;
+  const int64_t rows = pack0_rows(N);
   const int64_t total = rows * 32;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = t / 32;
     const int c = (int)(t % 32);
-    const double z = (r < N && c < P0) ? Z[r * Lp + c] : 0.0;
-    const _Float16 hi = (_Float16)z;
-    const _Float16 lo = (_Float16)(z - (double)hi);
-    Z16[r * kZ16Row + c] = hi;
-    Z16[r * kZ16Row + 32 + c] = lo;
+    if (r < N + kPad0) {
+      const double z = (r < N && c < P0) ? Z[r * Lp + c] : 0.0;
+      const _Float16 hi = (_Float16)z;
+      const _Float16 lo = (_Float16)(z - (double)hi);
+      Z16[r * kZ16Row + c] = hi;
+      Z16[r * kZ16Row + 32 + c] = lo;
+    }
     if (c == 0) {
-      float* o = S32 + r * 4;
+      float* o = S32 + (r >> 2) * 16 + (r & 3);
       if (r < N) {
         const double* st = S + r * nseg * 4;
         const double sd = st[1], mean = st[0], msq = st[2];
         int flag = sd == 0.0 ? 1 : 0;
         if (!(msq >= 0x1p-60 && msq <= 0x1p60)) flag |= 2;
-        o[0] = (float)sd; o[1] = (float)mean; o[2] = (float)msq; o[3] = __int_as_float(flag);
+        o[0] = (float)sd; o[4] = (float)mean; o[8] = (float)msq; o[12] = __int_as_float(flag);
       } else {
-        o[0] = 0.0f; o[1] = 0.0f; o[2] = 1.0f; o[3] = __int_as_float(4);
+        o[0] = 0.0f; o[4] = 0.0f; o[8] = 1.0f; o[12] = __int_as_float(4);
       }
     }
   }
@@ -2317,7 +2361,8 @@ int hq_level_scores(const double* Rq, const double* Zq, const double* Sq, int Q,
 int hq_refine_topk(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc, const double* Zc,
                    const double* Sc, int64_t N, int L, int mode, const double* cand_score, const int64_t* cand_id,
                    int kp, int k, double threshold, int thr_mode, double eps, int64_t id_base, double* out_score,
-                   int64_t* out_id, int* out_count, int* out_resolved, hq_stream_t stream) {
+                   int64_t* out_id, int* out_count, int* out_resolved, int count_empty, int* out_redo,
+                   hq_stream_t stream) {
   if (Q < 0 || N < 0 || L <= 0 || kp <= 0 || kp > kMaxTopK || k <= 0 || k > kp)
     return fail(HQ_E_INVALID, "bad sizes kp=%d k=%d", kp, k);
   if (Q == 0) return HQ_OK;
@@ -2327,9 +2372,10 @@ int hq_refine_topk(const double* Rq, const double* Zq, const double* Sq, int Q, 
   SegInfo si;
   seg_info(L, si);
   int grid = Q < 8192 ? Q : 8192;
+  if (out_redo) HQ_CHECK_HIP(hipMemsetAsync(out_redo, 0, sizeof(int), (hipStream_t)stream));
   hipLaunchKernelGGL(k_refine, dim3(grid), dim3(64), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
                      VecSet{Rc, Zc, Sc}, N, si, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base,
-                     out_score, out_id, out_count, out_resolved);
+                     out_score, out_id, out_count, out_resolved, count_empty ? 1 : 0, out_redo);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
@@ -2421,7 +2467,7 @@ int hq_seg_pack0_split(const double* Z, const double* S, int64_t N, int L, void*
   seg_info(L, si);
   if (si.nseg == 0) return fail(HQ_E_INVALID, "no level structure for L=%d", L);
   if (si.plen[0] > 32) return fail(HQ_E_UNSUPPORTED, "level-0 segment of %d values (<= 32)", si.plen[0]);
-  int64_t blocks = ((N + kPad0) * 32 + 255) / 256;
+  int64_t blocks = (pack0_rows(N) * 32 + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(k_pack0, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, Z, S, N, si.Lp, si.plen[0],
                      si.nseg, reinterpret_cast<_Float16*>(Z16), S32);

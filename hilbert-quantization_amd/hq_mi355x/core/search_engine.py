@@ -240,22 +240,34 @@ class IndexCorpus:
             oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
             return oid, odet[..., 0], odet[..., 1:], ocnt
         threshold = self._thr(qp, threshold, 1)
-        s0, ids, cnt, res = self._scan_refine(qp, 0, M, float(threshold), 1)
+        nredo = self._redo_counter(qp.Z.device)
+        s0, ids, cnt, res = self._scan_refine(qp, 0, M, float(threshold), 1, nredo)
         # no arg-max on this path: a query where nothing passed (count 0) is recomputed by the dense path
         # below, so the fallback slot is a constant (-inf, id -1, zero re-scores) kept per batch size
         best, bid, bdet = self._no_fallback(Q, qp.Z.device)
         oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out, bdet)
-        redo = (res == 0) | (cnt == 0)
         forced = self._forced(qp)
-        if forced is not None:
-            redo = redo | forced
-        if bool(redo.any()):
+        # the one host sync: k_refine counted the unresolved / empty queries on the device
+        if forced is not None or int(nredo.item()) > 0:
+            redo = (res == 0) | (cnt == 0)
+            if forced is not None:
+                redo = redo | forced
             sel = t.nonzero(redo).view(-1)
-            s2, i2, b2, bi2 = self._dense(qp, sel, 0, M, float(threshold), 1)
-            sub = qp.rows(sel)
-            o2, d2, c2 = self._final(sub, s2, i2, b2, bi2, K_out)
-            oid[sel], odet[sel], ocnt[sel] = o2, d2, c2
+            if sel.numel():
+                s2, i2, b2, bi2 = self._dense(qp, sel, 0, M, float(threshold), 1)
+                sub = qp.rows(sel)
+                o2, d2, c2 = self._final(sub, s2, i2, b2, bi2, K_out)
+                oid[sel], odet[sel], ocnt[sel] = o2, d2, c2
         return oid, odet[..., 0], odet[..., 1:], ocnt
+
+    def _redo_counter(self, dev):
+        """Device int32 [1] the exact re-rank sets to the number of queries needing the dense path."""
+        t = torch()
+        cache = self.__dict__.setdefault("_redo", {})
+        key = (str(dev), K.stream())
+        if key not in cache:
+            cache[key] = t.zeros(1, dtype=t.int32, device=dev)
+        return cache[key]
 
     def _no_fallback(self, Q: int, dev):
         t = torch()
@@ -267,11 +279,13 @@ class IndexCorpus:
                           t.zeros((Q, 1 + self.nseg), dtype=t.float64, device=dev))
         return cache[key]
 
-    def _scan_refine(self, qp, mode: int, k: int, thr: float, thr_mode: int):
-        """Fused scan (SLACK extra list entries) + exact re-rank; resolved[q] == 0 marks an unproven list."""
+    def _scan_refine(self, qp, mode: int, k: int, thr: float, thr_mode: int, nredo=None):
+        """Fused scan (SLACK extra list entries) + exact re-rank; resolved[q] == 0 marks an unproven list.
+        nredo: device counter of queries needing the dense path (unresolved or nothing passed)."""
         lo_mode = 0 if thr_mode == 0 else 1
         asc, aid, _, _ = K.scan_topk(qp, self.prep, mode, k + self.SLACK, thr - self.EPS, lo_mode, self.id_base)
-        return K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, thr_mode, self.EPS, self.id_base)
+        return K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, thr_mode, self.EPS, self.id_base, redo=nredo,
+                             count_empty=True)
 
     def _final(self, qp, s0, ids, best, bid, K_out: int, bdet=None):
         """Exact overall + per-level re-score of the survivors and of the arg-max, then the final ranking."""

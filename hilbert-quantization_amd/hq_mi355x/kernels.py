@@ -288,7 +288,7 @@ def pack0(p: Prepared, exc=None) -> Prepared:
     if int(_L().hq_seg_level0_len(p.L)) > 32:
         return p
     p.Z16 = t.empty((p.N + PAD0, 64), dtype=t.float16, device=p.Z.device)
-    p.S32 = t.empty((p.N + PAD0, 4), dtype=t.float32, device=p.Z.device)
+    p.S32 = t.empty(((p.N + 3) // 4 * 4 + PAD0, 4), dtype=t.float32, device=p.Z.device)  # SoA groups of 4 rows
     _chk(_L().hq_seg_pack0_split(ptr(p.Z), ptr(p.S), p.N, p.L, ptr(p.Z16), ptr(p.S32), stream()), exc)
     return p
 
@@ -345,8 +345,10 @@ def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.
 
 
 def refine_topk(q: Prepared, c: Prepared, mode: int, cand_score, cand_id, k: int, threshold: float = 0.0,
-                thr_mode: int = 0, eps: float = 1e-9, id_base: int = 0, exc=None):
-    """Exact re-rank of a scan list -> (scores [Q, k], ids [Q, k], count [Q], resolved [Q])."""
+                thr_mode: int = 0, eps: float = 1e-9, id_base: int = 0, exc=None, redo=None, count_empty: bool = False):
+    """Exact re-rank of a scan list -> (scores [Q, k], ids [Q, k], count [Q], resolved [Q]).  redo (device
+    int32 [1], optional): set to the number of queries needing the dense path (unresolved, or with
+    count_empty, nothing passed)."""
     t = torch()
     Q, kp = cand_id.shape
     dev = cand_id.device
@@ -356,7 +358,8 @@ def refine_topk(q: Prepared, c: Prepared, mode: int, cand_score, cand_id, k: int
     res = t.empty(Q, dtype=t.int32, device=dev)
     _chk(_L().hq_refine_topk(ptr(q.R), ptr(q.Z), ptr(q.S), Q, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L, mode,
                              ptr(_contig(cand_score)), ptr(_contig(cand_id)), kp, k, float(threshold), thr_mode,
-                             float(eps), int(id_base), ptr(os_), ptr(oi), ptr(cnt), ptr(res), stream()), exc)
+                             float(eps), int(id_base), ptr(os_), ptr(oi), ptr(cnt), ptr(res), 1 if count_empty else 0,
+                             ptr(redo), stream()), exc)
     return os_, oi, cnt, res
 
 

@@ -194,9 +194,9 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
  * v_mfma_f32_16x16x32_f16 per 16x16 tile) and the filter and list scores in f32.
  * |approx - exact| <= ~5.5e-6, so callers re-rank with hq_refine_topk at eps >= 2e-5.
  * hq_seg_pack0_split builds, from hq_seg_prepare's Z and S, Z16 [N + 48, 64] f16 (hi[32], lo[32]
- * of the zero-padded level-0 segment) and S32 [N + 48, 4] f32 (std, mean, msq, flag bits), with 48
- * pad rows; Sq/Sc are the f64 statistics of hq_seg_prepare.  Level-0 segments of up to 32 values,
- * N < 2^31.                                                                                        */
+ * of the zero-padded level-0 segment) and S32, f32 statistics (std, mean, msq, flag bits) in SoA
+ * groups of 4 rows (std[4], mean[4], msq[4], flags[4]) for round_up(N, 4) + 48 rows (16 B per row);
+ * Sq/Sc are the f64 statistics of hq_seg_prepare.  Level-0 segments of up to 32 values, N < 2^31. */
 int hq_seg_level0_len(int L);
 int hq_seg_pack0_split(const double* Z, const double* S, int64_t N, int L, void* Z16, float* S32,
                        hq_stream_t stream);
@@ -210,12 +210,15 @@ int hq_scan0_topk_split(const void* Zq16, const float* Sq32, const double* Sq, i
  * candidate exactly (as hq_level_scores), applies the threshold test exactly and writes the exact
  * top-k (score desc, id asc): out_score/out_id Q x k, out_count Q, and out_resolved Q = 1 when the
  * result is provably the exact top-k over the whole corpus given |approx - exact| <= eps (else the
- * caller re-runs that query on the dense exact path).  kp <= 64, k <= kp.                        */
+ * caller re-runs that query on the dense exact path).  kp <= 64, k <= kp.  out_redo (device int, may
+ * be NULL): the number of queries that need the dense path — unresolved, or (count_empty != 0) with
+ * no candidate passing — so the caller syncs on one int.                                          */
 int hq_refine_topk(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
                    const double* Zc, const double* Sc, int64_t N, int L, int mode,
                    const double* cand_score, const int64_t* cand_id, int kp, int k,
                    double threshold, int thr_mode, double eps, int64_t id_base, double* out_score,
-                   int64_t* out_id, int* out_count, int* out_resolved, hq_stream_t stream);
+                   int64_t* out_id, int* out_count, int* out_resolved, int count_empty, int* out_redo,
+                   hq_stream_t stream);
 
 /* ---- S4 on candidate lists: EXACT overall + per-level scores of selected pairs ---------------
  * ids: int64 Q x k GLOBAL ids (row = id - id_base; out of range / < 0 -> zeros);
