@@ -328,25 +328,65 @@ __global__ __launch_bounds__(256) void k_level_scores(VecSet Qs, int Q, VecSet C
   }
 }
 
-// exact overall + per-level for selected (query, candidate) pairs; ids are global, id_base subtracted
+// exact overall + per-level for selected (query, candidate) pairs; ids are global, id_base subtracted.
+// G lanes per pair (G >= nseg): lane s computes level s, the pair's first lane adds them up in level
+// order with the reference's typing (exact_pair's sum), so the 5-7 level scores run in parallel.
+template <int G>
 __global__ __launch_bounds__(256) void k_rescore(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si,
                                                  const int64_t* __restrict__ ids, int k, int64_t id_base,
                                                  double* __restrict__ out) {
   const int64_t total = (int64_t)Q * k;
   const int W = 1 + si.nseg;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
+  const int sub = threadIdx.x % G;
+  for (int64_t t0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G; t0 < total;
+       t0 += ((int64_t)gridDim.x * blockDim.x) / G) {
+    const int64_t t = t0;
     const int64_t q = t / k;
     const int64_t gid = ids[t];
     double* o = out + t * W;
     const int64_t c = gid - id_base;
-    if (gid < 0 || c < 0 || c >= N) {
-      for (int i = 0; i < W; ++i) o[i] = 0.0;
-      continue;
+    const bool ok = !(gid < 0 || c < 0 || c >= N);
+    double v = 0.0;
+    int t32 = 0;
+    if (ok && sub < si.nseg) {
+      const int s = sub;
+      v = exact_level(Qs.raw + q * si.L + si.src[s], Qs.Z + q * si.Lp + si.poff[s], Qs.S + (q * si.nseg + s) * 4,
+                      Cs.raw + c * si.L + si.src[s], Cs.Z + c * si.Lp + si.poff[s], Cs.S + (c * si.nseg + s) * 4,
+                      si.len[s], &t32);
     }
-    double lv[kMaxSeg];
-    o[0] = exact_pair(Qs, q, Cs, c, si, -1, lv);
-    for (int s = 0; s < si.nseg; ++s) o[1 + s] = lv[s];
+    if (sub < si.nseg) o[1 + sub] = v;
+    // search_engine.py:191-230 typed running sum (see exact_pair), gathered from the group's lanes
+    double tws = 0.0, tw = 0.0;
+    bool acc32 = false;
+    for (int s = 0; s < si.nseg; ++s) {
+      const int src = (threadIdx.x & 63) - sub + s;
+      const double vs = __shfl(v, src, 64);
+      const int ts = __shfl(t32, src, 64);
+      const double w = 1.0 / (double)(s + 1);
+      const double term = ts ? (double)((float)vs * (float)w) : vs * w;
+      if (!acc32 && !ts) {
+        tws = tws + term;
+      } else {
+        tws = (double)((float)tws + (float)term);
+        acc32 = true;
+      }
+      tw = tw + w;
+    }
+    if (sub == 0) {
+      double ov;
+      if (!ok) {
+        ov = 0.0;
+      } else if (acc32) {
+        const float of = (float)tws / (float)tw;
+        ov = of < 1.0f ? (double)of : 1.0;
+        ov = ov > 0.0 ? ov : 0.0;
+      } else {
+        ov = tw > 0.0 ? tws / tw : 0.0;
+        ov = ov < 1.0 ? ov : 1.0;
+        ov = ov > 0.0 ? ov : 0.0;
+      }
+      o[0] = ov;
+    }
   }
 }
 
@@ -1494,6 +1534,50 @@ __global__ __launch_bounds__(64) void k_pool_select(const float* __restrict__ po
       return c;
     };
     const int k = T < K ? T : K;
+    // Fast path (pool in registers, > K entries): T0 = the K-th largest lane maximum.  At least K
+    // entries are >= T0 (those K maxima), so the top K all are; when at most 64 entries are >= T0
+    // (the common case) they are gathered and rank-sorted directly, without the bisection.
+    if (inreg && T > K) {
+      float lm = -1.0f;
+#pragma unroll
+      for (int e = 0; e < kPoolReg; ++e) lm = rs[e] > lm ? rs[e] : lm;
+      int lr = 0;  // rank of this lane's maximum (value desc, lane asc)
+      for (int o = 0; o < 64; ++o) {
+        const float mo = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lm), o));
+        lr += (mo > lm || (mo == lm && o < lane)) ? 1 : 0;
+      }
+      const unsigned long long mk = __ballot(lr == K - 1);
+      const float t0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lm), __builtin_ctzll(mk)));
+      __shared__ float fs[64];
+      __shared__ int fi[64];
+      int c = 0;
+#pragma unroll
+      for (int e = 0; e < kPoolReg; ++e) {
+        const bool sel = rs[e] >= t0 && lane + 64 * e < T;
+        const unsigned long long m = __ballot(sel);
+        const int pre = c + __popcll(m & ((1ull << lane) - 1ull));
+        if (sel && pre < 64) { fs[pre] = rs[e]; fi[pre] = ri[e]; }
+        c += __popcll(m);
+      }
+      if (c <= 64) {
+        __syncthreads();
+        const float es = lane < c ? fs[lane] : -1.0f;
+        const int ei = lane < c ? fi[lane] : 0x7FFFFFFF;
+        int rank = 0;
+        for (int o = 0; o < c; ++o) {
+          const float so = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(es), o));
+          const int io = __builtin_amdgcn_readlane(ei, o);
+          rank += (so > es || (so == es && io < ei)) ? 1 : 0;
+        }
+        if (lane < c && rank < K) {
+          out_score[(int64_t)q * K + rank] = (double)es;
+          out_id[(int64_t)q * K + rank] = (int64_t)ei + id_base;
+        }
+        __syncthreads();
+        continue;
+      }
+      __syncthreads();
+    }
     float sv = -1.0f;
     int iv = 0x7FFFFFFF;  // select all
     if (T > K) {
@@ -2509,10 +2593,15 @@ int hq_rescore(const double* Rq, const double* Zq, const double* Sq, int Q, cons
   SegInfo si;
   seg_info(L, si);
   const int64_t total = (int64_t)Q * k;
-  int64_t blocks = (total + 255) / 256;
+  const int G = si.nseg <= 8 ? 8 : 16;
+  int64_t blocks = (total * G + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(k_rescore, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
-                     VecSet{Rc, Zc, Sc}, N, si, ids, k, id_base, out);
+  if (G == 8)
+    hipLaunchKernelGGL(k_rescore<8>, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
+                       VecSet{Rc, Zc, Sc}, N, si, ids, k, id_base, out);
+  else
+    hipLaunchKernelGGL(k_rescore<16>, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
+                       VecSet{Rc, Zc, Sc}, N, si, ids, k, id_base, out);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
