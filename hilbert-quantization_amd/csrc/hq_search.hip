@@ -1018,6 +1018,7 @@ struct SampleArgs {
   int64_t chunk_len; int nchunks; int nqb;
   int K;
   unsigned int* hist;  // Q x kBins
+  float* top;          // k_sample_topf: Q x 4 nchunks x kTopT
 };
 
 constexpr int kHRow = kBins / 2 + 1;  // LDS words per query histogram (odd: conflict-free rows)
@@ -1749,6 +1750,164 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
   flush_hist_top(hs, q0, a.Q, a.K, a.hist);
 }
 
+// f32 sample pass, top-T form (default): no histogram.  Every lane (g, j) keeps, for each of its
+// four queries 16b + j, the kTopT best approximate scores of its own stream of sample rows (rows 4g ..
+// 4g + 3 of every step of its chunk), tested division-free against its own kTopT-th best.  The values
+// of all streams are real scores of distinct (query, row) pairs, so the K-th best of their union
+// (k_sample_kth) is a lower bound of the K-th best over the sample and hence over the corpus; it is
+// as tight as the sample's own K-th unless a stream held more than kTopT of the sample's top K.
+// No LDS, no atomics: occupancy is set by VGPRs alone.  Output: top[(q * nstreams + 4 chunk + g) *
+// kTopT + t], every entry of every existing query written (-1 = empty).
+constexpr int kTopT = 2;
+
+__global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
+  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
+  const int chunk = xcd + 8 * (slot / a.nqb);
+  const int qb = slot % a.nqb;
+  if (chunk >= a.nchunks) return;
+  const int64_t c_begin = (int64_t)chunk * a.chunk_len;
+  int64_t c_end = c_begin + a.chunk_len;
+  if (c_end > a.S) c_end = a.S;
+  const int q0 = qb * kQW;
+  const float c1f = (float)a.c1;
+
+  half8 qh[4], ql[4];
+  float qA[4], qB[4], qQ[4];
+  int qok = 0;  // bit b: valid, unflagged query
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int q = q0 + 16 * b + j;
+    const bool v = q < a.Q;
+    const int qq = v ? q : 0;
+    const _Float16* zr = a.Zq16 + (int64_t)qq * kZ16Row + 8 * g;
+    qh[b] = *reinterpret_cast<const half8*>(zr);
+    ql[b] = *reinterpret_cast<const half8*>(zr + 32);
+    const int64_t gq = (int64_t)(qq >> 2) * 16 + (qq & 3);  // SoA-per-4 statistics
+    qA[b] = (float)(0.6 * a.inv_m) * a.Sq32[gq];
+    qB[b] = 0.6f * a.Sq32[gq + 4];
+    qQ[b] = a.Sq32[gq + 8];
+    if (v && __float_as_int(a.Sq32[gq + 12]) == 0) qok |= 1 << b;
+  }
+  float top[4][kTopT];
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int t = 0; t < kTopT; ++t) top[b][t] = -1.0f;
+  // k0[b] = 0.35 - (current kTopT-th best); +inf-free: an invalid / flagged query never passes
+  float k0[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) k0[b] = ((qok >> b) & 1) ? 1.35f : -__builtin_huge_valf();
+  auto row_of = [&](int64_t i) -> int64_t { return (i < a.S ? i : a.S - 1) * a.stride; };
+  auto load_frag = [&](int64_t cs, half8* dst) {
+    const _Float16* p = a.Zc16 + row_of(cs + j) * kZ16Row + 8 * g;
+    dst[0] = *reinterpret_cast<const half8*>(p);
+    dst[1] = *reinterpret_cast<const half8*>(p + 32);
+  };
+  half8 cf[2];
+  load_frag(c_begin, cf);
+  for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
+    flt4 cst[4];  // (std, mean, msq, flags) of rows 4g + r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = row_of(cs + 4 * g + r);
+      const float* p = a.Sc32 + (row >> 2) * 16 + (row & 3);
+      cst[r] = flt4{p[0], p[4], p[8], p[12]};
+    }
+    half8 cfn[2];
+    load_frag(cs + kCS, cfn);
+    flt4 acc[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[0], qh[b], flt4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[0], ql[b], acc[b], 0, 0, 0);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[1], qh[b], acc[b], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    // division-free test against the lane's own kTopT-th best: score > t <=> max(E, E den + num) > 0
+    int bits = 0;  // bit 4b + r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool ok = cs + 4 * g + r < c_end && __float_as_int(cst[r].w) == 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float G = acc[b][r];
+        const float E = fmaf(G, c1f, k0[b]);
+        const float num = fmaf(G, qA[b] * cst[r].x, qB[b] * cst[r].y);
+        const float d = fmaf(E, qQ[b] + cst[r].z, num);
+        bits |= (int)(ok && fmaxf(E, d) > 0.0f) << (4 * b + r);
+      }
+    }
+    if (__ballot(bits != 0)) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if ((bits >> (4 * b + r)) & 1) {
+            const float G = acc[b][r];
+            const float num = fmaf(G, qA[b] * cst[r].x, qB[b] * cst[r].y);
+            float t = num * __builtin_amdgcn_rcpf(qQ[b] + cst[r].z);
+            t = t > 0.0f ? t : 0.0f;
+            float sc = fmaf(G, c1f, 0.35f) + t;
+            sc = sc < 1.0f ? sc : 1.0f;
+            sc = sc > 0.0f ? sc : 0.0f;  // +0 for -0 and negatives (k_sample_kth orders bit patterns)
+            // sorted insert (descending), branch-free
+#pragma unroll
+            for (int u = 0; u < kTopT; ++u) {
+              const float hi = fmaxf(top[b][u], sc);
+              sc = fminf(top[b][u], sc);
+              top[b][u] = hi;
+            }
+          }
+        }
+        k0[b] = ((qok >> b) & 1) ? 0.35f - top[b][kTopT - 1] : -__builtin_huge_valf();
+      }
+    }
+    cf[0] = cfn[0];
+    cf[1] = cfn[1];
+  }
+  const int ns = 4 * a.nchunks;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int q = q0 + 16 * b + j;
+    if (q >= a.Q) continue;
+    float* o = a.top + ((int64_t)q * ns + 4 * chunk + g) * kTopT;
+#pragma unroll
+    for (int t = 0; t < kTopT; ++t) o[t] = top[b][t];
+  }
+}
+
+// per-query starting threshold from the top-T sample pools (one wave per query): the K-th largest
+// value v (bisection on the bit pattern of the non-negative f32 scores), th0 = v - margin, or -inf
+// when fewer than K sample scores exist
+__global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top, int ns, int Q, int K, double margin,
+                                                   double* __restrict__ th0) {
+  const int lane = threadIdx.x;
+  const int P = ns * kTopT;
+  for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    const float* p = top + (int64_t)q * P;
+    auto count_ge = [&](uint32_t bits) {
+      int c = 0;
+      for (int x = lane; x < P; x += 64) {
+        const float v = p[x];
+        c += (v >= 0.0f && __float_as_uint(v) >= bits) ? 1 : 0;
+      }
+      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+      return c;
+    };
+    double t = -__builtin_huge_val();
+    if (count_ge(0u) >= K) {
+      uint32_t lo = 0u, hi = 0x3F800001u;  // count_ge(lo) >= K, count_ge(hi) < K (scores <= 1)
+      while (hi - lo > 1u) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (count_ge(mid) >= K) lo = mid; else hi = mid;
+      }
+      t = (double)__uint_as_float(lo) - margin;
+    }
+    if (lane == 0) th0[q] = t;
+  }
+}
+
 // per-query starting threshold from the sample histogram (-inf when the sample has < K scores)
 __global__ void k_hist_tau(const unsigned int* __restrict__ hist, int Q, int K, double margin,
                            double* __restrict__ th0) {
@@ -2167,14 +2326,40 @@ static void scan0_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& ch
   if (chunk_len < kCS) chunk_len = kCS;
 }
 
+// top-T sample pass (k_sample_topf): same stride rule as the histogram pass; ~2048 waves (no per-wave
+// setup cost, so more waves only add occupancy), chunks a multiple of 8 (XCD map) and of kCS rows
+static void sample_top_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, int& nqb, int& nchunks,
+                                int64_t& chunk_len) {
+  const int64_t sd = getenv("HQ_SAMPLE_STRIDE") ? atoi(getenv("HQ_SAMPLE_STRIDE")) : 16;  // A/B knob
+  stride = N >= sd * 4096 ? sd : (N / 4096 > 1 ? N / 4096 : 1);
+  S = (N + stride - 1) / stride;
+  nqb = (Q + kQW - 1) / kQW;
+  const int waves = getenv("HQ_SAMPLE_WAVES") ? atoi(getenv("HQ_SAMPLE_WAVES")) : 2048;
+  int64_t target = (waves + nqb - 1) / nqb;
+  const int64_t max_chunks = (S + kCS - 1) / kCS;
+  if (target > max_chunks) target = max_chunks;
+  if (target > 256) target = 256;
+  nchunks = (int)(((target + 7) / 8) * 8);
+  if (nchunks < 8) nchunks = 8;
+  chunk_len = (S + nchunks - 1) / nchunks;
+  chunk_len = ((chunk_len + kCS - 1) / kCS) * kCS;
+}
+static size_t sample_top_bytes(int Q, int64_t N) {
+  int64_t stride, S, chunk_len;
+  int nqb, nchunks;
+  sample_top_geometry(Q, N, stride, S, nqb, nchunks, chunk_len);
+  return (size_t)Q * 4 * nchunks * kTopT * 4;
+}
+
 static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
   int nqb, nchunks, nqb2, nchunks2;
   int64_t chunk_len, chunk_len2;
   scan0_geometry(Q, N, nqb, nchunks, chunk_len);
   scan0_geometry(Q, N, nqb2, nchunks2, chunk_len2, 32);
   if (nchunks2 > nchunks) nchunks = nchunks2;
-  // lists / pools + global thresholds + sample histogram + starting thresholds + pool counts
-  return (size_t)nchunks * Q * k * 16 + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 8 + (size_t)Q * 4 + 256;
+  // lists / pools + global thresholds + sample histogram + starting thresholds + pool counts + sample tops
+  return (size_t)nchunks * Q * k * 16 + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 8 + (size_t)Q * 4 +
+         sample_top_bytes(Q, N) + 256;
 }
 
 // sample pass: stride 16 once the corpus is large, else a sample of ~4096 rows (the whole corpus
@@ -2290,12 +2475,33 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   b.pool_s = reinterpret_cast<float*>(ws);
   b.pool_i = reinterpret_cast<int*>(ws + (size_t)Q * b.pool_cap * 4);
   const bool sample = getenv("HQ_SCAN_NOSAMPLE") == nullptr;
+  const bool top_sample = sample && f32 && getenv("HQ_SAMPLE_HIST") == nullptr;  // default: top-T sample
+  float* top = reinterpret_cast<float*>(ws + lists + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 4 +
+                                        (size_t)Q * 8);
+  // (the histogram region lies between gtau and pool_n, so it is cleared with them in every mode)
   HQ_CHECK_HIP(hipMemsetAsync(b.gtau, 0, (size_t)Q * 8 + (sample ? (size_t)Q * kBins * 4 : 0) + (f32 ? (size_t)Q * 4 : 0),
                               s));
   if (f32 && !sample) HQ_CHECK_HIP(hipMemsetAsync(b.pool_n, 0, sizeof(int) * Q, s));
   int rc;
-  if (getenv("HQ_SCAN_NOSAMPLE") == nullptr) {
+  if (top_sample) {
     SampleArgs sa;
+    sa.Zq = Zq; sa.Sq = Sq; sa.Q = Q; sa.Zc = Zc; sa.Sc = Sc; sa.N = N;
+    sa.Zq32 = nullptr; sa.Zc32 = nullptr; sa.Zq16 = Zq16; sa.Zc16 = Zc16; sa.Sq32 = Sq32; sa.Sc32 = Sc32;
+    sa.Lp = b.Lp; sa.nseg = b.nseg; sa.P0 = b.P0; sa.inv_m = b.inv_m; sa.c1 = b.c1;
+    sample_top_geometry(Q, N, sa.stride, sa.S, sa.nqb, sa.nchunks, sa.chunk_len);
+    sa.hist = nullptr;
+    sa.top = top;
+    sa.K = k;
+    hipLaunchKernelGGL(k_sample_topf, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
+    HQ_CHECK_LAUNCH();
+    const int mg = Q < 8192 ? Q : 8192;
+    hipLaunchKernelGGL(k_sample_kth, dim3(mg), dim3(64), 0, s, (const float*)top, 4 * sa.nchunks, Q, k,
+                       (double)kMarginF, th0);
+    HQ_CHECK_LAUNCH();
+    b.th0 = th0;
+  } else if (sample) {
+    SampleArgs sa;
+    sa.top = nullptr;
     sa.Zq = Zq; sa.Sq = Sq; sa.Q = Q; sa.Zc = Zc; sa.Sc = Sc; sa.N = N;
     sa.Zq32 = nullptr; sa.Zc32 = nullptr; sa.Zq16 = Zq16; sa.Zc16 = Zc16; sa.Sq32 = Sq32; sa.Sc32 = Sc32;
     sa.Lp = b.Lp; sa.nseg = b.nseg; sa.P0 = b.P0; sa.inv_m = b.inv_m; sa.c1 = b.c1;
