@@ -308,6 +308,18 @@ __device__ __forceinline__ float wmax64(float v) {
   v = fmaxf(v, dppf<0x140>(v));
   return fmaxf(fmaxf(lanef(v, 0), lanef(v, 16)), fmaxf(lanef(v, 32), lanef(v, 48)));
 }
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int wsum64i(int v) {
+  v += dppi<0xB1>(v);
+  v += dppi<0x4E>(v);
+  v += dppi<0x141>(v);
+  v += dppi<0x140>(v);
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
+}
 // Fast form of qz: with d = fl(x - mn) >= 0 (shared by both forms), the reference's
 // y = fl(fl(d / rng) * 255) = Y (1+e1)(1+e2) and y' = fl(fl(d * fl(1/rng)) * 255) = Y (1+e3)(1+e4)(1+e5)
 // with Y = 255 d / rng <= 255 and |ei| <= 2^-24, so |y - y'| <= 255 * 5 * 2^-24 < 7.7e-5.  Hence

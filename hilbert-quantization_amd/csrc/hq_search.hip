@@ -1174,6 +1174,22 @@ __device__ __forceinline__ int shr1_f32i(float v) { return shr1_i32(__float_as_i
 // T = thl - kMarginF; 0.35 - T is kept per query (k0) and refreshed only when a threshold moves.
 // The step loop is unrolled by two (ping-pong registers for the next step's fragments/statistics),
 // candidate pointers advance by a constant per step.
+// G-only pre-filter threshold of k_scan0f (see the comment at refresh_k0): smallest G that can pass
+// the filter for list threshold t; out of line (rare: called when a threshold moves)
+__device__ __noinline__ float gstar0(float t, float qA, float qB, float qQ, float c1f) {
+  if (!(t > -__builtin_huge_valf())) return -__builtin_huge_valf();
+  if (!(t < __builtin_huge_valf())) return __builtin_huge_valf();
+  const double A = qA, B = qB, Qq = qQ, c1 = c1f;
+  const double R = ((double)t - (double)kMarginF - 1e-5) - 0.35;
+  const double a2 = 4.0 * Qq * c1 * c1 - A * A;
+  const double bp = 8.0 * Qq * R * c1;  // the quadratic is a2 G^2 - bp G + c2
+  const double c2 = 4.0 * Qq * R * R - B * B;
+  double disc = bp * bp - 4.0 * a2 * c2;
+  disc = disc > 0.0 ? sqrt(disc) : 0.0;
+  const double G = bp >= 0.0 ? (2.0 * c2) / (bp + disc) : (bp - disc) / (2.0 * a2);
+  return (float)(G - 1e-6 * (1.0 + fabs(G))) - 1e-5f * (1.0f + fabsf((float)G));
+}
+
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_scan0f(Scan0Args a) {
   constexpr int NB = 4;
   constexpr int QW = 16 * NB;  // queries per wave
@@ -1195,7 +1211,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 
   // queries: fragments, f32 constants, list thresholds (f32, exact list values)
   half8 qh[NB], ql[NB];  // query fragments: k range [8g, 8g + 8) of the hi and lo halves
-  float qA[NB], qB[NB], qQ[NB], thl[NB], k0[NB];
+  float qA[NB], qB[NB], qQ[NB], thl[NB], k0[NB], gs[NB];
   int qsp = 0;  // bit b: query 16b + j is flagged (zero variance / f32-unsafe)
   int qvb = 0;  // bit b: query 16b + j exists
 #pragma unroll
@@ -1218,10 +1234,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     if (v && a.th0 && a.th0[q] > t0) t0 = a.th0[q];
     thl[b] = v ? lower_f32(t0) : __builtin_huge_valf();
   }
-  // k0 = 0.35 - (thl - margin); flagged queries always pass (+inf), absent ones never (-inf)
+  // k0 = 0.35 - (thl - margin); flagged queries always pass (+inf), absent ones never (-inf).
+  // gs = G-only pre-filter threshold: by Cauchy-Schwarz (num <= sqrt(A^2 G^2 + B^2) sqrt(msq_c)) and
+  // AM-GM (den = Q + msq_c >= 2 sqrt(Q msq_c)) every approximate score is at most
+  //   U(G) = 0.35 + c1 G + sqrt(A^2 G^2 + B^2) / (2 sqrt(Q))      (A = qA, B = qB, Q = qQ)
+  // whatever the candidate; U is strictly increasing (c1 = 0.35/m > A / (2 sqrt Q) <= 0.3/m), so a pair
+  // can pass the filter only if G >= G* with U(G*) = T' (T' = thl - margin - 1e-5 slack for the f32
+  // evaluation).  G* is the smaller root of 4Q (R - c1 G)^2 = A^2 G^2 + B^2, R = T' - 0.35 (the
+  // larger one has R - c1 G < 0), evaluated in f64 and rounded down.
   auto refresh_k0 = [&](const int b) {
     k0[b] = ((qvb >> b) & 1) == 0 ? -__builtin_huge_valf()
                                   : (((qsp >> b) & 1) != 0 ? __builtin_huge_valf() : 0.35f - (thl[b] - kMarginF));
+    gs[b] = ((qvb >> b) & 1) == 0 ? __builtin_huge_valf()
+                                  : (((qsp >> b) & 1) != 0 ? -__builtin_huge_valf() : gstar0(thl[b], qA[b], qB[b], qQ[b], c1f));
   };
 #pragma unroll
   for (int b = 0; b < NB; ++b) refresh_k0(b);
@@ -1268,6 +1293,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   // past the chunk end are bit masks, applied only when some lane of the wave has a candidate pass
   // (the common half-step ends after one ballot).
   auto filter_half = [&](const int h, const flt4* acc, const CStep& c, const int rem) -> int {
+    // G-only pre-filter (see gstar0): most half-steps end here after 4 max and 2 compares
+    const float g0 = fmaxf(fmaxf(acc[0].x, acc[0].y), fmaxf(acc[0].z, acc[0].w));
+    const float g1 = fmaxf(fmaxf(acc[1].x, acc[1].y), fmaxf(acc[1].z, acc[1].w));
+    if (a.expt != 5 && !__ballot((g0 >= gs[2 * h]) | (g1 >= gs[2 * h + 1]) | (c.fm != 0))) return 0;
     const flt2 c1v = {c1f, c1f};
     flt2 m[4];  // [2u + p]: rows (2p, 2p + 1) of query block 2h + u
     float mx = -__builtin_huge_valf();
@@ -1804,18 +1833,24 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
     dst[0] = *reinterpret_cast<const half8*>(p);
     dst[1] = *reinterpret_cast<const half8*>(p + 32);
   };
-  half8 cf[2];
-  load_frag(c_begin, cf);
-  for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
-    flt4 cst[4];  // (std, mean, msq, flags) of rows 4g + r
+  auto load_stats = [&](int64_t cs, flt4* dst) {  // (std, mean, msq, flags) of rows 4g + r
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t row = row_of(cs + 4 * g + r);
       const float* p = a.Sc32 + (row >> 2) * 16 + (row & 3);
-      cst[r] = flt4{p[0], p[4], p[8], p[12]};
+      dst[r] = flt4{p[0], p[4], p[8], p[12]};
     }
+  };
+  // fragments and statistics of the next step are loaded one step ahead
+  half8 cf[2];
+  flt4 cst[4];
+  load_frag(c_begin, cf);
+  load_stats(c_begin, cst);
+  for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
     half8 cfn[2];
+    flt4 cstn[4];
     load_frag(cs + kCS, cfn);
+    load_stats(cs + kCS, cstn);
     flt4 acc[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[0], qh[b], flt4{0, 0, 0, 0}, 0, 0, 0);
@@ -1865,6 +1900,8 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
     }
     cf[0] = cfn[0];
     cf[1] = cfn[1];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cst[r] = cstn[r];
   }
   const int ns = 4 * a.nchunks;
 #pragma unroll
@@ -1878,31 +1915,37 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
 }
 
 // per-query starting threshold from the top-T sample pools (one wave per query): the K-th largest
-// value v (bisection on the bit pattern of the non-negative f32 scores), th0 = v - margin, or -inf
-// when fewer than K sample scores exist
+// value v (bisection on the bit pattern of the non-negative f32 scores, pool held in registers as
+// bits + 1, 0 = empty), th0 = v - margin, or -inf when fewer than K sample scores exist
+constexpr int kKthReg = 32;  // pool entries per lane: 4 * 256 chunks * kTopT / 64
+
 __global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top, int ns, int Q, int K, double margin,
                                                    double* __restrict__ th0) {
   const int lane = threadIdx.x;
   const int P = ns * kTopT;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
     const float* p = top + (int64_t)q * P;
-    auto count_ge = [&](uint32_t bits) {
+    uint32_t u[kKthReg];
+#pragma unroll
+    for (int e = 0; e < kKthReg; ++e) {
+      const int x = lane + 64 * e;
+      const float v = x < P ? p[x] : -1.0f;
+      u[e] = v >= 0.0f ? __float_as_uint(v) + 1u : 0u;
+    }
+    auto count_ge = [&](uint32_t t) {  // entries with u >= t (t >= 1): DPP sum, no LDS round trips
       int c = 0;
-      for (int x = lane; x < P; x += 64) {
-        const float v = p[x];
-        c += (v >= 0.0f && __float_as_uint(v) >= bits) ? 1 : 0;
-      }
-      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
-      return c;
+#pragma unroll
+      for (int e = 0; e < kKthReg; ++e) c += u[e] >= t ? 1 : 0;
+      return wsum64i(c);
     };
     double t = -__builtin_huge_val();
-    if (count_ge(0u) >= K) {
-      uint32_t lo = 0u, hi = 0x3F800001u;  // count_ge(lo) >= K, count_ge(hi) < K (scores <= 1)
+    if (count_ge(1u) >= K) {
+      uint32_t lo = 1u, hi = 0x3F800002u;  // count_ge(lo) >= K, count_ge(hi) < K (scores <= 1)
       while (hi - lo > 1u) {
         const uint32_t mid = lo + (hi - lo) / 2u;
         if (count_ge(mid) >= K) lo = mid; else hi = mid;
       }
-      t = (double)__uint_as_float(lo) - margin;
+      t = (double)__uint_as_float(lo - 1u) - margin;
     }
     if (lane == 0) th0[q] = t;
   }
@@ -2338,7 +2381,7 @@ static void sample_top_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, i
   int64_t target = (waves + nqb - 1) / nqb;
   const int64_t max_chunks = (S + kCS - 1) / kCS;
   if (target > max_chunks) target = max_chunks;
-  if (target > 256) target = 256;
+  if (target > 64 * kKthReg / (4 * kTopT)) target = 64 * kKthReg / (4 * kTopT);  // k_sample_kth pool in registers
   nchunks = (int)(((target + 7) / 8) * 8);
   if (nchunks < 8) nchunks = 8;
   chunk_len = (S + nchunks - 1) / nchunks;
