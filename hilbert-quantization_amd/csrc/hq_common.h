@@ -268,10 +268,16 @@ __device__ __noinline__ T pw_rec(const F& f, int off, int n) {
   }
 }
 
-template <typename T, class F>
+// SM = true: the caller guarantees n <= 128 (no out-of-line split levels: a kernel without calls keeps
+// its registers and needs no stack)
+template <typename T, bool SM = false, class F>
 __device__ __forceinline__ T np_sum(const F& f, int n) {
-  if (n <= 128) return T(0) + pw_leaf<T>(f, 0, n);
-  return T(0) + pw_rec<10, T>(f, 0, n);
+  if constexpr (SM) {
+    return T(0) + pw_leaf<T>(f, 0, n);
+  } else {
+    if (n <= 128) return T(0) + pw_leaf<T>(f, 0, n);
+    return T(0) + pw_rec<10, T>(f, 0, n);
+  }
 }
 
 // element size of an HQ dtype code (0 if unknown)

@@ -183,6 +183,7 @@ struct Side {
   bool f32;
 };
 
+template <bool SM = false>
 __device__ __forceinline__ Side make_side(const double* x, const double* z, const double* st, int m, bool f32) {
   Side r;
   r.x = x;
@@ -190,25 +191,25 @@ __device__ __forceinline__ Side make_side(const double* x, const double* z, cons
   r.f32 = f32;
   if (f32) {
     auto gx = [=](int k) -> float { return (float)x[k]; };
-    const float mean = np_sum<float>(gx, m) / (float)m;
+    const float mean = np_sum<float, SM>(gx, m) / (float)m;
     auto gd = [=](int k) -> float { const float d = (float)x[k] - mean; return d * d; };
-    const float sd = sqrtf(np_sum<float>(gd, m) / (float)m);
+    const float sd = sqrtf(np_sum<float, SM>(gd, m) / (float)m);
     auto gs = [=](int k) -> float { const float v = (float)x[k]; return v * v; };
     r.mean = mean;
     r.sd = sd;
-    r.msq = np_sum<float>(gs, m) / (float)m;
+    r.msq = np_sum<float, SM>(gs, m) / (float)m;
   } else if (st) {
     r.mean = st[0];
     r.sd = st[1];
     r.msq = st[2];
   } else {
     auto fx = [=](int k) -> double { return x[k]; };
-    r.mean = np_sum<double>(fx, m) / (double)m;
+    r.mean = np_sum<double, SM>(fx, m) / (double)m;
     const double mu = r.mean;
     auto fd = [=](int k) -> double { const double d = x[k] - mu; return d * d; };
-    r.sd = sqrt(np_sum<double>(fd, m) / (double)m);
+    r.sd = sqrt(np_sum<double, SM>(fd, m) / (double)m);
     auto fs = [=](int k) -> double { return x[k] * x[k]; };
-    r.msq = np_sum<double>(fs, m) / (double)m;
+    r.msq = np_sum<double, SM>(fs, m) / (double)m;
   }
   return r;
 }
@@ -223,6 +224,7 @@ __device__ __forceinline__ double side_z(const Side& s, int k) {
 // compare_indices_at_level (search_engine.py:111-189) for one segment in the reference's operation
 // order and dtype.  *np32 = 1 when the result is a numpy float32 (both sides f32, general branch,
 // not clamped), else it is a Python float: the type decides the overall weighted sum's arithmetic.
+template <bool SM = false>
 __device__ double exact_level_sides(const Side& q, const Side& c, int m, int* np32) {
   *np32 = 0;
   const bool both32 = q.f32 && c.f32;
@@ -231,10 +233,10 @@ __device__ double exact_level_sides(const Side& q, const Side& c, int m, int* np
     // float32 throughout: np.mean = f32(f64(f32 pairwise sum) / m) = f32 division (exact double
     // rounding); Python float literals are cast to float32 (NEP 50); no FMA contraction
     auto fp = [&](int k) -> float { return (float)side_z(q, k) * (float)side_z(c, k); };
-    const float corr = np_sum<float>(fp, m) / (float)m;                          // :154
+    const float corr = np_sum<float, SM>(fp, m) / (float)m;                          // :154
     const float sim = (corr + 1.0f) / 2.0f;                                        // :158
     auto fd = [&](int k) -> float { const float d = (float)q.x[k] - (float)c.x[k]; return d * d; };
-    const float mse = np_sum<float>(fd, m) / (float)m;                             // :161
+    const float mse = np_sum<float, SM>(fd, m) / (float)m;                             // :161
     const float maxmse = (float)q.msq + (float)c.msq;                              // :162
     float ds = 1.0f;
     if (maxmse > 0.0f) {
@@ -249,10 +251,10 @@ __device__ double exact_level_sides(const Side& q, const Side& c, int m, int* np
     return comb < 1.0f ? 0.0 : 1.0;                                                // :174 (Python floats)
   }
   auto fp = [&](int k) -> double { return side_z(q, k) * side_z(c, k); };
-  const double corr = np_sum<double>(fp, m) / (double)m;                         // :154
+  const double corr = np_sum<double, SM>(fp, m) / (double)m;                         // :154
   const double sim = (corr + 1.0) / 2.0;                                         // :158
   auto fd = [&](int k) -> double { double d = q.x[k] - c.x[k]; return d * d; };
-  const double mse = np_sum<double>(fd, m) / (double)m;                          // :161
+  const double mse = np_sum<double, SM>(fd, m) / (double)m;                          // :161
   const double maxmse = q.msq + c.msq;                                           // :162
   double ds = 1.0;
   if (maxmse > 0.0) {
@@ -266,25 +268,22 @@ __device__ double exact_level_sides(const Side& q, const Side& c, int m, int* np
   return comb > 0.0 ? comb : 0.0;
 }
 
+template <bool SM = false>
 __device__ double exact_level(const double* q, const double* zq, const double* sq, const double* c,
                               const double* zc, const double* sc, int m, int* np32) {
   const bool qf = (aux_bits(sq) & kAuxF32) != 0, cf = (aux_bits(sc) & kAuxF32) != 0;
-  return exact_level_sides(make_side(q, zq, sq, m, qf), make_side(c, zc, sc, m, cf), m, np32);
+  return exact_level_sides<SM>(make_side<SM>(q, zq, sq, m, qf), make_side<SM>(c, zc, sc, m, cf), m, np32);
 }
 
-__device__ double exact_pair(const VecSet& A, int64_t ia, const VecSet& B, int64_t ib, const SegInfo& si, int level,
-                             double* lv) {
-  const double* ra = A.raw + ia * si.L;
-  const double* rb = B.raw + ib * si.L;
-  const double* za = A.Z + ia * si.Lp;
-  const double* zb = B.Z + ib * si.Lp;
-  const double* sa = A.S + ia * si.nseg * 4;
-  const double* sb = B.S + ib * si.nseg * 4;
+// exact_pair on explicit row pointers (raw [L], Z [Lp], S [nseg x 4] of each side; global or LDS)
+template <bool SM = false>
+__device__ double exact_pair_rows(const double* ra, const double* za, const double* sa, const double* rb,
+                                  const double* zb, const double* sb, const SegInfo& si, int level, double* lv) {
   int t32;
   if (level >= 0) {
     if (level >= si.nseg) return 0.0;
     const int s = level;
-    return exact_level(ra + si.src[s], za + si.poff[s], sa + 4 * s, rb + si.src[s], zb + si.poff[s], sb + 4 * s,
+    return exact_level<SM>(ra + si.src[s], za + si.poff[s], sa + 4 * s, rb + si.src[s], zb + si.poff[s], sb + 4 * s,
                        si.len[s], &t32);
   }
   // search_engine.py:191-230: running weighted sum in level order, divide, clamp.  Python typing:
@@ -293,7 +292,7 @@ __device__ double exact_pair(const VecSet& A, int64_t ia, const VecSet& B, int64
   double tws = 0.0, tw = 0.0;
   bool acc32 = false;
   for (int s = 0; s < si.nseg; ++s) {
-    const double v = exact_level(ra + si.src[s], za + si.poff[s], sa + 4 * s, rb + si.src[s], zb + si.poff[s],
+    const double v = exact_level<SM>(ra + si.src[s], za + si.poff[s], sa + 4 * s, rb + si.src[s], zb + si.poff[s],
                                  sb + 4 * s, si.len[s], &t32);
     if (lv) lv[s] = v;
     const double w = 1.0 / (double)(s + 1);
@@ -317,6 +316,13 @@ __device__ double exact_pair(const VecSet& A, int64_t ia, const VecSet& B, int64
   return ov > 0.0 ? ov : 0.0;
 }
 
+template <bool SM = false>
+__device__ double exact_pair(const VecSet& A, int64_t ia, const VecSet& B, int64_t ib, const SegInfo& si, int level,
+                             double* lv) {
+  return exact_pair_rows<SM>(A.raw + ia * si.L, A.Z + ia * si.Lp, A.S + ia * si.nseg * 4, B.raw + ib * si.L,
+                         B.Z + ib * si.Lp, B.S + ib * si.nseg * 4, si, level, lv);
+}
+
 // dense Q x N exact scores (drop-in path and rare exact fallbacks)
 __global__ __launch_bounds__(256) void k_level_scores(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si, int level,
                                                       double* __restrict__ out) {
@@ -331,7 +337,7 @@ __global__ __launch_bounds__(256) void k_level_scores(VecSet Qs, int Q, VecSet C
 // exact overall + per-level for selected (query, candidate) pairs; ids are global, id_base subtracted.
 // G lanes per pair (G >= nseg): lane s computes level s, the pair's first lane adds them up in level
 // order with the reference's typing (exact_pair's sum), so the 5-7 level scores run in parallel.
-template <int G>
+template <int G, bool SM = false>
 __global__ __launch_bounds__(256) void k_rescore(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si,
                                                  const int64_t* __restrict__ ids, int k, int64_t id_base,
                                                  double* __restrict__ out) {
@@ -350,7 +356,7 @@ __global__ __launch_bounds__(256) void k_rescore(VecSet Qs, int Q, VecSet Cs, in
     int t32 = 0;
     if (ok && sub < si.nseg) {
       const int s = sub;
-      v = exact_level(Qs.raw + q * si.L + si.src[s], Qs.Z + q * si.Lp + si.poff[s], Qs.S + (q * si.nseg + s) * 4,
+      v = exact_level<SM>(Qs.raw + q * si.L + si.src[s], Qs.Z + q * si.Lp + si.poff[s], Qs.S + (q * si.nseg + s) * 4,
                       Cs.raw + c * si.L + si.src[s], Cs.Z + c * si.Lp + si.poff[s], Cs.S + (c * si.nseg + s) * 4,
                       si.len[s], &t32);
     }
@@ -1273,8 +1279,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const flt4 fl = *reinterpret_cast<const flt4*>(pst + 12);
     c.fm = (int)(__float_as_int(fl.x) != 0) | ((int)(__float_as_int(fl.y) != 0) << 1) |
            ((int)(__float_as_int(fl.z) != 0) << 2) | ((int)(__float_as_int(fl.w) != 0) << 3);
-    pz += kCS * kZ16Row;
-    pst += kCS * 4;
+    if (a.expt != 6) {  // 6: diagnostics only (wrong results) - every step re-reads the first step's rows
+      pz += kCS * kZ16Row;
+      pst += kCS * 4;
+    }
   };
   // G of two 16-query blocks: hi.hi + hi.lo + lo.hi, two accumulation chains interleaved
   auto mfma_half = [&](const int h, const half8* f, flt4* acc) {
@@ -1296,7 +1304,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     // G-only pre-filter (see gstar0): most half-steps end here after 4 max and 2 compares
     const float g0 = fmaxf(fmaxf(acc[0].x, acc[0].y), fmaxf(acc[0].z, acc[0].w));
     const float g1 = fmaxf(fmaxf(acc[1].x, acc[1].y), fmaxf(acc[1].z, acc[1].w));
-    if (a.expt != 5 && !__ballot((g0 >= gs[2 * h]) | (g1 >= gs[2 * h + 1]) | (c.fm != 0))) return 0;
+    const unsigned long long pre = __ballot((g0 >= gs[2 * h]) | (g1 >= gs[2 * h + 1]) | (c.fm != 0));
+    if (a.expt == 3 && lane == 0) {
+      atomicAdd(a.dbg + 6, 1ull);
+      if (pre) atomicAdd(a.dbg + 5, 1ull);
+    }
+    if (a.expt != 5 && !pre) return 0;
     const flt2 c1v = {c1f, c1f};
     flt2 m[4];  // [2u + p]: rows (2p, 2p + 1) of query block 2h + u
     float mx = -__builtin_huge_valf();
@@ -2240,6 +2253,7 @@ __global__ __launch_bounds__(256) void k_pair_raw(const double* __restrict__ q, 
 // unlisted candidate can belong to the exact top-k given |approx - exact| <= eps:
 //   list not full (every candidate with approx >= thr - eps is listed), or
 //   last listed approx + eps < k-th exact score (enough passed), or < / <= thr (too few passed).
+template <bool SM = false>
 __global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si, int mode,
                                                const double* __restrict__ cs, const int64_t* __restrict__ cid, int kp,
                                                int k, double thr, int thr_mode, double eps, int64_t id_base,
@@ -2256,7 +2270,7 @@ __global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int6
       int64_t id = cid[base + lane];
       const int64_t c = id - id_base;
       if (id >= 0 && c >= 0 && c < N) {
-        e = exact_pair(Qs, q, Cs, c, si, mode == 0 ? 0 : -1, nullptr);
+        e = exact_pair<SM>(Qs, q, Cs, c, si, mode == 0 ? 0 : -1, nullptr);
         const bool pass = thr_mode == 0 || (thr_mode == 1 ? e >= thr : e > thr);
         if (!pass) id = -1;
       } else {
@@ -2301,6 +2315,184 @@ __global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int6
       }
       ores[q] = res;
       if (oredo && (res == 0 || (count_empty && cnt == 0))) atomicAdd(oredo, 1);
+    }
+    __syncthreads();
+  }
+}
+
+// LDS-staged exact re-rank (default when the rows fit): one wave per query copies the query's and the
+// kp listed candidates' rows (raw [L], Z [Lp], S [nseg x 4] = RW doubles each) into LDS with all loads
+// in flight at once (8 per lane per round), then scores from LDS, so the random corpus rows cost one
+// memory round trip instead of one per dependent load.  Same contract and arithmetic as k_refine (the
+// same exact_pair code on other addresses).  odet != NULL: also the exact [overall, level 0..] record of
+// every output entry (hq_rescore's values for the output ids, zeros for empty slots), from the rows
+// already staged - the progressive search then needs no separate re-score launch.
+// staged doubles: the query row (raw [L], Z [Lp], S [nseg x 4]) and kp candidate rows of raw + S (a
+// candidate's normalised values are recomputed as (x - mean) / std from its statistics: the same f64
+// operations k_seg_prepare stored in Z, so bit-identical, and 45% fewer bytes gathered)
+__host__ __device__ inline int refine_rw(const SegInfo& si) { return si.L + 4 * si.nseg; }
+__host__ __device__ inline int refine_qw(const SegInfo& si) { return si.L + si.Lp + 4 * si.nseg; }
+// every level segment <= 128 values: the exact scorers' NumPy sums are single pairwise leaves (SM kernels)
+inline bool seg_small(const SegInfo& si) {
+  for (int s = 0; s < si.nseg; ++s)
+    if (si.len[s] > 128) return false;
+  return true;
+}
+
+// nbytes (multiple of 16) from g to LDS byte address d (16-B aligned) by LDS-DMA, 1 KiB per instruction
+__device__ __forceinline__ void dma_seg(const double* g, uint32_t d, int nbytes, int lane) {
+  for (int off = 0; off < nbytes; off += 1024) {
+    if (off + 16 * lane < nbytes) {
+      uint32_t keep;
+      const char* src = reinterpret_cast<const char*>(g) + off + 16 * lane;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(d + (uint32_t)off)) : "memory");
+    }
+  }
+}
+
+// the reference's typed weighted sum of the level scores (search_engine.py:191-230; see exact_pair_rows)
+__device__ __forceinline__ double overall_from_levels(const double* lv, const int* t32, int nseg) {
+  double tws = 0.0, tw = 0.0;
+  bool acc32 = false;
+  for (int s = 0; s < nseg; ++s) {
+    const double w = 1.0 / (double)(s + 1);
+    const double term = t32[s] ? (double)((float)lv[s] * (float)w) : lv[s] * w;
+    if (!acc32 && !t32[s]) {
+      tws = tws + term;
+    } else {
+      tws = (double)((float)tws + (float)term);
+      acc32 = true;
+    }
+    tw = tw + w;
+  }
+  double ov;
+  if (acc32) {
+    const float o = (float)tws / (float)tw;
+    ov = o < 1.0f ? (double)o : 1.0;
+  } else {
+    ov = tw > 0.0 ? tws / tw : 0.0;
+    ov = ov < 1.0 ? ov : 1.0;
+  }
+  return ov > 0.0 ? ov : 0.0;
+}
+
+// One 256-thread workgroup per query: the four waves stage the rows by LDS-DMA (wave w: rows w, w + 4,
+// ...), then every (candidate, level) score is one task over the 256 threads in level-major order (the
+// long level-0 tasks all in the first round), wave 0 adds each candidate's levels in the reference's
+// order and typing, ranks and writes.  Needed tasks: level 0 only for mode 0 without odet.
+template <bool SM = false>
+__global__ __launch_bounds__(256) void k_refine_lds(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si, int mode,
+                                                    const double* __restrict__ cs, const int64_t* __restrict__ cid,
+                                                    int kp, int k, double thr, int thr_mode, double eps,
+                                                    int64_t id_base, double* __restrict__ os,
+                                                    int64_t* __restrict__ oid, int* __restrict__ ocnt,
+                                                    int* __restrict__ ores, int count_empty, int* __restrict__ oredo,
+                                                    double* __restrict__ odet, int expt) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  __shared__ int64_t srow[kMaxTopK + 1];  // source row per staged row (-1: empty)
+  __shared__ int t32s[kMaxTopK * kMaxSeg];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int RW = refine_rw(si), QW = refine_qw(si), W = 1 + si.nseg, nr = kp + 1;
+  double* rq = sm;                            // query row: raw, Z, S
+  double* rows = sm + QW;                     // kp x RW candidate rows: raw, S
+  double* lvs = rows + (int64_t)kp * RW;      // kp x W: overall, levels
+  const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)sm;
+  const int nlev = (mode == 0 && !odet) ? 1 : si.nseg;
+  for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    const int64_t base = (int64_t)q * kp;
+    if (tid < nr) {
+      int64_t r = q;
+      if (tid > 0) {
+        const int64_t id = cid[base + tid - 1];
+        const int64_t c = id - id_base;
+        r = (id >= 0 && c >= 0 && c < N) ? c : -1;
+      }
+      srow[tid] = r;
+    }
+    __syncthreads();
+    // stage by LDS-DMA (global_load_lds_dwordx4: lane l writes 16 B at m0 + 16 l), all pieces in flight
+    for (int r = wave; r < nr && expt != 1; r += 4) {  // expt: diagnostics (1 no staging, 2 no scoring)
+      const int64_t i = srow[r];
+      if (i < 0) continue;
+      if (r == 0) {
+        dma_seg(Qs.raw + i * si.L, lbase, 8 * si.L, lane);
+        dma_seg(Qs.Z + i * si.Lp, lbase + 8u * si.L, 8 * si.Lp, lane);
+        dma_seg(Qs.S + i * si.nseg * 4, lbase + 8u * (si.L + si.Lp), 32 * si.nseg, lane);
+      } else {
+        const uint32_t d0 = lbase + 8u * (uint32_t)(QW + (r - 1) * RW);
+        dma_seg(Cs.raw + i * si.L, d0, 8 * si.L, lane);
+        dma_seg(Cs.S + i * si.nseg * 4, d0 + 8u * si.L, 32 * si.nseg, lane);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // level scores: task t = s * kp + p
+    for (int t = tid; t < nlev * kp && expt != 2; t += 256) {
+      const int sg = t / kp, p = t - sg * kp;
+      double v = 0.0;
+      int f32 = 0;
+      if (srow[p + 1] >= 0) {
+        const double* rc = rows + (int64_t)p * RW;
+        v = exact_level<SM>(rq + si.src[sg], rq + si.L + si.poff[sg], rq + si.L + si.Lp + 4 * sg, rc + si.src[sg],
+                            nullptr, rc + si.L + 4 * sg, si.len[sg], &f32);
+      }
+      lvs[(int64_t)p * W + 1 + sg] = v;
+      t32s[p * kMaxSeg + sg] = f32;
+    }
+    __syncthreads();
+    if (wave == 0) {
+      double e = -__builtin_huge_val();
+      int64_t id = -1;
+      if (lane < kp) {
+        id = cid[base + lane];
+        if (srow[lane + 1] >= 0) {
+          double* lv = lvs + (int64_t)lane * W;
+          const double ov = nlev == si.nseg ? overall_from_levels(lv + 1, t32s + lane * kMaxSeg, si.nseg) : 0.0;
+          lv[0] = ov;
+          e = mode == 0 ? lv[1] : ov;
+          const bool pass = thr_mode == 0 || (thr_mode == 1 ? e >= thr : e > thr);
+          if (!pass) id = -1;
+        } else {
+          id = -1;
+        }
+      }
+      const bool valid = id >= 0;
+      const int n = __popcll(__ballot(valid));
+      int rank = 0;
+      for (int o = 0; o < kp; ++o) {
+        const double so = rl_f64(e, o);
+        const long long io = __double_as_longlong(rl_f64(__longlong_as_double((long long)id), o));
+        rank += (io >= 0 && (so > e || (so == e && io < id))) ? 1 : 0;
+      }
+      const int cnt = n < k ? n : k;
+      if (valid && rank < k) {
+        os[(int64_t)q * k + rank] = e;
+        oid[(int64_t)q * k + rank] = id;
+        if (odet)
+          for (int w = 0; w < W; ++w) odet[((int64_t)q * k + rank) * W + w] = lvs[(int64_t)lane * W + w];
+      }
+      for (int j = cnt + lane; j < k; j += 64) {
+        os[(int64_t)q * k + j] = -__builtin_huge_val();
+        oid[(int64_t)q * k + j] = -1;
+        if (odet)
+          for (int w = 0; w < W; ++w) odet[((int64_t)q * k + j) * W + w] = 0.0;
+      }
+      const unsigned long long mk = __ballot(valid && rank == k - 1);
+      const double kth = mk ? rl_f64(e, __builtin_ctzll(mk)) : -__builtin_huge_val();
+      if (lane == 0) {
+        ocnt[q] = cnt;
+        const bool full = cid[base + kp - 1] >= 0;
+        int res = 1;
+        if (full) {
+          const double bound = cs[base + kp - 1] + eps;
+          if (n >= k) res = bound < kth;
+          else if (thr_mode == 0) res = 0;
+          else res = thr_mode == 1 ? (bound < thr) : (bound <= thr);
+        }
+        ores[q] = res;
+        if (oredo && (res == 0 || (count_empty && cnt == 0))) atomicAdd(oredo, 1);
+      }
     }
     __syncthreads();
   }
@@ -2568,11 +2760,12 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     HQ_CHECK_LAUNCH();
   }
   if (b.expt == 3) {
-    unsigned long long h[5];
+    unsigned long long h[7];
     HQ_CHECK_HIP(hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, s));
     HQ_CHECK_HIP(hipStreamSynchronize(s));
     fprintf(stderr, "k_scan0f: waves %d, insert entries %llu, passing pairs %llu, list inserts %llu, filter passes "
-            "%llu in %llu (u, r) iterations\n", b.nqb * b.nchunks, h[0], h[1], h[2], h[3], h[4]);
+            "%llu in %llu (u, r) iterations, pre-filter fired in %llu of %llu half-steps\n", b.nqb * b.nchunks, h[0],
+            h[1], h[2], h[3], h[4], h[5], h[6]);
   }
   if (!f32) {
     int mg = Q < 4096 ? Q : 4096;
@@ -2628,6 +2821,48 @@ static int launch_scan(const ScanArgs& a, hipStream_t s) {
   const int grid = a.nqb * a.nchunks;
   hipLaunchKernelGGL((k_scan<KSMAX, OVERALL>), dim3(grid), dim3(256), lds, s, a);
   HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+// exact re-rank launcher: the LDS-staged kernel when the staged rows fit (<= 96 KiB), else k_refine
+// (which has no re-score output: odet then takes hq_rescore's kernel afterwards)
+static int refine_launch(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
+                         const double* Zc, const double* Sc, int64_t N, int L, int mode, const double* cand_score,
+                         const int64_t* cand_id, int kp, int k, double threshold, int thr_mode, double eps,
+                         int64_t id_base, double* out_score, int64_t* out_id, int* out_count, int* out_resolved,
+                         int count_empty, int* out_redo, double* out_det, hq_stream_t stream) {
+  SegInfo si;
+  seg_info(L, si);
+  const hipStream_t s = (hipStream_t)stream;
+  const int grid = Q < 8192 ? Q : 8192;
+  if (out_redo) HQ_CHECK_HIP(hipMemsetAsync(out_redo, 0, sizeof(int), s));
+  const size_t lds = ((size_t)refine_qw(si) + (size_t)kp * refine_rw(si) + (size_t)kp * (1 + si.nseg)) * 8;
+  const bool sm = seg_small(si);
+  const int expt = getenv("HQ_REFINE_EXPT") ? atoi(getenv("HQ_REFINE_EXPT")) : 0;
+  if (lds <= 96 * 1024 && L % 2 == 0 && getenv("HQ_REFINE_GLOBAL") == nullptr) {  // 16-B pieces: L even
+    const void* fn = sm ? (const void*)k_refine_lds<true> : (const void*)k_refine_lds<false>;
+    HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (sm)
+      hipLaunchKernelGGL(k_refine_lds<true>, dim3(grid), dim3(256), lds, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc},
+                         N, si, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
+                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, expt);
+    else
+      hipLaunchKernelGGL(k_refine_lds<false>, dim3(grid), dim3(256), lds, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc},
+                         N, si, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
+                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, expt);
+    HQ_CHECK_LAUNCH();
+    return HQ_OK;
+  }
+  if (sm)
+    hipLaunchKernelGGL(k_refine<true>, dim3(grid), dim3(64), 0, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
+                       mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id, out_count,
+                       out_resolved, count_empty ? 1 : 0, out_redo);
+  else
+    hipLaunchKernelGGL(k_refine<false>, dim3(grid), dim3(64), 0, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
+                       mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id, out_count,
+                       out_resolved, count_empty ? 1 : 0, out_redo);
+  HQ_CHECK_LAUNCH();
+  if (out_det) return hq_rescore(Rq, Zq, Sq, Q, Rc, Zc, Sc, N, L, out_id, k, id_base, out_det, stream);
   return HQ_OK;
 }
 
@@ -2702,15 +2937,23 @@ int hq_refine_topk(const double* Rq, const double* Zq, const double* Sq, int Q, 
   if (!Rq || !Zq || !Sq || !cand_score || !cand_id || !out_score || !out_id || !out_count || !out_resolved ||
       (N > 0 && (!Rc || !Zc || !Sc)))
     return fail(HQ_E_INVALID, "null buffer");
-  SegInfo si;
-  seg_info(L, si);
-  int grid = Q < 8192 ? Q : 8192;
-  if (out_redo) HQ_CHECK_HIP(hipMemsetAsync(out_redo, 0, sizeof(int), (hipStream_t)stream));
-  hipLaunchKernelGGL(k_refine, dim3(grid), dim3(64), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
-                     VecSet{Rc, Zc, Sc}, N, si, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base,
-                     out_score, out_id, out_count, out_resolved, count_empty ? 1 : 0, out_redo);
-  HQ_CHECK_LAUNCH();
-  return HQ_OK;
+  return refine_launch(Rq, Zq, Sq, Q, Rc, Zc, Sc, N, L, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps,
+                       id_base, out_score, out_id, out_count, out_resolved, count_empty, out_redo, nullptr, stream);
+}
+
+int hq_refine_rescore_topk(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
+                           const double* Zc, const double* Sc, int64_t N, int L, int mode, const double* cand_score,
+                           const int64_t* cand_id, int kp, int k, double threshold, int thr_mode, double eps,
+                           int64_t id_base, double* out_score, int64_t* out_id, int* out_count, int* out_resolved,
+                           int count_empty, int* out_redo, double* out_det, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || L <= 0 || kp <= 0 || kp > kMaxTopK || k <= 0 || k > kp)
+    return fail(HQ_E_INVALID, "bad sizes kp=%d k=%d", kp, k);
+  if (Q == 0) return HQ_OK;
+  if (!Rq || !Zq || !Sq || !cand_score || !cand_id || !out_score || !out_id || !out_count || !out_resolved ||
+      !out_det || (N > 0 && (!Rc || !Zc || !Sc)))
+    return fail(HQ_E_INVALID, "null buffer");
+  return refine_launch(Rq, Zq, Sq, Q, Rc, Zc, Sc, N, L, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps,
+                       id_base, out_score, out_id, out_count, out_resolved, count_empty, out_redo, out_det, stream);
 }
 
 size_t hq_scan_workspace_size(int Q, int64_t N, int k) {
@@ -2845,12 +3088,19 @@ int hq_rescore(const double* Rq, const double* Zq, const double* Sq, int Q, cons
   const int G = si.nseg <= 8 ? 8 : 16;
   int64_t blocks = (total * G + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  if (G == 8)
-    hipLaunchKernelGGL(k_rescore<8>, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
-                       VecSet{Rc, Zc, Sc}, N, si, ids, k, id_base, out);
+  const bool sm = seg_small(si);
+  if (G == 8 && sm)
+    hipLaunchKernelGGL((k_rescore<8, true>), dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq},
+                       Q, VecSet{Rc, Zc, Sc}, N, si, ids, k, id_base, out);
+  else if (G == 8)
+    hipLaunchKernelGGL((k_rescore<8, false>), dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq},
+                       Q, VecSet{Rc, Zc, Sc}, N, si, ids, k, id_base, out);
+  else if (sm)
+    hipLaunchKernelGGL((k_rescore<16, true>), dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq},
+                       Q, VecSet{Rc, Zc, Sc}, N, si, ids, k, id_base, out);
   else
-    hipLaunchKernelGGL(k_rescore<16>, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
-                       VecSet{Rc, Zc, Sc}, N, si, ids, k, id_base, out);
+    hipLaunchKernelGGL((k_rescore<16, false>), dim3((int)blocks), dim3(256), 0, (hipStream_t)stream,
+                       VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si, ids, k, id_base, out);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }

@@ -241,11 +241,11 @@ class IndexCorpus:
             return oid, odet[..., 0], odet[..., 1:], ocnt
         threshold = self._thr(qp, threshold, 1)
         nredo = self._redo_counter(qp.Z.device)
-        s0, ids, cnt, res = self._scan_refine(qp, 0, M, float(threshold), 1, nredo)
+        s0, ids, cnt, res, det = self._scan_refine(qp, 0, M, float(threshold), 1, nredo, det=True)
         # no arg-max on this path: a query where nothing passed (count 0) is recomputed by the dense path
         # below, so the fallback slot is a constant (-inf, id -1, zero re-scores) kept per batch size
         best, bid, bdet = self._no_fallback(Q, qp.Z.device)
-        oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out, bdet)
+        oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out, bdet, det)
         forced = self._forced(qp)
         # the one host sync: k_refine counted the unresolved / empty queries on the device
         if forced is not None or int(nredo.item()) > 0:
@@ -279,18 +279,21 @@ class IndexCorpus:
                           t.zeros((Q, 1 + self.nseg), dtype=t.float64, device=dev))
         return cache[key]
 
-    def _scan_refine(self, qp, mode: int, k: int, thr: float, thr_mode: int, nredo=None):
+    def _scan_refine(self, qp, mode: int, k: int, thr: float, thr_mode: int, nredo=None, det: bool = False):
         """Fused scan (SLACK extra list entries) + exact re-rank; resolved[q] == 0 marks an unproven list.
-        nredo: device counter of queries needing the dense path (unresolved or nothing passed)."""
+        nredo: device counter of queries needing the dense path (unresolved or nothing passed).  det: also
+        the exact [overall, levels] re-score of the output (hq_refine_rescore_topk, rows staged once)."""
         lo_mode = 0 if thr_mode == 0 else 1
         asc, aid, _, _ = K.scan_topk(qp, self.prep, mode, k + self.SLACK, thr - self.EPS, lo_mode, self.id_base)
-        return K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, thr_mode, self.EPS, self.id_base, redo=nredo,
-                             count_empty=True)
+        fn = K.refine_rescore_topk if det else K.refine_topk
+        return fn(qp, self.prep, mode, asc, aid, k, thr, thr_mode, self.EPS, self.id_base, redo=nredo,
+                  count_empty=True)
 
-    def _final(self, qp, s0, ids, best, bid, K_out: int, bdet=None):
+    def _final(self, qp, s0, ids, best, bid, K_out: int, bdet=None, det=None):
         """Exact overall + per-level re-score of the survivors and of the arg-max, then the final ranking."""
         Q = qp.N
-        det = K.rescore(qp, self.prep, ids, self.id_base)
+        if det is None:
+            det = K.rescore(qp, self.prep, ids, self.id_base)
         if bdet is None:
             bdet = K.rescore(qp, self.prep, bid.view(Q, 1), self.id_base).view(Q, -1)
         return K.progressive_final(s0.unsqueeze(0), ids.unsqueeze(0), det.unsqueeze(0),

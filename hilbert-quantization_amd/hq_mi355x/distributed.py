@@ -67,16 +67,18 @@ class ShardedIndexCorpus:
         c = self.local
         Q = qp.N
         threshold = c._thr(qp, threshold, 1)
-        s0, ids, cnt, res = c._scan_refine(qp, 0, M, float(threshold), 1)
-        best = t.full((Q,), -float("inf"), dtype=t.float64, device=qp.Z.device)
-        bid = t.full((Q,), -1, dtype=t.int64, device=qp.Z.device)
+        s0, ids, cnt, res, det0 = c._scan_refine(qp, 0, M, float(threshold), 1, det=True)
+        # no arg-max on the scan path (count-0 rows are redone below): constant fallback slot
+        best, bid, bdet0 = c._no_fallback(Q, qp.Z.device)
 
-        def records(q, s0_, ids_, best_, bid_):
-            det = K.rescore(q, c.prep, ids_, c.id_base)
-            bdet = K.rescore(q, c.prep, bid_.view(-1, 1), c.id_base)
+        def records(q, s0_, ids_, best_, bid_, det=None, bdet=None):
+            if det is None:
+                det = K.rescore(q, c.prep, ids_, c.id_base)
+            if bdet is None:
+                bdet = K.rescore(q, c.prep, bid_.view(-1, 1), c.id_base)
             return t.cat([pack(s0_, ids_, det), pack(best_.view(-1, 1), bid_.view(-1, 1), bdet)], dim=1)
 
-        rec = records(qp, s0, ids, best, bid)
+        rec = records(qp, s0, ids, best, bid, det0, bdet0.view(Q, 1, -1))
         redo = (res == 0) | (cnt == 0)
         forced = c._forced(qp)
         if forced is not None:

@@ -363,6 +363,26 @@ def refine_topk(q: Prepared, c: Prepared, mode: int, cand_score, cand_id, k: int
     return os_, oi, cnt, res
 
 
+def refine_rescore_topk(q: Prepared, c: Prepared, mode: int, cand_score, cand_id, k: int, threshold: float = 0.0,
+                        thr_mode: int = 0, eps: float = 1e-9, id_base: int = 0, exc=None, redo=None,
+                        count_empty: bool = False):
+    """refine_topk + the exact [overall, level_0..] re-score of its output (rescore's values for the output
+    ids, zeros in empty slots) -> (scores, ids, count, resolved, det [Q, k, 1 + nseg])."""
+    t = torch()
+    Q, kp = cand_id.shape
+    dev = cand_id.device
+    os_ = t.empty((Q, k), dtype=t.float64, device=dev)
+    oi = t.empty((Q, k), dtype=t.int64, device=dev)
+    cnt = t.empty(Q, dtype=t.int32, device=dev)
+    res = t.empty(Q, dtype=t.int32, device=dev)
+    det = t.empty((Q, k, 1 + q.nseg), dtype=t.float64, device=dev)
+    _chk(_L().hq_refine_rescore_topk(ptr(q.R), ptr(q.Z), ptr(q.S), Q, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L, mode,
+                                     ptr(_contig(cand_score)), ptr(_contig(cand_id)), kp, k, float(threshold),
+                                     thr_mode, float(eps), int(id_base), ptr(os_), ptr(oi), ptr(cnt), ptr(res),
+                                     1 if count_empty else 0, ptr(redo), ptr(det), stream()), exc)
+    return os_, oi, cnt, res, det
+
+
 def rescore(q: Prepared, c: Prepared, ids, id_base: int = 0, exc=None):
     """EXACT [overall, level_0..] for (query, global id) pairs in ids [Q, k] -> f64 [Q, k, 1 + nseg]."""
     t = torch()

@@ -219,6 +219,16 @@ int hq_refine_topk(const double* Rq, const double* Zq, const double* Sq, int Q, 
                    double threshold, int thr_mode, double eps, int64_t id_base, double* out_score,
                    int64_t* out_id, int* out_count, int* out_resolved, int count_empty, int* out_redo,
                    hq_stream_t stream);
+/* hq_refine_topk + the exact re-score of its output (core/search_engine.py:191-230 for each output
+ * pair, as hq_rescore computes it): out_det [Q, k, 1 + nseg] = [overall, level 0, level 1, ...] of
+ * every output entry, zeros for empty slots.  The candidates' rows are staged once per query in LDS,
+ * so the progressive search needs no separate hq_rescore launch for its survivors.                  */
+int hq_refine_rescore_topk(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
+                           const double* Zc, const double* Sc, int64_t N, int L, int mode,
+                           const double* cand_score, const int64_t* cand_id, int kp, int k,
+                           double threshold, int thr_mode, double eps, int64_t id_base,
+                           double* out_score, int64_t* out_id, int* out_count, int* out_resolved,
+                           int count_empty, int* out_redo, double* out_det, hq_stream_t stream);
 
 /* ---- S4 on candidate lists: EXACT overall + per-level scores of selected pairs ---------------
  * ids: int64 Q x k GLOBAL ids (row = id - id_base; out of range / < 0 -> zeros);

@@ -302,3 +302,39 @@ def test_cosine_dma_kernels_match_regstage(hq_lib, Q, N, K, monkeypatch):
     for kern in ("lockstep", "regstage"):
         monkeypatch.setenv("HQ_COS_KERNEL", kern)
         np.testing.assert_array_equal(got, _np(K_.cosine_scores_mfma(pa, pb)), err_msg=kern)
+
+
+@pytest.mark.parametrize("L", [64, 32, 256])
+def test_refine_rescore_equals_refine_then_rescore(hq_lib, monkeypatch, L):
+    """hq_refine_rescore_topk (rows staged once in LDS, the re-score of the output from the same rows)
+    returns exactly refine_topk's ranking plus hq_rescore's records for the output ids (zeros in empty
+    slots), for the level-0 and the overall mode, on the LDS-staged and the global-memory kernels
+    (L = 256 stages 97 KiB per query -> the global kernel + hq_rescore)."""
+    from hq_mi355x import kernels as K
+    from hq_mi355x.core.search_engine import IndexCorpus
+    rng = np.random.default_rng(5 + L)
+    N = 3000
+    C = rng.standard_normal((N, L))
+    C[10:14, : L // 2] = 0.5                   # constant level-0 segments
+    C[40:45] = C[9]                            # duplicates (ties by id)
+    Q = np.concatenate([C[[9, 10, 300]], C[500:560] + rng.normal(0, 0.05, (60, L))])
+    corpus = IndexCorpus(C)
+    qp = corpus.prepare_queries(Q)
+    for mode, thr, tm in ((0, 0.1, 1), (1, 0.0, 0), (0, 0.97, 1)):
+        if mode == 1 and not corpus._fused_ok(1):
+            continue  # L = 256: the overall scan does not fuse (Lp > 256)
+        asc, aid, _, _ = K.scan_topk(qp, corpus.prep, mode, 28, thr - corpus.EPS, 0 if tm == 0 else 1)
+        for glob in (False, True):
+            if glob:
+                monkeypatch.setenv("HQ_REFINE_GLOBAL", "1")
+            else:
+                monkeypatch.delenv("HQ_REFINE_GLOBAL", raising=False)
+            s1, i1, c1, r1 = K.refine_topk(qp, corpus.prep, mode, asc, aid, 20, thr, tm, corpus.EPS)
+            s2, i2, c2, r2, det = K.refine_rescore_topk(qp, corpus.prep, mode, asc, aid, 20, thr, tm, corpus.EPS)
+            for x, y in ((s1, s2), (i1, i2), (c1, c2), (r1, r2)):
+                np.testing.assert_array_equal(_np(x), _np(y), err_msg=f"mode {mode} thr {thr} global {glob}")
+            ref = _np(K.rescore(qp, corpus.prep, i1))
+            ids = _np(i1)
+            ref[ids < 0] = 0.0
+            np.testing.assert_array_equal(_np(det), ref, err_msg=f"mode {mode} thr {thr} global {glob}")
+        assert (_np(c1) > 0).any()
