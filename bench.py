@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--dim", type=int, default=1536)
     ap.add_argument("--corpus", type=int, default=1_000_000)
     ap.add_argument("--queries", type=int, default=1000)
-    ap.add_argument("--search-steps", type=int, default=5)
+    ap.add_argument("--search-steps", type=int, default=20)
     ap.add_argument("--no-search", action="store_true")
     ap.add_argument("--no-stream", action="store_true")
     ap.add_argument("--no-precomputed", action="store_true")

@@ -324,13 +324,14 @@ __device__ double exact_pair(const VecSet& A, int64_t ia, const VecSet& B, int64
 }
 
 // dense Q x N exact scores (drop-in path and rare exact fallbacks)
+template <bool SM = false>
 __global__ __launch_bounds__(256) void k_level_scores(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si, int level,
                                                       double* __restrict__ out) {
   const int64_t total = (int64_t)Q * N;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t q = t / N, c = t % N;
-    out[t] = exact_pair(Qs, q, Cs, c, si, level, nullptr);
+    out[t] = exact_pair<SM>(Qs, q, Cs, c, si, level, nullptr);
   }
 }
 
@@ -2920,7 +2921,11 @@ int hq_level_scores(const double* Rq, const double* Zq, const double* Sq, int Q,
   const int64_t total = (int64_t)Q * N;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(k_level_scores, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
+  if (seg_small(si))
+    hipLaunchKernelGGL(k_level_scores<true>, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
+                     VecSet{Rc, Zc, Sc}, N, si, level, scores);
+  else
+    hipLaunchKernelGGL(k_level_scores<false>, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q,
                      VecSet{Rc, Zc, Sc}, N, si, level, scores);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
