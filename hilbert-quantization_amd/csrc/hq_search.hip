@@ -1181,6 +1181,12 @@ __device__ __forceinline__ int shr1_f32i(float v) { return shr1_i32(__float_as_i
 // T = thl - kMarginF; 0.35 - T is kept per query (k0) and refreshed only when a threshold moves.
 // The step loop is unrolled by two (ping-pong registers for the next step's fragments/statistics),
 // candidate pointers advance by a constant per step.
+// broadcast lane k of each 16-lane row (DPP row_newbcast)
+template <int K>
+__device__ __forceinline__ float rbc(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + K, 0xF, 0xF, false));
+}
+
 // G-only pre-filter threshold of k_scan0f (see the comment at refresh_k0): smallest G that can pass
 // the filter for list threshold t; out of line (rare: called when a threshold moves)
 __device__ __noinline__ float gstar0(float t, float qA, float qB, float qQ, float c1f) {
@@ -1264,26 +1270,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   const bool myq = lane < QW && q0 + lane < a.Q;
 
   // candidate rows are padded (kPad0, hq_seg_pack0_split): no clamping, rows past c_end are masked
+  // Candidate statistics: the 16 rows of a step are 4 SoA groups = 64 contiguous floats; lane (g, j)
+  // loads float j of group g (one coalesced dword per lane instead of four 16-B loads that 16 lanes
+  // repeat), and the values are broadcast within the 16-lane row by DPP row_newbcast when the full
+  // filter needs them (rbc<k>).  The flag bits come from one ballot over lanes j >= 12.
   struct CStep {
-    half8 f[2];   // fragment: hi, lo of row cs + j, k range [8g, 8g + 8)
+    half8 f[2];  // fragment: hi, lo of row cs + j, k range [8g, 8g + 8)
+    float st;    // SoA statistics float j of group g: std[4], mean[4], msq[4], flags[4]
+  };
+  struct SStat {
     flt4 sd, mn, ms;  // statistics of rows 4g .. 4g + 3
-    int fm;       // bit r: row 4g + r flagged (zero variance / f32-unsafe / pad)
   };
   const _Float16* pz = a.Zc16 + (c_begin + j) * kZ16Row + 8 * g;
-  const float* pst = a.Sc32 + (c_begin / 4 + g) * 16;
+  const float* pst = a.Sc32 + (c_begin / 4 + g) * 16 + j;
   auto load_step = [&](CStep& c) {
     c.f[0] = *reinterpret_cast<const half8*>(pz);
     c.f[1] = *reinterpret_cast<const half8*>(pz + 32);
-    c.sd = *reinterpret_cast<const flt4*>(pst);
-    c.mn = *reinterpret_cast<const flt4*>(pst + 4);
-    c.ms = *reinterpret_cast<const flt4*>(pst + 8);
-    const flt4 fl = *reinterpret_cast<const flt4*>(pst + 12);
-    c.fm = (int)(__float_as_int(fl.x) != 0) | ((int)(__float_as_int(fl.y) != 0) << 1) |
-           ((int)(__float_as_int(fl.z) != 0) << 2) | ((int)(__float_as_int(fl.w) != 0) << 3);
-    if (a.expt != 6) {  // 6: diagnostics only (wrong results) - every step re-reads the first step's rows
-      pz += kCS * kZ16Row;
-      pst += kCS * 4;
-    }
+    c.st = *pst;
+    pz += kCS * kZ16Row;
+    pst += kCS * 4;
+  };
+  auto expand = [&](const float st, SStat& x) {
+    x.sd = flt4{rbc<0>(st), rbc<1>(st), rbc<2>(st), rbc<3>(st)};
+    x.mn = flt4{rbc<4>(st), rbc<5>(st), rbc<6>(st), rbc<7>(st)};
+    x.ms = flt4{rbc<8>(st), rbc<9>(st), rbc<10>(st), rbc<11>(st)};
+  };
+  // bit r: row 4g + r flagged (zero variance / f32-unsafe / pad)
+  auto flags = [&](const float st) -> int {
+    return (int)(__ballot(j >= 12 && __float_as_int(st) != 0) >> (16 * g + 12)) & 0xF;
   };
   // G of two 16-query blocks: hi.hi + hi.lo + lo.hi, two accumulation chains interleaved
   auto mfma_half = [&](const int h, const half8* f, flt4* acc) {
@@ -1301,16 +1315,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   // (den > 0; E den + num is one fma, its sign exact).  Flagged candidates, absent queries and rows
   // past the chunk end are bit masks, applied only when some lane of the wave has a candidate pass
   // (the common half-step ends after one ballot).
-  auto filter_half = [&](const int h, const flt4* acc, const CStep& c, const int rem) -> int {
+  auto filter_half = [&](const int h, const flt4* acc, const float st, const int fm, SStat& x, bool& have,
+                         const int rem) -> int {
     // G-only pre-filter (see gstar0): most half-steps end here after 4 max and 2 compares
     const float g0 = fmaxf(fmaxf(acc[0].x, acc[0].y), fmaxf(acc[0].z, acc[0].w));
     const float g1 = fmaxf(fmaxf(acc[1].x, acc[1].y), fmaxf(acc[1].z, acc[1].w));
-    const unsigned long long pre = __ballot((g0 >= gs[2 * h]) | (g1 >= gs[2 * h + 1]) | (c.fm != 0));
+    const unsigned long long pre = a.expt == 8 ? 0ull : __ballot((g0 >= gs[2 * h]) | (g1 >= gs[2 * h + 1]) | (fm != 0));
     if (a.expt == 3 && lane == 0) {
       atomicAdd(a.dbg + 6, 1ull);
       if (pre) atomicAdd(a.dbg + 5, 1ull);
     }
     if (a.expt != 5 && !pre) return 0;
+    if (a.expt == 7) return 0;  // diagnostics only: base cost of the step (no full filter, no inserts)
+    if (!have) {
+      expand(st, x);
+      have = true;
+    }
     const flt2 c1v = {c1f, c1f};
     flt2 m[4];  // [2u + p]: rows (2p, 2p + 1) of query block 2h + u
     float mx = -__builtin_huge_valf();
@@ -1321,9 +1341,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const flt2 G2 = p == 0 ? acc[u].xy : acc[u].zw;
-        const flt2 sd2 = p == 0 ? c.sd.xy : c.sd.zw;
-        const flt2 mn2 = p == 0 ? c.mn.xy : c.mn.zw;
-        const flt2 ms2 = p == 0 ? c.ms.xy : c.ms.zw;
+        const flt2 sd2 = p == 0 ? x.sd.xy : x.sd.zw;
+        const flt2 mn2 = p == 0 ? x.mn.xy : x.mn.zw;
+        const flt2 ms2 = p == 0 ? x.ms.xy : x.ms.zw;
         const flt2 E = __builtin_elementwise_fma(G2, c1v, K0);
         const flt2 num = __builtin_elementwise_fma(G2, A2 * sd2, B2 * mn2);
         const flt2 d = __builtin_elementwise_fma(E, Q2 + ms2, num);
@@ -1332,14 +1352,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         mx = fmaxf(mx, fmaxf(mm.x, mm.y));
       }
     }
-    if (!__ballot((mx >= 0.0f) | (c.fm != 0))) return 0;
+    if (!__ballot((mx >= 0.0f) | (fm != 0))) return 0;
     int bits = 0;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int p = 0; p < 2; ++p)
         bits |= ((int)(m[2 * u + p].x >= 0.0f) << (4 * u + 2 * p)) | ((int)(m[2 * u + p].y >= 0.0f) << (4 * u + 2 * p + 1));
-    bits |= c.fm * 0x11;
+    bits |= fm * 0x11;
     const int nv = rem - 4 * g;  // rows of this lane group inside the chunk
     const int rowm = nv >= 4 ? 0xF : (nv <= 0 ? 0 : (1 << nv) - 1);
     const int b0 = 2 * h, b1 = 2 * h + 1;
@@ -1400,7 +1420,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   };
   // score, test and file the passing pairs of one half: f32 for plain pairs (the filter's expression
   // with the division), f64 statistics for flagged pairs
-  auto insert_half = [&](const int h, const flt4* acc, const CStep& c, const int64_t cs, const int bits) {
+  auto insert_half = [&](const int h, const flt4* acc, const SStat& c, const int fm, const int64_t cs,
+                         const int bits) {
     if (a.expt == 3 && lane == 0) atomicAdd(a.dbg, 1ull);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -1415,7 +1436,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
           atomicAdd(a.dbg + 4, 1ull);
         }
         float s = -__builtin_huge_valf();
-        const bool flagged = (((qsp >> b) & 1) != 0) | (((c.fm >> r) & 1) != 0);
+        const bool flagged = (((qsp >> b) & 1) != 0) | (((fm >> r) & 1) != 0);
         if (pb && !flagged) {
           const float G = acc[u][r];
           const float num = fmaf(G, qA[b] * c.sd[r], qB[b] * c.mn[r]);
@@ -1485,11 +1506,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     load_step(nxt);  // rows past the chunk (padded array): harmless, masked
     const int rem = (int)(c_end - cs);
     mfma_half(1, cur.f, acc1);
-    const int bits0 = filter_half(0, acc0, cur, rem);
-    if (__ballot(bits0 != 0)) insert_half(0, acc0, cur, cs, bits0);
+    const int fm = flags(cur.st);
+    SStat x;
+    bool have = false;
+    const int bits0 = filter_half(0, acc0, cur.st, fm, x, have, rem);
+    if (__ballot(bits0 != 0)) insert_half(0, acc0, x, fm, cs, bits0);
     mfma_half(0, nxt.f, acc0);
-    const int bits1 = filter_half(1, acc1, cur, rem);
-    if (__ballot(bits1 != 0)) insert_half(1, acc1, cur, cs, bits1);
+    const int bits1 = filter_half(1, acc1, cur.st, fm, x, have, rem);
+    if (__ballot(bits1 != 0)) insert_half(1, acc1, x, fm, cs, bits1);
     if ((step & 3) == 0) {
       if (gt_bits != 0ull) {
         const float gf = (float)__longlong_as_double((long long)gt_bits);  // exact: list values are f32
