@@ -1564,10 +1564,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 // registers; larger ones are re-read per bisection step.
 constexpr int kPoolReg = 16;
 
+// th0 / thr0: the scan's sampled starting thresholds and the caller's threshold.  A starting threshold
+// from the sample's K'-th best (K' < K, see k_sample_kth) is not a provable lower bound of the K-th
+// best: a query whose pool then holds fewer than K entries while th0 > thr0 may miss pairs below th0,
+// so its empty slots are marked with score +inf (id -1), which hq_refine_topk reads as "unresolved".
 __global__ __launch_bounds__(64) void k_pool_select(const float* __restrict__ pool_s, const int* __restrict__ pool_i,
                                                     const int* __restrict__ pool_n, int cap, int Q, int K,
                                                     int64_t id_base, double* __restrict__ out_score,
-                                                    int64_t* __restrict__ out_id) {
+                                                    int64_t* __restrict__ out_id, const double* __restrict__ th0,
+                                                    double thr0) {
   const int lane = threadIdx.x;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
     const int T = pool_n[q];
@@ -1701,7 +1706,8 @@ __global__ __launch_bounds__(64) void k_pool_select(const float* __restrict__ po
       out_id[(int64_t)q * K + rank] = (int64_t)ei + id_base;
     }
     if (lane >= k && lane < K) {
-      out_score[(int64_t)q * K + lane] = -__builtin_huge_val();
+      const bool trunc = th0 != nullptr && th0[q] > thr0;
+      out_score[(int64_t)q * K + lane] = trunc ? __builtin_huge_val() : -__builtin_huge_val();
       out_id[(int64_t)q * K + lane] = -1;
     }
     __syncthreads();
@@ -1826,6 +1832,7 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
 // No LDS, no atomics: occupancy is set by VGPRs alone.  Output: top[(q * nstreams + 4 chunk + g) *
 // kTopT + t], every entry of every existing query written (-1 = empty).
 constexpr int kTopT = 2;
+constexpr int kSampleKth = 16;
 
 __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
@@ -2203,59 +2210,107 @@ __global__ __launch_bounds__(64) void k_progressive_final(int R, int Q, int M, i
 // top-k of a dense score matrix per query (one wave per query): (score desc, id asc) with the
 // threshold test, plus the first arg-max over all candidates.  Used when k exceeds the fused
 // scan's LDS lists (e.g. the reference engine's default max_candidates_per_level = 100).
+// Top-k (score desc, id asc) of one candidate row among entries passing the threshold test, plus the
+// first arg-max over all entries; one wave.  Candidate c has id rid[c] (rid != NULL; -1 = empty) or c;
+// ids are written with id_base added.  k passes, each after the previous pick in the total order.
+__device__ void select_row(const double* __restrict__ row, const int64_t* __restrict__ rid, int64_t n, int k,
+                           double thr, int thr_mode, int64_t id_base, double* __restrict__ out_s,
+                           int64_t* __restrict__ out_id, double* __restrict__ best, int64_t* __restrict__ best_id) {
+  const int lane = threadIdx.x & 63;
+  double ps = __builtin_huge_val();
+  int64_t pid = -1;
+  for (int j = 0; j < k; ++j) {
+    double bs = 0.0;
+    int64_t bi = -1;
+    for (int64_t c = lane; c < n; c += 64) {
+      const int64_t id = rid ? rid[c] : c;
+      if (id < 0) continue;
+      const double s = row[c];
+      const bool ok = thr_mode == 0 || (thr_mode == 1 ? s >= thr : s > thr);
+      if (!ok) continue;
+      if (pid >= 0 && !better(ps, pid, s, id)) continue;  // must come after the previous pick
+      if (bi < 0 || better(s, id, bs, bi)) { bs = s; bi = id; }
+    }
+    for (int o = 1; o < 64; o <<= 1) {
+      const double s2 = __shfl_xor(bs, o, 64);
+      const int64_t i2 = __shfl_xor(bi, o, 64);
+      if (i2 >= 0 && (bi < 0 || better(s2, i2, bs, bi))) { bs = s2; bi = i2; }
+    }
+    if (lane == 0) {
+      out_s[j] = bi >= 0 ? bs : -__builtin_huge_val();
+      out_id[j] = bi >= 0 ? bi + id_base : -1;
+    }
+    if (bi < 0) {
+      for (int jj = j + 1 + lane; jj < k; jj += 64) {
+        out_s[jj] = -__builtin_huge_val();
+        out_id[jj] = -1;
+      }
+      break;
+    }
+    ps = bs;
+    pid = bi;
+  }
+  if (best) {
+    double bs = 0.0;
+    int64_t bi = -1;
+    for (int64_t c = lane; c < n; c += 64) {
+      const int64_t id = rid ? rid[c] : c;
+      if (id < 0) continue;
+      if (bi < 0 || better(row[c], id, bs, bi)) { bs = row[c]; bi = id; }
+    }
+    for (int o = 1; o < 64; o <<= 1) {
+      const double s2 = __shfl_xor(bs, o, 64);
+      const int64_t i2 = __shfl_xor(bi, o, 64);
+      if (i2 >= 0 && (bi < 0 || better(s2, i2, bs, bi))) { bs = s2; bi = i2; }
+    }
+    if (lane == 0) {
+      *best = bi >= 0 ? bs : -__builtin_huge_val();
+      *best_id = bi >= 0 ? bi + id_base : -1;
+    }
+  }
+}
+
 __global__ __launch_bounds__(64) void k_select(const double* __restrict__ sc, int Q, int64_t N, int k, double thr,
                                                int thr_mode, int64_t id_base, double* __restrict__ out_s,
                                                int64_t* __restrict__ out_id, double* __restrict__ best,
                                                int64_t* __restrict__ best_id) {
-  const int lane = threadIdx.x;
+  for (int q = blockIdx.x; q < Q; q += gridDim.x)
+    select_row(sc + (int64_t)q * N, nullptr, N, k, thr, thr_mode, id_base, out_s + (int64_t)q * k,
+               out_id + (int64_t)q * k, best ? best + q : nullptr, best ? best_id + q : nullptr);
+}
+
+// Two-stage select for long rows: stage 1, one wave per (query, part of plen entries): the part's
+// top-k and arg-max with row-local ids into the workspace; stage 2 (k_select_merge): the same
+// selection over each query's P x k candidates (ids carried) and P arg-maxes.  The total order is the
+// same, so the result equals the one-stage select.
+__global__ __launch_bounds__(64) void k_select_part(const double* __restrict__ sc, int Q, int64_t N, int P,
+                                                    int64_t plen, int k, double thr, int thr_mode,
+                                                    double* __restrict__ ws_s, int64_t* __restrict__ ws_id,
+                                                    double* __restrict__ ws_b, int64_t* __restrict__ ws_bid) {
+  for (int64_t t = blockIdx.x; t < (int64_t)Q * P; t += gridDim.x) {
+    const int64_t q = t / P, p = t % P;
+    const int64_t c0 = p * plen;
+    const int64_t n = c0 >= N ? 0 : (N - c0 < plen ? N - c0 : plen);
+    select_row(sc + q * N + c0, nullptr, n, k, thr, thr_mode, c0, ws_s + t * k, ws_id + t * k, ws_b + t,
+               ws_bid + t);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_select_merge(int Q, int P, int k, double thr, int thr_mode, int64_t id_base,
+                                                     const double* __restrict__ ws_s,
+                                                     const int64_t* __restrict__ ws_id,
+                                                     const double* __restrict__ ws_b,
+                                                     const int64_t* __restrict__ ws_bid, double* __restrict__ out_s,
+                                                     int64_t* __restrict__ out_id, double* __restrict__ best,
+                                                     int64_t* __restrict__ best_id) {
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
-    const double* row = sc + (int64_t)q * N;
-    // previous pick (strictly worse order follows it)
-    double ps = __builtin_huge_val();
-    int64_t pid = -1;
-    for (int j = 0; j < k; ++j) {
-      double bs = 0.0;
-      int64_t bi = -1;
-      for (int64_t c = lane; c < N; c += 64) {
-        const double s = row[c];
-        const bool ok = thr_mode == 0 || (thr_mode == 1 ? s >= thr : s > thr);
-        if (!ok) continue;
-        if (pid >= 0 && !better(ps, pid, s, c)) continue;  // must come after the previous pick
-        if (bi < 0 || better(s, c, bs, bi)) { bs = s; bi = c; }
-      }
-      for (int o = 1; o < 64; o <<= 1) {
-        const double s2 = __shfl_xor(bs, o, 64);
-        const int64_t i2 = __shfl_xor(bi, o, 64);
-        if (i2 >= 0 && (bi < 0 || better(s2, i2, bs, bi))) { bs = s2; bi = i2; }
-      }
-      if (lane == 0) {
-        out_s[(int64_t)q * k + j] = bi >= 0 ? bs : -__builtin_huge_val();
-        out_id[(int64_t)q * k + j] = bi >= 0 ? bi + id_base : -1;
-      }
-      if (bi < 0) {
-        for (int jj = j + 1 + lane; jj < k; jj += 64) {
-          out_s[(int64_t)q * k + jj] = -__builtin_huge_val();
-          out_id[(int64_t)q * k + jj] = -1;
-        }
-        break;
-      }
-      ps = bs;
-      pid = bi;
-    }
+    const int64_t o = (int64_t)q * P * k;
+    select_row(ws_s + o, ws_id + o, (int64_t)P * k, k, thr, thr_mode, id_base, out_s + (int64_t)q * k,
+               out_id + (int64_t)q * k, nullptr, nullptr);
     if (best) {
-      double bs = 0.0;
-      int64_t bi = -1;
-      for (int64_t c = lane; c < N; c += 64)
-        if (bi < 0 || better(row[c], c, bs, bi)) { bs = row[c]; bi = c; }
-      for (int o = 1; o < 64; o <<= 1) {
-        const double s2 = __shfl_xor(bs, o, 64);
-        const int64_t i2 = __shfl_xor(bi, o, 64);
-        if (i2 >= 0 && (bi < 0 || better(s2, i2, bs, bi))) { bs = s2; bi = i2; }
-      }
-      if (lane == 0) {
-        best[q] = bi >= 0 ? bs : -__builtin_huge_val();
-        best_id[q] = bi >= 0 ? bi + id_base : -1;
-      }
+      // arg-max of the part arg-maxes: thr_mode 0 top-1 over (score, id) = the first arg-max
+      select_row(ws_b + (int64_t)q * P, ws_bid + (int64_t)q * P, P, 1, 0.0, 0, id_base, best + q, best_id + q,
+                 nullptr, nullptr);
     }
   }
 }
@@ -2331,7 +2386,9 @@ __global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int6
     if (lane == 0) {
       ocnt[q] = cnt;
       const bool full = cid[base + kp - 1] >= 0;
-      int res = 1;
+      // an empty last slot with score +inf: the scan's list may be incomplete (k_pool_select)
+      const bool trunc = !full && cs[base + kp - 1] == __builtin_huge_val();
+      int res = trunc ? 0 : 1;
       if (full) {
         const double bound = cs[base + kp - 1] + eps;
         if (n >= k) res = bound < kth;
@@ -2508,7 +2565,9 @@ __global__ __launch_bounds__(256) void k_refine_lds(VecSet Qs, int Q, VecSet Cs,
       if (lane == 0) {
         ocnt[q] = cnt;
         const bool full = cid[base + kp - 1] >= 0;
-        int res = 1;
+        // an empty last slot with score +inf: the scan's list may be incomplete (k_pool_select)
+        const bool trunc = !full && cs[base + kp - 1] == __builtin_huge_val();
+        int res = trunc ? 0 : 1;
         if (full) {
           const double bound = cs[base + kp - 1] + eps;
           if (n >= k) res = bound < kth;
@@ -2736,6 +2795,10 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   b.pool_i = reinterpret_cast<int*>(ws + (size_t)Q * b.pool_cap * 4);
   const bool sample = getenv("HQ_SCAN_NOSAMPLE") == nullptr;
   const bool top_sample = sample && f32 && getenv("HQ_SAMPLE_HIST") == nullptr;  // default: top-T sample
+  // K' of the starting threshold: the sample's K'-th best (statistical for K' < k: pools left short are
+  // marked for the exact path, k_pool_select); HQ_SAMPLE_KTH=0 -> k (a provable bound)
+  int sample_kth = getenv("HQ_SAMPLE_KTH") ? atoi(getenv("HQ_SAMPLE_KTH")) : kSampleKth;
+  if (sample_kth <= 0 || sample_kth > k) sample_kth = k;
   float* top = reinterpret_cast<float*>(ws + lists + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 4 +
                                         (size_t)Q * 8);
   // (the histogram region lies between gtau and pool_n, so it is cleared with them in every mode)
@@ -2749,13 +2812,14 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     sa.Zq32 = nullptr; sa.Zc32 = nullptr; sa.Zq16 = Zq16; sa.Zc16 = Zc16; sa.Sq32 = Sq32; sa.Sc32 = Sc32;
     sa.Lp = b.Lp; sa.nseg = b.nseg; sa.P0 = b.P0; sa.inv_m = b.inv_m; sa.c1 = b.c1;
     sample_top_geometry(Q, N, sa.stride, sa.S, sa.nqb, sa.nchunks, sa.chunk_len);
+    if (sa.stride < 16) sample_kth = k;  // dense samples (small corpora): the provable bound is tight enough
     sa.hist = nullptr;
     sa.top = top;
     sa.K = k;
     hipLaunchKernelGGL(k_sample_topf, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
     HQ_CHECK_LAUNCH();
     const int mg = Q < 8192 ? Q : 8192;
-    hipLaunchKernelGGL(k_sample_kth, dim3(mg), dim3(64), 0, s, (const float*)top, 4 * sa.nchunks, Q, k,
+    hipLaunchKernelGGL(k_sample_kth, dim3(mg), dim3(64), 0, s, (const float*)top, 4 * sa.nchunks, Q, sample_kth,
                        (double)kMarginF, th0);
     HQ_CHECK_LAUNCH();
     b.th0 = th0;
@@ -2781,7 +2845,8 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   if (f32) {
     const int mg = Q < 8192 ? Q : 8192;
     hipLaunchKernelGGL(k_pool_select, dim3(mg), dim3(64), 0, s, (const float*)b.pool_s, (const int*)b.pool_i,
-                       (const int*)b.pool_n, b.pool_cap, Q, k, id_base, out_score, out_id);
+                       (const int*)b.pool_n, b.pool_cap, Q, k, id_base, out_score, out_id,
+                       top_sample && sample_kth < k ? (const double*)th0 : (const double*)nullptr, b.thr0);
     HQ_CHECK_LAUNCH();
   }
   if (b.expt == 3) {
@@ -3146,6 +3211,54 @@ int hq_progressive_final(int R, int Q, int M, int nseg, const double* s0, const 
   const int grid = Q < 8192 ? Q : 8192;
   hipLaunchKernelGGL(k_progressive_final, dim3(grid), dim3(64), 0, (hipStream_t)stream, R, Q, M, W, s0, ids, det,
                      best, best_id, best_det, K, out_id, out_det, out_count);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+// parts of the two-stage select: ~8192 entries each, <= 1024 per query
+static void select_parts(int Q, int64_t N, int& P, int64_t& plen) {
+  int64_t p = (N + 8191) / 8192;
+  if (p > 1024) p = 1024;
+  if (p < 1) p = 1;
+  P = (int)p;
+  plen = (N + P - 1) / P;
+}
+
+size_t hq_select_workspace_size(int Q, int64_t N, int k) {
+  if (Q <= 0 || N <= 0 || k <= 0) return 0;
+  int P;
+  int64_t plen;
+  select_parts(Q, N, P, plen);
+  return (size_t)Q * P * ((size_t)k + 1) * 16 + 256;
+}
+
+int hq_select_topk_ws(const double* scores, int Q, int64_t N, int k, double threshold, int thr_mode,
+                      int64_t id_base, void* workspace, size_t workspace_bytes, double* out_score, int64_t* out_id,
+                      double* out_best, int64_t* out_best_id, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || k <= 0) return fail(HQ_E_INVALID, "bad shape");
+  if (Q == 0) return HQ_OK;
+  int P;
+  int64_t plen;
+  select_parts(Q, N, P, plen);
+  if (P == 1 || !workspace)
+    return hq_select_topk(scores, Q, N, k, threshold, thr_mode, id_base, out_score, out_id, out_best, out_best_id,
+                          stream);
+  if (!out_score || !out_id || !scores) return fail(HQ_E_INVALID, "null buffer");
+  if (workspace_bytes < hq_select_workspace_size(Q, N, k)) return fail(HQ_E_INVALID, "workspace too small");
+  uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
+  const size_t nk = (size_t)Q * P * k;
+  double* ws_s = reinterpret_cast<double*>(ws);
+  int64_t* ws_id = reinterpret_cast<int64_t*>(ws + nk * 8);
+  double* ws_b = reinterpret_cast<double*>(ws + nk * 16);
+  int64_t* ws_bid = reinterpret_cast<int64_t*>(ws + nk * 16 + (size_t)Q * P * 8);
+  const int64_t g1 = (int64_t)Q * P < 65536 ? (int64_t)Q * P : 65536;
+  hipLaunchKernelGGL(k_select_part, dim3((unsigned)g1), dim3(64), 0, (hipStream_t)stream, scores, Q, N, P, plen, k,
+                     threshold, thr_mode, ws_s, ws_id, ws_b, ws_bid);
+  HQ_CHECK_LAUNCH();
+  const int g2 = Q < 4096 ? Q : 4096;
+  hipLaunchKernelGGL(k_select_merge, dim3(g2), dim3(64), 0, (hipStream_t)stream, Q, P, k, threshold, thr_mode, id_base,
+                     (const double*)ws_s, (const int64_t*)ws_id, (const double*)ws_b, (const int64_t*)ws_bid,
+                     out_score, out_id, out_best, out_best_id);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }

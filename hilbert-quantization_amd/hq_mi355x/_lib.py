@@ -66,6 +66,8 @@ SIGNATURES = {
     "hq_progressive_final": (_i, [_i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
     "hq_cosine_scores": (_i, [_p, _i, _p, _i64, _i, _p, _p]),
     "hq_select_topk": (_i, [_p, _i, _i64, _i, _d, _i, _i64, _p, _p, _p, _p, _p]),
+    "hq_select_workspace_size": (_sz, [_i, _i64, _i]),
+    "hq_select_topk_ws": (_i, [_p, _i, _i64, _i, _d, _i, _i64, _p, _sz, _p, _p, _p, _p, _p]),
     "hq_pair_scores_raw": (_i, [_p, _p, _i64, _i, _p, _p]),
     "hq_pair_scores_raw_src": (_i, [_p, _p, _i64, _i, _i, _i, _p, _p]),
     "hq_precomputed_layout": (_i, [_i, _i, _i, _p, _i]),

@@ -435,8 +435,10 @@ def select_topk(scores, k: int, threshold: float = 0.0, thr_mode: int = 0, id_ba
     oi = t.empty((Q, k), dtype=t.int64, device=dev)
     b = t.empty(Q, dtype=t.float64, device=dev)
     bi = t.empty(Q, dtype=t.int64, device=dev)
-    _chk(_L().hq_select_topk(ptr(sc), Q, N, k, float(threshold), thr_mode, int(id_base), ptr(os_), ptr(oi), ptr(b),
-                             ptr(bi), stream()), exc)
+    ws_bytes = int(_L().hq_select_workspace_size(Q, N, k))
+    ws = t.empty(max(ws_bytes, 1), dtype=t.uint8, device=dev)
+    _chk(_L().hq_select_topk_ws(ptr(sc), Q, N, k, float(threshold), thr_mode, int(id_base), ptr(ws), ws_bytes,
+                                ptr(os_), ptr(oi), ptr(b), ptr(bi), stream()), exc)
     return os_, oi, b, bi
 
 

@@ -197,6 +197,11 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
  * of the zero-padded level-0 segment) and S32, f32 statistics (std, mean, msq, flag bits) in SoA
  * groups of 4 rows (std[4], mean[4], msq[4], flags[4]) for round_up(N, 4) + 48 rows (16 B per row);
  * Sq/Sc are the f64 statistics of hq_seg_prepare.  Level-0 segments of up to 32 values, N < 2^31. */
+/* Starting threshold of hq_scan0_topk_split: the K'-th best score of a 1/16 row sample minus the error
+ * margin, K' = 16 (HQ_SAMPLE_KTH; K' = k, a provable lower bound of the k-th best, for corpora below
+ * 16 x 4096 rows).  With K' < k a query can end with fewer than k listed candidates although more pass
+ * the caller's threshold: its empty slots then carry score +inf (id -1), which hq_refine_topk /
+ * hq_refine_rescore_topk report as unresolved (the caller's dense exact path answers the query).    */
 int hq_seg_level0_len(int L);
 int hq_seg_pack0_split(const double* Z, const double* S, int64_t N, int L, void* Z16, float* S32,
                        hq_stream_t stream);
@@ -255,6 +260,14 @@ int hq_progressive_final(int R, int Q, int M, int nseg, const double* s0, const 
 int hq_select_topk(const double* scores, int Q, int64_t N, int k, double threshold, int thr_mode,
                    int64_t id_base, double* out_score, int64_t* out_id, double* out_best,
                    int64_t* out_best_id, hq_stream_t stream);
+/* Two-stage form of hq_select_topk for long rows (the dense exact fallback: few queries x a 1M-row
+ * corpus): parts of ~8192 entries select their own top-k and arg-max in parallel (one wave each), then
+ * one wave per query merges the parts' candidates in the same total order - identical results.
+ * workspace: hq_select_workspace_size(Q, N, k) bytes (0 / NULL -> the one-stage kernel).           */
+size_t hq_select_workspace_size(int Q, int64_t N, int k);
+int hq_select_topk_ws(const double* scores, int Q, int64_t N, int k, double threshold, int thr_mode,
+                      int64_t id_base, void* workspace, size_t workspace_bytes, double* out_score,
+                      int64_t* out_id, double* out_best, int64_t* out_best_id, hq_stream_t stream);
 
 /* ---- S3 on raw segments (candidate pools of mixed index length) -------------------------------
  * compare_indices_at_level for the level segments already sliced and truncated to a common length

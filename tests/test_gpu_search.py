@@ -338,3 +338,68 @@ def test_refine_rescore_equals_refine_then_rescore(hq_lib, monkeypatch, L):
             ref[ids < 0] = 0.0
             np.testing.assert_array_equal(_np(det), ref, err_msg=f"mode {mode} thr {thr} global {glob}")
         assert (_np(c1) > 0).any()
+
+
+@pytest.mark.parametrize("Q,N,k,thr,tm", [(3, 100_003, 20, 0.5, 1), (2, 70_000, 28, 0.0, 0), (5, 20_000, 10, 0.75, 2),
+                                          (1, 8_193, 64, 0.0, 0)])
+def test_two_stage_select_equals_one_stage(hq_lib, Q, N, k, thr, tm):
+    """hq_select_topk_ws (parts of ~8192 entries in parallel, then a merge in the same total order) gives the
+    one-stage hq_select_topk's top-k, ids and first arg-max exactly, with heavy ties (scores on a coarse
+    grid), entries below the threshold and rows where fewer than k entries pass."""
+    import torch
+    from hq_mi355x import _lib, kernels as K
+    from hq_mi355x._dev import ptr, stream
+    rng = np.random.default_rng(Q * 7 + k)
+    sc = np.round(rng.random((Q, N)), 2)       # ties everywhere
+    sc[0, N // 3] = 2.0                        # unique maximum in a middle part
+    if Q > 1:
+        sc[1, :] = np.minimum(sc[1, :], thr)   # nothing (or everything at thr) passes in row 1
+    S = _t(sc)
+    a = K.select_topk(S, k, thr, tm, 5)
+    os_ = torch.empty((Q, k), dtype=torch.float64, device=S.device)
+    oi = torch.empty((Q, k), dtype=torch.int64, device=S.device)
+    b = torch.empty(Q, dtype=torch.float64, device=S.device)
+    bi = torch.empty(Q, dtype=torch.int64, device=S.device)
+    _lib.check(_lib.lib().hq_select_topk(ptr(S), Q, N, k, float(thr), tm, 5, ptr(os_), ptr(oi), ptr(b), ptr(bi),
+                                         stream()))
+    for x, y in zip(a, (os_, oi, b, bi)):
+        np.testing.assert_array_equal(_np(x), _np(y))
+    ok = sc >= thr if tm == 1 else (sc > thr if tm == 2 else np.ones_like(sc, bool))
+    for q in range(Q):
+        pos = np.nonzero(ok[q])[0]
+        ref = pos[np.lexsort((pos, -sc[q, pos]))][:k] + 5
+        got = _np(a[1])[q]
+        assert list(got[got >= 0]) == list(ref)
+
+
+def test_statistical_start_threshold_is_exact(hq_lib, monkeypatch):
+    """A starting threshold from the sample's K'-th best (K' < K; the default is 16 on sparse samples) is not
+    a provable bound: lists left short are marked (+inf in the empty slots) and their queries answered by
+    the dense exact path.  With K' = 1 most lists are short; the progressive results must equal the
+    provable mode's (HQ_SAMPLE_KTH=0) and the oracle's."""
+    from hq_mi355x import kernels as K
+    from hq_mi355x.core.search_engine import IndexCorpus
+    rng = np.random.default_rng(31)
+    N, L = 70_000, 64                           # sample stride 17: the statistical threshold applies
+    C = rng.standard_normal((N, L))
+    C[500:520] = C[77]                          # duplicates of a query row
+    Q = np.concatenate([C[[77, 5, 9000]], C[100:140] + rng.normal(0, 0.05, (40, L))])
+    corpus = IndexCorpus(C)
+    out = {}
+    for kth in ("0", "16", "1"):
+        monkeypatch.setenv("HQ_SAMPLE_KTH", kth)
+        ids, ov, lv, cnt = corpus.progressive(Q, 10, 0.1, 20)
+        out[kth] = (_np(ids), _np(ov), _np(lv), _np(cnt))
+        if kth == "1":
+            qp = corpus.prepare_queries(Q)
+            asc, aid, _, _ = K.scan_topk(qp, corpus.prep, 0, 28, 0.1 - corpus.EPS, 1)
+            _, _, _, res = K.refine_topk(qp, corpus.prep, 0, asc, aid, 20, 0.1, 1, corpus.EPS)
+            trunc = (_np(aid)[:, -1] < 0) & (_np(asc)[:, -1] == np.inf)
+            assert trunc.any() and not _np(res)[trunc].any()
+    for kth in ("16", "1"):
+        for x, y in zip(out["0"], out[kth]):
+            np.testing.assert_array_equal(x, y, err_msg=kth)
+    ids, cnt = out["1"][0], out["1"][3]
+    for a in (0, 1, 20):
+        rid, _, _, _ = O.progressive_search(Q[a], C, 10, 0.1, 20)
+        assert list(ids[a][: cnt[a]]) == list(rid), a
