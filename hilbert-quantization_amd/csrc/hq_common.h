@@ -314,6 +314,12 @@ __device__ __forceinline__ float wmax64(float v) {
   v = fmaxf(v, dppf<0x140>(v));
   return fmaxf(fmaxf(lanef(v, 0), lanef(v, 16)), fmaxf(lanef(v, 32), lanef(v, 48)));
 }
+// broadcast lane k of each 16-lane row (DPP row_newbcast)
+template <int K>
+__device__ __forceinline__ float rbc(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + K, 0xF, 0xF, false));
+}
+
 template <int CTRL>
 __device__ __forceinline__ int dppi(int v) {
   return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);

@@ -1181,12 +1181,6 @@ __device__ __forceinline__ int shr1_f32i(float v) { return shr1_i32(__float_as_i
 // T = thl - kMarginF; 0.35 - T is kept per query (k0) and refreshed only when a threshold moves.
 // The step loop is unrolled by two (ping-pong registers for the next step's fragments/statistics),
 // candidate pointers advance by a constant per step.
-// broadcast lane k of each 16-lane row (DPP row_newbcast)
-template <int K>
-__device__ __forceinline__ float rbc(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + K, 0xF, 0xF, false));
-}
-
 // G-only pre-filter threshold of k_scan0f (see the comment at refresh_k0): smallest G that can pass
 // the filter for list threshold t; out of line (rare: called when a threshold moves)
 __device__ __noinline__ float gstar0(float t, float qA, float qB, float qQ, float c1f) {
@@ -1832,7 +1826,7 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
 // No LDS, no atomics: occupancy is set by VGPRs alone.  Output: top[(q * nstreams + 4 chunk + g) *
 // kTopT + t], every entry of every existing query written (-1 = empty).
 constexpr int kTopT = 2;
-constexpr int kSampleKth = 16;
+constexpr int kSampleKth = 12;
 
 __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
@@ -1878,24 +1872,24 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
     dst[0] = *reinterpret_cast<const half8*>(p);
     dst[1] = *reinterpret_cast<const half8*>(p + 32);
   };
-  auto load_stats = [&](int64_t cs, flt4* dst) {  // (std, mean, msq, flags) of rows 4g + r
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = row_of(cs + 4 * g + r);
-      const float* p = a.Sc32 + (row >> 2) * 16 + (row & 3);
-      dst[r] = flt4{p[0], p[4], p[8], p[12]};
-    }
+  // statistics: lane (g, j) loads stat (j & 3) (std, mean, msq, flags) of row 4g + (j >> 2) - one dword
+  // per lane - and the 16 values of the lane group are broadcast by DPP row_newbcast
+  auto load_stats = [&](int64_t cs) -> float {
+    const int64_t row = row_of(cs + 4 * g + (j >> 2));
+    return a.Sc32[(row >> 2) * 16 + (j & 3) * 4 + (row & 3)];
   };
   // fragments and statistics of the next step are loaded one step ahead
   half8 cf[2];
-  flt4 cst[4];
   load_frag(c_begin, cf);
-  load_stats(c_begin, cst);
+  float stv = load_stats(c_begin);
   for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
     half8 cfn[2];
-    flt4 cstn[4];
     load_frag(cs + kCS, cfn);
-    load_stats(cs + kCS, cstn);
+    const float stn = load_stats(cs + kCS);
+    const flt4 cst[4] = {flt4{rbc<0>(stv), rbc<1>(stv), rbc<2>(stv), rbc<3>(stv)},
+                         flt4{rbc<4>(stv), rbc<5>(stv), rbc<6>(stv), rbc<7>(stv)},
+                         flt4{rbc<8>(stv), rbc<9>(stv), rbc<10>(stv), rbc<11>(stv)},
+                         flt4{rbc<12>(stv), rbc<13>(stv), rbc<14>(stv), rbc<15>(stv)}};
     flt4 acc[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[0], qh[b], flt4{0, 0, 0, 0}, 0, 0, 0);
@@ -1945,8 +1939,7 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
     }
     cf[0] = cfn[0];
     cf[1] = cfn[1];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) cst[r] = cstn[r];
+    stv = stn;
   }
   const int ns = 4 * a.nchunks;
 #pragma unroll

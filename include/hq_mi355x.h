@@ -198,7 +198,7 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
  * groups of 4 rows (std[4], mean[4], msq[4], flags[4]) for round_up(N, 4) + 48 rows (16 B per row);
  * Sq/Sc are the f64 statistics of hq_seg_prepare.  Level-0 segments of up to 32 values, N < 2^31. */
 /* Starting threshold of hq_scan0_topk_split: the K'-th best score of a 1/16 row sample minus the error
- * margin, K' = 16 (HQ_SAMPLE_KTH; K' = k, a provable lower bound of the k-th best, for corpora below
+ * margin, K' = 12 (HQ_SAMPLE_KTH; K' = k, a provable lower bound of the k-th best, for corpora below
  * 16 x 4096 rows).  With K' < k a query can end with fewer than k listed candidates although more pass
  * the caller's threshold: its empty slots then carry score +inf (id -1), which hq_refine_topk /
  * hq_refine_rescore_topk report as unresolved (the caller's dense exact path answers the query).    */

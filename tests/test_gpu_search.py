@@ -373,7 +373,7 @@ def test_two_stage_select_equals_one_stage(hq_lib, Q, N, k, thr, tm):
 
 
 def test_statistical_start_threshold_is_exact(hq_lib, monkeypatch):
-    """A starting threshold from the sample's K'-th best (K' < K; the default is 16 on sparse samples) is not
+    """A starting threshold from the sample's K'-th best (K' < K; the default is 12 on sparse samples) is not
     a provable bound: lists left short are marked (+inf in the empty slots) and their queries answered by
     the dense exact path.  With K' = 1 most lists are short; the progressive results must equal the
     provable mode's (HQ_SAMPLE_KTH=0) and the oracle's."""
