@@ -1158,7 +1158,7 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
 constexpr float kMarginF = 6e-5f;
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 constexpr int kZ16Row = 64;  // halfs per split row: hi[32] then lo[32]
-constexpr int kPad0 = 3 * kCS;  // pad rows of the f32 copies (hq_seg_pack0_split); reads reach cs + 31
+constexpr int kPad0 = 3 * kCS;  // pad rows of the f32 copies (hq_seg_pack0_split); k_scan0f reads reach cs + 47
 
 __device__ __forceinline__ float lower_f32(double x) {  // largest float <= x (x finite or +-inf)
   float f = (float)x;
@@ -1490,14 +1490,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   // Software pipeline: the MFMAs of one half run while the VALU filters the other half
   //   block A: MFMA(step i, half 1)   || filter(step i, half 0)
   //   block B: MFMA(step i+1, half 0) || filter(step i, half 1)
-  CStep cA, cB;
+  // Three step buffers: body(i) loads step i + 2 (two bodies of latency cover, the next step's
+  // fragments used by this body's second MFMA half were loaded one body earlier)
+  CStep cA, cB, cC;
   load_step(cA);
+  load_step(cB);
   flt4 acc0[2], acc1[2];
   mfma_half(0, cA.f, acc0);
   unsigned long long gt_bits = 0ull;
   int step = 0;
-  auto body = [&](const int64_t cs, const CStep& cur, CStep& nxt) {
-    load_step(nxt);  // rows past the chunk (padded array): harmless, masked
+  auto body = [&](const int64_t cs, const CStep& cur, const CStep& nxt, CStep& nn) {
+    load_step(nn);  // rows past the chunk (padded array, kPad0 rows): harmless, masked
     const int rem = (int)(c_end - cs);
     mfma_half(1, cur.f, acc1);
     const int fm = flags(cur.st);
@@ -1525,11 +1528,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     ++step;
   };
   int64_t cs = c_begin;
-  for (; cs + kCS < c_end; cs += 2 * kCS) {
-    body(cs, cA, cB);
-    body(cs + kCS, cB, cA);
+  for (; cs + 2 * kCS < c_end; cs += 3 * kCS) {
+    body(cs, cA, cB, cC);
+    body(cs + kCS, cB, cC, cA);
+    body(cs + 2 * kCS, cC, cA, cB);
   }
-  if (cs < c_end) body(cs, cA, cB);
+  if (cs < c_end) body(cs, cA, cB, cC);
+  if (cs + kCS < c_end) body(cs + kCS, cB, cC, cA);
 
   // hand the lists (unordered is fine) to the per-query pools: one atomic per query, lane-parallel
   int nl = 0;  // entries of query `lane`
