@@ -1181,6 +1181,14 @@ __device__ __forceinline__ int shr1_f32i(float v) { return shr1_i32(__float_as_i
 // T = thl - kMarginF; 0.35 - T is kept per query (k0) and refreshed only when a threshold moves.
 // The step loop is unrolled by two (ping-pong registers for the next step's fragments/statistics),
 // candidate pointers advance by a constant per step.
+// diagnostics knobs of k_scan0f (HQ_SCAN_EXPT: debug counters, phase skips) exist only in a
+// `make DIAG=1` build; the default build compiles them away
+#ifdef HQ_DIAG
+#define HQ_EXPT(a) ((a).expt)
+#else
+#define HQ_EXPT(a) 0
+#endif
+
 // G-only pre-filter threshold of k_scan0f (see the comment at refresh_k0): smallest G that can pass
 // the filter for list threshold t; out of line (rare: called when a threshold moves)
 __device__ __noinline__ float gstar0(float t, float qA, float qB, float qQ, float c1f) {
@@ -1314,13 +1322,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     // G-only pre-filter (see gstar0): most half-steps end here after 4 max and 2 compares
     const float g0 = fmaxf(fmaxf(acc[0].x, acc[0].y), fmaxf(acc[0].z, acc[0].w));
     const float g1 = fmaxf(fmaxf(acc[1].x, acc[1].y), fmaxf(acc[1].z, acc[1].w));
-    const unsigned long long pre = a.expt == 8 ? 0ull : __ballot((g0 >= gs[2 * h]) | (g1 >= gs[2 * h + 1]) | (fm != 0));
-    if (a.expt == 3 && lane == 0) {
+    const unsigned long long pre = HQ_EXPT(a) == 8 ? 0ull : __ballot((g0 >= gs[2 * h]) | (g1 >= gs[2 * h + 1]) | (fm != 0));
+    if (HQ_EXPT(a) == 3 && lane == 0) {
       atomicAdd(a.dbg + 6, 1ull);
       if (pre) atomicAdd(a.dbg + 5, 1ull);
     }
-    if (a.expt != 5 && !pre) return 0;
-    if (a.expt == 7) return 0;  // diagnostics only: base cost of the step (no full filter, no inserts)
+    if (HQ_EXPT(a) != 5 && !pre) return 0;
+    if (HQ_EXPT(a) == 7) return 0;  // diagnostics only: base cost of the step (no full filter, no inserts)
     if (!have) {
       expand(st, x);
       have = true;
@@ -1416,7 +1424,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   // with the division), f64 statistics for flagged pairs
   auto insert_half = [&](const int h, const flt4* acc, const SStat& c, const int fm, const int64_t cs,
                          const int bits) {
-    if (a.expt == 3 && lane == 0) atomicAdd(a.dbg, 1ull);
+    if (HQ_EXPT(a) == 3 && lane == 0) atomicAdd(a.dbg, 1ull);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -1425,7 +1433,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const bool pb = (bits >> (4 * u + r)) & 1;
         const unsigned long long mpb = __ballot(pb);
         if (!mpb) continue;
-        if (a.expt == 3 && lane == 0) {
+        if (HQ_EXPT(a) == 3 && lane == 0) {
           atomicAdd(a.dbg + 3, (unsigned long long)__popcll(mpb));
           atomicAdd(a.dbg + 4, 1ull);
         }
@@ -1456,7 +1464,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const int qi = 16 * b + j;
         const int id = (int)(cs + 4 * g + r);
         const unsigned long long mok = __ballot(ok);
-        if (a.expt == 3 && lane == 0) atomicAdd(a.dbg + 1, (unsigned long long)__popcll(mok));
+        if (HQ_EXPT(a) == 3 && lane == 0) atomicAdd(a.dbg + 1, (unsigned long long)__popcll(mok));
         const unsigned long long mine = (mok >> j) & 0x0001000100010001ull;  // query j's pairs, bit 16g
         const int pos = cntr[b] + __popcll(mine & ((1ull << (16 * g)) - 1ull));
         cntr[b] += __popcll(mine);
@@ -1475,7 +1483,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         }
         // pairs offered to sorted lists
         unsigned long long mo = __ballot(ok && pos >= K);
-        if (a.expt == 3 && lane == 0) atomicAdd(a.dbg + 2, (unsigned long long)__popcll(mo));
+        if (HQ_EXPT(a) == 3 && lane == 0) atomicAdd(a.dbg + 2, (unsigned long long)__popcll(mo));
         while (mo) {
           const int l = __builtin_ctzll(mo);
           mo &= mo - 1;
@@ -2926,7 +2934,11 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
   if (out_redo) HQ_CHECK_HIP(hipMemsetAsync(out_redo, 0, sizeof(int), s));
   const size_t lds = ((size_t)refine_qw(si) + (size_t)kp * refine_rw(si) + (size_t)kp * (1 + si.nseg)) * 8;
   const bool sm = seg_small(si);
-  const int expt = getenv("HQ_REFINE_EXPT") ? atoi(getenv("HQ_REFINE_EXPT")) : 0;
+#ifdef HQ_DIAG
+  const int expt = getenv("HQ_REFINE_EXPT") ? atoi(getenv("HQ_REFINE_EXPT")) : 0;  // diagnostics build only
+#else
+  const int expt = 0;
+#endif
   if (lds <= 96 * 1024 && L % 2 == 0 && getenv("HQ_REFINE_GLOBAL") == nullptr) {  // 16-B pieces: L even
     const void* fn = sm ? (const void*)k_refine_lds<true> : (const void*)k_refine_lds<false>;
     HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

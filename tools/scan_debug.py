@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
 """Debug counters of the level-0 scan on the bench corpus (HQ_SCAN_EXPT=3)."""
+# HQ_SCAN_EXPT=3 counters need the diagnostics build (make -C hilbert-quantization_amd/csrc DIAG=1).
 import os
 import sys
 

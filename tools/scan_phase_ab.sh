@@ -1,5 +1,6 @@
 #!/bin/bash
 # k_scan0f time under diagnostic knobs (HQ_SCAN_EXPT): 0 default, 7 no full filter / inserts,
+# Needs the diagnostics build (make -C hilbert-quantization_amd/csrc DIAG=1): the default build compiles HQ_SCAN_EXPT away.
 # 8 pre-filter never fires (results wrong; timing only)
 for e in ${EXPTS:-0 7 8}; do
   HQ_SCAN_EXPT=$e bash tools/search_only_prof.sh e$e > /dev/null 2>&1
