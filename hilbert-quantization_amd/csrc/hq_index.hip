@@ -365,7 +365,8 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
   // order for 64 values is eight column accumulators r_j (rows in order), then
   // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)); four lanes per block hold two columns each and combine by
   // xor-1 / xor-2 exchanges (IEEE addition is commutative, so both partners get the same bits).
-  const int gm = plan.gm, fm = plan.fm;
+  constexpr int gm = NS / 8;  // the fast form runs only when the first level is NS/8 x NS/8 blocks of 8 x 8
+  const int fm = plan.fm;
   for (int r = 0; r < (fm + 15) / 16; ++r) {
     const int b = (lane >> 2) + 16 * r, q = lane & 3;
     const int bb = b < fm ? b : 0;
