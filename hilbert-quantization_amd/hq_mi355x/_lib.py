@@ -109,12 +109,18 @@ def load(path: str = LIB_PATH):
         return lib
 
 
+_gpu_ok = False
+
+
 def lib():
-    """The library, on a process that can run kernels (a GPU must be visible)."""
-    import torch
-    if not torch.cuda.is_available():
-        raise NativeLibraryError("hq_mi355x needs an MI355X (torch.cuda.is_available() is False); "
-                                 "there is no CPU fallback")
+    """The library, on a process that can run kernels (a GPU must be visible; checked until it is)."""
+    global _gpu_ok
+    if not _gpu_ok:
+        import torch
+        if not torch.cuda.is_available():
+            raise NativeLibraryError("hq_mi355x needs an MI355X (torch.cuda.is_available() is False); "
+                                     "there is no CPU fallback")
+        _gpu_ok = True
     return load()
 
 
@@ -135,5 +141,10 @@ def check(rc: int, exc=None):
 
 
 def stream_ptr(device=None) -> int:
+    """hipStream_t of torch's current stream (the raw-pointer query: a few microseconds less per launch)."""
     import torch
+    if device is None:
+        raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        if raw is not None:
+            return raw(torch._C._cuda_getDevice())
     return torch.cuda.current_stream(device).cuda_stream

@@ -143,7 +143,7 @@ class IndexCorpus:
     def _fused_ok(self, mode: int) -> bool:
         """The fused scans hold the contracted columns in registers: <= 256 padded values (hq_scan_topk)."""
         if mode == 0:
-            return int(K._L().hq_seg_level0_len(self.L)) <= 256
+            return K.seg_level0_len(self.L) <= 256
         return self.prep.Lp <= 256
 
     def _thr(self, qp, thr: float, thr_mode: int) -> float:

@@ -7,6 +7,7 @@ SURVEY.md §7); the reference-shaped classes in `hq_mi355x.core` / `hq_mi355x.ra
 """
 from __future__ import annotations
 
+import functools
 import os
 
 import ctypes
@@ -221,10 +222,17 @@ def parse_structure(L: int):
     return [(buf[4 * i], buf[4 * i + 1], buf[4 * i + 2], bool(buf[4 * i + 3])) for i in range(min(n, 16))]
 
 
+@functools.lru_cache(maxsize=None)
 def seg_count(L: int) -> int:
     return _lib.load().hq_seg_count(int(L))
 
 
+@functools.lru_cache(maxsize=None)
+def seg_level0_len(L: int) -> int:
+    return int(_lib.load().hq_seg_level0_len(int(L)))
+
+
+@functools.lru_cache(maxsize=None)
 def seg_padded_len(L: int) -> int:
     return _lib.load().hq_seg_padded_len(int(L))
 
@@ -285,7 +293,7 @@ def pack0(p: Prepared, exc=None) -> Prepared:
     """Attach the split-f16 level-0 copies (hq_seg_pack0_split) used by the level-0 scan; indexes whose
     level-0 segment is longer than 32 values keep the f64 scan."""
     t = torch()
-    if int(_L().hq_seg_level0_len(p.L)) > 32:
+    if seg_level0_len(p.L) > 32:
         return p
     p.Z16 = t.empty((p.N + PAD0, 64), dtype=t.float16, device=p.Z.device)
     p.S32 = t.empty(((p.N + 3) // 4 * 4 + PAD0, 4), dtype=t.float32, device=p.Z.device)  # SoA groups of 4 rows
