@@ -34,6 +34,9 @@ struct PreLevel {
   int g, s, count, off;  // grid side, square side, squares, first output
   int lsh;               // log2(s)
   int leaf0;             // first leaf task of this level (levels with s*s > 128)
+  // zero-padding skip (1-D streams of d < n*n values): squares that touch a value < d, their list
+  // offset in LDS and, for leaf levels, the first leaf task over the listed squares
+  int zcnt, zoff, zleaf0;
 };
 struct PrePlan {
   int nlev, total, n_small, nleaves, lsh_n;
@@ -41,6 +44,8 @@ struct PrePlan {
   int tree_lds;  // 1: combine the leaves through LDS (squares of > 64 leaves, or HQ_PRECOMP_TREE=lds)
   int diag;      // A/B diagnostics only (wrong averages): bit 0 skip small squares, 1 leaves, 2 load, 3 store
   int nt;        // non-temporal output stores
+  int znz;       // zero-padding skip: squares listed over all levels (LDS list entries)
+  int znleaves;  // zero-padding skip: leaf tasks over the listed squares
   PreLevel lv[kPreMaxLevels];
 };
 
@@ -89,6 +94,62 @@ static int pre_plan(int n, int max_levels, int min_sq, PrePlan& p) {
   p.nlev = c;
   if (2 * p.maxper > 64) p.tree_lds = 1;  // a square's leaf lanes would span waves
   return HQ_OK;
+}
+
+// Zero-padding skip for a 1-D stream of d < n*n values (pipeline padding, core/pipeline.py:325-349):
+// every cell at Hilbert index >= d is +0.0 in every image, so a square none of whose cells lies below
+// d averages to exactly +0.0 (np.mean of zeros) and is never computed — its output slot is zeroed once
+// per workgroup.  A square (aligned or offset by half a side) is the union of four aligned sub-blocks
+// of side h = s/2, each a contiguous Hilbert range starting at a multiple of h^2 (layout invariant,
+// SURVEY.md §8a); the kernel reads a sub-block's start from the 2x2-group map (group j holds indices
+// 4j..4j+3), so for h = 1 the test uses 4j, a lower bound: a listed square may still be all zero
+// (computed, exact), an unlisted one never holds data.  The host applies the same rule to size the
+// lists; returns 1 when the skip removes squares.
+static int pre_zero_plan(int n, int d, PrePlan& p) {
+  p.znz = 0;
+  p.znleaves = 0;
+  if (d >= n * n || n > 64) return 0;
+  static thread_local uint16_t hidx[64 * 64];
+  for (uint32_t i = 0; i < (uint32_t)(n * n); ++i) {
+    uint32_t x, y;
+    d2xy((uint32_t)n, i, x, y);
+    hidx[y * n + x] = (uint16_t)i;
+  }
+  for (int l = 0; l < p.nlev; ++l) {
+    PreLevel& L = p.lv[l];
+    const int h = L.s >> 1, lg = ilog2(L.g);
+    L.zcnt = 0;
+    L.zoff = p.znz;
+    for (int k = 0; k < L.count; ++k) {
+      int x0, y0;
+      if (k < L.g * L.g) {
+        y0 = (k >> lg) * L.s;
+        x0 = (k & (L.g - 1)) * L.s;
+      } else {
+        const int kk = k - L.g * L.g, hw = L.g - 1;
+        y0 = (kk / hw) * L.s + L.s / 2;
+        x0 = (kk % hw) * L.s + L.s / 2;
+      }
+      bool nz = false;
+      for (int q = 0; q < (h > 0 ? 4 : 1); ++q) {
+        const int cx = x0 + (q & 1) * h, cy = y0 + (q >> 1) * h;
+        int start = hidx[cy * n + cx] & ~3;
+        if (h >= 2) start &= ~(h * h - 1);
+        nz |= start < d;
+      }
+      L.zcnt += nz;
+    }
+    p.znz += L.zcnt;
+    L.zleaf0 = -1;
+    if (L.leaf0 >= 0) {
+      const int per = L.s * L.s / 128;
+      p.znleaves = (p.znleaves + per - 1) / per * per;
+      L.zleaf0 = p.znleaves;
+      p.znleaves += L.zcnt * per;
+    }
+  }
+  if (2 * p.znleaves > kPreThreads || p.total > 4096) return 0;  // one leaf round; 12-bit slots
+  return p.znz < p.total;
 }
 
 // top-left corner of square k of a level (grid squares row-major, then offset squares).  g is a power
@@ -204,12 +265,23 @@ __device__ __forceinline__ T sq_sum(const T* b, int ld) {
 }
 
 // all squares of one level with S x S <= 128 values (S = 1, 2, 4, 8): one NumPy pairwise leaf per thread
-template <typename T, int S>
-__device__ __forceinline__ void pre_small(const PreLevel& L, const T* img, int ld, float* res, int tid) {
-  for (int k = tid; k < L.count; k += kPreThreads) {
-    int x0, y0;
-    pre_square(L, k, x0, y0);
-    const T* b = img + y0 * ld + x0;
+template <typename T, int S, bool SK>
+__device__ __forceinline__ void pre_small(const PreLevel& L, const T* img, int ld, float* res, int tid,
+                                          const uint32_t* zl) {
+  const int cnt = SK ? L.zcnt : L.count;
+  for (int i = tid; i < cnt; i += kPreThreads) {
+    int k;
+    const T* b;
+    if constexpr (SK) {
+      const uint32_t ent = zl[L.zoff + i];  // (square << 16) | LDS offset of its corner
+      k = (int)(ent >> 16);
+      b = img + (ent & 0xFFFFu);
+    } else {
+      k = i;
+      int x0, y0;
+      pre_square(L, k, x0, y0);
+      b = img + y0 * ld + x0;
+    }
     T sum;
     if constexpr (S == 8) sum = sq_sum<T, 8>(b, ld);
     else if constexpr (S == 4) sum = sq_sum<T, 4>(b, ld);
@@ -219,10 +291,60 @@ __device__ __forceinline__ void pre_small(const PreLevel& L, const T* img, int l
   }
 }
 
+// once per workgroup before the image loop: see k_precomp's SK path
+template <typename T>
+__device__ __forceinline__ void pre_zero_setup(T* img, float* res, uint32_t* zl, int* zcnt,
+                                                         const PreLevel* lv, int nlev, int total, int n, int d,
+                                                         int ld, int tid) {
+  auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  // once per workgroup (pre_zero_plan): the lists of squares that touch a value < d, built from the
+  // 2x2-group map (group index of every 2x2 block, staged in the image's space); then the image and
+  // the averages are zeroed — the padding cells and the unlisted averages stay +0.0 for every image
+  uint16_t* gmap = reinterpret_cast<uint16_t*>(img);
+  const int lsh_n = __builtin_ctz((unsigned)n), G = (n * n) >> 2;
+  const uint32_t* glut = n == 16 ? kPreLut16.v : (n == 32 ? kPreLut32.v : kPreLut64.v);
+  const int hn = n >> 1;
+  for (int j = tid; j < G; j += kPreThreads) {
+    const uint32_t off = glut[j] & 0xFFFFu;
+    gmap[((off >> lsh_n) >> 1) * hn + ((off & (n - 1)) >> 1)] = (uint16_t)j;
+  }
+  if (tid < nlev) zcnt[tid] = 0;
+  lds_barrier();
+  for (int l = 0; l < nlev; ++l) {
+    const PreLevel L = lv[l];
+    const int h = L.s >> 1;
+    for (int k0 = 0; k0 < L.count; k0 += kPreThreads) {
+      const int k = k0 + tid;
+      bool nz = false;
+      int x0 = 0, y0 = 0;
+      if (k < L.count) {
+        pre_square(L, k, x0, y0);
+        for (int q = 0; q < (h > 0 ? 4 : 1); ++q) {
+          const int cx = x0 + (q & 1) * h, cy = y0 + (q >> 1) * h;
+          int start = 4 * (int)gmap[(cy >> 1) * hn + (cx >> 1)];
+          if (h >= 2) start &= ~(h * h - 1);
+          nz |= start < d;
+        }
+      }
+      const uint64_t bal = __builtin_amdgcn_ballot_w64(nz);
+      int base = 0;
+      if ((tid & 63) == 0 && bal) base = atomicAdd(&zcnt[l], (int)__popcll(bal));
+      base = __shfl(base, 0, 64);
+      const int r = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      if (nz && base + r < L.zcnt)  // counts agree with the host's
+        zl[L.zoff + base + r] = ((uint32_t)k << 16) | (uint32_t)(y0 * ld + x0);
+    }
+  }
+  lds_barrier();
+  for (int i = tid; i < ld * n; i += kPreThreads) img[i] = T(0);
+  for (int i = tid; i < total; i += kPreThreads) res[i] = 0.0f;
+  lds_barrier();
+}
+
 // kind 0: images (n x n row-major, image stride `stride` elements); kind 1: 1-D Hilbert-ordered
 // parameter streams of d values (row stride `stride`), zero-padded to n*n and mapped to 2-D
 // (core/pipeline.py:298-319 _get_2d_representation).
-template <typename T, int PF>
+template <typename T, int PF, bool SK, int KG>
 __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))) void k_precomp(const T* __restrict__ in, int kind, int64_t N, int64_t stride,
                                                          int d, int n, PrePlan plan, float* __restrict__ out,
                                                          int64_t out_stride, int use_lut, int ld) {
@@ -230,7 +352,9 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
   __shared__ PreLevel lv[kPreMaxLevels];  // per-thread level lookups index LDS, not the kernarg block
   T* img = reinterpret_cast<T*>(smem);
   T* part = img + ld * n;  // row stride ld = n + pad (16-B aligned rows spread the bank pattern)
-  float* res = reinterpret_cast<float*>(part + plan.nleaves);
+  float* res = reinterpret_cast<float*>(part + (plan.tree_lds ? plan.nleaves : 0));  // part: LDS tree only
+  uint32_t* zl = reinterpret_cast<uint32_t*>(res + plan.total);  // SK: listed squares, per level at zoff
+  __shared__ int zcnt[kPreMaxLevels];
   const int tid = threadIdx.x;
   const int lsh_n = plan.lsh_n;
   if (tid < plan.nlev) lv[tid] = plan.lv[tid];
@@ -241,7 +365,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
   // 1-D streams with the compile-time group LUT (n = 16 / 32 / 64): each thread owns float4 groups
   // j = tid + 256 i (2x2 blocks, Hilbert layout invariant); their LUT entries live in registers and
   // the next image's values are fetched while the current one is reduced
-  constexpr int kPreG = 4;  // groups per thread at n = 64
+  constexpr int kPreG = KG;  // groups per thread: 4 at n = 64; 2 when a skip run reads only d <= 2048 values
   const int G = (n * n) >> 2;
   uint32_t lut[kPreG];
   T pf[kPreG][4];
@@ -277,6 +401,25 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
       }
     }
   };
+  // SK: this thread's half-leaf task is fixed for the workgroup (one round, 2 * znleaves <= 256):
+  // resolved once here — LDS offset of its first value (lt_b) and, packed in lt_m, the average's slot
+  // (bits 0-11), log2 of the square side (12-15), the leaf within the square (16-20), live (24)
+  int lt_b = 0, lt_m = 0;
+  if constexpr (SK) {
+    pre_zero_setup<T>(img, res, zl, zcnt, lv, plan.nlev, plan.total, n, d, ld, tid);
+    const int t = tid >> 1;
+    if (t < plan.znleaves) {
+      int l = plan.nlev - 1;
+      while (lv[l].zleaf0 < 0 || t < lv[l].zleaf0) --l;
+      const int lper = 2 * lv[l].lsh - 7;  // log2 of the leaves per square
+      const int slot = (t - lv[l].zleaf0) >> lper, leaf = (t - lv[l].zleaf0) & ((1 << lper) - 1);
+      if (slot < lv[l].zcnt) {  // else an alignment gap before the next level
+        const uint32_t ent = zl[lv[l].zoff + slot];
+        lt_b = (int)(ent & 0xFFFFu) + 4 * (tid & 1);
+        lt_m = (lv[l].off + (int)(ent >> 16)) | (lv[l].lsh << 12) | (leaf << 16) | (1 << 24);
+      }
+    }
+  }
   if (PF && use_lut && (int64_t)blockIdx.x < N) fetch(blockIdx.x);
   for (int64_t e = blockIdx.x; e < N; e += gridDim.x) {
     const T* src = in + e * stride;
@@ -288,6 +431,11 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
 #pragma unroll
       for (int i = 0; i < kPreG; ++i) {
         if (tid + kPreThreads * i >= G) continue;
+        if constexpr (SK) {  // all padding: stays +0.0 from the setup (bound laundered per image, as in fetch)
+          int dz = d;
+          asm volatile("" : "+s"(dz));
+          if (4 * (tid + kPreThreads * i) >= dz) continue;
+        }
         uint32_t ent = lut[i];
         asm volatile("" : "+v"(ent));
         const uint32_t off0 = ent & 0xFFFFu, code = ent >> 16;
@@ -321,10 +469,12 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
       L.leaf0 = __builtin_amdgcn_readfirstlane(lv[l].leaf0);
       if (L.leaf0 >= 0) continue;
       // one straight-line loop per square size (the size is uniform per level)
-      if (L.s == 2) pre_small<T, 2>(L, img, ld, res, tid);
-      else if (L.s == 4) pre_small<T, 4>(L, img, ld, res, tid);
-      else if (L.s == 8) pre_small<T, 8>(L, img, ld, res, tid);
-      else pre_small<T, 1>(L, img, ld, res, tid);
+      L.zcnt = __builtin_amdgcn_readfirstlane(lv[l].zcnt);
+      L.zoff = __builtin_amdgcn_readfirstlane(lv[l].zoff);
+      if (L.s == 2) pre_small<T, 2, SK>(L, img, ld, res, tid, zl);
+      else if (L.s == 4) pre_small<T, 4, SK>(L, img, ld, res, tid, zl);
+      else if (L.s == 8) pre_small<T, 8, SK>(L, img, ld, res, tid, zl);
+      else pre_small<T, 1, SK>(L, img, ld, res, tid, zl);
     }
     // 128-value leaves of the larger squares: 16 steps of 8 consecutive values (one row segment,
     // 8-aligned because x0 is a multiple of s/2 >= 8), eight accumulators as NumPy's pairwise leaf
@@ -360,6 +510,40 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
       return (r[0] + r[1]) + (r[2] + r[3]);
     };
     if (plan.diag & 2) {
+    } else if constexpr (SK) {
+      // the same leaf sums and shuffle tree as below, from the task resolved before the image loop
+      const int h = tid & 1;
+      // laundered per image: hoisted out of the image loop, the 16 load addresses would hold VGPRs
+      asm volatile("" : "+v"(lt_b), "+v"(lt_m));
+      const bool live = (lt_m >> 24) & 1;
+      const int lsh = (lt_m >> 12) & 15, leaf = (lt_m >> 16) & 31;
+      T v = T(0);
+      if (live) {
+        const T* b = img + lt_b;
+        const int msk = (1 << lsh) - 1;
+        T r[4];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int q = (leaf << 7) + 8 * i;
+          T w4[4];
+          load4<T>(b + (q >> lsh) * ld + (q & msk), w4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r[j] = i == 0 ? w4[j] : r[j] + w4[j];
+          if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // at most 8 steps of loads in flight
+        }
+        v = (r[0] + r[1]) + (r[2] + r[3]);
+      }
+      const int per = live ? 1 << (2 * lsh - 7) : 0;
+      {
+        const T o = __shfl_down(v, 1, 64);
+        if (h == 0) v = v + o;
+      }
+      for (int w = 1; w < plan.maxper; w <<= 1) {
+        const T o = __shfl_down(v, 2 * w, 64);
+        if (w < per && h == 0 && (leaf & (2 * w - 1)) == 0) v = v + o;
+      }
+      if (live && h == 0 && leaf == 0) res[lt_m & 0xFFF] = pre_mean<T>(T(0) + v, 2 * lsh);
+      lds_barrier();
     } else if (!plan.tree_lds) {
       // a square's <= 32 leaves sit on 2 * per consecutive lanes of one wave (leaf0 is aligned to
       // per): the balanced tree over them (adjacent pairs first) by shuffles, the first lane stores
@@ -626,27 +810,39 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   const char* dev = getenv("HQ_PRECOMP_DIAG");
   if (dev) p.diag = atoi(dev);
 #endif
-  const char* gev = getenv("HQ_PRECOMP_GRID");  // A/B: workgroups (each loops over images)
-  const int64_t gcap = gev ? atoll(gev) : 65536 * 4;
-  const int64_t grid64 = N < gcap ? N : gcap;
   const int esz = dtype == HQ_F64 ? 8 : 4;
   const char* pev = getenv("HQ_PRECOMP_PAD");
   const int pad = pev ? atoi(pev) : 4;
   if (pad < 0 || (pad & 3)) return fail(HQ_E_INVALID, "HQ_PRECOMP_PAD must be a multiple of 4");
   const int ld = n + pad;
-  const size_t lds = (size_t)esz * ((size_t)ld * n + p.nleaves) + 4 * (size_t)p.total;
+  const int use_lut = kind == 1 && n >= 16 && n <= 64;  // compile-time group LUT exists for this n
+  // zero-padding skip (pre_zero_plan): 1-D streams with padding, leaves combined in registers;
+  // A/B: HQ_PRECOMP_SKIP=0 computes every square
+  const char* zev = getenv("HQ_PRECOMP_SKIP");
+  const bool skip = use_lut && !p.tree_lds && !(zev && atoi(zev) == 0) && pre_zero_plan(n, d, p);
+  const size_t lds = (size_t)esz * ((size_t)ld * n + (p.tree_lds ? p.nleaves : 0)) + 4 * (size_t)p.total +
+                     (skip ? 4 * (size_t)p.znz : 0);
   if (lds > 160 * 1024) return fail(HQ_E_UNSUPPORTED, "pre-computed index n=%d dtype %d needs %zu B of LDS", n, dtype, lds);
   hipStream_t s = (hipStream_t)stream;
-  const int use_lut = kind == 1 && n >= 16 && n <= 64;  // compile-time group LUT exists for this n
-  const char* fev = getenv("HQ_PRECOMP_PF");           // A/B: 1 = prefetch the next image into registers
-  const int pf = fev ? atoi(fev) : 0;
+  // skip runs: a workgroup loops over many images (the list setup is amortised) and prefetches the
+  // next image into registers (A/B, M emb/s at d = 1536: grid 262144 / 16384 / 8192 without prefetch
+  // 110 / 169 / 157, with it 125 / 192 / 195; no skip 142)
+  const char* gev = getenv("HQ_PRECOMP_GRID");  // A/B: workgroups (each loops over images)
+  const int64_t gcap = gev ? atoll(gev) : (skip ? 8192 : 65536 * 4);
+  const int64_t grid64 = N < gcap ? N : gcap;
+  const char* fev = getenv("HQ_PRECOMP_PF");  // A/B: 1 = prefetch the next image into registers
+  const int pf = fev ? atoi(fev) : (skip ? 1 : 0);
   if (dtype == HQ_F32) {
-    auto kern = pf ? k_precomp<float, 1> : k_precomp<float, 0>;
+    // groups of 4 values a thread scatters: a skip run touches only groups below d
+    const bool kg2 = skip && (d + 3) / 4 <= 2 * kPreThreads;
+    auto kern = skip ? (kg2 ? (pf ? k_precomp<float, 1, true, 2> : k_precomp<float, 0, true, 2>)
+                            : (pf ? k_precomp<float, 1, true, 4> : k_precomp<float, 0, true, 4>))
+                     : (pf ? k_precomp<float, 1, false, 4> : k_precomp<float, 0, false, 4>);
     HQ_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(kern, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const float*)in, kind, N,
                        in_stride, d, n, p, out, out_stride, use_lut, ld);
   } else if (dtype == HQ_F64) {
-    auto kern = k_precomp<double, 0>;
+    auto kern = skip ? k_precomp<double, 0, true, 4> : k_precomp<double, 0, false, 4>;
     HQ_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(kern, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const double*)in, kind,
                        N, in_stride, d, n, p, out, out_stride, use_lut, ld);

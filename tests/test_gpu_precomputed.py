@@ -157,3 +157,26 @@ def test_quantizer_builds_precomputed_index(hq_lib):
     assert np.concatenate([lv.averages for lv in pre.levels]).tobytes() == want[0].tobytes()
     assert HilbertQuantizer(use_precomputed_indexing=False).quantize(p, model_id="x") is not None
     assert qm.metadata.model_name == "pm"
+
+
+@pytest.mark.parametrize("grid", [None, "3"])
+@pytest.mark.parametrize("n,dtype,levels", [(16, np.float32, (6, 2)), (32, np.float32, (6, 2)),
+                                             (64, np.float32, (6, 2)), (64, np.float64, (6, 2)),
+                                             (32, np.float32, (2, 1)), (64, np.float32, (3, 4))])
+def test_precomputed_stream_zero_padding_skip(hq_lib, monkeypatch, grid, n, dtype, levels):
+    """1-D streams shorter than n*n: squares wholly in the zero padding are skipped (pre_zero_plan) and
+    their averages stay +0.0.  d sweeps group edges (d % 4 != 0), block edges and the full image; with
+    HQ_PRECOMP_GRID=3 each workgroup loops over several images, so the padding cells and the skipped
+    averages are reused from the once-per-workgroup setup."""
+    from hq_mi355x import kernels as K
+    if grid is not None:
+        monkeypatch.setenv("HQ_PRECOMP_GRID", grid)
+    rng = np.random.default_rng(n * 7 + len(levels))
+    ml, ms = levels
+    for d in sorted({1, 3, 4, 5, 63, 64, 65, n * n // 4 + 1, 3 * n * n // 8, n * n - 1, n * n}):
+        p = (rng.standard_normal((7, d)) * 10 ** rng.uniform(-2, 2)).astype(dtype)
+        p[2] = 0.5
+        p[3, ::2] = -0.0
+        want, _ = O.precomputed_index(O.map_to_2d(O.pad_parameters(p, n), n), ml, ms)
+        got = _np(K.precomputed_index(_t(p), n, 1, None, ml, ms))
+        assert got.tobytes() == want.tobytes(), f"n={n} d={d}"
