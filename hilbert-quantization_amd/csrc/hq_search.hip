@@ -1891,14 +1891,17 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
     const int64_t row = row_of(cs + 4 * g + (j >> 2));
     return a.Sc32[(row >> 2) * 16 + (j & 3) * 4 + (row & 3)];
   };
-  // fragments and statistics of the next step are loaded one step ahead
-  half8 cf[2];
+  // fragments and statistics are loaded two steps ahead (3-buffer rotation, as in k_scan0f): at 2 waves
+  // per SIMD one step of strided-row latency was exposed per step
+  half8 cf[2], cf1[2];
   load_frag(c_begin, cf);
   float stv = load_stats(c_begin);
+  load_frag(c_begin + kCS, cf1);
+  float st1 = load_stats(c_begin + kCS);
   for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
     half8 cfn[2];
-    load_frag(cs + kCS, cfn);
-    const float stn = load_stats(cs + kCS);
+    load_frag(cs + 2 * kCS, cfn);
+    const float stn = load_stats(cs + 2 * kCS);
     const flt4 cst[4] = {flt4{rbc<0>(stv), rbc<1>(stv), rbc<2>(stv), rbc<3>(stv)},
                          flt4{rbc<4>(stv), rbc<5>(stv), rbc<6>(stv), rbc<7>(stv)},
                          flt4{rbc<8>(stv), rbc<9>(stv), rbc<10>(stv), rbc<11>(stv)},
@@ -1950,9 +1953,12 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
         k0[b] = ((qok >> b) & 1) ? 0.35f - top[b][kTopT - 1] : -__builtin_huge_valf();
       }
     }
-    cf[0] = cfn[0];
-    cf[1] = cfn[1];
-    stv = stn;
+    cf[0] = cf1[0];
+    cf[1] = cf1[1];
+    cf1[0] = cfn[0];
+    cf1[1] = cfn[1];
+    stv = st1;
+    st1 = stn;
   }
   const int ns = 4 * a.nchunks;
 #pragma unroll
