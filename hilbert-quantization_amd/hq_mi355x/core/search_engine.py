@@ -100,6 +100,19 @@ def combine_levels(lv: np.ndarray, both32: bool) -> np.ndarray:
     return np.maximum(0.0, np.minimum(1.0, out))
 
 
+class PendingSearch:
+    """A progressive search batch queued on the GPU (IndexCorpus.progressive_submit): its device outputs,
+    the pinned copy of its redo count and the event behind that copy; `done` holds the results of the
+    synchronous paths (small corpora, dense exact path)."""
+
+    __slots__ = ("done", "qp", "out", "res", "cnt", "forced", "nredo", "event", "threshold", "M", "K_out")
+
+    def __init__(self, done=None, qp=None, out=None, res=None, cnt=None, forced=None, nredo=None, event=None,
+                 threshold=0.0, M=0, K_out=0):
+        self.done, self.qp, self.out, self.res, self.cnt, self.forced = done, qp, out, res, cnt, forced
+        self.nredo, self.event, self.threshold, self.M, self.K_out = nredo, event, threshold, M, K_out
+
+
 class IndexCorpus:
     """A corpus of equal-length hierarchical index vectors resident in HBM.
 
@@ -222,6 +235,15 @@ class IndexCorpus:
         """search_engine.py:232-300 + :340-388 for a query batch.
         Returns (ids [Q, K], overall [Q, K], levels [Q, K, nseg], count [Q]) with K = max_results;
         rows are padded with id -1 beyond count."""
+        return self.progressive_finish(self.progressive_submit(queries, max_results, threshold,
+                                                               max_candidates_per_level))
+
+    def progressive_submit(self, queries, max_results: int, threshold: float = 0.1,
+                           max_candidates_per_level: int = 100) -> "PendingSearch":
+        """Queue a progressive search without waiting for it: the scan, exact re-rank, re-score and final
+        ranking are launched on the current stream and the count of queries needing the dense exact path
+        is copied to pinned host memory behind them.  `progressive_finish` waits for that copy alone, so
+        batch i + 1 can be queued before batch i is finished (the GPU never idles on the host)."""
         t = torch()
         qp = self.prepare_queries(queries)
         Q = qp.N
@@ -231,32 +253,43 @@ class IndexCorpus:
             # the level loop never filters (:298): every candidate is re-scored and stable-sorted
             ids, ov, lv = self.brute_force(queries, min(K_out, max(self.N, 1)))
             cnt = (ids >= 0).sum(dim=1).to(t.int32)
-            return ids, ov, lv, cnt
-        # Whole pipeline queued first (scan, exact re-rank, re-score, final ranking); the one host sync
-        # comes last and checks whether any query needs the dense exact path (list not proven complete,
-        # or nothing passed the threshold -> first arg-max).  Those rows are recomputed and replaced.
+            return PendingSearch(done=(ids, ov, lv, cnt))
         if M + self.SLACK > MAX_FUSED_K or self.dense_only or not self._fused_ok(0):
             s0, ids, cnt, best, bid = self.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)
             oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
-            return oid, odet[..., 0], odet[..., 1:], ocnt
+            return PendingSearch(done=(oid, odet[..., 0], odet[..., 1:], ocnt))
         threshold = self._thr(qp, threshold, 1)
         nredo = self._redo_counter(qp.Z.device)
         s0, ids, cnt, res, det = self._scan_refine(qp, 0, M, float(threshold), 1, nredo, det=True)
         # no arg-max on this path: a query where nothing passed (count 0) is recomputed by the dense path
-        # below, so the fallback slot is a constant (-inf, id -1, zero re-scores) kept per batch size
+        # in progressive_finish, so the fallback slot is a constant (-inf, id -1, zero re-scores)
         best, bid, bdet = self._no_fallback(Q, qp.Z.device)
         oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out, bdet, det)
-        forced = self._forced(qp)
-        # the one host sync: k_refine counted the unresolved / empty queries on the device
-        if forced is not None or int(nredo.item()) > 0:
-            redo = (res == 0) | (cnt == 0)
-            if forced is not None:
-                redo = redo | forced
+        # the shared device counter is overwritten by the next batch: this batch's value leaves now
+        host = t.empty(1, dtype=nredo.dtype, pin_memory=True)
+        host.copy_(nredo, non_blocking=True)
+        ev = t.cuda.Event()
+        ev.record()
+        return PendingSearch(qp=qp, out=(oid, odet, ocnt), res=res, cnt=cnt, forced=self._forced(qp),
+                             nredo=host, event=ev, threshold=float(threshold), M=M, K_out=K_out)
+
+    def progressive_finish(self, p: "PendingSearch"):
+        """Wait for a submitted batch's redo count (the one host sync) and recompute the queries whose
+        list is not proven complete or where nothing passed, by the dense exact path."""
+        if p.done is not None:
+            return p.done
+        t = torch()
+        oid, odet, ocnt = p.out
+        p.event.synchronize()
+        if p.forced is not None or int(p.nredo[0]) > 0:
+            redo = (p.res == 0) | (p.cnt == 0)
+            if p.forced is not None:
+                redo = redo | p.forced
             sel = t.nonzero(redo).view(-1)
             if sel.numel():
-                s2, i2, b2, bi2 = self._dense(qp, sel, 0, M, float(threshold), 1)
-                sub = qp.rows(sel)
-                o2, d2, c2 = self._final(sub, s2, i2, b2, bi2, K_out)
+                s2, i2, b2, bi2 = self._dense(p.qp, sel, 0, p.M, p.threshold, 1)
+                sub = p.qp.rows(sel)
+                o2, d2, c2 = self._final(sub, s2, i2, b2, bi2, p.K_out)
                 oid[sel], odet[sel], ocnt[sel] = o2, d2, c2
         return oid, odet[..., 0], odet[..., 1:], ocnt
 

@@ -63,6 +63,10 @@ class ShardedIndexCorpus:
         (used only when no shard has a passing candidate).  The scan, re-rank, re-scores and packing
         are queued before the one host sync, which only checks for rows that need the dense exact path
         (list not proven complete, or nothing passed -> arg-max)."""
+        return self._local_finish(self._local_submit(qp, M, threshold))
+
+    def _local_submit(self, qp, M: int, threshold: float):
+        """Queue the shard's records; the redo flag leaves for pinned host memory behind them."""
         t = torch()
         c = self.local
         Q = qp.N
@@ -70,24 +74,35 @@ class ShardedIndexCorpus:
         s0, ids, cnt, res, det0 = c._scan_refine(qp, 0, M, float(threshold), 1, det=True)
         # no arg-max on the scan path (count-0 rows are redone below): constant fallback slot
         best, bid, bdet0 = c._no_fallback(Q, qp.Z.device)
-
-        def records(q, s0_, ids_, best_, bid_, det=None, bdet=None):
-            if det is None:
-                det = K.rescore(q, c.prep, ids_, c.id_base)
-            if bdet is None:
-                bdet = K.rescore(q, c.prep, bid_.view(-1, 1), c.id_base)
-            return t.cat([pack(s0_, ids_, det), pack(best_.view(-1, 1), bid_.view(-1, 1), bdet)], dim=1)
-
-        rec = records(qp, s0, ids, best, bid, det0, bdet0.view(Q, 1, -1))
+        rec = self._records(qp, s0, ids, best, bid, det0, bdet0.view(Q, 1, -1))
         redo = (res == 0) | (cnt == 0)
         forced = c._forced(qp)
         if forced is not None:
             redo = redo | forced
-        if bool(redo.any()):
+        flag = t.empty(1, dtype=t.bool, pin_memory=True)
+        flag.copy_(redo.any().view(1), non_blocking=True)
+        ev = t.cuda.Event()
+        ev.record()
+        return qp, M, float(threshold), rec, redo, flag, ev
+
+    def _local_finish(self, pending):
+        t = torch()
+        qp, M, threshold, rec, redo, flag, ev = pending
+        ev.synchronize()
+        if bool(flag[0]):
             sel = t.nonzero(redo).view(-1)
-            s2, i2, b2, bi2 = c._dense(qp, sel, 0, M, float(threshold), 1)
-            rec[sel] = records(qp.rows(sel), s2, i2, b2, bi2)
+            s2, i2, b2, bi2 = self.local._dense(qp, sel, 0, M, threshold, 1)
+            rec[sel] = self._records(qp.rows(sel), s2, i2, b2, bi2)
         return rec
+
+    def _records(self, q, s0_, ids_, best_, bid_, det=None, bdet=None):
+        t = torch()
+        c = self.local
+        if det is None:
+            det = K.rescore(q, c.prep, ids_, c.id_base)
+        if bdet is None:
+            bdet = K.rescore(q, c.prep, bid_.view(-1, 1), c.id_base)
+        return t.cat([pack(s0_, ids_, det), pack(best_.view(-1, 1), bid_.view(-1, 1), bdet)], dim=1)
 
     @staticmethod
     def merge(g, M: int, max_results: int):
@@ -99,10 +114,17 @@ class ShardedIndexCorpus:
 
     def progressive(self, queries, max_results: int, threshold: float = 0.1, max_candidates_per_level: int = 100):
         """Global progressive search; every rank returns the same (ids, overall, levels, count)."""
+        return self.progressive_finish(self.progressive_submit(queries, max_results, threshold,
+                                                               max_candidates_per_level))
+
+    def progressive_submit(self, queries, max_results: int, threshold: float = 0.1,
+                           max_candidates_per_level: int = 100):
+        """Queue this shard's part of a global progressive search (IndexCorpus.progressive_submit); the
+        all-gather and merge run in progressive_finish, which every rank calls in the same batch order."""
         c = self.local
         M = int(max_candidates_per_level)
         if self.n_total <= M:
-            return self.brute_force(queries, max_results)
+            return ("done", self.brute_force(queries, max_results))
         qp = c.prepare_queries(queries)
         if M + c.SLACK > 64 or c.dense_only or not c._fused_ok(0):  # the dense exact path per shard (list length / f32 model)
             t = torch()
@@ -111,9 +133,14 @@ class ShardedIndexCorpus:
             det = K.rescore(qp, c.prep, ids, c.id_base)
             bdet = K.rescore(qp, c.prep, bid.view(Q, 1), c.id_base)
             rec = t.cat([pack(s0, ids, det), pack(best.view(Q, 1), bid.view(Q, 1), bdet)], dim=1)
-        else:
-            rec = self.local_records(qp, M, threshold)
-        return self.merge(all_gather(rec, self.group), M, max_results)
+            return ("rec", rec, M, max_results)
+        return ("pending", self._local_submit(qp, M, threshold), M, max_results)
+
+    def progressive_finish(self, p):
+        if p[0] == "done":
+            return p[1]
+        rec = p[1] if p[0] == "rec" else self._local_finish(p[1])
+        return self.merge(all_gather(rec, self.group), p[2], p[3])
 
     def brute_force(self, queries, max_results: int):
         """Global top-k by the overall score: local top-k, all-gather, R-way merge."""

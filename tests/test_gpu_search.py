@@ -197,6 +197,30 @@ def test_sharded_corpus_records_equal_single(hq_lib):
         assert np.array_equal(_np(one[0]), ref[0])
 
 
+def test_pipelined_submit_finish_equals_sequential(hq_lib):
+    """Batches queued before the previous one is finished (progressive_submit / _finish, as bench.py
+    runs them): every batch's results equal its own synchronous call, including batches whose queries
+    take the dense path (nothing passes at 0.97: count-0 rows are redone after the next batch was
+    queued, so the shared redo counter and scan workspace must not leak between batches)."""
+    from hq_mi355x.core.search_engine import IndexCorpus
+    from hq_mi355x.distributed import ShardedIndexCorpus
+    C = _corpus(4000, 64, 51)
+    rng = np.random.default_rng(52)
+    batches = [(C[[1, 2, 3]] + rng.normal(0, 0.01, (3, 64)), 0.1), (C[[7, 8]] + 0.02, 0.97),
+               (C[100:140] + rng.normal(0, 0.01, (40, 64)), 0.1), (rng.standard_normal((5, 64)), 0.97)]
+    for corpus in (IndexCorpus(C), ShardedIndexCorpus(C, id_base=0, n_total=len(C))):
+        ref = [[_np(x) for x in corpus.progressive(q, 10, thr, 20)] for q, thr in batches]
+        pend, got = [], []
+        for q, thr in batches:
+            pend.append(corpus.progressive_submit(q, 10, thr, 20))
+            if len(pend) > 1:
+                got.append([_np(x) for x in corpus.progressive_finish(pend.pop(0))])
+        got += [[_np(x) for x in corpus.progressive_finish(p)] for p in pend]
+        for b, (r, g) in enumerate(zip(ref, got)):
+            for x, y in zip(r, g):
+                assert np.array_equal(x, y), (type(corpus).__name__, b)
+
+
 def test_rag_scores(hq_lib, golden):
     from hq_mi355x.rag import similarity as S
     g = golden("rag_score")
