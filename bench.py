@@ -439,17 +439,27 @@ def main():
         prep_s = time.perf_counter() - tp0
         # every step answers one whole 1000-query batch; batch i + 1 is queued before batch i's one host
         # sync (progressive_submit / progressive_finish), so the GPU does not idle on the host between
-        # batches; the last batch is finished inside the timed region
-        pend = []
+        # batches; the last batch is finished inside the timed region.  HQ_SEARCH_STREAMS=n (A/B knob)
+        # alternates the batches over n HIP streams: 2 / 3 streams measured 1.43M / 0.7-1.05M vs 2.07M QPS
+        # on one (two batches' scans contend for the CUs), so one stream is the default
+        nstreams = int(os.environ.get("HQ_SEARCH_STREAMS", "1"))
+        streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
+        pend, nsub = [], [0]
 
         def run():
-            pend.append(engine.progressive_submit(queries, 10, 0.1, 20))
+            st = streams[nsub[0] % len(streams)]
+            nsub[0] += 1
+            with torch.cuda.stream(st):
+                pend.append((st, engine.progressive_submit(queries, 10, 0.1, 20)))
             if len(pend) > 1:
-                engine.progressive_finish(pend.pop(0))
+                drain(1)
 
-        def drain():
-            while pend:
-                engine.progressive_finish(pend.pop(0))
+        def drain(n=None):
+            while pend and (n is None or n > 0):
+                st, p = pend.pop(0)
+                with torch.cuda.stream(st):
+                    engine.progressive_finish(p)
+                n = None if n is None else n - 1
 
         swall, skern = timed(run, args.search_steps, 1, world, drain)
         qps = Qn * args.search_steps / swall

@@ -1217,6 +1217,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   const int qb = slot % a.nqb;
   if (chunk >= a.nchunks) return;
   const int64_t c_begin = (int64_t)chunk * a.chunk_len;
+  // chunks past the corpus end exist when nchunks * chunk_len (both rounded up) exceeds N by more than
+  // a chunk (small corpora: N = 3000 -> 192 chunks of 16 rows); their prologue loads (rows c_begin ..
+  // c_begin + 31, unclamped) would read past the kPad0 padding rows, so they leave before any load.
+  // Every other chunk reads at most row c_end + 46 < N + kPad0.
+  if (c_begin >= a.N) return;
   int64_t c_end = c_begin + a.chunk_len;
   if (c_end > a.N) c_end = a.N;
   const int q0 = qb * QW;

@@ -208,17 +208,27 @@ def test_pipelined_submit_finish_equals_sequential(hq_lib):
     rng = np.random.default_rng(52)
     batches = [(C[[1, 2, 3]] + rng.normal(0, 0.01, (3, 64)), 0.1), (C[[7, 8]] + 0.02, 0.97),
                (C[100:140] + rng.normal(0, 0.01, (40, 64)), 0.1), (rng.standard_normal((5, 64)), 0.97)]
+    import torch
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
     for corpus in (IndexCorpus(C), ShardedIndexCorpus(C, id_base=0, n_total=len(C))):
         ref = [[_np(x) for x in corpus.progressive(q, 10, thr, 20)] for q, thr in batches]
-        pend, got = [], []
-        for q, thr in batches:
-            pend.append(corpus.progressive_submit(q, 10, thr, 20))
-            if len(pend) > 1:
-                got.append([_np(x) for x in corpus.progressive_finish(pend.pop(0))])
-        got += [[_np(x) for x in corpus.progressive_finish(p)] for p in pend]
-        for b, (r, g) in enumerate(zip(ref, got)):
-            for x, y in zip(r, g):
-                assert np.array_equal(x, y), (type(corpus).__name__, b)
+        for nst in (1, 2):  # one stream, or batches alternating between two (as bench.py runs them)
+            pend, got = [], []
+            for i, (q, thr) in enumerate(batches):
+                st = streams[i % nst]
+                with torch.cuda.stream(st):
+                    pend.append((st, corpus.progressive_submit(q, 10, thr, 20)))
+                if len(pend) > 1:
+                    st0, p = pend.pop(0)
+                    with torch.cuda.stream(st0):
+                        got.append([_np(x) for x in corpus.progressive_finish(p)])
+            for st0, p in pend:
+                with torch.cuda.stream(st0):
+                    got.append([_np(x) for x in corpus.progressive_finish(p)])
+            torch.cuda.synchronize()
+            for b, (r, g) in enumerate(zip(ref, got)):
+                for x, y in zip(r, g):
+                    assert np.array_equal(x, y), (type(corpus).__name__, nst, b)
 
 
 def test_rag_scores(hq_lib, golden):
