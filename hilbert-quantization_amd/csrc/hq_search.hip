@@ -80,6 +80,55 @@ constexpr int kAuxF32 = 1, kAuxUnsafe = 2;
 
 __device__ __forceinline__ int aux_bits(const double* st) { return (int)st[3]; }
 
+// one (row, segment): x = the row's raw values (global memory or an LDS copy of the row)
+__device__ __forceinline__ void seg_prepare_one(const double* xrow, int64_t row, int s, const SegInfo& si,
+                                                int all_f32, const uint8_t* __restrict__ row_f32,
+                                                double* __restrict__ Z, double* __restrict__ stats) {
+  const double* x = xrow + si.src[s];
+  const int m = si.len[s];
+  auto fx = [=](int k) -> double { return x[k]; };
+  const double mean = np_sum<double>(fx, m) / (double)m;            // np.mean
+  auto fd = [=](int k) -> double { double d = x[k] - mean; return d * d; };
+  const double sd = sqrt(np_sum<double>(fd, m) / (double)m);        // np.std (_methods._var)
+  auto fs = [=](int k) -> double { return x[k] * x[k]; };
+  const double msq = np_sum<double>(fs, m) / (double)m;             // np.mean(q ** 2)
+  double* z = Z + row * si.Lp + si.poff[s];
+  double* st = stats + (row * si.nseg + s) * 4;
+  if (row_f32 ? row_f32[row] != 0 : all_f32 != 0) {
+    // _methods._var on float32: f32 pairwise sum, divide, x - mean, x * x, f32 pairwise sum, divide,
+    // sqrt (np.mean = f32(f64(sum) / m) = the f32 division: the double rounding is innocuous)
+    auto gx = [=](int k) -> float { return (float)x[k]; };
+    const float mean32 = np_sum<float>(gx, m) / (float)m;
+    auto gd = [=](int k) -> float { float d = (float)x[k] - mean32; return d * d; };
+    const float sd32 = sqrtf(np_sum<float>(gd, m) / (float)m);
+    int aux = kAuxF32;
+    if (!(msq >= 0x1p-100 && msq <= 0x1p100)) aux |= kAuxUnsafe;
+    if (sd32 == 0.0f) {
+      for (int i = 0; i < si.plen[s]; ++i) z[i] = 0.0;
+      st[0] = (double)mean32;
+      st[1] = 0.0;
+    } else {
+      for (int i = 0; i < m; ++i) z[i] = (double)(((float)x[i] - mean32) / sd32);  // (q - mean(q)) / std
+      for (int i = m; i < si.plen[s]; ++i) z[i] = 0.0;
+      st[0] = mean;
+      st[1] = (double)sd32;
+    }
+    st[2] = msq;
+    st[3] = (double)aux;
+    return;
+  }
+  if (sd == 0.0) {
+    for (int i = 0; i < si.plen[s]; ++i) z[i] = 0.0;
+  } else {
+    for (int i = 0; i < m; ++i) z[i] = (x[i] - mean) / sd;          // (q - mean(q)) / std (:150-151)
+    for (int i = m; i < si.plen[s]; ++i) z[i] = 0.0;
+  }
+  st[0] = mean;
+  st[1] = sd;
+  st[2] = msq;
+  st[3] = 0.0;
+}
+
 __global__ __launch_bounds__(256) void k_seg_prepare(const double* __restrict__ idx, int64_t N, SegInfo si,
                                                      int all_f32, const uint8_t* __restrict__ row_f32,
                                                      double* __restrict__ Z, double* __restrict__ stats) {
@@ -87,50 +136,24 @@ __global__ __launch_bounds__(256) void k_seg_prepare(const double* __restrict__ 
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t row = t / si.nseg;
-    const int s = (int)(t % si.nseg);
-    const double* x = idx + row * si.L + si.src[s];
-    const int m = si.len[s];
-    auto fx = [=](int k) -> double { return x[k]; };
-    const double mean = np_sum<double>(fx, m) / (double)m;            // np.mean
-    auto fd = [=](int k) -> double { double d = x[k] - mean; return d * d; };
-    const double sd = sqrt(np_sum<double>(fd, m) / (double)m);        // np.std (_methods._var)
-    auto fs = [=](int k) -> double { return x[k] * x[k]; };
-    const double msq = np_sum<double>(fs, m) / (double)m;             // np.mean(q ** 2)
-    double* z = Z + row * si.Lp + si.poff[s];
-    double* st = stats + (row * si.nseg + s) * 4;
-    if (row_f32 ? row_f32[row] != 0 : all_f32 != 0) {
-      // _methods._var on float32: f32 pairwise sum, divide, x - mean, x * x, f32 pairwise sum, divide,
-      // sqrt (np.mean = f32(f64(sum) / m) = the f32 division: the double rounding is innocuous)
-      auto gx = [=](int k) -> float { return (float)x[k]; };
-      const float mean32 = np_sum<float>(gx, m) / (float)m;
-      auto gd = [=](int k) -> float { float d = (float)x[k] - mean32; return d * d; };
-      const float sd32 = sqrtf(np_sum<float>(gd, m) / (float)m);
-      int aux = kAuxF32;
-      if (!(msq >= 0x1p-100 && msq <= 0x1p100)) aux |= kAuxUnsafe;
-      if (sd32 == 0.0f) {
-        for (int i = 0; i < si.plen[s]; ++i) z[i] = 0.0;
-        st[0] = (double)mean32;
-        st[1] = 0.0;
-      } else {
-        for (int i = 0; i < m; ++i) z[i] = (double)(((float)x[i] - mean32) / sd32);  // (q - mean(q)) / std
-        for (int i = m; i < si.plen[s]; ++i) z[i] = 0.0;
-        st[0] = mean;
-        st[1] = (double)sd32;
-      }
-      st[2] = msq;
-      st[3] = (double)aux;
-      continue;
-    }
-    if (sd == 0.0) {
-      for (int i = 0; i < si.plen[s]; ++i) z[i] = 0.0;
-    } else {
-      for (int i = 0; i < m; ++i) z[i] = (x[i] - mean) / sd;          // (q - mean(q)) / std (:150-151)
-      for (int i = m; i < si.plen[s]; ++i) z[i] = 0.0;
-    }
-    st[0] = mean;
-    st[1] = sd;
-    st[2] = msq;
-    st[3] = 0.0;
+    seg_prepare_one(idx + row * si.L, row, (int)(t % si.nseg), si, all_f32, row_f32, Z, stats);
+  }
+}
+
+// Small batches (query preparation: 1,000 rows x 5 segments is only ~20 workgroups of the kernel
+// above, each thread walking three dependent chains of global loads, ~18 us): one wave per row copies
+// the row to LDS with one coalesced load, then one lane per segment runs the same arithmetic on the
+// LDS copy (bit-identical results).
+__global__ __launch_bounds__(64) void k_seg_prepare_lds(const double* __restrict__ idx, int64_t N, SegInfo si,
+                                                        int all_f32, const uint8_t* __restrict__ row_f32,
+                                                        double* __restrict__ Z, double* __restrict__ stats) {
+  extern __shared__ double xs[];  // L values
+  const int lane = threadIdx.x;
+  for (int64_t row = blockIdx.x; row < N; row += gridDim.x) {
+    for (int i = lane; i < si.L; i += 64) xs[i] = idx[row * si.L + i];
+    __syncthreads();
+    for (int s = lane; s < si.nseg; s += 64) seg_prepare_one(xs, row, s, si, all_f32, row_f32, Z, stats);
+    __syncthreads();
   }
 }
 
@@ -3013,10 +3036,15 @@ int hq_seg_prepare_rows(const double* idx, int64_t N, int L, int src_f32, const 
   seg_info(L, si);
   if (si.nseg == 0) return fail(HQ_E_INVALID, "no level structure for L=%d", L);
   const int64_t total = N * si.nseg;
-  int64_t blocks = (total + 255) / 256;
-  if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(k_seg_prepare, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, idx, N, si, src_f32 ? 1 : 0,
-                     row_f32, Z, stats);
+  if (N <= 16384 && si.L <= 4096 && !getenv("HQ_SEG_PREPARE_FLAT")) {  // A/B knob: the flat kernel
+    hipLaunchKernelGGL(k_seg_prepare_lds, dim3((unsigned)N), dim3(64), (size_t)8 * si.L, (hipStream_t)stream, idx, N,
+                       si, src_f32 ? 1 : 0, row_f32, Z, stats);
+  } else {
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(k_seg_prepare, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, idx, N, si,
+                       src_f32 ? 1 : 0, row_f32, Z, stats);
+  }
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
