@@ -2004,11 +2004,18 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
 // bits + 1, 0 = empty), th0 = v - margin, or -inf when fewer than K sample scores exist
 constexpr int kKthReg = 32;  // pool entries per lane: 4 * 256 chunks * kTopT / 64
 
+// Also clears the scan's per-query published threshold and pool count (gtau, pool_n; top-T mode has no
+// histogram, so no memset runs before the scan).
 __global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top, int ns, int Q, int K, double margin,
-                                                   double* __restrict__ th0) {
+                                                   double* __restrict__ th0, unsigned long long* __restrict__ gtau,
+                                                   int* __restrict__ pool_n) {
   const int lane = threadIdx.x;
   const int P = ns * kTopT;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    if (lane == 0) {
+      gtau[q] = 0ull;
+      pool_n[q] = 0;
+    }
     const float* p = top + (int64_t)q * P;
     uint32_t u[kKthReg];
 #pragma unroll
@@ -2841,9 +2848,11 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   if (sample_kth <= 0 || sample_kth > k) sample_kth = k;
   float* top = reinterpret_cast<float*>(ws + lists + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 4 +
                                         (size_t)Q * 8);
-  // (the histogram region lies between gtau and pool_n, so it is cleared with them in every mode)
-  HQ_CHECK_HIP(hipMemsetAsync(b.gtau, 0, (size_t)Q * 8 + (sample ? (size_t)Q * kBins * 4 : 0) + (f32 ? (size_t)Q * 4 : 0),
-                              s));
+  // (the histogram region lies between gtau and pool_n, so it is cleared with them; the top-T sample
+  // has no histogram and k_sample_kth clears gtau and pool_n per query)
+  if (!top_sample)
+    HQ_CHECK_HIP(hipMemsetAsync(b.gtau, 0, (size_t)Q * 8 + (sample ? (size_t)Q * kBins * 4 : 0) + (f32 ? (size_t)Q * 4 : 0),
+                                s));
   if (f32 && !sample) HQ_CHECK_HIP(hipMemsetAsync(b.pool_n, 0, sizeof(int) * Q, s));
   int rc;
   if (top_sample) {
@@ -2860,7 +2869,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     HQ_CHECK_LAUNCH();
     const int mg = Q < 8192 ? Q : 8192;
     hipLaunchKernelGGL(k_sample_kth, dim3(mg), dim3(64), 0, s, (const float*)top, 4 * sa.nchunks, Q, sample_kth,
-                       (double)kMarginF, th0);
+                       (double)kMarginF, th0, b.gtau, b.pool_n);
     HQ_CHECK_LAUNCH();
     b.th0 = th0;
   } else if (sample) {

@@ -266,7 +266,7 @@ class IndexCorpus:
         best, bid, bdet = self._no_fallback(Q, qp.Z.device)
         oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out, bdet, det)
         # the shared device counter is overwritten by the next batch: this batch's value leaves now
-        host = t.empty(1, dtype=nredo.dtype, pin_memory=True)
+        host = self._pinned(nredo.dtype)
         host.copy_(nredo, non_blocking=True)
         ev = t.cuda.Event()
         ev.record()
@@ -281,7 +281,9 @@ class IndexCorpus:
         t = torch()
         oid, odet, ocnt = p.out
         p.event.synchronize()
-        if p.forced is not None or int(p.nredo[0]) > 0:
+        nredo = int(p.nredo[0])
+        self._pinned_free.setdefault(p.nredo.dtype, []).append(p.nredo)  # read: reusable
+        if p.forced is not None or nredo > 0:
             redo = (p.res == 0) | (p.cnt == 0)
             if p.forced is not None:
                 redo = redo | p.forced
@@ -292,6 +294,12 @@ class IndexCorpus:
                 o2, d2, c2 = self._final(sub, s2, i2, b2, bi2, p.K_out)
                 oid[sel], odet[sel], ocnt[sel] = o2, d2, c2
         return oid, odet[..., 0], odet[..., 1:], ocnt
+
+    def _pinned(self, dtype):
+        """A one-element pinned host buffer: recycled once its batch is finished (a fresh pinned
+        allocation per batch can stall the host between launches)."""
+        free = self.__dict__.setdefault("_pinned_free", {}).setdefault(dtype, [])
+        return free.pop() if free else torch().empty(1, dtype=dtype, pin_memory=True)
 
     def _redo_counter(self, dev):
         """Device int32 [1] the exact re-rank sets to the number of queries needing the dense path."""

@@ -79,7 +79,7 @@ class ShardedIndexCorpus:
         forced = c._forced(qp)
         if forced is not None:
             redo = redo | forced
-        flag = t.empty(1, dtype=t.bool, pin_memory=True)
+        flag = c._pinned(t.bool)
         flag.copy_(redo.any().view(1), non_blocking=True)
         ev = t.cuda.Event()
         ev.record()
@@ -89,7 +89,9 @@ class ShardedIndexCorpus:
         t = torch()
         qp, M, threshold, rec, redo, flag, ev = pending
         ev.synchronize()
-        if bool(flag[0]):
+        any_redo = bool(flag[0])
+        self.local._pinned_free.setdefault(flag.dtype, []).append(flag)  # read: reusable
+        if any_redo:
             sel = t.nonzero(redo).view(-1)
             s2, i2, b2, bi2 = self.local._dense(qp, sel, 0, M, threshold, 1)
             rec[sel] = self._records(qp.rows(sel), s2, i2, b2, bi2)
