@@ -2362,6 +2362,122 @@ __global__ __launch_bounds__(64) void k_select_merge(int Q, int P, int k, double
   }
 }
 
+// Register-resident multi-stage select for few queries (the dense redo of a handful of queries: the
+// two-stage form above then runs only N / 8192 waves per query, each making k passes over its part in
+// memory — 1.1 ms for one 1M-entry row).  Stage 1: one wave per (query, part of kRegSel entries) holds
+// its entries in registers (kSelR per lane) and makes the k passes there; merge stages take fan-in F
+// parts' candidates the same way until one part remains.  Same total order (score desc, row asc), same
+// threshold test and first arg-max as select_row, so the result is identical.
+constexpr int kSelR = 16;
+constexpr int kRegSel = 64 * kSelR;
+
+__device__ __forceinline__ void wave_best(double& bs, int64_t& bi) {
+  for (int o = 1; o < 64; o <<= 1) {
+    const double s2 = __shfl_xor(bs, o, 64);
+    const int64_t i2 = __shfl_xor(bi, o, 64);
+    if (i2 >= 0 && (bi < 0 || better(s2, i2, bs, bi))) { bs = s2; bi = i2; }
+  }
+}
+
+// k passes over the wave's register entries (id < 0: empty): (score, id + id_add), padded with -inf / -1
+__device__ __forceinline__ void reg_topk(const double (&s)[kSelR], const int64_t (&id)[kSelR], int k, int64_t id_add,
+                                         double* __restrict__ out_s, int64_t* __restrict__ out_id) {
+  const int lane = threadIdx.x & 63;
+  double ps = __builtin_huge_val();
+  int64_t pid = -1;
+  for (int j = 0; j < k; ++j) {
+    double bs = 0.0;
+    int64_t bi = -1;
+#pragma unroll
+    for (int r = 0; r < kSelR; ++r) {
+      const bool after = pid < 0 || better(ps, pid, s[r], id[r]);  // must come after the previous pick
+      if (id[r] >= 0 && after && (bi < 0 || better(s[r], id[r], bs, bi))) { bs = s[r]; bi = id[r]; }
+    }
+    wave_best(bs, bi);
+    if (lane == 0) {
+      out_s[j] = bi >= 0 ? bs : -__builtin_huge_val();
+      out_id[j] = bi >= 0 ? bi + id_add : -1;
+    }
+    if (bi < 0) {
+      for (int jj = j + 1 + lane; jj < k; jj += 64) {
+        out_s[jj] = -__builtin_huge_val();
+        out_id[jj] = -1;
+      }
+      break;
+    }
+    ps = bs;
+    pid = bi;
+  }
+}
+
+// stage 1: parts of a dense [Q, N] row; ids = row index (+ id_add when this is the last stage)
+__global__ __launch_bounds__(64) void k_select_reg1(const double* __restrict__ sc, int Q, int64_t N, int P, int k,
+                                                    double thr, int thr_mode, int64_t id_add,
+                                                    double* __restrict__ o_s, int64_t* __restrict__ o_id,
+                                                    double* __restrict__ o_b, int64_t* __restrict__ o_bid) {
+  const int lane = threadIdx.x;
+  for (int64_t t = blockIdx.x; t < (int64_t)Q * P; t += gridDim.x) {
+    const int64_t q = t / P, c0 = (t % P) * kRegSel;
+    double s[kSelR];
+    int64_t id[kSelR];
+    double bs = 0.0;
+    int64_t bi = -1;  // first arg-max over every entry (no threshold)
+#pragma unroll
+    for (int r = 0; r < kSelR; ++r) {
+      const int64_t c = c0 + lane + 64 * r;
+      const bool valid = c < N;
+      const double v = valid ? sc[q * N + c] : 0.0;
+      if (valid && (bi < 0 || better(v, c, bs, bi))) { bs = v; bi = c; }
+      const bool pass = thr_mode == 0 || (thr_mode == 1 ? v >= thr : v > thr);
+      s[r] = v;
+      id[r] = valid && pass ? c : -1;
+    }
+    wave_best(bs, bi);
+    if (lane == 0 && o_b) {
+      o_b[t] = bi >= 0 ? bs : -__builtin_huge_val();
+      o_bid[t] = bi >= 0 ? bi + id_add : -1;
+    }
+    reg_topk(s, id, k, id_add, o_s + t * k, o_id + t * k);
+  }
+}
+
+// merge stage: group g of query q = parts [g F, g F + F) of the previous stage (P parts) -> one part
+__global__ __launch_bounds__(64) void k_select_regm(int Q, int P, int F, int P2, int k, int64_t id_add,
+                                                    const double* __restrict__ i_s, const int64_t* __restrict__ i_id,
+                                                    const double* __restrict__ i_b, const int64_t* __restrict__ i_bid,
+                                                    double* __restrict__ o_s, int64_t* __restrict__ o_id,
+                                                    double* __restrict__ o_b, int64_t* __restrict__ o_bid) {
+  const int lane = threadIdx.x;
+  for (int64_t t = blockIdx.x; t < (int64_t)Q * P2; t += gridDim.x) {
+    const int64_t q = t / P2, p0 = (t % P2) * F;
+    const int np = (int)(P - p0 < F ? P - p0 : F);
+    const int64_t base = (q * P + p0) * k;
+    double s[kSelR];
+    int64_t id[kSelR];
+#pragma unroll
+    for (int r = 0; r < kSelR; ++r) {
+      const int e = lane + 64 * r;
+      const bool valid = e < np * k;
+      s[r] = valid ? i_s[base + e] : 0.0;
+      id[r] = valid ? i_id[base + e] : -1;  // threshold already applied in stage 1
+    }
+    reg_topk(s, id, k, id_add, o_s + t * k, o_id + t * k);
+    if (o_b) {
+      double bs = 0.0;
+      int64_t bi = -1;
+      if (lane < np) {
+        const int64_t i = i_bid[q * P + p0 + lane];
+        if (i >= 0) { bs = i_b[q * P + p0 + lane]; bi = i; }
+      }
+      wave_best(bs, bi);
+      if (lane == 0) {
+        o_b[t] = bi >= 0 ? bs : -__builtin_huge_val();
+        o_bid[t] = bi >= 0 ? bi + id_add : -1;
+      }
+    }
+  }
+}
+
 // compare_indices_at_level on raw equal-length segments (mixed-length candidate pools): the query
 // segment q[0..m) against each row of C (N x m), statistics computed in place in NumPy order and in each
 // side's dtype (q_f32 / c_f32: float32 values).
@@ -3282,12 +3398,23 @@ static void select_parts(int Q, int64_t N, int& P, int64_t& plen) {
   plen = (N + P - 1) / P;
 }
 
+// the register-resident multi-stage select runs when the two-stage form would have few waves
+static bool select_reg_ok(int Q, int64_t N, int k) {
+  return N > 0 && k >= 16 && k <= 64 && (int64_t)Q * ((N + 8191) / 8192) < 4096 && !getenv("HQ_SELECT_2STAGE");
+}
+static int64_t select_reg_parts(int64_t N) { return (N + kRegSel - 1) / kRegSel; }
+
 size_t hq_select_workspace_size(int Q, int64_t N, int k) {
   if (Q <= 0 || N <= 0 || k <= 0) return 0;
   int P;
   int64_t plen;
   select_parts(Q, N, P, plen);
-  return (size_t)Q * P * ((size_t)k + 1) * 16 + 256;
+  size_t two = (size_t)Q * P * ((size_t)k + 1) * 16 + 256;
+  if (select_reg_ok(Q, N, k)) {  // two ping-pong stage buffers of the stage-1 size
+    const size_t reg = 2 * (size_t)Q * select_reg_parts(N) * ((size_t)k + 1) * 16 + 256;
+    if (reg > two) two = reg;
+  }
+  return two;
 }
 
 int hq_select_topk_ws(const double* scores, int Q, int64_t N, int k, double threshold, int thr_mode,
@@ -3298,6 +3425,51 @@ int hq_select_topk_ws(const double* scores, int Q, int64_t N, int k, double thre
   int P;
   int64_t plen;
   select_parts(Q, N, P, plen);
+  if (workspace && out_score && out_id && scores && select_reg_ok(Q, N, k) && P > 1) {
+    if (workspace_bytes < hq_select_workspace_size(Q, N, k)) return fail(HQ_E_INVALID, "workspace too small");
+    const hipStream_t s = (hipStream_t)stream;
+    const int64_t P1 = select_reg_parts(N);
+    const int F = kRegSel / k < 64 ? kRegSel / k : 64;  // fan-in: F k <= kRegSel candidates, F <= 64 arg-maxes
+    const size_t cap = (size_t)Q * P1;                   // parts a stage buffer holds
+    uint8_t* w = reinterpret_cast<uint8_t*>(workspace);
+    auto region = [&](int r, double*& rs, int64_t*& ri, double*& rb, int64_t*& rbi) {
+      uint8_t* b = w + (size_t)r * cap * ((size_t)k + 1) * 16;
+      rs = reinterpret_cast<double*>(b);
+      ri = reinterpret_cast<int64_t*>(b + cap * k * 8);
+      rb = reinterpret_cast<double*>(b + cap * k * 16);
+      rbi = reinterpret_cast<int64_t*>(b + cap * k * 16 + cap * 8);
+    };
+    double *as, *bs_, *ab, *bb;
+    int64_t *ai, *bi, *abi, *bbi;
+    region(0, as, ai, ab, abi);
+    region(1, bs_, bi, bb, bbi);
+    // every stage keeps the arg-maxes (the final one writes them only when requested)
+    int64_t P = P1;
+    const bool last1 = P == 1;
+    int64_t g = (int64_t)Q * P < 65536 ? (int64_t)Q * P : 65536;
+    hipLaunchKernelGGL(k_select_reg1, dim3((unsigned)g), dim3(64), 0, s, scores, Q, N, (int)P, k, threshold, thr_mode,
+                       last1 ? id_base : 0, last1 ? out_score : as, last1 ? out_id : ai, last1 ? out_best : ab,
+                       last1 ? out_best_id : abi);
+    HQ_CHECK_LAUNCH();
+    int cur = 0;
+    while (P > 1) {
+      const int64_t P2 = (P + F - 1) / F;
+      const bool last = P2 == 1;
+      double *is_, *ib, *os_, *ob;
+      int64_t *ii, *ibi, *oi, *obi;
+      if (cur == 0) { is_ = as; ii = ai; ib = ab; ibi = abi; os_ = bs_; oi = bi; ob = bb; obi = bbi; }
+      else { is_ = bs_; ii = bi; ib = bb; ibi = bbi; os_ = as; oi = ai; ob = ab; obi = abi; }
+      g = (int64_t)Q * P2 < 65536 ? (int64_t)Q * P2 : 65536;
+      hipLaunchKernelGGL(k_select_regm, dim3((unsigned)g), dim3(64), 0, s, Q, (int)P, F, (int)P2, k,
+                         last ? id_base : 0, (const double*)is_, (const int64_t*)ii, (const double*)ib,
+                         (const int64_t*)ibi, last ? out_score : os_, last ? out_id : oi, last ? out_best : ob,
+                         last ? out_best_id : obi);
+      HQ_CHECK_LAUNCH();
+      P = P2;
+      cur ^= 1;
+    }
+    return HQ_OK;
+  }
   if (P == 1 || !workspace)
     return hq_select_topk(scores, Q, N, k, threshold, thr_mode, id_base, out_score, out_id, out_best, out_best_id,
                           stream);

@@ -437,3 +437,37 @@ def test_statistical_start_threshold_is_exact(hq_lib, monkeypatch):
     for a in (0, 1, 20):
         rid, _, _, _ = O.progressive_search(Q[a], C, 10, 0.1, 20)
         assert list(ids[a][: cnt[a]]) == list(rid), a
+
+
+def _np_select(row, k, thr, thr_mode):
+    """Reference of hq_select_topk: top-k by (score desc, index asc) among entries passing the
+    threshold test, padded with (-inf, -1); first arg-max over all entries."""
+    idx = np.arange(len(row))
+    ok = np.ones(len(row), bool) if thr_mode == 0 else (row >= thr if thr_mode == 1 else row > thr)
+    cand = sorted(zip(-row[ok], idx[ok]))[:k]
+    s = [-a for a, _ in cand] + [-np.inf] * (k - len(cand))
+    i = [b for _, b in cand] + [-1] * (k - len(cand))
+    b = min(zip(-row, idx))
+    return np.array(s), np.array(i), -b[0], b[1]
+
+
+@pytest.mark.parametrize("N", [1, 100, 1025, 9000, 70000])
+def test_select_topk_register_stages(hq_lib, monkeypatch, N):
+    """The register-resident multi-stage select (few queries: the dense redo) equals the reference order
+    and the two-stage select, with ties (quantised scores), thresholds and id_base."""
+    import torch
+    from hq_mi355x import kernels as K
+    rng = np.random.default_rng(N)
+    sc = np.round(rng.random((3, N)), 2)  # many ties
+    for k in (16, 20, 28, 64):
+        for thr, mode in ((0.0, 0), (0.5, 1), (0.5, 2), (0.995, 1)):
+            got = [_np(x) for x in K.select_topk(torch.tensor(sc, device="cuda"), k, thr, mode, 7)]
+            monkeypatch.setenv("HQ_SELECT_2STAGE", "1")
+            two = [_np(x) for x in K.select_topk(torch.tensor(sc, device="cuda"), k, thr, mode, 7)]
+            monkeypatch.delenv("HQ_SELECT_2STAGE")
+            for x, y in zip(got, two):
+                assert np.array_equal(x, y), (N, k, thr, mode)
+            for q in range(3):
+                s, i, b, bi = _np_select(sc[q], k, thr, mode)
+                assert np.array_equal(got[0][q], s) and np.array_equal(got[1][q], np.where(i >= 0, i + 7, -1)), (N, k, q)
+                assert got[2][q] == b and got[3][q] == bi + 7
