@@ -293,7 +293,8 @@ class IndexCorpus:
                 sub = p.qp.rows(sel)
                 o2, d2, c2 = self._final(sub, s2, i2, b2, bi2, p.K_out)
                 oid[sel], odet[sel], ocnt[sel] = o2, d2, c2
-        return oid, odet[..., 0], odet[..., 1:], ocnt
+        p.done = (oid, odet[..., 0], odet[..., 1:], ocnt)  # finishing again returns the same results
+        return p.done
 
     def _pinned(self, dtype):
         """A one-element pinned host buffer: recycled once its batch is finished (a fresh pinned

@@ -126,7 +126,7 @@ class ShardedIndexCorpus:
         c = self.local
         M = int(max_candidates_per_level)
         if self.n_total <= M:
-            return ("done", self.brute_force(queries, max_results))
+            return ["done", self.brute_force(queries, max_results)]
         qp = c.prepare_queries(queries)
         if M + c.SLACK > 64 or c.dense_only or not c._fused_ok(0):  # the dense exact path per shard (list length / f32 model)
             t = torch()
@@ -135,14 +135,17 @@ class ShardedIndexCorpus:
             det = K.rescore(qp, c.prep, ids, c.id_base)
             bdet = K.rescore(qp, c.prep, bid.view(Q, 1), c.id_base)
             rec = t.cat([pack(s0, ids, det), pack(best.view(Q, 1), bid.view(Q, 1), bdet)], dim=1)
-            return ("rec", rec, M, max_results)
-        return ("pending", self._local_submit(qp, M, threshold), M, max_results)
+            return ["rec", rec, M, max_results]
+        return ["pending", self._local_submit(qp, M, threshold), M, max_results]
 
     def progressive_finish(self, p):
+        """Gather and merge a submitted batch (once: the handle then holds the results)."""
         if p[0] == "done":
             return p[1]
         rec = p[1] if p[0] == "rec" else self._local_finish(p[1])
-        return self.merge(all_gather(rec, self.group), p[2], p[3])
+        out = self.merge(all_gather(rec, self.group), p[2], p[3])
+        p[:] = ["done", out]
+        return out
 
     def brute_force(self, queries, max_results: int):
         """Global top-k by the overall score: local top-k, all-gather, R-way merge."""

@@ -225,6 +225,8 @@ def test_pipelined_submit_finish_equals_sequential(hq_lib):
             for st0, p in pend:
                 with torch.cuda.stream(st0):
                     got.append([_np(x) for x in corpus.progressive_finish(p)])
+                    again = [_np(x) for x in corpus.progressive_finish(p)]  # a handle finishes once
+                    assert all(np.array_equal(x, y) for x, y in zip(got[-1], again))
             torch.cuda.synchronize()
             for b, (r, g) in enumerate(zip(ref, got)):
                 for x, y in zip(r, g):
