@@ -35,6 +35,26 @@ int fail(int code, const char* fmt, ...);
     if (_e != hipSuccess) return ::hq::fail(HQ_E_HIP, "kernel launch: %s", hipGetErrorString(_e)); \
   } while (0)
 
+// ------------------------------------------------------------------------------------------------
+// kernel-variant options (hq_set_option, include/hq_mi355x.h).  The library never reads the
+// environment in a default build: a variant is selected only by an explicit hq_set_option call
+// (parity tests, A/B tools).  `make DIAG=1` builds also take HQ_<NAME> from the environment once, at
+// load.  opt(id, dflt) = the set value, else the call site's default.
+// ------------------------------------------------------------------------------------------------
+enum Opt {
+  OPT_FUSED_V, OPT_FUSED_GENERIC,
+  OPT_CHUNK_NT, OPT_CHUNK_EXACTDIV, OPT_CHUNK_GENERIC, OPT_CHUNK_WPB, OPT_CHUNK_CPW,
+  OPT_PRECOMP_NT, OPT_PRECOMP_TREE_LDS, OPT_PRECOMP_PAD, OPT_PRECOMP_SKIP, OPT_PRECOMP_GRID, OPT_PRECOMP_PF,
+  OPT_PRECOMP_DIAG,
+  OPT_COS_KERNEL,
+  OPT_SAMPLE_STRIDE, OPT_SAMPLE_WAVES, OPT_SAMPLE_KTH,
+  OPT_SCAN_V1, OPT_SCAN_NOSAMPLE, OPT_SCAN_EXPT, OPT_SCAN_VARIANT,
+  OPT_REFINE_GLOBAL, OPT_REFINE_EXPT, OPT_SEG_PREPARE_FLAT, OPT_SELECT_2STAGE,
+  OPT_COUNT
+};
+int64_t opt(Opt id, int64_t dflt);
+inline bool opt_on(Opt id) { return opt(id, 0) != 0; }
+
 inline bool is_pow2(int64_t n) { return n > 0 && (n & (n - 1)) == 0; }
 inline int ilog2(int64_t n) { int k = 0; while ((int64_t(1) << k) < n) ++k; return k; }
 

@@ -457,12 +457,12 @@ int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* 
   a.Kp = hq_cos_padded_k(K);
   a.ntiles = hq_cos_padded_rows(N) / kCosT;
   a.out = out;
-  // A/B: HQ_COS_KERNEL=regstage (register-staged two-buffer kernel) or lockstep (the DMA kernel without
-  // the ping-pong stagger); DESIGN.md §4.5 has the measurements
-  const char* ek = getenv("HQ_COS_KERNEL");
-  if (ek && strcmp(ek, "regstage") == 0) return launch_cos<128>(a, (hipStream_t)stream);
-  if (ek && strcmp(ek, "lockstep") == 0) return launch_g3<256, 0>(a, (hipStream_t)stream);
-  if (ek && strcmp(ek, "temporal") == 0) return launch_g3<256, 1, false>(a, (hipStream_t)stream);
+  // A/B (option cos_kernel): 1 register-staged two-buffer kernel, 2 lockstep (the DMA kernel without the
+  // ping-pong stagger), 3 temporal score stores; DESIGN.md §4.5 has the measurements
+  const int64_t ek = opt(OPT_COS_KERNEL, 0);
+  if (ek == 1) return launch_cos<128>(a, (hipStream_t)stream);
+  if (ek == 2) return launch_g3<256, 0>(a, (hipStream_t)stream);
+  if (ek == 3) return launch_g3<256, 1, false>(a, (hipStream_t)stream);
   return launch_g3<256, 1>(a, (hipStream_t)stream);
 }
 

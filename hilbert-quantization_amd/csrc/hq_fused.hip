@@ -535,8 +535,7 @@ int fused_fast(const float* in, int64_t N, int64_t stride, int d, int n, int L, 
   }
   if (L < n) plan.zero_row = 1;
   const int nd = (((d + 3) / 4) + 63) / 64;
-  const char* ev = getenv("HQ_FUSED_V");
-  const int variant = ev ? atoi(ev) : kDefaultV;
+  const int variant = (int)opt(OPT_FUSED_V, kDefaultV);
   switch (n) {
     case 16: return pick_nd<16, 1>(variant, nd, in, N, stride, d, L, plan, frame, idx, mm, s);
     case 32: return pick_nd<32, 1>(variant, nd, in, N, stride, d, L, plan, frame, idx, mm, s);

@@ -550,9 +550,8 @@ static int launch_chunk_np(const uint16_t* in, int64_t nchunks, const TradPlan& 
     if (cell == -2) return HQ_E_UNSUPPORTED;
     cp.cell[i] = (int16_t)cell;
   }
-  const char* nev = getenv("HQ_CHUNK_NT");  // A/B bits: 1 non-temporal stores (measured equal), 2 loads
-  const int nt = nev ? atoi(nev) : 0;
-  if (getenv("HQ_CHUNK_EXACTDIV"))
+  const int nt = (int)opt(OPT_CHUNK_NT, 0);  // A/B bits: 1 non-temporal stores (measured equal), 2 loads
+  if (opt_on(OPT_CHUNK_EXACTDIV))
     hipLaunchKernelGGL((k_chunk_np<NS, WPB, false, CPW, 0>), dim3((unsigned)grid), dim3(64 * WPB), 0, s, in,
                        nchunks, cp, frame, idx, mm);
   else if (nt == 1)
@@ -581,11 +580,9 @@ static int launch_chunk(const uint16_t* in, int64_t total, int chunk, int64_t c0
     const bool aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(frame)) & 15) == 0 &&
                          (reinterpret_cast<uintptr_t>(mm) & 7) == 0;
     if (chunk == NS * NS && c0 == 0 && fstride == (int64_t)(NS + 1) * NS && istride == NS && aligned &&
-        !getenv("HQ_CHUNK_GENERIC")) {
-      // launch form (A/B: HQ_CHUNK_WPB waves per workgroup, HQ_CHUNK_CPW chunks per wave)
-      const char* wev = getenv("HQ_CHUNK_WPB");
-      const char* cev = getenv("HQ_CHUNK_CPW");
-      const int wpb = wev ? atoi(wev) : 1, cpw = cev ? atoi(cev) : 2;
+        !opt_on(OPT_CHUNK_GENERIC)) {
+      // launch form (options chunk_wpb: waves per workgroup, chunk_cpw: chunks per wave)
+      const int wpb = (int)opt(OPT_CHUNK_WPB, 1), cpw = (int)opt(OPT_CHUNK_CPW, 2);
       int rc;
       if (wpb == 2) rc = launch_chunk_np<NS, 2>(in, c1, plan, frame, idx, mm, s);
       else if (wpb == 4) rc = launch_chunk_np<NS, 4>(in, c1, plan, frame, idx, mm, s);

@@ -7,6 +7,7 @@
 // exactly one coalesced write of the image and one read of the input rows.
 #include "hq_common.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 namespace hq {
@@ -27,6 +28,50 @@ int fail(int code, const char* fmt, ...) {
   va_end(ap);
   return code;
 }
+
+// kernel-variant options: name table (hq_set_option), values set explicitly; DIAG builds also read
+// HQ_<NAME> once at load
+static const char* const kOptNames[OPT_COUNT] = {
+    "fused_v", "fused_generic",
+    "chunk_nt", "chunk_exactdiv", "chunk_generic", "chunk_wpb", "chunk_cpw",
+    "precomp_nt", "precomp_tree_lds", "precomp_pad", "precomp_skip", "precomp_grid", "precomp_pf",
+    "precomp_diag",
+    "cos_kernel",
+    "sample_stride", "sample_waves", "sample_kth",
+    "scan_v1", "scan_nosample", "scan_expt", "scan_variant",
+    "refine_global", "refine_expt", "seg_prepare_flat", "select_2stage"};
+static int64_t g_opt_val[OPT_COUNT];
+static bool g_opt_set[OPT_COUNT];
+
+static int opt_find(const char* name) {
+  if (!name) return -1;
+  for (int i = 0; i < OPT_COUNT; ++i)
+    if (strcmp(kOptNames[i], name) == 0) return i;
+  return -1;
+}
+
+#ifdef HQ_DIAG
+// diagnostics builds: HQ_FUSED_V=... etc. from the environment, read once when the library loads
+__attribute__((constructor)) static void opt_from_env() {
+  for (int i = 0; i < OPT_COUNT; ++i) {
+    char env[64] = "HQ_";
+    for (int k = 0; kOptNames[i][k] && k < 56; ++k) {
+      const char c = kOptNames[i][k];
+      env[3 + k] = (c >= 'a' && c <= 'z') ? (char)(c - 32) : c;
+      env[4 + k] = 0;
+    }
+    const char* v = getenv(env);
+    if (!v) continue;
+    int64_t x = atoll(v);
+    if (i == OPT_COS_KERNEL) x = strcmp(v, "regstage") == 0 ? 1 : strcmp(v, "lockstep") == 0 ? 2
+                                 : strcmp(v, "temporal") == 0 ? 3 : x;
+    g_opt_val[i] = x;
+    g_opt_set[i] = true;
+  }
+}
+#endif
+
+int64_t opt(Opt id, int64_t dflt) { return g_opt_set[id] ? g_opt_val[id] : dflt; }
 
 int persistent_grid(const void* kernel, int block, size_t dyn_lds, int64_t work_items) {
   int dev = 0;
@@ -147,6 +192,36 @@ extern "C" {
 int hq_version(void) { return 1; }
 
 const char* hq_last_error(void) { return g_err; }
+
+int hq_set_option(const char* name, int64_t value) {
+  const int i = opt_find(name);
+  if (i < 0) return fail(HQ_E_INVALID, "unknown option '%s'", name ? name : "(null)");
+  g_opt_val[i] = value;
+  g_opt_set[i] = true;
+  return HQ_OK;
+}
+
+int hq_reset_option(const char* name) {
+  const int i = opt_find(name);
+  if (i < 0) return fail(HQ_E_INVALID, "unknown option '%s'", name ? name : "(null)");
+  g_opt_set[i] = false;
+  return HQ_OK;
+}
+
+int hq_get_option(const char* name, int64_t* value) {
+  const int i = opt_find(name);
+  if (i < 0) return fail(HQ_E_INVALID, "unknown option '%s'", name ? name : "(null)");
+  if (value) *value = g_opt_val[i];
+  return g_opt_set[i] ? 1 : 0;
+}
+
+int hq_diag_build(void) {
+#ifdef HQ_DIAG
+  return 1;
+#else
+  return 0;
+#endif
+}
 
 int hq_hilbert_table(int n, int32_t* xs, int32_t* ys, int32_t* tab, hq_stream_t stream) {
   if (!is_pow2(n)) return fail(HQ_E_NOT_POW2, "Grid size must be a power of 2, got %d", n);

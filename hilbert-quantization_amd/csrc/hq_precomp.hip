@@ -802,24 +802,19 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
     return fail(HQ_E_UNSUPPORTED, "layout n=%d max_levels=%d min_square_size=%d (power-of-two squares, <= 8 levels)",
                 n, max_levels, min_square_size);
   if (out_stride < p.total) return fail(HQ_E_INVALID, "out_stride %lld < %d averages", (long long)out_stride, p.total);
-  const char* nev = getenv("HQ_PRECOMP_NT");
-  if (nev) p.nt = atoi(nev) != 0;
-  const char* tev = getenv("HQ_PRECOMP_TREE");  // A/B: "lds" = combine leaves through LDS
-  if (tev && strcmp(tev, "lds") == 0) p.tree_lds = 1;
+  p.nt = opt(OPT_PRECOMP_NT, p.nt) != 0;
+  if (opt_on(OPT_PRECOMP_TREE_LDS)) p.tree_lds = 1;  // A/B: combine leaves through LDS
 #ifdef HQ_DIAG  // phase-skipping diagnostics (wrong averages): A/B builds only (make DIAG=1)
-  const char* dev = getenv("HQ_PRECOMP_DIAG");
-  if (dev) p.diag = atoi(dev);
+  p.diag = (int)opt(OPT_PRECOMP_DIAG, p.diag);
 #endif
   const int esz = dtype == HQ_F64 ? 8 : 4;
-  const char* pev = getenv("HQ_PRECOMP_PAD");
-  const int pad = pev ? atoi(pev) : 4;
-  if (pad < 0 || (pad & 3)) return fail(HQ_E_INVALID, "HQ_PRECOMP_PAD must be a multiple of 4");
+  const int pad = (int)opt(OPT_PRECOMP_PAD, 4);
+  if (pad < 0 || (pad & 3)) return fail(HQ_E_INVALID, "option precomp_pad must be a multiple of 4");
   const int ld = n + pad;
   const int use_lut = kind == 1 && n >= 16 && n <= 64;  // compile-time group LUT exists for this n
   // zero-padding skip (pre_zero_plan): 1-D streams with padding, leaves combined in registers;
-  // A/B: HQ_PRECOMP_SKIP=0 computes every square
-  const char* zev = getenv("HQ_PRECOMP_SKIP");
-  const bool skip = use_lut && !p.tree_lds && !(zev && atoi(zev) == 0) && pre_zero_plan(n, d, p);
+  // A/B: option precomp_skip = 0 computes every square
+  const bool skip = use_lut && !p.tree_lds && opt(OPT_PRECOMP_SKIP, 1) != 0 && pre_zero_plan(n, d, p);
   const size_t lds = (size_t)esz * ((size_t)ld * n + (p.tree_lds ? p.nleaves : 0)) + 4 * (size_t)p.total +
                      (skip ? 4 * (size_t)p.znz : 0);
   if (lds > 160 * 1024) return fail(HQ_E_UNSUPPORTED, "pre-computed index n=%d dtype %d needs %zu B of LDS", n, dtype, lds);
@@ -827,11 +822,9 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   // skip runs: a workgroup loops over many images (the list setup is amortised) and prefetches the
   // next image into registers (A/B, M emb/s at d = 1536: grid 262144 / 16384 / 8192 without prefetch
   // 110 / 169 / 157, with it 125 / 192 / 195; no skip 142)
-  const char* gev = getenv("HQ_PRECOMP_GRID");  // A/B: workgroups (each loops over images)
-  const int64_t gcap = gev ? atoll(gev) : (skip ? 8192 : 65536 * 4);
-  const int64_t grid64 = N < gcap ? N : gcap;
-  const char* fev = getenv("HQ_PRECOMP_PF");  // A/B: 1 = prefetch the next image into registers
-  const int pf = fev ? atoi(fev) : (skip ? 1 : 0);
+  const int64_t gcap = opt(OPT_PRECOMP_GRID, skip ? 8192 : 65536 * 4);  // A/B: workgroups (each loops over images)
+  const int64_t grid64 = N < gcap ? N : (gcap > 0 ? gcap : 1);
+  const int pf = (int)opt(OPT_PRECOMP_PF, skip ? 1 : 0);  // A/B: 1 = prefetch the next image into registers
   if (dtype == HQ_F32) {
     // groups of 4 values a thread scatters: a skip run touches only groups below d
     const bool kg2 = skip && (d + 3) / 4 <= 2 * kPreThreads;

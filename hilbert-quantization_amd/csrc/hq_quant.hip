@@ -393,7 +393,7 @@ int hq_map_index_quantize(const float* in, int64_t N, int64_t in_stride, int d, 
   if (N == 0) return HQ_OK;
   if (!frame || (d > 0 && !in)) return fail(HQ_E_INVALID, "null buffer");
   hipStream_t s = (hipStream_t)stream;
-  if (!getenv("HQ_FUSED_GENERIC")) {  // software-pipelined path for n in {16, 32, 64}, L <= 64
+  if (!opt_on(OPT_FUSED_GENERIC)) {  // software-pipelined path for n in {16, 32, 64}, L <= 64
     const int rc = fused_fast(in, N, in_stride, d, n, L, frame, idx, minmax, s);
     if (rc != HQ_E_UNSUPPORTED) return rc;
   }

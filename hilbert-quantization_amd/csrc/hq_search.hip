@@ -23,6 +23,23 @@ namespace hq {
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
+// Bounds guard of the DIAG build (make DIAG=1): HQ_GUARD(p, base, lim) checks that the element offset
+// p - base lies in [0, lim); a violation is counted (hq_diag_violations, with the source line of the
+// first one) and the pointer is clamped, so a faulty corpus-row index shows up as a count, never as a
+// GPU fault.  The default build compiles the guard away.
+#ifdef HQ_DIAG
+__device__ unsigned long long g_diag_count;
+__device__ int g_diag_line;
+__device__ __noinline__ int64_t diag_bound(int64_t off, int64_t lim, int line) {
+  if (off >= 0 && off < lim) return off;
+  if (atomicAdd(&g_diag_count, 1ull) == 0ull) atomicExch(&g_diag_line, line);
+  return off < 0 ? 0 : (lim > 0 ? lim - 1 : 0);
+}
+#define HQ_GUARD(p, base, lim) ((p) = (base) + diag_bound((int64_t)((p) - (base)), (int64_t)(lim), __LINE__))
+#else
+#define HQ_GUARD(p, base, lim) ((void)0)
+#endif
+
 // ------------------------------------------------------------------------------------------------
 // segment layout
 // ------------------------------------------------------------------------------------------------
@@ -791,6 +808,7 @@ template <> struct ZOps<false> {
   static __device__ __forceinline__ const T* zc(const Scan0Args& a, int64_t c) { return a.Zc + c * a.Lp; }
 };
 
+#ifdef HQ_DIAG
 // f64 sources only (hq_seg_prepare without float32 rows): the constant branch compares means in f64
 template <int KS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_scan0(Scan0Args a) {
@@ -1026,6 +1044,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     a.ws_id[o] = id >= 0 ? (int64_t)id + a.id_base : -1;
   }
 }
+#endif  // HQ_DIAG
 
 // ------------------------------------------------------------------------------------------------
 // sample pass for k_scan0: a strided subset of the corpus (row i*stride) is scored with the same
@@ -1051,6 +1070,7 @@ struct SampleArgs {
   float* top;          // k_sample_topf: Q x 4 nchunks x kTopT
 };
 
+#ifdef HQ_DIAG
 constexpr int kHRow = kBins / 2 + 1;  // LDS words per query histogram (odd: conflict-free rows)
 
 // Flush the top of a wave's per-query histograms (lane = query): bins from the top down until K
@@ -1163,6 +1183,7 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
   __syncthreads();
   flush_hist_top(hs, q0, a.Q, a.K, a.hist);
 }
+#endif  // HQ_DIAG
 
 // ------------------------------------------------------------------------------------------------
 // Split-f16 level-0 scan (default).  On gfx950 the f32/f64 MFMAs run on the vector ALUs (they never
@@ -1182,6 +1203,8 @@ constexpr float kMarginF = 6e-5f;
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 constexpr int kZ16Row = 64;  // halfs per split row: hi[32] then lo[32]
 constexpr int kPad0 = 3 * kCS;  // pad rows of the f32 copies (hq_seg_pack0_split); k_scan0f reads reach cs + 47
+// rows of the split statistics S32 (SoA groups of 4 rows, padded)
+__host__ __device__ __forceinline__ int64_t pack0_rows(int64_t N) { return ((N + 3) & ~int64_t(3)) + kPad0; }
 
 __device__ __forceinline__ float lower_f32(double x) {  // largest float <= x (x finite or +-inf)
   float f = (float)x;
@@ -1263,6 +1286,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const bool v = q < a.Q;
     const int qq = v ? q : 0;
     const _Float16* zr = a.Zq16 + (int64_t)qq * kZ16Row + 8 * g;
+    HQ_GUARD(zr, a.Zq16, (int64_t)a.Q * kZ16Row - 39);
     qh[b] = *reinterpret_cast<const half8*>(zr);
     ql[b] = *reinterpret_cast<const half8*>(zr + 32);
     const int64_t gq = (int64_t)(qq >> 2) * 16 + (qq & 3);  // SoA-per-4 statistics
@@ -1314,6 +1338,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   const _Float16* pz = a.Zc16 + (c_begin + j) * kZ16Row + 8 * g;
   const float* pst = a.Sc32 + (c_begin / 4 + g) * 16 + j;
   auto load_step = [&](CStep& c) {
+    HQ_GUARD(pz, a.Zc16, (a.N + kPad0) * kZ16Row - 39);  // half8 at pz and pz + 32
+    HQ_GUARD(pst, a.Sc32, pack0_rows(a.N) * 4);
     c.f[0] = *reinterpret_cast<const half8*>(pz);
     c.f[1] = *reinterpret_cast<const half8*>(pz + 32);
     c.st = *pst;
@@ -1481,6 +1507,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             const int q = q0 + 16 * b + j;
             const double* sq = a.Sq + (int64_t)q * a.nseg * 4;
             const double* sc = a.Sc + (cs + 4 * g + r) * a.nseg * 4;
+            HQ_GUARD(sq, a.Sq, (int64_t)a.Q * a.nseg * 4 - 3);
+            HQ_GUARD(sc, a.Sc, a.N * a.nseg * 4 - 3);
             const double qm = sq[0], qs = sq[1], qq = sq[2], cm = sc[0], csd = sc[1], cq = sc[2];
             const double v = (qs == 0.0 || csd == 0.0)
                                  ? const0(qs == 0.0, csd == 0.0, qm, cm, (aux_bits(sq) & aux_bits(sc) & kAuxF32) != 0)
@@ -1610,7 +1638,11 @@ __global__ __launch_bounds__(64) void k_pool_select(const float* __restrict__ po
                                                     double thr0) {
   const int lane = threadIdx.x;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+#ifdef HQ_DIAG
+    const int T = (int)diag_bound(pool_n[q], (int64_t)cap + 1, __LINE__);
+#else
     const int T = pool_n[q];
+#endif
     const float* ps = pool_s + (int64_t)q * cap;
     const int* pi = pool_i + (int64_t)q * cap;
     const bool inreg = T <= 64 * kPoolReg;
@@ -1749,6 +1781,7 @@ __global__ __launch_bounds__(64) void k_pool_select(const float* __restrict__ po
   }
 }
 
+#ifdef HQ_DIAG
 // f32 sample pass: f32 scores of a strided subset into per-query histograms; flagged pairs are not
 // counted (which only lowers the bound)
 __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
@@ -1787,6 +1820,7 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
   auto row_of = [&](int64_t i) -> int64_t { return (i < a.S ? i : a.S - 1) * a.stride; };
   auto load_frag = [&](int64_t cs, half8* dst) {
     const _Float16* p = a.Zc16 + row_of(cs + j) * kZ16Row + 8 * g;
+    HQ_GUARD(p, a.Zc16, a.N * kZ16Row - 39);
     dst[0] = *reinterpret_cast<const half8*>(p);
     dst[1] = *reinterpret_cast<const half8*>(p + 32);
   };
@@ -1857,6 +1891,7 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
   __syncthreads();
   flush_hist_top(hs, q0, a.Q, a.K, a.hist);
 }
+#endif  // HQ_DIAG
 
 // f32 sample pass, top-T form (default): no histogram.  Every lane (g, j) keeps, for each of its
 // four queries 16b + j, the kTopT best approximate scores of its own stream of sample rows (rows 4g ..
@@ -1917,7 +1952,9 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
   // per lane - and the 16 values of the lane group are broadcast by DPP row_newbcast
   auto load_stats = [&](int64_t cs) -> float {
     const int64_t row = row_of(cs + 4 * g + (j >> 2));
-    return a.Sc32[(row >> 2) * 16 + (j & 3) * 4 + (row & 3)];
+    const float* p = a.Sc32 + (row >> 2) * 16 + (j & 3) * 4 + (row & 3);
+    HQ_GUARD(p, a.Sc32, ((a.N + 3) & ~int64_t(3)) * 4);
+    return *p;
   };
   // fragments and statistics are loaded two steps ahead (3-buffer rotation, as in k_scan0f): at 2 waves
   // per SIMD one step of strided-row latency was exposed per step
@@ -2043,6 +2080,7 @@ __global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top
   }
 }
 
+#ifdef HQ_DIAG
 // per-query starting threshold from the sample histogram (-inf when the sample has < K scores)
 __global__ void k_hist_tau(const unsigned int* __restrict__ hist, int Q, int K, double margin,
                            double* __restrict__ th0) {
@@ -2059,6 +2097,7 @@ __global__ void k_hist_tau(const unsigned int* __restrict__ hist, int Q, int K, 
   }
   th0[q] = t;
 }
+#endif  // HQ_DIAG
 
 // merge nchunks sorted lists per query (one wave per query)
 __global__ __launch_bounds__(64) void k_merge(const double* __restrict__ ws_score, const int64_t* __restrict__ ws_id,
@@ -2812,11 +2851,11 @@ static void scan0_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& ch
 // setup cost, so more waves only add occupancy), chunks a multiple of 8 (XCD map) and of kCS rows
 static void sample_top_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, int& nqb, int& nchunks,
                                 int64_t& chunk_len) {
-  const int64_t sd = getenv("HQ_SAMPLE_STRIDE") ? atoi(getenv("HQ_SAMPLE_STRIDE")) : 16;  // A/B knob
+  const int64_t sd = opt(OPT_SAMPLE_STRIDE, 16) > 0 ? opt(OPT_SAMPLE_STRIDE, 16) : 16;  // A/B option
   stride = N >= sd * 4096 ? sd : (N / 4096 > 1 ? N / 4096 : 1);
   S = (N + stride - 1) / stride;
   nqb = (Q + kQW - 1) / kQW;
-  const int waves = getenv("HQ_SAMPLE_WAVES") ? atoi(getenv("HQ_SAMPLE_WAVES")) : 2048;
+  const int waves = opt(OPT_SAMPLE_WAVES, 2048) > 0 ? (int)opt(OPT_SAMPLE_WAVES, 2048) : 2048;
   int64_t target = (waves + nqb - 1) / nqb;
   const int64_t max_chunks = (S + kCS - 1) / kCS;
   if (target > max_chunks) target = max_chunks;
@@ -2844,16 +2883,17 @@ static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
          sample_top_bytes(Q, N) + 256;
 }
 
+#ifdef HQ_DIAG
 // sample pass: stride 16 once the corpus is large, else a sample of ~4096 rows (the whole corpus
 // below that); chunks of <= 65520 rows (u16 histogram counters), ~1024 waves (a wave has a fixed
 // cost: histogram init and flush)
 static void sample_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, int& nqb, int& nchunks,
                             int64_t& chunk_len) {
-  const int64_t sd = getenv("HQ_SAMPLE_STRIDE") ? atoi(getenv("HQ_SAMPLE_STRIDE")) : 16;  // A/B knob
+  const int64_t sd = opt(OPT_SAMPLE_STRIDE, 16) > 0 ? opt(OPT_SAMPLE_STRIDE, 16) : 16;  // A/B option
   stride = N >= sd * 4096 ? sd : (N / 4096 > 1 ? N / 4096 : 1);
   S = (N + stride - 1) / stride;
   nqb = (Q + kQW - 1) / kQW;
-  const int waves = getenv("HQ_SAMPLE_WAVES") ? atoi(getenv("HQ_SAMPLE_WAVES")) : 1024;
+  const int waves = opt(OPT_SAMPLE_WAVES, 1024) > 0 ? (int)opt(OPT_SAMPLE_WAVES, 1024) : 1024;
   int64_t target = (waves + nqb - 1) / nqb;
   const int64_t max_chunks = (S + kCS - 1) / kCS;
   if (target > max_chunks) target = max_chunks;
@@ -2862,7 +2902,17 @@ static void sample_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, int& 
   chunk_len = (S + nchunks - 1) / nchunks;
   chunk_len = ((chunk_len + kCS - 1) / kCS) * kCS;
 }
+#endif  // HQ_DIAG
 
+static int launch_scan0f(const Scan0Args& a, hipStream_t s) {
+  const size_t lds = (size_t)kQW * a.K * 8;
+  HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_scan0f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_scan0f, dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+#ifdef HQ_DIAG
 template <int KS, bool F32>
 static int launch_sample(const SampleArgs& a, hipStream_t s) {
   const size_t lds = (size_t)kQW * kHRow * 4;
@@ -2876,13 +2926,7 @@ static int launch_sample(const SampleArgs& a, hipStream_t s) {
 
 template <int KS, bool F32>
 static int launch_scan0(const Scan0Args& a, hipStream_t s) {
-  if constexpr (F32) {
-    const size_t lds = (size_t)kQW * a.K * 8;
-    HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_scan0f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_scan0f, dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
-    HQ_CHECK_LAUNCH();
-    return HQ_OK;
-  }
+  if constexpr (F32) return launch_scan0f(a, s);
   const size_t lds = (size_t)kQW * 32 + (size_t)kQW * a.K * 12;
   HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_scan0<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL((k_scan0<KS>), dim3(a.nqb * a.nchunks), dim3(64), lds, s, a);
@@ -2919,11 +2963,18 @@ static int scan0_dispatch(int ks, const Scan0Args& b, const SampleArgs* sa, hipS
   return rc;
 }
 
-// level-0 scan (sample pass -> thresholds -> k_scan0 -> k_merge); f32 selects the f32 contraction
+#endif  // HQ_DIAG
+
+// level-0 scan: top-T sample pass -> starting thresholds -> k_scan0f -> k_pool_select (split-f16
+// contraction, f32 == true).  DIAG builds keep the superseded forms for A/B: the f64 wave-level scan
+// k_scan0 (f32 == false, merged by k_merge) and the histogram sample pass (option sample_hist).
 static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const _Float16* Zq16, const float* Sq32,
                      int Q, const double* Zc, const double* Sc, const _Float16* Zc16, const float* Sc32, int64_t N,
                      const SegInfo& si, int k, double threshold, int thr_mode, int64_t id_base, void* workspace,
                      double* out_score, int64_t* out_id, hipStream_t s) {
+#ifndef HQ_DIAG
+  if (!f32) return fail(HQ_E_UNSUPPORTED, "the f64 level-0 scan exists only in DIAG builds");
+#endif
   Scan0Args b;
   b.Zq = Zq; b.Sq = Sq; b.Q = Q; b.Zc = Zc; b.Sc = Sc; b.N = N;
   b.Zq32 = nullptr; b.Zc32 = nullptr; b.Zq16 = Zq16; b.Zc16 = Zc16; b.Sq32 = Sq32; b.Sc32 = Sc32;
@@ -2933,18 +2984,22 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   b.K = k;
   b.thr0 = thr_mode == 0 ? -__builtin_huge_val() : threshold;
   b.id_base = id_base;
-  b.expt = getenv("HQ_SCAN_EXPT") ? atoi(getenv("HQ_SCAN_EXPT")) : 0;
+  b.expt = 0;
+  b.dbg = nullptr;
+#ifdef HQ_DIAG
+  b.expt = (int)opt(OPT_SCAN_EXPT, 0);
   static unsigned long long* dbg = nullptr;
   if (b.expt == 3) {
     if (!dbg) HQ_CHECK_HIP(hipMalloc(&dbg, 64));
     HQ_CHECK_HIP(hipMemsetAsync(dbg, 0, 64, s));
   }
   b.dbg = dbg;
+#endif
   scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len);
   uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
   b.ws_score = reinterpret_cast<double*>(ws);
   b.ws_id = reinterpret_cast<int64_t*>(ws + (size_t)b.nchunks * Q * k * 8);
-  // [lists / pools][gtau Q x 8][hist Q x kBins x 4][pool_n Q x 4][th0 Q x 8]: the three zeroed
+  // [lists / pools][gtau Q x 8][hist Q x kBins x 4][pool_n Q x 4][th0 Q x 8][sample tops]: the zeroed
   // regions are adjacent, so one memset clears them
   const size_t lists = (size_t)b.nchunks * Q * k * 16;
   b.gtau = reinterpret_cast<unsigned long long*>(ws + lists);
@@ -2956,16 +3011,19 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   b.pool_cap = b.nchunks * k;
   b.pool_s = reinterpret_cast<float*>(ws);
   b.pool_i = reinterpret_cast<int*>(ws + (size_t)Q * b.pool_cap * 4);
-  const bool sample = getenv("HQ_SCAN_NOSAMPLE") == nullptr;
-  const bool top_sample = sample && f32 && getenv("HQ_SAMPLE_HIST") == nullptr;  // default: top-T sample
+  // option scan_nosample: no sample pass, the scan starts from the caller's threshold
+  const bool sample = !opt_on(OPT_SCAN_NOSAMPLE);
+  bool top_sample = sample && f32;
+#ifdef HQ_DIAG
+  if (top_sample && opt(OPT_SCAN_VARIANT, 0) == 100) top_sample = false;  // the histogram sample pass
+#endif
   // K' of the starting threshold: the sample's K'-th best (statistical for K' < k: pools left short are
-  // marked for the exact path, k_pool_select); HQ_SAMPLE_KTH=0 -> k (a provable bound)
-  int sample_kth = getenv("HQ_SAMPLE_KTH") ? atoi(getenv("HQ_SAMPLE_KTH")) : kSampleKth;
+  // marked for the exact path, k_pool_select); option sample_kth = 0 -> k (a provable bound)
+  int sample_kth = (int)opt(OPT_SAMPLE_KTH, kSampleKth);
   if (sample_kth <= 0 || sample_kth > k) sample_kth = k;
   float* top = reinterpret_cast<float*>(ws + lists + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 4 +
                                         (size_t)Q * 8);
-  // (the histogram region lies between gtau and pool_n, so it is cleared with them; the top-T sample
-  // has no histogram and k_sample_kth clears gtau and pool_n per query)
+  // (the top-T sample has no histogram and k_sample_kth clears gtau and pool_n per query)
   if (!top_sample)
     HQ_CHECK_HIP(hipMemsetAsync(b.gtau, 0, (size_t)Q * 8 + (sample ? (size_t)Q * kBins * 4 : 0) + (f32 ? (size_t)Q * 4 : 0),
                                 s));
@@ -2988,7 +3046,9 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
                        (double)kMarginF, th0, b.gtau, b.pool_n);
     HQ_CHECK_LAUNCH();
     b.th0 = th0;
-  } else if (sample) {
+  }
+#ifdef HQ_DIAG
+  else if (sample) {
     SampleArgs sa;
     sa.top = nullptr;
     sa.Zq = Zq; sa.Sq = Sq; sa.Q = Q; sa.Zc = Zc; sa.Sc = Sc; sa.N = N;
@@ -2997,7 +3057,6 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     sample_geometry(Q, N, sa.stride, sa.S, sa.nqb, sa.nchunks, sa.chunk_len);
     sa.hist = hist;
     sa.K = k;
-
     rc = f32 ? scan0_dispatch<true>(ks, b, &sa, s) : scan0_dispatch<false>(ks, b, &sa, s);
     if (rc) return rc;
     hipLaunchKernelGGL(k_hist_tau, dim3((Q + 255) / 256), dim3(256), 0, s, (const unsigned int*)hist, Q, k,
@@ -3006,6 +3065,10 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     b.th0 = th0;
   }
   rc = f32 ? scan0_dispatch<true>(ks, b, nullptr, s) : scan0_dispatch<false>(ks, b, nullptr, s);
+#else
+  (void)hist;
+  rc = launch_scan0f(b, s);
+#endif
   if (rc) return rc;
   if (f32) {
     const int mg = Q < 8192 ? Q : 8192;
@@ -3014,6 +3077,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
                        top_sample && sample_kth < k ? (const double*)th0 : (const double*)nullptr, b.thr0);
     HQ_CHECK_LAUNCH();
   }
+#ifdef HQ_DIAG
   if (b.expt == 3) {
     unsigned long long h[7];
     HQ_CHECK_HIP(hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, s));
@@ -3029,6 +3093,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
                        (int64_t*)nullptr);
     HQ_CHECK_LAUNCH();
   }
+#endif
   return HQ_OK;
 }
 
@@ -3037,7 +3102,6 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
 // 2 msq outside [2^-60, 2^60], 4 pad row) in SoA groups of 4 rows: group G = rows 4G .. 4G + 3 holds
 // std[4], mean[4], msq[4], flags[4] (16 floats), for the rows [0, round_up(N, 4) + kPad0).  k_scan0f
 // reads up to 31 rows past a step start.
-__host__ __device__ __forceinline__ int64_t pack0_rows(int64_t N) { return ((N + 3) & ~int64_t(3)) + kPad0; }
 
 __global__ void k_pack0(const double* __restrict__ Z, const double* __restrict__ S, int64_t N, int Lp, int P0,
                         int nseg, _Float16* __restrict__ Z16, float* __restrict__ S32) {
@@ -3094,11 +3158,11 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
   const size_t lds = ((size_t)refine_qw(si) + (size_t)kp * refine_rw(si) + (size_t)kp * (1 + si.nseg)) * 8;
   const bool sm = seg_small(si);
 #ifdef HQ_DIAG
-  const int expt = getenv("HQ_REFINE_EXPT") ? atoi(getenv("HQ_REFINE_EXPT")) : 0;  // diagnostics build only
+  const int expt = (int)opt(OPT_REFINE_EXPT, 0);  // diagnostics build only
 #else
   const int expt = 0;
 #endif
-  if (lds <= 96 * 1024 && L % 2 == 0 && getenv("HQ_REFINE_GLOBAL") == nullptr) {  // 16-B pieces: L even
+  if (lds <= 96 * 1024 && L % 2 == 0 && !opt_on(OPT_REFINE_GLOBAL)) {  // 16-B pieces: L even
     const void* fn = sm ? (const void*)k_refine_lds<true> : (const void*)k_refine_lds<false>;
     HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (sm)
@@ -3131,6 +3195,33 @@ using namespace hq;
 
 extern "C" {
 
+int hq_diag_violations(int64_t* count, int* first_line) {
+  unsigned long long c = 0;
+  int line = 0;
+#ifdef HQ_DIAG
+  HQ_CHECK_HIP(hipDeviceSynchronize());
+  HQ_CHECK_HIP(hipMemcpyFromSymbol(&c, HIP_SYMBOL(g_diag_count), sizeof(c)));
+  HQ_CHECK_HIP(hipMemcpyFromSymbol(&line, HIP_SYMBOL(g_diag_line), sizeof(line)));
+#endif
+  if (count) *count = (int64_t)c;
+  if (first_line) *first_line = line;
+  return HQ_OK;
+}
+
+int hq_scan0_geometry(int Q, int64_t N, int* nqb, int* nchunks, int64_t* chunk_len, int64_t* z_rows,
+                      int64_t* s_rows) {
+  if (Q <= 0 || N <= 0) return fail(HQ_E_INVALID, "bad shape Q=%d N=%lld", Q, (long long)N);
+  int a = 0, b = 0;
+  int64_t c = 0;
+  scan0_geometry(Q, N, a, b, c);
+  if (nqb) *nqb = a;
+  if (nchunks) *nchunks = b;
+  if (chunk_len) *chunk_len = c;
+  if (z_rows) *z_rows = N + kPad0;
+  if (s_rows) *s_rows = pack0_rows(N);
+  return HQ_OK;
+}
+
 int hq_seg_count(int L) {
   SegInfo si;
   seg_info(L, si);
@@ -3161,7 +3252,7 @@ int hq_seg_prepare_rows(const double* idx, int64_t N, int L, int src_f32, const 
   seg_info(L, si);
   if (si.nseg == 0) return fail(HQ_E_INVALID, "no level structure for L=%d", L);
   const int64_t total = N * si.nseg;
-  if (N <= 16384 && si.L <= 4096 && !getenv("HQ_SEG_PREPARE_FLAT")) {  // A/B knob: the flat kernel
+  if (N <= 16384 && si.L <= 4096 && !opt_on(OPT_SEG_PREPARE_FLAT)) {  // A/B option: the flat kernel
     hipLaunchKernelGGL(k_seg_prepare_lds, dim3((unsigned)N), dim3(64), (size_t)8 * si.L, (hipStream_t)stream, idx, N,
                        si, src_f32 ? 1 : 0, row_f32, Z, stats);
   } else {
@@ -3250,7 +3341,9 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
   }
   if (!Zq || !Sq || !Zc || !Sc || !workspace) return fail(HQ_E_INVALID, "null buffer");
   if (workspace_bytes < hq_scan_workspace_size(Q, N, k)) return fail(HQ_E_INVALID, "workspace too small");
-  if (mode == 0 && !out_best && !out_best_id && N < 0x7FFFFFFF && getenv("HQ_SCAN_V1") == nullptr) {
+#ifdef HQ_DIAG
+  // diagnostics builds: the f64 wave-level level-0 scan (option scan_variant = 64)
+  if (mode == 0 && !out_best && !out_best_id && N < 0x7FFFFFFF && opt(OPT_SCAN_VARIANT, 0) == 64) {
     SegInfo si;
     seg_info(L, si);
     const int ks = si.plen[0] / 4;
@@ -3258,6 +3351,7 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
       return scan0_run(false, ks, Zq, Sq, nullptr, nullptr, Q, Zc, Sc, nullptr, nullptr, N, si, k, threshold,
                        thr_mode, id_base, workspace, out_score, out_id, s);
   }
+#endif
   ScanArgs a;
   a.Zq = Zq; a.Sq = Sq; a.Q = Q; a.Zc = Zc; a.Sc = Sc; a.N = N;
   seg_info(L, a.si);
@@ -3400,7 +3494,7 @@ static void select_parts(int Q, int64_t N, int& P, int64_t& plen) {
 
 // the register-resident multi-stage select runs when the two-stage form would have few waves
 static bool select_reg_ok(int Q, int64_t N, int k) {
-  return N > 0 && k >= 16 && k <= 64 && (int64_t)Q * ((N + 8191) / 8192) < 4096 && !getenv("HQ_SELECT_2STAGE");
+  return N > 0 && k >= 16 && k <= 64 && (int64_t)Q * ((N + 8191) / 8192) < 4096 && !opt_on(OPT_SELECT_2STAGE);
 }
 static int64_t select_reg_parts(int64_t N) { return (N + kRegSel - 1) / kRegSel; }
 

@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("HQ_LIB_VARIANT") or os.path.join(_HERE, "libhq_mi355x.so")  # variant: A/B builds
+# HQ_LIB_VARIANT: path of another build of the library (the `make DIAG=1` diagnostics build for A/B tools)
+LIB_PATH = os.environ.get("HQ_LIB_VARIANT") or os.path.join(_HERE, "libhq_mi355x.so")
 
 HQ_OK = 0
 HQ_E_INVALID = -1
@@ -34,6 +35,13 @@ _sz = _c.c_size_t
 SIGNATURES = {
     "hq_version": (_i, []),
     "hq_last_error": (_c.c_char_p, []),
+    "hq_set_option": (_i, [_c.c_char_p, _i64]),
+    "hq_reset_option": (_i, [_c.c_char_p]),
+    "hq_get_option": (_i, [_c.c_char_p, _c.POINTER(_i64)]),
+    "hq_diag_build": (_i, []),
+    "hq_diag_violations": (_i, [_c.POINTER(_i64), _c.POINTER(_i)]),
+    "hq_scan0_geometry": (_i, [_i, _i64, _c.POINTER(_i), _c.POINTER(_i), _c.POINTER(_i64), _c.POINTER(_i64),
+                               _c.POINTER(_i64)]),
     "hq_hilbert_table": (_i, [_i, _p, _p, _p, _p]),
     "hq_map_to_2d": (_i, [_i, _p, _i64, _i64, _i, _i, _p, _p]),
     "hq_map_from_2d": (_i, [_i, _p, _i64, _i, _i, _p, _p]),
@@ -148,3 +156,40 @@ def stream_ptr(device=None) -> int:
         if raw is not None:
             return raw(torch._C._cuda_getDevice())
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def set_option(name: str, value: int) -> None:
+    """Select a kernel variant (hq_set_option; parity tests / A/B only, process-wide)."""
+    check(load().hq_set_option(name.encode(), int(value)))
+
+
+def reset_option(name: str) -> None:
+    check(load().hq_reset_option(name.encode()))
+
+
+def get_option(name: str):
+    """The option's value, or None when it is at its default."""
+    v = _c.c_int64(0)
+    rc = load().hq_get_option(name.encode(), _c.byref(v))
+    if rc < 0:
+        check(rc)
+    return int(v.value) if rc == 1 else None
+
+
+class option:
+    """Context manager: `with option("fused_generic", 1): ...` runs the block with that kernel variant."""
+
+    def __init__(self, name: str, value: int):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        self.prev = get_option(self.name)
+        set_option(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev is None:
+            reset_option(self.name)
+        else:
+            set_option(self.name, self.prev)
+        return False

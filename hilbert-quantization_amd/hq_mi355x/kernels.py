@@ -8,7 +8,6 @@ SURVEY.md §7); the reference-shaped classes in `hq_mi355x.core` / `hq_mi355x.ra
 from __future__ import annotations
 
 import functools
-import os
 
 import ctypes
 from typing import Optional, Tuple
@@ -340,9 +339,9 @@ def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.
     ids = t.empty((Q, k), dtype=t.int64, device=dev)
     best = t.empty(Q, dtype=t.float64, device=dev) if need_best else None
     bid = t.empty(Q, dtype=t.int64, device=dev) if need_best else None
-    # HQ_SCAN_F64 (A/B knob): the f64 wave-level kernel, f64 sources only
+    # option scan_v1 (parity tests): the LDS-tiled k_scan instead of the split-f16 level-0 scan
     if (mode == 0 and not need_best and q.Z16 is not None and c.Z16 is not None
-            and (not os.environ.get("HQ_SCAN_F64") or q.f32 or c.f32)):
+            and (q.f32 or c.f32 or _lib.get_option("scan_v1") is None)):
         _chk(_L().hq_scan0_topk_split(ptr(q.Z16), ptr(q.S32), ptr(q.S), Q, ptr(c.Z16), ptr(c.S32), ptr(c.S), N, c.L,
                                       k, float(threshold), thr_mode, int(id_base), ptr(ws), ws_bytes, ptr(sc),
                                       ptr(ids), stream()), exc)
@@ -594,6 +593,6 @@ def cosine_scores(a, b, exc=None):
     b2 = b.reshape(b.shape[0], -1)
     Q, N = int(a2.shape[0]), int(b2.shape[0])
     K = min(int(a2.shape[1]), int(b2.shape[1]))  # the reference truncates to the common length
-    if Q * N * max(K, 1) >= MFMA_COS_MIN_WORK and K > 0 and not os.environ.get("HQ_COS_F64"):
+    if Q * N * max(K, 1) >= MFMA_COS_MIN_WORK and K > 0:
         return cosine_scores_mfma(cos_prepare(a2[:, :K], exc), cos_prepare(b2[:, :K], exc), exc)
     return cosine_scores_f64(a, b, exc)

@@ -48,6 +48,31 @@ typedef void* hq_stream_t; /* hipStream_t */
 int hq_version(void);
 const char* hq_last_error(void);
 
+/* ---- kernel-variant options (parity tests and A/B only) ------------------------------------------
+ * Every entry point runs its tuned kernel by default and a default build never reads the environment.
+ * hq_set_option selects an alternative form of a kernel (same results, checked by the parity tests):
+ * e.g. "fused_v" (fused-kernel variant bits), "fused_generic", "chunk_generic", "chunk_exactdiv",
+ * "chunk_wpb", "chunk_cpw", "precomp_grid", "precomp_tree_lds", "cos_kernel" (1 register-staged,
+ * 2 lockstep), "refine_global", "select_2stage", "sample_kth" (0 = provable bound), "scan_v1" (the
+ * LDS-tiled level-0 scan), "scan_variant".  Options are process-wide: set them before launching, not
+ * while other host threads launch.  hq_reset_option restores the default; hq_get_option returns 1 when
+ * the option is set (value in *value), 0 when it is at its default, HQ_E_INVALID for an unknown name.
+ * hq_diag_build() = 1 for a `make DIAG=1` library (diagnostics kernels; HQ_<NAME> environment variables
+ * are read once at load).                                                                         */
+int hq_set_option(const char* name, int64_t value);
+int hq_reset_option(const char* name);
+int hq_get_option(const char* name, int64_t* value);
+int hq_diag_build(void);
+/* DIAG builds: bounds violations counted by the guarded corpus-row loads of the level-0 scan (k_scan0f,
+ * k_sample_topf, k_pool_select; the load is clamped instead of faulting) since the library loaded, and
+ * the source line of the first.  Synchronises the device.  Default builds report 0.                  */
+int hq_diag_violations(int64_t* count, int* first_line);
+/* Launch geometry of the level-0 scan k_scan0f (host only): query blocks of 64, corpus chunks (a multiple
+ * of 8: XCD map) of chunk_len rows (a multiple of 16), and the row counts of the split copies it reads
+ * (Z16: z_rows = N + 48, S32: s_rows = round_up(N, 4) + 48).  Exported for the bounds test.          */
+int hq_scan0_geometry(int Q, int64_t N, int* nqb, int* nchunks, int64_t* chunk_len, int64_t* z_rows,
+                      int64_t* s_rows);
+
 /* ---- M1/M2/M4: coordinate tables ------------------------------------------------------------
  * replaces core/hilbert_mapper.py:17-40 generate_hilbert_coordinates (+ :42-113 d2xy/xy2d/rotate)
  * and rag/embedding_generation/hilbert_mapper.py:122-204.

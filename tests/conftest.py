@@ -43,3 +43,22 @@ def hq_lib():
         pytest.skip("no GPU in this container")
     from hq_mi355x import _lib
     return _lib.lib()
+
+
+@pytest.fixture
+def hq_option():
+    """set(name, value) selects a kernel variant (hq_set_option) for this test; every option it touched
+    is restored to its default afterwards."""
+    from hq_mi355x import _lib
+    touched = []
+
+    def set_(name, value=None):
+        touched.append(name)
+        if value is None:
+            _lib.reset_option(name)
+        else:
+            _lib.set_option(name, int(value))
+
+    yield set_
+    for name in touched:
+        _lib.reset_option(name)

@@ -202,11 +202,11 @@ def test_fused_kernel_vs_oracle(hq_lib, n, d, L):
 
 @pytest.mark.parametrize("variant", [4, 0, 64, 192, 320, 448, 322, 576, 704, 832, 706, 1728, 3776])
 @pytest.mark.parametrize("n,d,L", [(64, 1536, 64), (32, 999, 20), (16, 200, 16)])
-def test_fused_launch_forms_vs_oracle(hq_lib, n, d, L, variant, monkeypatch):
+def test_fused_launch_forms_vs_oracle(hq_lib, n, d, L, variant, hq_option):
     """Every launch form of the fast kernel (persistent triple/double buffered, non-persistent with 1-8
     waves per workgroup and a ragged last workgroup, reciprocal quantize) is bit-exact."""
     from hq_mi355x import kernels as K
-    monkeypatch.setenv("HQ_FUSED_V", str(variant))
+    hq_option("fused_v", variant)
     rng = np.random.default_rng(variant + d)
     P = (rng.standard_normal((45, d)) * 3).astype(np.float32)
     P[7] = 0.0
@@ -219,10 +219,10 @@ def test_fused_launch_forms_vs_oracle(hq_lib, n, d, L, variant, monkeypatch):
 
 
 @pytest.mark.parametrize("n,d,L", [(32, 1000, 32), (64, 1536, 64), (64, 4096, 30), (16, 256, 16)])
-def test_fused_generic_path_vs_oracle(hq_lib, n, d, L, monkeypatch):
+def test_fused_generic_path_vs_oracle(hq_lib, n, d, L, hq_option):
     """The non-pipelined kernel (n outside {16,32,64}, L > 64, unaligned rows) stays bit-exact too."""
     from hq_mi355x import kernels as K
-    monkeypatch.setenv("HQ_FUSED_GENERIC", "1")
+    hq_option("fused_generic", 1)
     rng = np.random.default_rng(d + L)
     P = rng.standard_normal((19, d)).astype(np.float32)
     fr, idx, mm = K.map_index_quantize(_t(P), n, L)
@@ -286,19 +286,19 @@ def test_chunk_encoder_vs_oracle(hq_lib):
 
 @pytest.mark.parametrize("chunk,nfull,tail", [(1024, 41, 512), (4096, 9, 2500), (1024, 8, 0)])
 @pytest.mark.parametrize("mode", ["fast", "exactdiv", "generic", "cpw1", "cpw4", "wpb2"])
-def test_chunk_encoder_shapes_vs_oracle(hq_lib, chunk, nfull, tail, mode, monkeypatch):
+def test_chunk_encoder_shapes_vs_oracle(hq_lib, chunk, nfull, tail, mode, hq_option):
     """Fast (one chunk per wave) and generic chunk kernels: odd chunk counts (a dead wave in the last
     workgroup), 64 x 64 chunks, the cfg5 512-value tail, constant chunks, caller-provided buffers."""
     from hq_mi355x import kernels as K
     import torch
     if mode == "generic":
-        monkeypatch.setenv("HQ_CHUNK_GENERIC", "1")
+        hq_option("chunk_generic", 1)
     if mode == "exactdiv":
-        monkeypatch.setenv("HQ_CHUNK_EXACTDIV", "1")
+        hq_option("chunk_exactdiv", 1)
     if mode in ("cpw1", "cpw4"):
-        monkeypatch.setenv("HQ_CHUNK_CPW", mode[-1])
+        hq_option("chunk_cpw", int(mode[-1]))
     if mode == "wpb2":
-        monkeypatch.setenv("HQ_CHUNK_WPB", "2")
+        hq_option("chunk_wpb", 2)
     rng = np.random.default_rng(chunk + nfull)
     total = chunk * nfull + tail
     x = (rng.standard_normal(total) * 0.02).astype(np.float16)

@@ -163,14 +163,14 @@ def test_quantizer_builds_precomputed_index(hq_lib):
 @pytest.mark.parametrize("n,dtype,levels", [(16, np.float32, (6, 2)), (32, np.float32, (6, 2)),
                                              (64, np.float32, (6, 2)), (64, np.float64, (6, 2)),
                                              (32, np.float32, (2, 1)), (64, np.float32, (3, 4))])
-def test_precomputed_stream_zero_padding_skip(hq_lib, monkeypatch, grid, n, dtype, levels):
+def test_precomputed_stream_zero_padding_skip(hq_lib, hq_option, grid, n, dtype, levels):
     """1-D streams shorter than n*n: squares wholly in the zero padding are skipped (pre_zero_plan) and
     their averages stay +0.0.  d sweeps group edges (d % 4 != 0), block edges and the full image; with
     HQ_PRECOMP_GRID=3 each workgroup loops over several images, so the padding cells and the skipped
     averages are reused from the once-per-workgroup setup."""
     from hq_mi355x import kernels as K
     if grid is not None:
-        monkeypatch.setenv("HQ_PRECOMP_GRID", grid)
+        hq_option("precomp_grid", int(grid))
     rng = np.random.default_rng(n * 7 + len(levels))
     ml, ms = levels
     for d in sorted({1, 3, 4, 5, 63, 64, 65, n * n // 4 + 1, 3 * n * n // 8, n * n - 1, n * n}):

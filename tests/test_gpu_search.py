@@ -246,10 +246,10 @@ def test_rag_scores(hq_lib, golden):
     assert abs(S.calculate_spatial_locality_similarity(a, b) - O.rag_spatial_locality_similarity(a, b)) < 1e-6
 
 
-def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, monkeypatch):
-    """The wave-independent level-0 scan (k_scan0: sampled thresholds, global threshold exchange,
-    division-free filter, exact constant branches; f32 and f64 contractions) gives the same exact
-    top-k as the LDS-tiled k_scan (HQ_SCAN_V1) and as the oracle, on a corpus with a ragged chunk tail, zero-variance level-0 segments on both sides,
+def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, hq_option):
+    """The wave-independent level-0 scan (k_scan0f: sampled thresholds, global threshold exchange,
+    division-free filter, exact constant branches; with and without the sample pass) gives the same exact
+    top-k as the LDS-tiled k_scan (option scan_v1) and as the oracle, on a corpus with a ragged chunk tail, zero-variance level-0 segments on both sides,
     duplicate runs across chunks and a query count that is not a multiple of 64."""
     from hq_mi355x.core.search_engine import IndexCorpus
     rng = np.random.default_rng(77)
@@ -264,18 +264,17 @@ def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, monkeypatch):
     corpus = IndexCorpus(C)
     qp = corpus.prepare_queries(Q)
     res = {}
-    for tag in ("v0", "v0-f64", "v0-nosample", "v1"):
-        if tag == "v0-f64":
-            monkeypatch.setenv("HQ_SCAN_F64", "1")
+    for tag in ("v0", "v0-nosample", "v1"):
         if tag == "v0-nosample":
-            monkeypatch.setenv("HQ_SCAN_NOSAMPLE", "1")
+            hq_option("scan_nosample", 1)
         if tag == "v1":
-            monkeypatch.setenv("HQ_SCAN_V1", "1")
+            hq_option("scan_nosample", None)
+            hq_option("scan_v1", 1)
         for thr, tm in ((0.1, 1), (0.6, 1), (0.1, 2)):
             sc, ids, cnt, _, _ = corpus.exact_topk(qp, 0, 20, thr, tm)
             res[(tag, thr, tm)] = (_np(sc), _np(ids), _np(cnt))
     for key in ((0.1, 1), (0.6, 1), (0.1, 2)):
-        for tag in ("v0-f64", "v0-nosample", "v1"):
+        for tag in ("v0-nosample", "v1"):
             a, b = res[("v0",) + key], res[(tag,) + key]
             assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]), (tag, key)
             np.testing.assert_array_equal(a[0][a[1] >= 0], b[0][b[1] >= 0])
@@ -323,7 +322,7 @@ def test_cosine_mfma_vs_reference_golden(hq_lib, golden):
 
 
 @pytest.mark.parametrize("Q,N,K", [(130, 300, 1024), (257, 700, 4096), (1, 257, 32), (5, 40, 64)])
-def test_cosine_dma_kernels_match_regstage(hq_lib, Q, N, K, monkeypatch):
+def test_cosine_dma_kernels_match_regstage(hq_lib, Q, N, K, hq_option):
     """The default LDS-DMA ping-pong kernel (k_cos_g3<256, 1>: 256-frame tiles, swizzled LDS, staggered
     wave groups), its lockstep form and the register-staged baseline (k_cos_mfma, 128-frame tiles) run
     the same MFMA sequence per output, so their scores are bit-identical; ragged last frame tile (N not
@@ -335,13 +334,13 @@ def test_cosine_dma_kernels_match_regstage(hq_lib, Q, N, K, monkeypatch):
     B = rng.standard_normal((N, K)).astype(np.float32)
     pa, pb = K_.cos_prepare(torch.from_numpy(A).cuda()), K_.cos_prepare(torch.from_numpy(B).cuda())
     got = _np(K_.cosine_scores_mfma(pa, pb))
-    for kern in ("lockstep", "regstage"):
-        monkeypatch.setenv("HQ_COS_KERNEL", kern)
+    for kern, code in (("lockstep", 2), ("regstage", 1)):
+        hq_option("cos_kernel", code)
         np.testing.assert_array_equal(got, _np(K_.cosine_scores_mfma(pa, pb)), err_msg=kern)
 
 
 @pytest.mark.parametrize("L", [64, 32, 256])
-def test_refine_rescore_equals_refine_then_rescore(hq_lib, monkeypatch, L):
+def test_refine_rescore_equals_refine_then_rescore(hq_lib, hq_option, L):
     """hq_refine_rescore_topk (rows staged once in LDS, the re-score of the output from the same rows)
     returns exactly refine_topk's ranking plus hq_rescore's records for the output ids (zeros in empty
     slots), for the level-0 and the overall mode, on the LDS-staged and the global-memory kernels
@@ -361,10 +360,7 @@ def test_refine_rescore_equals_refine_then_rescore(hq_lib, monkeypatch, L):
             continue  # L = 256: the overall scan does not fuse (Lp > 256)
         asc, aid, _, _ = K.scan_topk(qp, corpus.prep, mode, 28, thr - corpus.EPS, 0 if tm == 0 else 1)
         for glob in (False, True):
-            if glob:
-                monkeypatch.setenv("HQ_REFINE_GLOBAL", "1")
-            else:
-                monkeypatch.delenv("HQ_REFINE_GLOBAL", raising=False)
+            hq_option("refine_global", 1 if glob else None)
             s1, i1, c1, r1 = K.refine_topk(qp, corpus.prep, mode, asc, aid, 20, thr, tm, corpus.EPS)
             s2, i2, c2, r2, det = K.refine_rescore_topk(qp, corpus.prep, mode, asc, aid, 20, thr, tm, corpus.EPS)
             for x, y in ((s1, s2), (i1, i2), (c1, c2), (r1, r2)):
@@ -408,11 +404,11 @@ def test_two_stage_select_equals_one_stage(hq_lib, Q, N, k, thr, tm):
         assert list(got[got >= 0]) == list(ref)
 
 
-def test_statistical_start_threshold_is_exact(hq_lib, monkeypatch):
+def test_statistical_start_threshold_is_exact(hq_lib, hq_option):
     """A starting threshold from the sample's K'-th best (K' < K; the default is 12 on sparse samples) is not
     a provable bound: lists left short are marked (+inf in the empty slots) and their queries answered by
     the dense exact path.  With K' = 1 most lists are short; the progressive results must equal the
-    provable mode's (HQ_SAMPLE_KTH=0) and the oracle's."""
+    provable mode's (option sample_kth = 0) and the oracle's."""
     from hq_mi355x import kernels as K
     from hq_mi355x.core.search_engine import IndexCorpus
     rng = np.random.default_rng(31)
@@ -423,7 +419,7 @@ def test_statistical_start_threshold_is_exact(hq_lib, monkeypatch):
     corpus = IndexCorpus(C)
     out = {}
     for kth in ("0", "16", "1"):
-        monkeypatch.setenv("HQ_SAMPLE_KTH", kth)
+        hq_option("sample_kth", int(kth))
         ids, ov, lv, cnt = corpus.progressive(Q, 10, 0.1, 20)
         out[kth] = (_np(ids), _np(ov), _np(lv), _np(cnt))
         if kth == "1":
@@ -454,7 +450,7 @@ def _np_select(row, k, thr, thr_mode):
 
 
 @pytest.mark.parametrize("N", [1, 100, 1025, 9000, 70000])
-def test_select_topk_register_stages(hq_lib, monkeypatch, N):
+def test_select_topk_register_stages(hq_lib, hq_option, N):
     """The register-resident multi-stage select (few queries: the dense redo) equals the reference order
     and the two-stage select, with ties (quantised scores), thresholds and id_base."""
     import torch
@@ -464,9 +460,9 @@ def test_select_topk_register_stages(hq_lib, monkeypatch, N):
     for k in (16, 20, 28, 64):
         for thr, mode in ((0.0, 0), (0.5, 1), (0.5, 2), (0.995, 1)):
             got = [_np(x) for x in K.select_topk(torch.tensor(sc, device="cuda"), k, thr, mode, 7)]
-            monkeypatch.setenv("HQ_SELECT_2STAGE", "1")
+            hq_option("select_2stage", 1)
             two = [_np(x) for x in K.select_topk(torch.tensor(sc, device="cuda"), k, thr, mode, 7)]
-            monkeypatch.delenv("HQ_SELECT_2STAGE")
+            hq_option("select_2stage", None)
             for x, y in zip(got, two):
                 assert np.array_equal(x, y), (N, k, thr, mode)
             for q in range(3):

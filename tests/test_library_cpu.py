@@ -146,3 +146,52 @@ def test_search_host_keeps_f32_index_vectors():
     assert se._idx([1, 2]).dtype == np.float64
     assert se._idx(np.zeros(3, np.float16)).dtype == np.float64
     assert np.stack([se._idx(a32), se._idx(a32)]).dtype == np.float32
+
+
+def test_kernel_options_are_explicit(lib):
+    """Kernel variants are selected only by hq_set_option: the default library imports no getenv (a stray
+    environment variable cannot change a kernel path), options set / read back / reset, unknown names fail."""
+    import subprocess
+    from hq_mi355x import _lib
+    syms = subprocess.run(["nm", "-D", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    if lib.hq_diag_build() == 0:
+        assert "getenv" not in syms
+    assert _lib.get_option("fused_v") is None
+    with _lib.option("fused_v", 5):
+        assert _lib.get_option("fused_v") == 5
+    assert _lib.get_option("fused_v") is None
+    with pytest.raises(_lib.NativeLibraryError, match="unknown option 'no_such_knob'"):
+        _lib.set_option("no_such_knob", 1)
+    assert lib.hq_get_option(b"no_such_knob", None) == _lib.HQ_E_INVALID
+
+
+def _scan0f_reads(chunk_len: int, n_rows: int) -> int:
+    """Rows past its first that one k_scan0f wave reads for a chunk of n_rows rows (hq_search.hip k_scan0f:
+    two steps of 16 rows are loaded before the loop, each body loads one more step; the loop runs three
+    bodies while cs + 32 < c_end, then up to two tail bodies)."""
+    loads, cs = 2, 0
+    while cs + 32 < n_rows:
+        loads += 3
+        cs += 48
+    loads += (cs < n_rows) + (cs + 16 < n_rows)
+    return 16 * loads
+
+
+def test_scan0f_reads_stay_inside_padded_copies(lib):
+    """Deterministic guard for the round-2 fault class (prologue rows past the kPad0 padding): for every
+    corpus size N = 1..70,000 and query counts 1..1000, the largest Z16 / S32 row any k_scan0f wave reads
+    (chunks starting at or past N exit before loading) lies inside the padded copies."""
+    g = [ctypes.c_int(), ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()]
+    refs = [ctypes.byref(x) for x in g]
+    worst = 0
+    for Q in (1, 5, 63, 64, 65, 127, 500, 999, 1000):
+        for N in range(1, 70_001):
+            assert lib.hq_scan0_geometry(Q, N, *refs) == 0
+            nchunks, cl, z_rows, s_rows = g[1].value, g[2].value, g[3].value, g[4].value
+            assert cl % 16 == 0 and nchunks % 8 == 0 and nchunks * cl >= N
+            last = (N - 1) // cl                       # last chunk that starts below N
+            m = max(last * cl + _scan0f_reads(cl, N - last * cl) - 1,
+                    (last - 1) * cl + _scan0f_reads(cl, cl) - 1 if last > 0 else -1)
+            assert m < z_rows and m < s_rows, (Q, N, m, z_rows)
+            worst = max(worst, m - N)
+    assert worst == 46  # reads reach row N + 46 (DESIGN.md §4.2): inside the 48 padding rows, 1 row to spare
