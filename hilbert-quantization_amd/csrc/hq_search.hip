@@ -316,15 +316,20 @@ __device__ double exact_level(const double* q, const double* zq, const double* s
 }
 
 // exact_pair on explicit row pointers (raw [L], Z [Lp], S [nseg x 4] of each side; global or LDS)
+// typed (level >= 0, nullable): 1 when the level score is a numpy float32 (the reference's threshold test
+// then compares in float32, NEP 50: see typed_pass)
 template <bool SM = false>
 __device__ double exact_pair_rows(const double* ra, const double* za, const double* sa, const double* rb,
-                                  const double* zb, const double* sb, const SegInfo& si, int level, double* lv) {
+                                  const double* zb, const double* sb, const SegInfo& si, int level, double* lv,
+                                  int* typed = nullptr) {
   int t32;
   if (level >= 0) {
     if (level >= si.nseg) return 0.0;
     const int s = level;
-    return exact_level<SM>(ra + si.src[s], za + si.poff[s], sa + 4 * s, rb + si.src[s], zb + si.poff[s], sb + 4 * s,
-                       si.len[s], &t32);
+    const double v = exact_level<SM>(ra + si.src[s], za + si.poff[s], sa + 4 * s, rb + si.src[s], zb + si.poff[s],
+                                     sb + 4 * s, si.len[s], &t32);
+    if (typed) *typed = t32;
+    return v;
   }
   // search_engine.py:191-230: running weighted sum in level order, divide, clamp.  Python typing:
   // the sum starts as the Python float 0.0; a float32 level score makes the term float32 (the weight
@@ -358,9 +363,25 @@ __device__ double exact_pair_rows(const double* ra, const double* za, const doub
 
 template <bool SM = false>
 __device__ double exact_pair(const VecSet& A, int64_t ia, const VecSet& B, int64_t ib, const SegInfo& si, int level,
-                             double* lv) {
+                             double* lv, int* typed = nullptr) {
   return exact_pair_rows<SM>(A.raw + ia * si.L, A.Z + ia * si.Lp, A.S + ia * si.nseg * 4, B.raw + ib * si.L,
-                         B.Z + ib * si.Lp, B.S + ib * si.nseg * 4, si, level, lv);
+                         B.Z + ib * si.Lp, B.S + ib * si.nseg * 4, si, level, lv, typed);
+}
+
+// The reference's threshold test of a level score (search_engine.py:284-292 `>=`, video_search.py:244 `>`)
+// with Python typing: a numpy float32 score is compared with the Python-float threshold in float32
+// (NEP 50: the threshold is rounded to float32), a Python-float score in float64.  Callers pass the
+// threshold as given (f32_threshold, hq_mi355x core/search_engine.py, folds the rounding into one value
+// only for all-float32 pools; this per-pair form also covers pools mixing float32 and float64 vectors).
+__device__ __forceinline__ bool typed_pass(double e, int typed, double thr, int thr_mode) {
+  if (thr_mode == 0) return true;
+  const double t = typed ? (double)(float)thr : thr;
+  return thr_mode == 1 ? e >= t : e > t;
+}
+// lowest threshold any pair is tested against (the completeness proofs must hold for both typings)
+__device__ __forceinline__ double thr_low(double thr) {
+  const double t32 = (double)(float)thr;
+  return t32 < thr ? t32 : thr;
 }
 
 // dense Q x N exact scores (drop-in path and rare exact fallbacks)
@@ -2552,8 +2573,10 @@ __global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int6
       int64_t id = cid[base + lane];
       const int64_t c = id - id_base;
       if (id >= 0 && c >= 0 && c < N) {
-        e = exact_pair<SM>(Qs, q, Cs, c, si, mode == 0 ? 0 : -1, nullptr);
-        const bool pass = thr_mode == 0 || (thr_mode == 1 ? e >= thr : e > thr);
+        int typed = 0;
+        e = exact_pair<SM>(Qs, q, Cs, c, si, mode == 0 ? 0 : -1, nullptr, &typed);
+        const bool pass = mode == 0 ? typed_pass(e, typed, thr, thr_mode)
+                                    : (thr_mode == 0 || (thr_mode == 1 ? e >= thr : e > thr));
         if (!pass) id = -1;
       } else {
         id = -1;
@@ -2595,7 +2618,7 @@ __global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int6
         const double bound = cs[base + kp - 1] + eps;
         if (n >= k) res = bound < kth;
         else if (thr_mode == 0) res = 0;
-        else res = thr_mode == 1 ? (bound < thr) : (bound <= thr);
+        else res = thr_mode == 1 ? (bound < thr_low(thr)) : (bound <= thr_low(thr));
       }
       ores[q] = res;
       if (oredo && (res == 0 || (count_empty && cnt == 0))) atomicAdd(oredo, 1);
@@ -2735,7 +2758,8 @@ __global__ __launch_bounds__(256) void k_refine_lds(VecSet Qs, int Q, VecSet Cs,
           const double ov = nlev == si.nseg ? overall_from_levels(lv + 1, t32s + lane * kMaxSeg, si.nseg) : 0.0;
           lv[0] = ov;
           e = mode == 0 ? lv[1] : ov;
-          const bool pass = thr_mode == 0 || (thr_mode == 1 ? e >= thr : e > thr);
+          const bool pass = mode == 0 ? typed_pass(e, t32s[lane * kMaxSeg], thr, thr_mode)
+                                      : (thr_mode == 0 || (thr_mode == 1 ? e >= thr : e > thr));
           if (!pass) id = -1;
         } else {
           id = -1;
@@ -2774,7 +2798,7 @@ __global__ __launch_bounds__(256) void k_refine_lds(VecSet Qs, int Q, VecSet Cs,
           const double bound = cs[base + kp - 1] + eps;
           if (n >= k) res = bound < kth;
           else if (thr_mode == 0) res = 0;
-          else res = thr_mode == 1 ? (bound < thr) : (bound <= thr);
+          else res = thr_mode == 1 ? (bound < thr_low(thr)) : (bound <= thr_low(thr));
         }
         ores[q] = res;
         if (oredo && (res == 0 || (count_empty && cnt == 0))) atomicAdd(oredo, 1);

@@ -40,6 +40,11 @@ SIGNATURES = {
     "hq_get_option": (_i, [_c.c_char_p, _c.POINTER(_i64)]),
     "hq_diag_build": (_i, []),
     "hq_diag_violations": (_i, [_c.POINTER(_i64), _c.POINTER(_i)]),
+    "hq_comm_unique_id": (_i, [_p]),
+    "hq_comm_init_rank": (_i, [_c.POINTER(_p), _i, _p, _i]),
+    "hq_comm_size": (_i, [_p, _c.POINTER(_i), _c.POINTER(_i)]),
+    "hq_comm_destroy": (_i, [_p]),
+    "hq_allgather_topk": (_i, [_p, _p, _p, _sz, _p]),
     "hq_scan0_geometry": (_i, [_i, _i64, _c.POINTER(_i), _c.POINTER(_i), _c.POINTER(_i64), _c.POINTER(_i64),
                                _c.POINTER(_i64)]),
     "hq_hilbert_table": (_i, [_i, _p, _p, _p, _p]),

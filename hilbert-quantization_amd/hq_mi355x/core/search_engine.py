@@ -66,18 +66,11 @@ def _stack_rows(rows):
 # of a float32 comparison is a numpy float32 (core/search_engine.py:141-174)
 _PY_LEVEL_VALUES = (0.0, 0.1, 1.0)
 
-
-def f32_threshold(t: float, thr_mode: int) -> float:
-    """Threshold that reproduces the reference's comparisons for float32 level scores.  NumPy compares
-    a float32 score with a Python float threshold in float32 (NEP 50): `s >= t` is `s >= f32(t)`.  Between
-    t and f32(t) there is no other float32 value, so only one side of the rounding changes a decision;
-    f32(t) is returned when it does and no Python-float score value (0, 0.1, 1) lies in between."""
-    t32 = float(np.float32(t))
-    if thr_mode == 1 and t32 < t:
-        return t if any(t32 <= p < t for p in _PY_LEVEL_VALUES) else t32
-    if thr_mode == 2 and t32 > t:
-        return t if any(t < p <= t32 for p in _PY_LEVEL_VALUES) else t32
-    return t
+# Threshold typing (NumPy 2, NEP 50): the reference compares a numpy float32 level score with the
+# Python-float threshold in float32 (`s >= t` is `s >= float32(t)`), a Python-float score in float64.
+# The exact re-rank kernels apply that per pair (hq_search.hip typed_pass: the level score's type is known
+# there); the dense exact path splits each row's candidates by score type (_select_typed).  Thresholds are
+# therefore always passed as given.
 
 
 def combine_levels(lv: np.ndarray, both32: bool) -> np.ndarray:
@@ -159,12 +152,6 @@ class IndexCorpus:
             return K.seg_level0_len(self.L) <= 256
         return self.prep.Lp <= 256
 
-    def _thr(self, qp, thr: float, thr_mode: int) -> float:
-        """Threshold for the float32 comparisons of an all-float32 query batch and corpus (f32_threshold)."""
-        if thr_mode and qp.all32 and self.prep.all32:
-            return f32_threshold(float(thr), thr_mode)
-        return float(thr)
-
     def _forced(self, qp):
         """Device bool [Q] of queries that must take the dense exact path (float32 outside the model)."""
         t = torch()
@@ -182,11 +169,39 @@ class IndexCorpus:
         sub = qp.rows(sel)
         outs = []
         chunk = max(1, (1 << 27) // max(1, self.N))  # <= 1 GiB of scores per launch
+        typed = (mode == 0 and thr_mode != 0 and float(np.float32(thr)) != float(thr) and sub.f32 and self.prep.f32)
         for i in range(0, sub.N, chunk):
             part = sub.rows(torch().arange(i, min(sub.N, i + chunk), device=sel.device))
             sc = K.level_scores(part, self.prep, 0 if mode == 0 else -1)
-            outs.append(K.select_topk(sc, k, thr, thr_mode, self.id_base))
+            if typed:
+                outs.append(self._select_typed(part, sc, k, float(thr), thr_mode))
+            else:
+                outs.append(K.select_topk(sc, k, thr, thr_mode, self.id_base))
         return [torch().cat([o[j] for o in outs], 0) for j in range(4)]
+
+    def _select_typed(self, qp, sc, k: int, thr: float, thr_mode: int):
+        """select_topk of level scores where float32(thr) != thr and float32 vectors are involved: the
+        numpy-float32 scores (both vectors float32, general branch: a value outside 0 / 0.1 / 1) are tested
+        against float32(thr), the Python-float ones against thr (NEP 50).  The top-k of each kind (the other
+        kind masked to -inf) merge by (score desc, id asc) into the row's top-k; the first arg-max is the
+        better of the two."""
+        t = torch()
+        qf = (qp.S[:, 0, 3].to(t.int64) & 1).bool()
+        cf = (self.prep.S[:, 0, 3].to(t.int64) & 1).bool()
+        py = (sc == 0.0) | (sc == 0.1) | (sc == 1.0)
+        f32 = qf.view(-1, 1) & cf.view(1, -1) & ~py
+        ninf = t.tensor(-float("inf"), dtype=sc.dtype, device=sc.device)
+        sa, ia, ba, bia = K.select_topk(t.where(f32, sc, ninf), k, float(np.float32(thr)), thr_mode, self.id_base)
+        sb, ib, bb, bib = K.select_topk(t.where(f32, ninf, sc), k, thr, thr_mode, self.id_base)
+        s, i = t.cat([sa, sb], 1), t.cat([ia, ib], 1)
+        key = t.where(i >= 0, i, t.full_like(i, 2 ** 62))
+        o = t.argsort(key, dim=1, stable=True)
+        s, i = s.gather(1, o), i.gather(1, o)
+        o = t.argsort(s, dim=1, descending=True, stable=True)[:, :k]
+        s, i = s.gather(1, o), i.gather(1, o)
+        i = t.where(s > -float("inf"), i, t.full_like(i, -1))
+        pick_b = (bb > ba) | ((bb == ba) & (bib < bia))
+        return s, i, t.where(pick_b, bb, ba), t.where(pick_b, bib, bia)
 
     def exact_topk(self, qp, mode: int, k: int, thr: float = 0.0, thr_mode: int = 0, need_best: bool = False):
         """Exact per-query top-k (score desc, id asc) among candidates passing the threshold test;
@@ -195,7 +210,6 @@ class IndexCorpus:
         t = torch()
         Q = qp.N
         dev = qp.Z.device
-        thr = self._thr(qp, thr, thr_mode)
         best = t.full((Q,), -float("inf"), dtype=t.float64, device=dev)
         bid = t.full((Q,), -1, dtype=t.int64, device=dev)
         kp = k + self.SLACK
@@ -258,19 +272,23 @@ class IndexCorpus:
             s0, ids, cnt, best, bid = self.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)
             oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
             return PendingSearch(done=(oid, odet[..., 0], odet[..., 1:], ocnt))
-        threshold = self._thr(qp, threshold, 1)
         nredo = self._redo_counter(qp.Z.device)
         s0, ids, cnt, res, det = self._scan_refine(qp, 0, M, float(threshold), 1, nredo, det=True)
         # no arg-max on this path: a query where nothing passed (count 0) is recomputed by the dense path
         # in progressive_finish, so the fallback slot is a constant (-inf, id -1, zero re-scores)
         best, bid, bdet = self._no_fallback(Q, qp.Z.device)
         oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out, bdet, det)
+        # queries forced onto the dense path (float32 outside the scans' model) join the redo count on the
+        # device, so finishing still waits for one pinned value only
+        forced = self._forced(qp)
+        if forced is not None:
+            nredo.add_(forced.sum(dtype=t.int32).view(1))
         # the shared device counter is overwritten by the next batch: this batch's value leaves now
         host = self._pinned(nredo.dtype)
         host.copy_(nredo, non_blocking=True)
         ev = t.cuda.Event()
         ev.record()
-        return PendingSearch(qp=qp, out=(oid, odet, ocnt), res=res, cnt=cnt, forced=self._forced(qp),
+        return PendingSearch(qp=qp, out=(oid, odet, ocnt), res=res, cnt=cnt, forced=forced,
                              nredo=host, event=ev, threshold=float(threshold), M=M, K_out=K_out)
 
     def progressive_finish(self, p: "PendingSearch"):
@@ -283,7 +301,7 @@ class IndexCorpus:
         p.event.synchronize()
         nredo = int(p.nredo[0])
         self._pinned_free.setdefault(p.nredo.dtype, []).append(p.nredo)  # read: reusable
-        if p.forced is not None or nredo > 0:
+        if nredo > 0:
             redo = (p.res == 0) | (p.cnt == 0)
             if p.forced is not None:
                 redo = redo | p.forced
@@ -312,9 +330,11 @@ class IndexCorpus:
         return cache[key]
 
     def _no_fallback(self, Q: int, dev):
+        """Constant (-inf, -1, zeros) fallback slot of a batch of Q queries, cached per stream: the fills
+        are stream-ordered, so a batch on another stream must not read them before they ran."""
         t = torch()
         cache = self.__dict__.setdefault("_nofb", {})
-        key = (Q, str(dev))
+        key = (Q, str(dev), K.stream())
         if key not in cache:
             cache[key] = (t.full((Q,), -float("inf"), dtype=t.float64, device=dev),
                           t.full((Q,), -1, dtype=t.int64, device=dev),

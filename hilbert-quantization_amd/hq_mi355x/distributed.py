@@ -37,8 +37,11 @@ def unpack(rec):
     return rec[..., 0].contiguous(), rec[..., 1].round().to(t.int64).contiguous(), rec[..., 2:].contiguous()
 
 
-def all_gather(x, group=None):
-    """Stack of every rank's tensor [R, ...] (one collective; RCCL on GPU tensors, gloo on CPU)."""
+def all_gather(x, group=None, comm=None):
+    """Stack of every rank's tensor [R, ...] (one collective).  comm (rccl.Communicator): RCCL through the
+    C-ABI (hq_allgather_topk); else torch.distributed on `group` (RCCL on GPU tensors, gloo on CPU)."""
+    if comm is not None:
+        return comm.all_gather(x)
     t = torch()
     import torch.distributed as dist
     if not dist.is_available() or not dist.is_initialized():
@@ -52,10 +55,13 @@ def all_gather(x, group=None):
 class ShardedIndexCorpus:
     """This rank's shard of a global corpus of index vectors (global ids start at `id_base`)."""
 
-    def __init__(self, local_indices, id_base: int, n_total: int, group=None):
+    def __init__(self, local_indices, id_base: int, n_total: int, group=None, comm=None):
+        """comm: an rccl.Communicator over the shard ranks (the C-ABI all-gather); without it the records
+        travel by torch.distributed.all_gather on `group`."""
         self.local = IndexCorpus(local_indices, id_base=id_base)
         self.n_total = int(n_total)
         self.group = group
+        self.comm = comm
 
     def local_records(self, qp, M: int, threshold: float):
         """This shard's exact contribution [Q, M + 1, 2 + W]: the level-0 top-M >= threshold by (score
@@ -70,7 +76,6 @@ class ShardedIndexCorpus:
         t = torch()
         c = self.local
         Q = qp.N
-        threshold = c._thr(qp, threshold, 1)
         s0, ids, cnt, res, det0 = c._scan_refine(qp, 0, M, float(threshold), 1, det=True)
         # no arg-max on the scan path (count-0 rows are redone below): constant fallback slot
         best, bid, bdet0 = c._no_fallback(Q, qp.Z.device)
@@ -143,7 +148,7 @@ class ShardedIndexCorpus:
         if p[0] == "done":
             return p[1]
         rec = p[1] if p[0] == "rec" else self._local_finish(p[1])
-        out = self.merge(all_gather(rec, self.group), p[2], p[3])
+        out = self.merge(all_gather(rec, self.group, self.comm), p[2], p[3])
         p[:] = ["done", out]
         return out
 
@@ -156,7 +161,7 @@ class ShardedIndexCorpus:
         k = max(1, int(max_results))
         sc, ids, _, _, _ = c.exact_topk(qp, 1, k)
         det = K.rescore(qp, c.prep, ids, c.id_base)
-        g = all_gather(pack(sc, ids, det), self.group)
+        g = all_gather(pack(sc, ids, det), self.group, self.comm)
         gs, gi, gd = unpack(g)
         R = g.shape[0]
         none_s = t.full((R, Q), -float("inf"), dtype=t.float64, device=g.device)
@@ -174,7 +179,7 @@ class ShardedIndexCorpus:
         Q = qp.N
         k = max(1, int(max_results))
         sc, ids, _, _, _ = c.exact_topk(qp, 0, k, float(threshold), 2)
-        g = all_gather(pack(sc, ids, sc.unsqueeze(-1)), self.group)
+        g = all_gather(pack(sc, ids, sc.unsqueeze(-1)), self.group, self.comm)
         gs, gi, gd = unpack(g)
         R = g.shape[0]
         none_s = t.full((R, Q), -float("inf"), dtype=t.float64, device=g.device)

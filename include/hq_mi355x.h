@@ -359,6 +359,23 @@ int hq_cos_prepare(const float* X, int64_t N, int64_t ld, int K, void* X16, doub
 int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* B16, const double* inv_b, int64_t N,
                        int K, double* out, hq_stream_t stream);
 
+/* ---- §8e: the sharded search's one collective (RCCL over xGMI) ----------------------------------
+ * The corpus is split into contiguous global-id ranges, one per GPU (one process per GPU); each rank
+ * answers the whole query batch against its shard and packs fixed-size top-k records, and ONE
+ * all-gather lets every rank merge them with hq_progressive_final (the reference's analogue: the
+ * thread fan-out + list-concatenation merge of core/video_search.py:722-875).
+ * hq_comm_unique_id: rank 0 creates the communicator id (HQ_COMM_ID_BYTES opaque bytes) and hands it
+ *   to every rank out of band (hq_mi355x.distributed uses the torch.distributed store / broadcast);
+ * hq_comm_init_rank: collective over the nranks processes, on the calling thread's current HIP device;
+ * hq_allgather_topk: recv [nranks x bytes] = every rank's send [bytes], in rank order, on `stream`;
+ *   bytes must be equal on all ranks.  Asynchronous like every other entry point.                   */
+#define HQ_COMM_ID_BYTES 128
+int hq_comm_unique_id(void* id_out);
+int hq_comm_init_rank(void** comm, int nranks, const void* id, int rank);
+int hq_comm_size(void* comm, int* nranks, int* rank);
+int hq_comm_destroy(void* comm);
+int hq_allgather_topk(void* comm, const void* send, void* recv, size_t bytes, hq_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -339,6 +339,57 @@ def search_f32_fixtures(hq):
                 out[f"{tag}_{ptag}_{stag}_sc"] = sc
         out[f"{tag}_C"] = C
         out[f"{tag}_Q"] = Q
+        if tag == "L64":
+            out.update(_threshold_rounding_fixtures(eng, models_of, pools, Q, N))
+    return out
+
+
+def _threshold_rounding_fixtures(eng, models_of, pools, Q, N):
+    """the reference compares a numpy.float32 level score with the Python-float threshold in
+    float32 (NumPy 2, NEP 50: the threshold is rounded to float32), a Python-float score in float64.  Per
+    query, s = the second-best float32-typed level-0 score over the pool; thresholds a quarter ulp above
+    (progressive, `>=`, core/search_engine.py:284-292) and below (the video engine's level-0 frame scan,
+    `>`, core/video_search.py:236-264) round to s in float32, so the reference keeps / drops s where a
+    float64 comparison would not.  Pools: float32 and mixed float32 / float64 rows, each with ("full") and
+    without ("safe": the scan path) the float32-unsafe rows 9 and 10."""
+    from hilbert_quantization.core.search_engine import ProgressiveSimilaritySearchEngine
+    out = {}
+    keep = [b for b in range(N) if b not in (9, 10)]
+    for ptag, rows_all in pools.items():
+        for sub, idxs in (("full", list(range(N))), ("safe", keep)):
+            rows = [rows_all[b] for b in idxs]
+            models = models_of(rows)
+            K = 10
+            t_ge, t_gt = np.zeros(len(Q)), np.zeros(len(Q))
+            pg_ids, fr_ids = np.full((len(Q), K), -1, np.int64), np.full((len(Q), K), -1, np.int64)
+            pg_sc, fr_sc = np.zeros((len(Q), K)), np.zeros((len(Q), K))
+            for a in range(len(Q)):
+                s0 = [eng.compare_indices_at_level(Q[a], r, 0) for r in rows]
+                typed = sorted({float(v) for v in s0 if isinstance(v, np.float32)}, reverse=True)
+                if typed:  # (a constant query has no float32-typed score: the plain threshold 0.1)
+                    s = np.float32(typed[1] if len(typed) > 1 else typed[0])
+                    up = float(np.nextafter(s, np.float32(2)) - s)
+                    down = float(s - np.nextafter(s, np.float32(-2)))
+                    t_ge[a], t_gt[a] = float(s) + up / 4, float(s) - down / 4
+                    assert np.float32(t_ge[a]) == s and np.float32(t_gt[a]) == s
+                else:
+                    t_ge[a] = t_gt[a] = 0.1
+                e2 = ProgressiveSimilaritySearchEngine(similarity_threshold=t_ge[a], max_candidates_per_level=20)
+                for j, x in enumerate(e2.progressive_search(Q[a], models, K)):
+                    pg_ids[a, j] = int(x.model.model_id[1:])
+                    pg_sc[a, j] = float(x.similarity_score)
+                # VideoEnhancedSearchEngine._hierarchical_search (video_search.py:236-264) over the pool's
+                # index vectors: level-0 similarity > threshold, stable sort desc, top K
+                hits = [(v, b) for b, v in enumerate(s0) if v > t_gt[a]]
+                hits.sort(key=lambda h: h[0], reverse=True)
+                for j, (v, b) in enumerate(hits[:K]):
+                    fr_ids[a, j] = b
+                    fr_sc[a, j] = float(v)
+            key = f"thr_{ptag}_{sub}"
+            out[f"{key}_t_ge"], out[f"{key}_t_gt"] = t_ge, t_gt
+            out[f"{key}_pg_ids"], out[f"{key}_pg_sc"] = pg_ids, pg_sc
+            out[f"{key}_fr_ids"], out[f"{key}_fr_sc"] = fr_ids, fr_sc
+            out[f"{key}_rows"] = np.array(idxs, np.int64)
     return out
 
 

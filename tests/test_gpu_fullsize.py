@@ -135,3 +135,55 @@ def test_frames_bench_shape(hq_lib):
         want = (B @ a / (nb * np.linalg.norm(a)) + 1.0) / 2.0
         got = _np(S[q, cols])
         assert np.max(np.abs(got - want)) < 2e-6, q
+
+
+def test_cfg4_full_size_8_shards(hq_lib):
+    """cfg4 on one GPU: the 8M-row corpus (L = 64 index vectors of seed-4 embeddings from the fused kernel,
+    generated 1M rows at a time) as 8 ShardedIndexCorpus shards of 1M rows, each answering the cfg3-style
+    1000-query batch (global rows 0..999 + N(0, 0.01) noise, seed 3); the records merged by
+    ShardedIndexCorpus.merge (hq_progressive_final, 8-way) == an unsharded IndexCorpus over all 8M rows:
+    ids, counts, overall and per-level scores bit-identical; sampled queries == the oracle
+    (core/search_engine.py:232-300, 340-388; merge analogue core/video_search.py:722-875).  One shard also
+    runs its all-gather through a one-rank RCCL communicator (hq_allgather_topk)."""
+    import torch
+    from hq_mi355x import kernels as K
+    from hq_mi355x.core.search_engine import IndexCorpus
+    from hq_mi355x.distributed import ShardedIndexCorpus, shard_range
+    from hq_mi355x.rccl import Communicator
+    R, per, Qn = 8, 1_000_000, 1000
+    N = R * per
+    g = torch.Generator(device="cuda").manual_seed(4)
+    C = torch.empty((N, 64), dtype=torch.float64, device="cuda")
+    for r in range(R):
+        Xc = torch.randn((per, 1536), generator=g, device="cuda", dtype=torch.float32)
+        _, C[r * per:(r + 1) * per], _ = K.map_index_quantize(Xc, 64, 64)
+        del Xc
+    gq = torch.Generator(device="cuda").manual_seed(3)
+    Q = C[:Qn] + 0.01 * torch.randn((Qn, 64), generator=gq, device="cuda", dtype=torch.float64)
+    full = IndexCorpus(C)
+    ref = [_np(x) for x in full.progressive(Q, 10, 0.1, 20)]
+    del full
+    recs = []
+    for r in range(R):
+        a, b = shard_range(N, r, R)
+        sh = ShardedIndexCorpus(C[a:b], id_base=a, n_total=N)
+        recs.append(sh.local_records(sh.local.prepare_queries(Q), 20, 0.1))
+        del sh
+    oid, ov, lv, cnt = ShardedIndexCorpus.merge(torch.stack(recs, 0), 20, 10)
+    for x, y, name in zip((oid, ov, lv, cnt), ref, ("ids", "overall", "levels", "count")):
+        np.testing.assert_array_equal(_np(x), y, err_msg=name)
+    ids = ref[0]
+    assert np.array_equal(ids[:, 0], np.arange(Qn)) and np.all(ref[3] == 10)
+    # the C-ABI all-gather on a one-rank communicator: the sharded path end to end (shard = whole corpus)
+    comm = Communicator.single()
+    one = ShardedIndexCorpus(C[:per], id_base=0, n_total=per, comm=comm)
+    got = [_np(x) for x in one.progressive(Q, 10, 0.1, 20)]
+    want = [_np(x) for x in IndexCorpus(C[:per]).progressive(Q, 10, 0.1, 20)]
+    for x, y in zip(got, want):
+        np.testing.assert_array_equal(x, y)
+    comm.close()
+    Ch, Qh = _np(C), _np(Q)
+    for a in (0, 333, 999):
+        rid, rsc, _, _ = O.progressive_search(Qh[a], Ch, 10, 0.1, 20)
+        assert list(ids[a]) == list(rid), a
+        np.testing.assert_allclose(ref[1][a], rsc, atol=1e-10)

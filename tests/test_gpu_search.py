@@ -469,3 +469,18 @@ def test_select_topk_register_stages(hq_lib, hq_option, N):
                 s, i, b, bi = _np_select(sc[q], k, thr, mode)
                 assert np.array_equal(got[0][q], s) and np.array_equal(got[1][q], np.where(i >= 0, i + 7, -1)), (N, k, q)
                 assert got[2][q] == b and got[3][q] == bi + 7
+
+
+def test_rccl_allgather_one_rank(hq_lib):
+    """hq_allgather_topk on a one-rank RCCL communicator (hq_comm_init_rank): recv == send, [1, ...] shaped,
+    for the record layout of the sharded search and an odd byte count."""
+    import torch
+    from hq_mi355x.rccl import Communicator
+    comm = Communicator.single()
+    assert (comm.nranks, comm.rank) == (1, 0)
+    x = torch.randn((1000, 21, 8), dtype=torch.float64, device="cuda")
+    y = comm.all_gather(x)
+    assert y.shape == (1,) + tuple(x.shape) and torch.equal(y[0], x)
+    b = torch.arange(37, dtype=torch.uint8, device="cuda")
+    assert torch.equal(comm.all_gather(b)[0], b)
+    comm.close()

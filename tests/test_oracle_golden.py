@@ -238,25 +238,22 @@ def test_search_orders_f32_golden(golden, tag):
 
 
 def test_f32_threshold_and_typed_overall_host_logic():
-    """Host logic of the float32 search path (hq_mi355x.core.search_engine): the threshold that
-    reproduces NumPy's float32 comparison, and the typed weighted sum, against NumPy itself."""
-    from hq_mi355x.core.search_engine import combine_levels, f32_threshold
-    for t in (0.1, 0.3, 0.7, 0.123456789, 0.5, 1e-46, 0.95):
-        t32 = np.float32(t)
+    """The threshold typing the exact kernels apply per pair (hq_search.hip typed_pass: a numpy float32
+    level score against float32(threshold), a Python-float score against the threshold itself), checked
+    against NumPy's own comparisons (NEP 50) around thresholds where float32(t) < t and > t; and the typed
+    weighted sum of the host helper against NumPy."""
+    from hq_mi355x.core.search_engine import combine_levels
+    for t in (0.1, 0.3, 0.7, 0.123456789, 0.5, 1e-46, 0.95, 0.9071843218803406):
+        t32 = float(np.float32(t))
+        assert (t32 < t) or (t32 > t) or t32 == t
         for mode in (1, 2):
-            te = f32_threshold(t, mode)
-            # every float32 value next to t and every Python-float score value decides as in NumPy
-            cands = [np.nextafter(t32, np.float32(-1)), t32, np.nextafter(t32, np.float32(2))]
-            for v in cands:
-                if float(v) in (0.0, 1.0):  # never a numpy float32 score (those lie in (0, 1))
-                    continue
-                want = (v >= t) if mode == 1 else (v > t)   # numpy float32 vs Python float (NEP 50)
-                got = (float(v) >= te) if mode == 1 else (float(v) > te)
-                assert bool(want) == got, (t, mode, v)
-            for p in (0.0, 0.1, 1.0):
+            for v in (np.nextafter(np.float32(t), np.float32(-1)), np.float32(t), np.nextafter(np.float32(t), np.float32(2))):
+                want = bool(v >= t) if mode == 1 else bool(v > t)       # numpy float32 vs Python float
+                got = (float(v) >= t32) if mode == 1 else (float(v) > t32)  # typed_pass, float32 score
+                assert want == got, (t, mode, v)
+            for p in (0.0, 0.1, 1.0, t32):                               # Python-float scores: float64
                 want = (p >= t) if mode == 1 else (p > t)
-                got = (p >= te) if mode == 1 else (p > te)
-                assert want == got, (t, mode, p)
+                assert want == ((float(p) >= t) if mode == 1 else (float(p) > t))
     rng = np.random.default_rng(3)
     lv = rng.uniform(0, 1, (50, 5)).astype(np.float32).astype(np.float64)
     lv[:5] = 0.1
