@@ -37,6 +37,7 @@ def hbm_roofline(achieved: float, traffic, **extra) -> dict:
 
 
 FP16_MATRIX_PEAK_TFS = 2500.0  # MI355X dense FP16/BF16 MFMA peak (MI355X_MICROARCH.md)
+FP64_MATRIX_PEAK_TFS = 78.6    # MI355X FP64 matrix peak (spec, SURVEY.md §8d / BASELINE.md §3)
 
 
 def parse():
@@ -185,6 +186,61 @@ def cpu_baseline_parallel(dim, seconds):
             counts = pool.map(_cpu_worker, [(kind, dim, seconds, 100 + w) for w in range(workers)])
             out[kind] = (sum(counts) / (time.perf_counter() - t0), workers)
     return out
+
+
+def cpu_baseline_quantize_loops(dim, seconds):
+    """the reference-SHAPED single-core port (oracle/hq_loops.py: per-element
+    coordinate, scatter / gather and streaming-tree loops, as core/hilbert_mapper.py:17-205 and
+    core/streaming_index_builder.py:45-243 run them)."""
+    from oracle import hq_loops as HL
+    from oracle import hq_oracle as O
+    rng = np.random.default_rng(1)
+    n = O.optimal_dimensions(dim)[0]
+    P = rng.standard_normal((64, dim)).astype(np.float32)
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        HL.quantize_one(P[done % 64], n, 64)
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "embeddings/sec", "cores": 1, "kind": "port",
+            "sample": f"{done} x {dim}-d f32 embeddings through the reference-shaped per-element port (oracle/hq_loops.py: "
+                      f"pad, per-cell d2xy + scatter, gather, per-value streaming tree, embed, u8 normalise) in {dt:.1f}s",
+            "structure": "reference-shaped (per-element Python loops, BASELINE.md §3 item 1)"}
+
+
+def cpu_baseline_search_loops(C, Q, seconds):
+    """Reference-shaped search: the per-candidate Python loop of core/search_engine.py:232-388 (both level
+    structures re-parsed per comparison) over a 10k-row slice, extrapolated linearly to 1M rows."""
+    from oracle import hq_loops as HL
+    C = C[:10_000]
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds and done < len(Q):
+        HL.progressive_search(Q[done], C, 10, 0.1, 20)
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done * len(C) / dt / 1_000_000, "unit": "queries/sec over a 1M corpus (extrapolated)",
+            "cores": 1, "kind": "port", "candidate_scores_per_sec": done * len(C) / dt,
+            "sample": f"{done} queries x {len(C)} candidates through the reference-shaped candidate loop "
+                      f"(oracle/hq_loops.py) in {dt:.1f}s, linear in corpus size",
+            "structure": "reference-shaped (per-candidate Python loop, BASELINE.md §3 item 1)"}
+
+
+def cpu_baseline_mode(mode, C, Q, seconds):
+    """Vectorised oracle (one core) for the other cfg3 modes: brute-force overall top-10 / strict level-0 scan."""
+    from oracle import hq_oracle as O
+    C = C[:20_000]
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds and done < len(Q):
+        if mode == "overall":
+            O.brute_force_search(Q[done], C, 10)
+        else:
+            O.hierarchical_frame_search(Q[done], C, 10, 0.1)
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done * len(C) / dt / 1_000_000, "unit": "queries/sec over a 1M corpus (extrapolated)",
+            "cores": 1, "kind": "port",
+            "sample": f"{done} queries x {len(C)} candidates, oracle {'brute_force_search' if mode == 'overall' else 'hierarchical_frame_search'} "
+                      f"(NumPy, single thread) in {dt:.1f}s, linear in corpus size"}
 
 
 def cpu_baseline_search(C, Q, seconds):
@@ -431,8 +487,14 @@ def main():
         queries = q0 + 0.01 * torch.randn(q0.shape, generator=gq, device=dev, dtype=torch.float64)
         torch.cuda.synchronize()
         tp0 = time.perf_counter()
+        comm = None
         if world > 1:
-            engine = ShardedIndexCorpus(corpus_idx, id_base=rank * Nc, n_total=Nc * world)
+            # the records all-gather runs through the C-ABI (hq_allgather_topk, RCCL over xGMI) when the
+            # ranks hold one GPU each; the one-GPU rehearsal (HQ_BENCH_SAME_DEVICE + gloo) uses torch.distributed
+            if os.environ.get("HQ_BENCH_BACKEND", "nccl") == "nccl":
+                from hq_mi355x.rccl import Communicator
+                comm = Communicator.from_process_group()
+            engine = ShardedIndexCorpus(corpus_idx, id_base=rank * Nc, n_total=Nc * world, comm=comm)
         else:
             engine = IndexCorpus(corpus_idx)
         torch.cuda.synchronize()
@@ -478,6 +540,31 @@ def main():
                                  "time; the scan is bound by the per-pair f32 filter on the VALUs (DESIGN.md)"},
             "self_match_rate": float((ids[:, 0].cpu() == torch.arange(Qn)).float().mean()),
         }
+        # the other two cfg3 modes: brute-force overall top-10 (core/search_engine.py:302-338,
+        # f64 MFMA scan over all segments + exact re-rank) and the video engine's strict level-0 frame scan
+        # (core/video_search.py:215-264, split-f16 scan + exact re-rank, `>` threshold)
+        Lp = K.seg_padded_len(L)
+        modes = {}
+        for mode, fn, flops, peak, pname in (
+                ("overall", lambda: engine.brute_force(queries, 10), 2.0 * pairs * Lp, FP64_MATRIX_PEAK_TFS,
+                 "FP64 matrix (spec)"),
+                ("level0", lambda: engine.frame_search(queries, 10, 0.1), 3 * 2.0 * pairs * 32, FP16_MATRIX_PEAK_TFS,
+                 "dense F16 MFMA")):
+            msteps = max(2, args.search_steps // 2)
+            mw, mk = timed(fn, msteps, 1, world)
+            modes[mode] = {
+                "value": Qn * msteps / mw, "unit": "queries/sec", "steps": msteps, "ms_per_step": mw / msteps * 1e3,
+                "roofline": {"bound": "mfma", "achieved": flops / mk / 1e12, "peak": peak, "unit": "TFLOP/s",
+                             "frac": flops / mk / 1e12 / peak,
+                             "note": f"algorithmic contraction flops per step ({'2*Q*N*Lp f64' if mode == 'overall' else '3 x 2*Q*N*32 split f16'}) / "
+                                     f"GPU step time (HIP events); peak = {pname}"}}
+        rec["search"]["modes"] = modes
+        if comm is not None:
+            # the one collective of the sharded search alone: the records block of one batch per rank
+            x = torch.zeros((Qn, 21, 3 + engine.local.nseg), dtype=torch.float64, device=dev)
+            _, ak = timed(lambda: comm.all_gather(x), 20, 3, world)
+            rec["search"]["allgather"] = {"ms": ak * 1e3, "bytes_per_rank": x.numel() * 8, "ranks": world,
+                                          "path": "hq_allgather_topk (ncclAllGather over xGMI)"}
 
     if not args.no_precomputed:
         rec["precomputed"] = bench_precomputed(args, X, world)
@@ -493,8 +580,9 @@ def main():
         rec["stream"] = bench_stream(args, world, rank, dev)
 
     if rank == 0 and world == 1 and not args.no_cpu:
-        rec["cpu_baseline"] = cpu_baseline_quantize(d, args.cpu_seconds)
+        rec["cpu_baseline"] = cpu_baseline_quantize_loops(d, args.cpu_seconds / 2)
         rec["cpu_baseline"]["threads_available"] = os.cpu_count()
+        rec["cpu_baseline"]["vectorised"] = cpu_baseline_quantize(d, args.cpu_seconds / 2)
         if cpu_par:
             v, w = cpu_par["quantize"]
             rec["cpu_baseline"]["multicore"] = {
@@ -505,7 +593,11 @@ def main():
             from hq_mi355x._dev import to_np
             C = to_np(corpus_idx[:100_000])
             Qh = to_np(queries[:50])
-            rec["search"]["cpu_baseline"] = cpu_baseline_search(C, Qh, args.cpu_seconds / 2)
+            rec["search"]["cpu_baseline"] = cpu_baseline_search_loops(C, Qh, args.cpu_seconds / 2)
+            rec["search"]["cpu_baseline"]["vectorised"] = cpu_baseline_search(C, Qh, args.cpu_seconds / 2)
+            for mode in ("overall", "level0"):
+                if mode in rec["search"].get("modes", {}):
+                    rec["search"]["modes"][mode]["cpu_baseline"] = cpu_baseline_mode(mode, C, Qh, args.cpu_seconds / 4)
             if cpu_par:
                 v, w = cpu_par["search"]
                 rec["search"]["cpu_baseline"]["multicore"] = {

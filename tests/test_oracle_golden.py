@@ -315,3 +315,21 @@ def test_precomputed_similarity_golden(golden):
     a = np.full(5, 0.5, dtype=np.float32)
     for v, want in zip(g["lvl_const_pairs"], g["lvl_const_vals"]):
         assert float(O.precomputed_level_similarity(a, np.full(5, v, dtype=np.float32))) == want
+
+
+def test_reference_shaped_loops_match_oracle():
+    """oracle/hq_loops.py (the per-element reference-shaped CPU port timed by bench.py's cpu_baseline) gives
+    the vectorised oracle's frames and the golden's index; its candidate loop ranks like the oracle."""
+    from oracle import hq_loops as HL
+    rng = np.random.default_rng(8)
+    for d, n in ((1536, 64), (1024, 32), (300, 32)):
+        p = rng.standard_normal(d).astype(np.float32)
+        img = O.map_to_2d(O.pad_parameters(p, n), n)
+        u8, _, _ = O.normalize_u8(O.embed_index_row(img, O.streaming_index(O.map_from_2d(img), n)))
+        assert HL.quantize_one(p, n, n).tobytes() == u8.tobytes()
+        assert np.array_equal(HL.map_from_2d(HL.map_to_2d(O.pad_parameters(p, n), n)), O.pad_parameters(p, n))
+    C = rng.standard_normal((300, 64))
+    for a in (3, 77):
+        q = C[a] + rng.normal(0, 0.01, 64)
+        rid, _, _, _ = O.progressive_search(q, C, 10, 0.1, 20)
+        assert HL.progressive_search(q, C, 10, 0.1, 20) == list(rid)
