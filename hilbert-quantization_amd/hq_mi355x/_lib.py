@@ -40,6 +40,10 @@ SIGNATURES = {
     "hq_get_option": (_i, [_c.c_char_p, _c.POINTER(_i64)]),
     "hq_diag_build": (_i, []),
     "hq_diag_violations": (_i, [_c.POINTER(_i64), _c.POINTER(_i)]),
+    "hq_cosine_scores_dt": (_i, [_i, _p, _i, _p, _i64, _i, _p, _p]),
+    "hq_detect_heights": (_i, [_i, _p, _i64, _i, _i, _p, _p]),
+    "hq_spatial_locality": (_i, [_i, _p, _i, _p, _i64, _i, _i, _p, _p]),
+    "hq_threshold_select": (_i, [_p, _p, _i, _i64, _d, _i64, _p, _p, _p]),
     "hq_comm_unique_id": (_i, [_p]),
     "hq_comm_init_rank": (_i, [_c.POINTER(_p), _i, _p, _i]),
     "hq_comm_size": (_i, [_p, _c.POINTER(_i), _c.POINTER(_i)]),

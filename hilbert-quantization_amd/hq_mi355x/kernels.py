@@ -432,6 +432,26 @@ def cosine_scores_f64(a, b, exc=None):
     return out
 
 
+def cosine_scores_dt(a, b, exc=None):
+    """(cos + 1) / 2 of float32 or float64 rows (hq_cosine_scores_dt; float64 stays float64) -> f64 [Q, N].
+    float32 problems large enough for the matrix cores take cosine_scores' split-f16 MFMA path."""
+    t = torch()
+    a2 = _contig(a.reshape(a.shape[0], -1))
+    b2 = _contig(b.reshape(b.shape[0], -1))
+    if a2.dtype == t.float32 and b2.dtype == t.float32:
+        return cosine_scores(a2, b2, exc)
+    a2, b2 = a2.to(t.float64), b2.to(t.float64)
+    Kd = min(a2.shape[1], b2.shape[1])
+    if a2.shape[1] != Kd:
+        a2 = _contig(a2[:, :Kd])
+    if b2.shape[1] != Kd:
+        b2 = _contig(b2[:, :Kd])
+    out = t.empty((a2.shape[0], b2.shape[0]), dtype=t.float64, device=a2.device)
+    _chk(_L().hq_cosine_scores_dt(dtype_code(t.float64), ptr(a2), a2.shape[0], ptr(b2), b2.shape[0], Kd, ptr(out),
+                                  stream()), exc)
+    return out
+
+
 def select_topk(scores, k: int, threshold: float = 0.0, thr_mode: int = 0, id_base: int = 0, exc=None):
     """Top-k (score desc, id asc) of a dense f64 [Q, N] score matrix + first arg-max."""
     t = torch()

@@ -359,6 +359,28 @@ int hq_cos_prepare(const float* X, int64_t N, int64_t ld, int K, void* X16, doub
 int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* B16, const double* inv_b, int64_t N,
                        int K, double* out, hq_stream_t stream);
 
+/* ---- S7: the rest of the RAG scorer (rag/search/engine.py) --------------------------------------
+ * hq_cosine_scores_dt: as hq_cosine_scores for float32 (HQ_F32) or float64 (HQ_F64) rows; float64
+ *   inputs are not narrowed (engine.py:622-660 computes in the input dtype).
+ * hq_detect_heights: _detect_original_embedding_height (engine.py:134-162) of N images [N, H, W]: the
+ *   first row from the bottom with fewer than half zeros ends the original embedding (height = row + 1,
+ *   H when none) -> out int32 [N].  _extract_original_embedding (:604-620) is the image's first rows.
+ * hq_spatial_locality: _calculate_spatial_locality_similarity (engine.py:662-714) of every query image
+ *   q [Q, H, W] against every stored image c [N, H, W] -> out f64 [Q, N]: original heights detected on
+ *   both (different -> 0.0), ws = min(4, h / 4, W / 4), one cosine over the block when ws < 2, else the
+ *   mean (NumPy pairwise order) of the (cos + 1) / 2 of ws x ws windows at stride ws / 2.  H * W <= 8192.
+ * hq_threshold_select: _apply_progressive_threshold (engine.py:243-287) for Q rows of candidate scores
+ *   [Q, N] in the caller's order: the first `cap` candidates with score >= threshold -> out_ids [Q, cap]
+ *   (ids[q, i] when ids is given, else the position i; -1 padded), out_count [Q].  The caller computes
+ *   the level's threshold and cap exactly as the reference (Python float arithmetic).               */
+int hq_cosine_scores_dt(int dtype, const void* a, int Q, const void* b, int64_t N, int K, double* out,
+                        hq_stream_t stream);
+int hq_detect_heights(int dtype, const void* imgs, int64_t N, int H, int W, int* out, hq_stream_t stream);
+int hq_spatial_locality(int dtype, const void* q, int Q, const void* c, int64_t N, int H, int W, double* out,
+                        hq_stream_t stream);
+int hq_threshold_select(const double* scores, const int64_t* ids, int Q, int64_t N, double threshold, int64_t cap,
+                        int64_t* out_ids, int64_t* out_count, hq_stream_t stream);
+
 /* ---- §8e: the sharded search's one collective (RCCL over xGMI) ----------------------------------
  * The corpus is split into contiguous global-id ranges, one per GPU (one process per GPU); each rank
  * answers the whole query batch against its shard and packs fixed-size top-k records, and ONE

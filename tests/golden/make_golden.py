@@ -414,6 +414,36 @@ def rag_score_fixtures(hq):
     out["ml"] = np.array([obj._compare_multi_level_indices(out["ml_Q"], ML[i]) for i in range(6)])
     out["ml_w3"] = obj._calculate_granularity_weights(3)
     out["ml_w5"] = obj._calculate_granularity_weights(5)
+    # spatial locality (engine.py:662-714) on enhanced images (the RAG generator's index rows appended):
+    # heights detected per image (engine.py:134-162, 604-620), float32 and float64 inputs
+    from hilbert_quantization.rag.embedding_generation.hierarchical_index_generator import (
+        HierarchicalIndexGenerator as RagGen)
+    rg = RagGen()
+    for tag, n, dt in (("s64f", 64, np.float32), ("s64d", 64, np.float64), ("s32f", 32, np.float32),
+                       ("s8d", 8, np.float64)):
+        base = rng.standard_normal((n, n)).astype(dt)
+        imgs = [base, base + rng.normal(0, 0.3, (n, n)).astype(dt), rng.standard_normal((n, n)).astype(dt),
+                -base, np.zeros((n, n), dt), base * 3.0 + 1.0]
+        short = base.copy()
+        short[n - 1, : (3 * n) // 4] = 0.0          # last data row mostly zeros: a different detected height
+        imgs.append(short)
+        enh = np.stack([np.asarray(rg.generate_multi_level_indices(im)).astype(dt) for im in imgs])
+        out[f"{tag}_enh"] = enh
+        out[f"{tag}_heights"] = np.array([obj._detect_original_embedding_height(e) for e in enh], dtype=np.int64)
+        out[f"{tag}_spatial"] = np.array([[float(obj._calculate_spatial_locality_similarity(enh[a], enh[b]))
+                                           for b in range(len(enh))] for a in range(2)])
+    tiny = rng.standard_normal((2, 5, 4))                  # ws < 2: one cosine over the block
+    out["tiny_enh"] = tiny
+    out["tiny_spatial"] = np.array([float(obj._calculate_spatial_locality_similarity(tiny[0], tiny[1]))])
+    # progressive threshold (engine.py:243-287): levels 0..4, candidate lists in arbitrary id order
+    sc = np.round(rng.uniform(0.0, 1.0, 200), 3)
+    sc[:5] = [0.6000000000000001, 0.6, 0.5, 0.3, 0.8]     # on the level thresholds (Python float sums)
+    ids = rng.permutation(1000)[:200]
+    out["thr_scores"], out["thr_ids"] = sc, ids
+    for level in range(5):
+        for cut in (200, 37, 1):
+            got = obj._apply_progressive_threshold(list(zip(ids[:cut].tolist(), sc[:cut].tolist())), level)
+            out[f"thr_l{level}_n{cut}"] = np.array(got + [-1] * (200 - len(got)), dtype=np.int64)
     return out
 
 

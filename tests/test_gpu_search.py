@@ -484,3 +484,57 @@ def test_rccl_allgather_one_rank(hq_lib):
     b = torch.arange(37, dtype=torch.uint8, device="cuda")
     assert torch.equal(comm.all_gather(b)[0], b)
     comm.close()
+
+
+def test_rag_spatial_locality_enhanced_golden(hq_lib, golden):
+    """S7 completed: _calculate_spatial_locality_similarity through _extract_original_embedding (original
+    height detected on each enhanced image: the RAG generator's index rows cut off, rag/search/engine.py:
+    134-162, 604-714) against the reference's own values, float32 AND float64 images (float64 kept in
+    float64), batched Q x N on the GPU (hq_spatial_locality) and as the pairwise drop-in."""
+    from hq_mi355x.rag import similarity as S
+    g = golden("rag_score")
+    for tag in ("s64f", "s64d", "s32f", "s8d"):
+        enh = g[f"{tag}_enh"]
+        tol = 1e-6 if enh.dtype == np.float32 else 1e-12
+        assert list(S.detect_original_embedding_heights(enh)) == list(g[f"{tag}_heights"]), tag
+        got = _np(S.spatial_locality_scores(enh[:2], enh))
+        np.testing.assert_allclose(got, g[f"{tag}_spatial"], atol=tol, err_msg=tag)
+        assert abs(S.calculate_spatial_locality_similarity(enh[0], enh[1]) - g[f"{tag}_spatial"][0, 1]) < tol
+        ex = S.extract_original_embedding(enh[0])
+        assert ex.shape == (g[f"{tag}_heights"][0], enh.shape[2]) and ex.dtype == enh.dtype
+    t = g["tiny_enh"]
+    assert abs(S.calculate_spatial_locality_similarity(t[0], t[1]) - g["tiny_spatial"][0]) < 1e-12
+
+
+def test_rag_progressive_threshold_golden(hq_lib, golden):
+    """S7 completed: _apply_progressive_threshold (rag/search/engine.py:243-287) as a device select
+    (hq_threshold_select): level thresholds 0.6 / 0.5 / 0.4 / 0.3 (Python float sums, scores placed on
+    them), caps 30 / 50 / 70 % of the list, candidate order kept; batched rows agree with the drop-in."""
+    from hq_mi355x.rag import similarity as S
+    g = golden("rag_score")
+    sc, ids = g["thr_scores"], g["thr_ids"]
+    for level in range(5):
+        for cut in (200, 37, 1):
+            got = S.apply_progressive_threshold(list(zip(ids[:cut].tolist(), sc[:cut].tolist())), level)
+            ref = g[f"thr_l{level}_n{cut}"]
+            assert got == list(ref[ref >= 0]), (level, cut)
+        rows = np.stack([sc, sc[::-1]])
+        out, cnt = S.progressive_threshold_batch(rows, level)
+        out, cnt = _np(out), _np(cnt)
+        for r in range(2):
+            want = O.rag_progressive_threshold(list(enumerate(rows[r].tolist())), level)
+            assert list(out[r][: cnt[r]]) == want and np.all(out[r][cnt[r]:] == -1)
+
+
+def test_rag_cosine_float64_kept(hq_lib):
+    """float64 embeddings are scored in float64 (no narrowing to float32): the drop-in cosine equals the
+    f64 oracle to 1e-14 on values whose float32 rounding alone would move the score by > 1e-9."""
+    from hq_mi355x.rag import similarity as S
+    rng = np.random.default_rng(3)
+    a = 1.0 + rng.standard_normal(4096) * 1e-7
+    b = 1.0 + rng.standard_normal(4096) * 1e-7
+    want = float(O.rag_cosine(a, b[None])[0])
+    assert abs(S.calculate_embedding_cosine_similarity(a, b) - want) < 1e-14
+    A = rng.standard_normal((5, 3, 64))
+    got = [S.compare_multi_level_indices(A[0], A[i]) for i in range(5)]
+    np.testing.assert_allclose(got, O.rag_multi_level_similarity(A[0], A), atol=1e-14)

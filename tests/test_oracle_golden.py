@@ -333,3 +333,23 @@ def test_reference_shaped_loops_match_oracle():
         q = C[a] + rng.normal(0, 0.01, 64)
         rid, _, _, _ = O.progressive_search(q, C, 10, 0.1, 20)
         assert HL.progressive_search(q, C, 10, 0.1, 20) == list(rid)
+
+
+def test_rag_spatial_and_threshold_oracle_golden(golden):
+    """Oracle restatement of the RAG scorer's height detection, spatial locality on enhanced images
+    (rag/search/engine.py:134-162, 604-714) and progressive threshold (:243-287) vs the reference's goldens."""
+    g = golden("rag_score")
+    for tag in ("s64f", "s64d", "s32f", "s8d"):
+        enh = g[f"{tag}_enh"]
+        assert [O.rag_detect_height(e) for e in enh] == list(g[f"{tag}_heights"])
+        for a in range(2):
+            got = [O.rag_spatial_locality_enhanced(enh[a], enh[b]) for b in range(len(enh))]
+            np.testing.assert_allclose(got, g[f"{tag}_spatial"][a], atol=1e-6 if enh.dtype == np.float32 else 1e-12)
+    t = g["tiny_enh"]
+    assert abs(O.rag_spatial_locality_enhanced(t[0], t[1]) - g["tiny_spatial"][0]) < 1e-12
+    sc, ids = g["thr_scores"], g["thr_ids"]
+    for level in range(5):
+        for cut in (200, 37, 1):
+            got = O.rag_progressive_threshold(list(zip(ids[:cut].tolist(), sc[:cut].tolist())), level)
+            ref = g[f"thr_l{level}_n{cut}"]
+            assert got == list(ref[ref >= 0]), (level, cut)
