@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--stream-steps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--option", action="append", default=[],
+                    help="name=value: select a kernel variant (hq_set_option; A/B runs only)")
     return ap.parse_args()
 
 
@@ -436,6 +438,11 @@ def main():
     cpu_par = cpu_baseline_parallel(args.dim, args.cpu_seconds / 4) if wr == (0, 1) and not args.no_cpu else None
     world, rank = dist_setup(args)
     from hq_mi355x import kernels as K
+    if args.option:
+        from hq_mi355x import _lib
+        for o in args.option:
+            name, value = o.split("=", 1)
+            _lib.set_option(name, int(value))
     from hq_mi355x.core.pipeline import quantize_batch
 
     dev = torch.device("cuda", torch.cuda.current_device())

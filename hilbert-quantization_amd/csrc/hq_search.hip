@@ -781,6 +781,7 @@ struct Scan0Args {
   int64_t chunk_len; int nchunks; int nqb;
   double* ws_score; int64_t* ws_id; unsigned long long* gtau;
   float* pool_s; int* pool_i; int* pool_n; int pool_cap;  // k_scan0f: per-query candidate pools
+  const void* qconst; // k_scan0g: per-query QConst table (k_sample_kth / k_scan_qprep)
   int expt;          // HQ_SCAN_EXPT=3: count insert-path entries, passing pairs and list merges
   unsigned long long* dbg;  // expt 3: [entries, passing pairs, list inserts]
 };
@@ -1642,6 +1643,301 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Level-0 scan, queue form (k_scan0g, default since round 3).  Same contraction as k_scan0f (split
+// f16, 12 MFMAs per 64 queries x 16 rows) and the same filter and score expressions, reorganised so
+// that the per-step vector work fits under the matrix instructions:
+//   * no per-wave lists: a pair whose score passes the query's starting threshold (the sampled bound,
+//     k_sample_kth, or the caller's threshold) is appended straight to the query's global pool, which
+//     k_pool_select reduces to the exact top K (the sample bound admits ~K' x stride pairs per query);
+//   * the per-query constants (QConst, computed once per query by k_sample_kth / k_scan_qprep) leave
+//     only the G-only pre-filter in the step: two v_max3 and one compare per 16-query block and lane;
+//   * a lane block (one query, four rows) passing the pre-filter is appended to a per-wave LDS queue
+//     (ballot + mbcnt); the queue is drained 64 entries at a time, one entry per lane: candidate
+//     statistics loaded for that entry's four rows, the division-free filter, the f32 score (the f64
+//     statistics for flagged rows) and the pool append;
+//   * candidate fragments / statistics addressed from a wave-uniform base (scalar step increments).
+// Flagged candidate rows (zero variance, f32-unsafe) are skipped by the scan and scored by
+// k_scan0_flagged from the f64 statistics (k_flag_rows lists them per call; normally none).  Flagged queries
+// (zero variance / f32-unsafe) never enter the scan: k_pool_select marks their lists unresolved and the
+// caller answers them on the dense exact path.  A pool that would overflow its capacity marks its query
+// unresolved the same way.
+// ------------------------------------------------------------------------------------------------
+struct QConst {
+  float qA, qB, qQ, k0;      // 0.6 std / m, 0.6 mean, mean of squares, 0.35 - (thl - margin)
+  float thl, gs, low, flag;  // list threshold (f32 lower bound), G* pre-filter bound, 0.1 admitted, query flags
+};
+
+// per-query constants of the scan from the query's statistics and starting threshold t0 (f64)
+__device__ __forceinline__ QConst qconst_of(const float* Sq32, int q, double t0, double inv_m, float c1f) {
+  const int64_t gq = (int64_t)(q >> 2) * 16 + (q & 3);  // SoA-per-4 statistics
+  QConst c;
+  const float sd = Sq32[gq], mn = Sq32[gq + 4], ms = Sq32[gq + 8];
+  const int fl = __float_as_int(Sq32[gq + 12]);
+  c.qA = (float)(0.6 * inv_m) * sd;
+  c.qB = 0.6f * mn;
+  c.qQ = ms;
+  c.thl = lower_f32(t0);
+  c.flag = __int_as_float(fl);
+  if (fl != 0) {  // flagged query: not scanned (dense exact path)
+    c.k0 = -__builtin_huge_valf();
+    c.gs = __builtin_huge_valf();
+    c.low = 0.0f;
+  } else {
+    c.k0 = 0.35f - (c.thl - kMarginF);
+    c.gs = gstar0(c.thl, c.qA, c.qB, c.qQ, (float)(0.35 * inv_m));
+    c.low = (0.1f >= c.thl - kMarginF) ? 1.0f : 0.0f;
+  }
+  (void)c1f;
+  return c;
+}
+
+// one thread per query: QConst from the caller's threshold alone (no sample pass)
+__global__ void k_scan_qprep(const float* __restrict__ Sq32, int Q, double thr0, double inv_m,
+                             QConst* __restrict__ qc, int* __restrict__ pool_n) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  qc[q] = qconst_of(Sq32, q, thr0, inv_m, 0.0f);
+  pool_n[q] = 0;
+}
+
+__device__ __forceinline__ float max4(const flt4 v) {
+  float t, r;
+  asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(t) : "v"(v.x), "v"(v.y), "v"(v.z));
+  asm volatile("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(t), "v"(v.w));
+  return r;
+}
+
+constexpr int kQCap = 256;  // LDS queue entries per wave (a half-step adds at most 128)
+struct QEntry {
+  flt4 g;        // G of rows row .. row + 3 for query qi
+  int qi, row;   // query within the wave, first row (absolute, multiple of 4)
+  int pad0, pad1;
+};
+
+__global__ __launch_bounds__(64) void k_scan0g(Scan0Args a) {
+  constexpr int NB = 4;
+  constexpr int QW = 16 * NB;
+  __shared__ QEntry qe[kQCap];
+  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
+  const int chunk = xcd + 8 * (slot / a.nqb);
+  const int qb = slot % a.nqb;
+  if (chunk >= a.nchunks) return;
+  const int64_t c_begin = (int64_t)chunk * a.chunk_len;
+  if (c_begin >= a.N) return;  // chunks past the corpus end (k_scan0f comment)
+  int64_t c_end = c_begin + a.chunk_len;
+  if (c_end > a.N) c_end = a.N;
+  const int q0 = qb * QW;
+  const float c1f = (float)a.c1;
+  const QConst* qc = reinterpret_cast<const QConst*>(a.qconst);
+
+  half8 qh[NB], ql[NB];
+  float gs[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int q = q0 + 16 * b + j;
+    const bool v = q < a.Q;
+    const int qq = v ? q : 0;
+    const _Float16* zr = a.Zq16 + (int64_t)qq * kZ16Row + 8 * g;
+    HQ_GUARD(zr, a.Zq16, (int64_t)a.Q * kZ16Row - 39);
+    qh[b] = *reinterpret_cast<const half8*>(zr);
+    ql[b] = *reinterpret_cast<const half8*>(zr + 32);
+    gs[b] = v ? qc[q].gs : __builtin_huge_valf();
+  }
+
+  // wave-uniform bases, per-lane constant offsets (scalar step increments)
+  const char* zb = reinterpret_cast<const char*>(a.Zc16 + c_begin * kZ16Row);
+  const int zoff = (j * kZ16Row + 8 * g) * 2;
+  struct CStep {
+    half8 f[2];
+  };
+  auto load_step = [&](CStep& c, const int64_t s) {
+    const _Float16* p = reinterpret_cast<const _Float16*>(zb + s * (int64_t)(kCS * kZ16Row * 2) + zoff);
+    HQ_GUARD(p, a.Zc16, (a.N + kPad0) * kZ16Row - 39);
+    c.f[0] = *reinterpret_cast<const half8*>(p);
+    c.f[1] = *reinterpret_cast<const half8*>(p + 32);
+  };
+  auto mfma_half = [&](const int h, const half8* f, flt4* acc) {
+    acc[0] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
+    acc[1] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[0], qh[2 * h + u], acc[u], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[0], ql[2 * h + u], acc[u], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[1], qh[2 * h + u], acc[u], 0, 0, 0);
+  };
+
+  int qn = 0;  // queue entries (wave-uniform)
+  // drain n <= 64 entries from the front of the queue, then shift the rest down
+  auto drain = [&](const int n) {
+    if (lane < n) {
+      const flt4 eg = qe[lane].g;
+      const int eqi = qe[lane].qi, erow = qe[lane].row;
+      const int q = q0 + eqi;
+      const QConst c = qc[q];
+      const float* st = a.Sc32 + (int64_t)(erow >> 2) * 16;  // the SoA group of rows row .. row + 3
+      HQ_GUARD(st, a.Sc32, pack0_rows(a.N) * 4 - 15);
+      const flt4 sd = *reinterpret_cast<const flt4*>(st);
+      const flt4 mn = *reinterpret_cast<const flt4*>(st + 4);
+      const flt4 ms = *reinterpret_cast<const flt4*>(st + 8);
+      const flt4 fl = *reinterpret_cast<const flt4*>(st + 12);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = erow + r;
+        const int f = __float_as_int(fl[r]);
+        if (row >= c_end || f != 0) continue;  // past the chunk; flagged rows: k_scan0_flagged
+        const float G = eg[r];
+        float s = -__builtin_huge_valf();
+        {
+          // division-free filter (k_scan0f filter_half), then the list score (k_scan0f insert_half)
+          const float E = fmaf(G, c1f, c.k0);
+          const float num = fmaf(G, c.qA * sd[r], c.qB * mn[r]);
+          const float d = fmaf(E, c.qQ + ms[r], num);
+          if (fmaxf(E, d) >= 0.0f) {
+            float t = num * __builtin_amdgcn_rcpf(c.qQ + ms[r]);
+            t = t > 0.0f ? t : 0.0f;
+            s = fmaf(G, c1f, 0.35f) + t;
+            s = s < 1.0f ? s : 1.0f;
+            s = s > 0.0f ? s : 0.0f;
+          }
+        }
+        if (s >= c.thl) {
+          const int slot = atomicAdd(a.pool_n + q, 1);
+          if (slot < a.pool_cap) {
+            a.pool_s[(int64_t)q * a.pool_cap + slot] = s;
+            a.pool_i[(int64_t)q * a.pool_cap + slot] = row;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // shift the remaining entries down (all reads of a 64-entry block before its writes)
+    for (int b0 = n; b0 < qn; b0 += 64) {
+      const bool mv = b0 + lane < qn;
+      flt4 tg = {0.0f, 0.0f, 0.0f, 0.0f};
+      int tq = 0, tr = 0;
+      if (mv) {
+        tg = qe[b0 + lane].g;
+        tq = qe[b0 + lane].qi;
+        tr = qe[b0 + lane].row;
+      }
+      __syncthreads();
+      if (mv) {
+        qe[b0 - n + lane].g = tg;
+        qe[b0 - n + lane].qi = tq;
+        qe[b0 - n + lane].row = tr;
+      }
+      __syncthreads();
+    }
+    qn -= n;
+  };
+  // enqueue the lane blocks of one half whose pre-filter passed (masks m0, m1: blocks 2h, 2h + 1)
+  auto enqueue = [&](const int h, const flt4* acc, const unsigned long long m0, const unsigned long long m1,
+                     const int64_t cs) {
+    const int c0 = __popcll(m0);
+    const unsigned lo0 = __builtin_amdgcn_mbcnt_lo((unsigned)m0, 0u), lo1 = __builtin_amdgcn_mbcnt_lo((unsigned)m1, 0u);
+    if ((m0 >> lane) & 1ull) {
+      const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m0 >> 32), lo0);
+      qe[pos].g = acc[0];
+      qe[pos].qi = 32 * h + j;
+      qe[pos].row = (int)(cs + 4 * g);
+    }
+    if ((m1 >> lane) & 1ull) {
+      const int pos = qn + c0 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m1 >> 32), lo1);
+      qe[pos].g = acc[1];
+      qe[pos].qi = 32 * h + 16 + j;
+      qe[pos].row = (int)(cs + 4 * g);
+    }
+    qn += c0 + __popcll(m1);
+  };
+  // pre-filter of one half: max of the lane's four rows per block against G* (the compare's lane mask
+  // is the ballot); blocks holding a flagged row (f32-unsafe; zero-variance for a query that admits 0.1)
+  // are queued regardless
+  auto half_step = [&](const int h, const flt4* acc, const int64_t cs) {
+    const unsigned long long m0 = __builtin_amdgcn_ballot_w64(max4(acc[0]) >= gs[2 * h]);
+    const unsigned long long m1 = __builtin_amdgcn_ballot_w64(max4(acc[1]) >= gs[2 * h + 1]);
+    if (m0 | m1) {
+      enqueue(h, acc, m0, m1, cs);
+      while (qn >= 64) drain(64);  // keeps qn < 64 before each half-step: the queue never exceeds 191
+    }
+  };
+
+  CStep cA, cB, cC;
+  load_step(cA, 0);
+  load_step(cB, 1);
+  flt4 acc0[2], acc1[2];
+  mfma_half(0, cA.f, acc0);
+  const int64_t nsteps = (c_end - c_begin + kCS - 1) / kCS;
+  auto body = [&](const int64_t s, const CStep& cur, const CStep& nxt, CStep& nn) {
+    load_step(nn, s + 2);  // padded copies: rows past the chunk are harmless (masked in the drain)
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch two steps ahead (the scheduler sinks it otherwise)
+    const int64_t cs = c_begin + s * kCS;
+    mfma_half(1, cur.f, acc1);
+    half_step(0, acc0, cs);
+    mfma_half(0, nxt.f, acc0);
+    half_step(1, acc1, cs);
+  };
+  int64_t s = 0;
+  for (; s + 2 < nsteps; s += 3) {
+    body(s, cA, cB, cC);
+    body(s + 1, cB, cC, cA);
+    body(s + 2, cC, cA, cB);
+  }
+  if (s < nsteps) body(s, cA, cB, cC);
+  if (s + 1 < nsteps) body(s + 1, cB, cC, cA);
+  while (qn > 0) drain(qn < 64 ? qn : 64);
+}
+
+// rows of the split copies with a zero-variance / f32-unsafe flag (S32 flag word bits 1, 2): compacted
+// into list[*count] (order irrelevant: the pools are selected by (score, row))
+__global__ __launch_bounds__(256) void k_flag_rows(const float* __restrict__ S32, int64_t N, int* __restrict__ list,
+                                                   int* __restrict__ count) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < N; r += (int64_t)gridDim.x * blockDim.x) {
+    const int f = __float_as_int(S32[(r >> 2) * 16 + 12 + (r & 3)]);
+    if (f & 3) list[atomicAdd(count, 1)] = (int)r;
+  }
+}
+
+// the flagged rows against every scanned query (lane = query): the f64 statistics as k_scan0f's insert
+// path (const0 for zero variance, approx0 with G from the split copies otherwise), appended to the pools
+// when the score reaches the query's list threshold
+__global__ __launch_bounds__(64) void k_scan0_flagged(Scan0Args a, const int* __restrict__ list,
+                                                      const int* __restrict__ count) {
+  const QConst* qc = reinterpret_cast<const QConst*>(a.qconst);
+  const int n = *count;
+  const int q = blockIdx.y * 64 + threadIdx.x;
+  if (q >= a.Q || n == 0) return;
+  const QConst c = qc[q];
+  if (__float_as_int(c.flag) != 0) return;  // flagged query: dense exact path
+  const double* sq = a.Sq + (int64_t)q * a.nseg * 4;
+  const _Float16* zq = a.Zq16 + (int64_t)q * kZ16Row;
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const int row = list[i];
+    const double* sc = a.Sc + (int64_t)row * a.nseg * 4;
+    const double qm = sq[0], qs = sq[1], qq = sq[2], cm = sc[0], csd = sc[1], cq = sc[2];
+    double v;
+    if (qs == 0.0 || csd == 0.0) {
+      v = const0(qs == 0.0, csd == 0.0, qm, cm, (aux_bits(sq) & aux_bits(sc) & kAuxF32) != 0);
+    } else {
+      const _Float16* zc = a.Zc16 + (int64_t)row * kZ16Row;
+      double G = 0.0;
+      for (int k = 0; k < 32; ++k)
+        G = fma((double)zq[k] + (double)zq[32 + k], (double)zc[k] + (double)zc[32 + k], G);
+      v = approx0(G, a.c1, (0.6 * a.inv_m) * qs, 0.6 * qm, qq, csd, cm, cq);
+    }
+    const float sv = (float)v;
+    if (sv >= c.thl) {
+      const int slot = atomicAdd(a.pool_n + q, 1);
+      if (slot < a.pool_cap) {
+        a.pool_s[(int64_t)q * a.pool_cap + slot] = sv;
+        a.pool_i[(int64_t)q * a.pool_cap + slot] = row;
+      }
+    }
+  }
+}
+
 // Exact top-K of each query's pool (one wave per query): (score desc, row asc).  The K-th largest
 // score v is found by bisection on the f32 bit pattern (scores >= 0), ties at v by bisection on the
 // row, then the K selected entries are rank-sorted.  Pools of up to 64*kPoolReg entries stay in
@@ -1656,9 +1952,18 @@ __global__ __launch_bounds__(64) void k_pool_select(const float* __restrict__ po
                                                     const int* __restrict__ pool_n, int cap, int Q, int K,
                                                     int64_t id_base, double* __restrict__ out_score,
                                                     int64_t* __restrict__ out_id, const double* __restrict__ th0,
-                                                    double thr0) {
+                                                    double thr0, const QConst* __restrict__ qc) {
   const int lane = threadIdx.x;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    // k_scan0g: a flagged query (not scanned) or an overflowing pool -> every slot +inf / -1, which the
+    // exact re-rank reads as unresolved (the caller's dense exact path answers the query)
+    if (qc && (__float_as_int(qc[q].flag) != 0 || pool_n[q] > cap)) {
+      for (int x = lane; x < K; x += 64) {
+        out_score[(int64_t)q * K + x] = __builtin_huge_val();
+        out_id[(int64_t)q * K + x] = -1;
+      }
+      continue;
+    }
 #ifdef HQ_DIAG
     const int T = (int)diag_bound(pool_n[q], (int64_t)cap + 1, __LINE__);
 #else
@@ -2066,7 +2371,8 @@ constexpr int kKthReg = 32;  // pool entries per lane: 4 * 256 chunks * kTopT / 
 // histogram, so no memset runs before the scan).
 __global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top, int ns, int Q, int K, double margin,
                                                    double* __restrict__ th0, unsigned long long* __restrict__ gtau,
-                                                   int* __restrict__ pool_n) {
+                                                   int* __restrict__ pool_n, const float* __restrict__ Sq32, double thr0,
+                                                   double inv_m, QConst* __restrict__ qc) {
   const int lane = threadIdx.x;
   const int P = ns * kTopT;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
@@ -2097,7 +2403,10 @@ __global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top
       }
       t = (double)__uint_as_float(lo - 1u) - margin;
     }
-    if (lane == 0) th0[q] = t;
+    if (lane == 0) {
+      th0[q] = t;
+      if (qc) qc[q] = qconst_of(Sq32, q, t > thr0 ? t : thr0, inv_m, 0.0f);
+    }
   }
 }
 
@@ -2904,7 +3213,7 @@ static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
   if (nchunks2 > nchunks) nchunks = nchunks2;
   // lists / pools + global thresholds + sample histogram + starting thresholds + pool counts + sample tops
   return (size_t)nchunks * Q * k * 16 + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 8 + (size_t)Q * 4 +
-         sample_top_bytes(Q, N) + 256;
+         sample_top_bytes(Q, N) + (size_t)Q * sizeof(QConst) + (size_t)N * 4 + 1024;
 }
 
 #ifdef HQ_DIAG
@@ -3047,6 +3356,14 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   if (sample_kth <= 0 || sample_kth > k) sample_kth = k;
   float* top = reinterpret_cast<float*>(ws + lists + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 4 +
                                         (size_t)Q * 8);
+  // k_scan0g (default; option scan_variant 1 = the list-based k_scan0f): per-query constants after the
+  // sample tops, 256-B aligned
+  const bool queue_scan = f32 && opt(OPT_SCAN_VARIANT, 0) != 1;
+  const size_t qc_off = ((size_t)(reinterpret_cast<uint8_t*>(top) - ws) + sample_top_bytes(Q, N) + 255) & ~(size_t)255;
+  QConst* qc = queue_scan ? reinterpret_cast<QConst*>(ws + qc_off) : nullptr;
+  b.qconst = qc;
+  int* flag_n = reinterpret_cast<int*>(ws + ((qc_off + (size_t)Q * sizeof(QConst) + 255) & ~(size_t)255));
+  int* flag_list = flag_n + 64;
   // (the top-T sample has no histogram and k_sample_kth clears gtau and pool_n per query)
   if (!top_sample)
     HQ_CHECK_HIP(hipMemsetAsync(b.gtau, 0, (size_t)Q * 8 + (sample ? (size_t)Q * kBins * 4 : 0) + (f32 ? (size_t)Q * 4 : 0),
@@ -3067,7 +3384,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     HQ_CHECK_LAUNCH();
     const int mg = Q < 8192 ? Q : 8192;
     hipLaunchKernelGGL(k_sample_kth, dim3(mg), dim3(64), 0, s, (const float*)top, 4 * sa.nchunks, Q, sample_kth,
-                       (double)kMarginF, th0, b.gtau, b.pool_n);
+                       (double)kMarginF, th0, b.gtau, b.pool_n, Sq32, b.thr0, b.inv_m, qc);
     HQ_CHECK_LAUNCH();
     b.th0 = th0;
   }
@@ -3088,17 +3405,39 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     HQ_CHECK_LAUNCH();
     b.th0 = th0;
   }
-  rc = f32 ? scan0_dispatch<true>(ks, b, nullptr, s) : scan0_dispatch<false>(ks, b, nullptr, s);
 #else
   (void)hist;
-  rc = launch_scan0f(b, s);
+  rc = HQ_OK;
 #endif
+  if (queue_scan) {
+    if (!top_sample) {  // no sample pass: the constants from the caller's threshold (and pool counts cleared)
+      hipLaunchKernelGGL(k_scan_qprep, dim3((Q + 255) / 256), dim3(256), 0, s, Sq32, Q, b.thr0, b.inv_m, qc, b.pool_n);
+      HQ_CHECK_LAUNCH();
+    }
+    HQ_CHECK_HIP(hipMemsetAsync(flag_n, 0, sizeof(int), s));
+    const int64_t fb = (N + 255) / 256;
+    hipLaunchKernelGGL(k_flag_rows, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, s, Sc32, N, flag_list,
+                       flag_n);
+    HQ_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_scan0g, dim3(b.nqb * b.nchunks), dim3(64), 0, s, b);
+    HQ_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_scan0_flagged, dim3(64, (Q + 63) / 64), dim3(64), 0, s, b, (const int*)flag_list,
+                       (const int*)flag_n);
+    HQ_CHECK_LAUNCH();
+  } else {
+#ifdef HQ_DIAG
+    rc = f32 ? scan0_dispatch<true>(ks, b, nullptr, s) : scan0_dispatch<false>(ks, b, nullptr, s);
+#else
+    rc = launch_scan0f(b, s);
+#endif
+  }
   if (rc) return rc;
   if (f32) {
     const int mg = Q < 8192 ? Q : 8192;
     hipLaunchKernelGGL(k_pool_select, dim3(mg), dim3(64), 0, s, (const float*)b.pool_s, (const int*)b.pool_i,
                        (const int*)b.pool_n, b.pool_cap, Q, k, id_base, out_score, out_id,
-                       top_sample && sample_kth < k ? (const double*)th0 : (const double*)nullptr, b.thr0);
+                       top_sample && sample_kth < k ? (const double*)th0 : (const double*)nullptr, b.thr0,
+                       (const QConst*)qc);
     HQ_CHECK_LAUNCH();
   }
 #ifdef HQ_DIAG

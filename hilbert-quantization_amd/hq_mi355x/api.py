@@ -143,6 +143,18 @@ class HilbertQuantizer:
         except Exception as e:
             raise ReconstructionError(f"Unexpected error during reconstruction: {e}") from e
 
+    def reconstruct_many(self, quantized_models: List[QuantizedModel], validate: bool = True) -> List[np.ndarray]:
+        """reconstruct() for many models: host JPEG decode on threads, one de-normalise and one inverse
+        Hilbert gather per frame shape (core.pipeline.reconstruct_batch); same arrays and errors."""
+        from .core.pipeline import reconstruct_batch
+        try:
+            out = reconstruct_batch(quantized_models, self.quantization_pipeline.compressor)
+            return [o if o is not None else self.reconstruct(m, validate) for o, m in zip(out, quantized_models)]
+        except (ReconstructionError, ValidationError):
+            raise
+        except Exception as e:
+            raise ReconstructionError(f"Unexpected error during reconstruction: {e}") from e
+
     def search(self, query_parameters, candidate_models: Optional[List[QuantizedModel]] = None,
                max_results: Optional[int] = None, similarity_threshold: Optional[float] = None) -> List[SearchResult]:
         try:
@@ -332,6 +344,10 @@ class BatchQuantizer:
         for (i, _), res in zip(done, found):
             results[i] = [r for r in res if r.similarity_score >= thr]
         return results
+
+    def reconstruct_batch(self, quantized_models: List[QuantizedModel]) -> List[np.ndarray]:
+        """Batched reconstruct (HilbertQuantizer.reconstruct_many)."""
+        return self.quantizer.reconstruct_many(quantized_models)
 
     def quantize_device(self, parameters, index_space_size: Optional[int] = None):
         """f32 [N, d] -> (frames u8 [N, n+1, n], indices f64 [N, L], minmax f32 [N, 2]) on the GPU."""

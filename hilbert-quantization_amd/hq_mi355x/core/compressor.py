@@ -17,6 +17,7 @@ import numpy as np
 from .. import kernels as K
 from .._dev import to_dev, to_np
 from ..exceptions import CompressionError
+from .._compat import bases as _bases
 
 
 def encode_jpeg(u8: np.ndarray, quality: float) -> bytes:
@@ -29,7 +30,21 @@ def encode_jpeg(u8: np.ndarray, quality: float) -> bytes:
     return buf.getvalue()
 
 
-class MPEGAICompressorImpl:
+def check_payload(compressed_data) -> None:
+    """core/compressor.py:121-124 argument checks of decompress."""
+    if not isinstance(compressed_data, bytes):
+        raise ValueError("Compressed data must be bytes")
+    if len(compressed_data) == 0:
+        raise ValueError("Compressed data cannot be empty")
+
+
+def decode_jpeg(compressed_data: bytes) -> np.ndarray:
+    """Host JPEG decode of one payload -> uint8 frame (the reference's np.array(Image.open(...)) values)."""
+    from PIL import Image
+    return np.array(Image.open(io.BytesIO(compressed_data)), dtype=np.uint8)
+
+
+class MPEGAICompressorImpl(*_bases("interfaces", "MPEGAICompressor")):
     def __init__(self, config: Optional[object] = None):
         self.config = config
         self._last_compression_metrics = None
@@ -47,10 +62,7 @@ class MPEGAICompressorImpl:
 
     def _denormalize_from_compression(self, image):
         u8 = np.asarray(image, dtype=np.uint8)
-        if not hasattr(self, "_norm_min") or not hasattr(self, "_norm_max"):
-            mm = np.array([0.0, 1.0], dtype=np.float32)   # u8 / 255 * 1 + 0 == u8 / 255 exactly
-        else:
-            mm = np.array([self._norm_min, self._norm_max], dtype=np.float32)
+        mm = self._state_minmax()  # no state: (0, 1), and u8 / 255 * 1 + 0 == u8 / 255 exactly
         return to_np(K.dequantize_u8(to_dev(u8), to_dev(mm), CompressionError))
 
     def compress(self, image, quality: float) -> bytes:
@@ -67,9 +79,19 @@ class MPEGAICompressorImpl:
             raise RuntimeError(f"Failed to compress image: {e}")
 
     def decompress(self, compressed_data: bytes):
-        from PIL import Image
-        u8 = np.array(Image.open(io.BytesIO(compressed_data)))
-        return self._denormalize_from_compression(u8)
+        """core/compressor.py:106-148: host JPEG decode, then the GPU de-normalise with this instance's
+        last (min, max)."""
+        check_payload(compressed_data)
+        try:
+            return self._denormalize_from_compression(decode_jpeg(compressed_data))
+        except Exception as e:
+            raise RuntimeError(f"Failed to decompress image: {e}")
+
+    def _state_minmax(self) -> np.ndarray:
+        """(min, max) the de-normalise uses: the instance's last non-constant frame, else (0, 1) = u8 / 255."""
+        if not hasattr(self, "_norm_min") or not hasattr(self, "_norm_max"):
+            return np.array([0.0, 1.0], dtype=np.float32)
+        return np.array([self._norm_min, self._norm_max], dtype=np.float32)
 
     def estimate_compression_ratio(self, original_size: int, compressed_size: int) -> float:
         if compressed_size <= 0:

@@ -10,6 +10,7 @@ import math
 from typing import List, Tuple
 
 from ..models import PaddingConfig
+from .._compat import bases as _bases
 
 VALID_DIMENSIONS = [4, 16, 64, 256, 1024, 4096, 16384]
 MIN_EFFICIENCY_RATIO = 0.5
@@ -32,7 +33,7 @@ def _optimal_side(count: int) -> int:
     return int(math.isqrt(_power_of_4_at_least(count)))
 
 
-class PowerOf4DimensionCalculator:
+class PowerOf4DimensionCalculator(*_bases("interfaces", "DimensionCalculator")):
     def __init__(self, min_efficiency_ratio: float = MIN_EFFICIENCY_RATIO):
         self.min_efficiency_ratio = min_efficiency_ratio
 

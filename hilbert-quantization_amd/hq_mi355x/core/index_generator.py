@@ -14,6 +14,7 @@ import numpy as np
 
 from .. import kernels as K
 from .._dev import is_tensor, to_dev, to_np
+from .._compat import bases as _bases
 
 
 class QuantizationConfig:
@@ -49,7 +50,7 @@ def level_allocation(total_space: int) -> List[Tuple[int, int]]:
     return out
 
 
-class HierarchicalIndexGeneratorImpl:
+class HierarchicalIndexGeneratorImpl(*_bases("interfaces", "HierarchicalIndexGenerator")):
     def __init__(self, config: Optional[object] = None):
         self.config = config or QuantizationConfig()
         if getattr(self.config, "use_streaming_optimization", False):

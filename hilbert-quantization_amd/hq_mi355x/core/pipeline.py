@@ -114,3 +114,53 @@ class QuantizationPipeline:
             return out
         except Exception as e:
             raise HilbertQuantizationError(f"Failed to reconstruct parameters: {e}")
+
+
+def reconstruct_batch(models, compressor: MPEGAICompressorImpl, workers: int = 16):
+    """Batched QuantizationPipeline.reconstruct_parameters (core/pipeline.py:183-235) for
+    many QuantizedModels: the JPEG payloads decode on a host thread pool (the codec), then per frame shape
+    ONE de-normalise launch (hq_dequantize_u8, with the compressor instance's last (min, max) for every
+    model, exactly as the per-model path reads that shared state) and ONE inverse-Hilbert gather
+    (hq_map_from_2d) of the image rows above the index row; each model's vector is truncated to its
+    parameter count.  Returns float32 NumPy vectors in model order; the errors are the per-model path's
+    (HilbertQuantizationError wrapping the decompress / shape failure of the first failing model)."""
+    import concurrent.futures as cf
+    from .compressor import check_payload, decode_jpeg
+    t = torch()
+    models = list(models)
+    out = [None] * len(models)
+
+    def decode(i):
+        m = models[i]
+        try:
+            check_payload(m.compressed_data)
+            try:
+                return decode_jpeg(m.compressed_data)
+            except Exception as e:
+                raise RuntimeError(f"Failed to decompress image: {e}")
+        except Exception as e:
+            raise HilbertQuantizationError(f"Failed to reconstruct parameters: {e}")
+
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(workers, len(models) or 1))) as pool:
+        frames = list(pool.map(decode, range(len(models))))
+    mm = compressor._state_minmax()
+    groups = {}
+    for i, f in enumerate(frames):
+        groups.setdefault(f.shape, []).append(i)
+    for shape, members in groups.items():
+        u8 = to_dev(np.stack([frames[i] for i in members]))
+        enh = K.dequantize_u8(u8, to_dev(np.repeat(mm[None], len(members), 0)), HilbertQuantizationError)
+        r, c = shape
+        if r < 2 or r - 1 != c or (c & (c - 1)) != 0:  # not an (n + 1) x n enhanced frame: per-model path
+            for i in members:
+                out[i] = None
+            continue
+        flat = to_np(K.map_from_2d(enh[:, :-1, :].contiguous(), None, HilbertQuantizationError))
+        for k, i in enumerate(members):
+            v = flat[k, : models[i].parameter_count]
+            if len(v) != models[i].parameter_count:
+                raise HilbertQuantizationError(
+                    f"Failed to reconstruct parameters: Reconstructed parameter count {len(v)} doesn't match "
+                    f"original {models[i].parameter_count}")
+            out[i] = v.copy()
+    return out

@@ -20,6 +20,7 @@ import numpy as np
 from .. import kernels as K
 from .._dev import is_tensor, to_dev, to_np, torch
 from ..models import QuantizedModel, SearchResult
+from .._compat import bases as _bases
 
 MAX_FUSED_K = 64
 
@@ -368,7 +369,7 @@ class IndexCorpus:
         return ids, sc
 
 
-class ProgressiveSimilaritySearchEngine:
+class ProgressiveSimilaritySearchEngine(*_bases("interfaces", "SimilaritySearchEngine")):
     """Drop-in for core/search_engine.py:23 (interfaces.py:191-225 SimilaritySearchEngine)."""
 
     def __init__(self, similarity_threshold: float = 0.1, max_candidates_per_level: int = 100):

@@ -71,3 +71,13 @@ class QuantizedModel:
             raise ValueError("Original dimensions must be a 2-tuple")
         if self.hierarchical_indices.ndim != 1:
             raise ValueError("Hierarchical indices must be 1-dimensional")
+
+
+# With the reference package importable, the data model IS the reference's (same fields and validation):
+# results and models then carry the reference's own dataclasses (_compat).
+from ._compat import ref_class as _ref_class  # noqa: E402
+
+for _name in ("ModelMetadata", "PaddingConfig", "SearchResult", "QuantizedModel"):
+    _cls = _ref_class("models", _name)
+    if _cls is not None:
+        globals()[_name] = _cls

@@ -351,10 +351,11 @@ def _threshold_rounding_fixtures(eng, models_of, pools, Q, N):
     (progressive, `>=`, core/search_engine.py:284-292) and below (the video engine's level-0 frame scan,
     `>`, core/video_search.py:236-264) round to s in float32, so the reference keeps / drops s where a
     float64 comparison would not.  Pools: float32 and mixed float32 / float64 rows, each with ("full") and
-    without ("safe": the scan path) the float32-unsafe rows 9 and 10."""
+    without ("safe": the scan path) the float32-unsafe rows 3 (all zero), 9 and 10.  Thresholds are Python floats (as a caller passes them;
+    a numpy float64 threshold would compare in float64)."""
     from hilbert_quantization.core.search_engine import ProgressiveSimilaritySearchEngine
     out = {}
-    keep = [b for b in range(N) if b not in (9, 10)]
+    keep = [b for b in range(N) if b not in (3, 9, 10)]
     for ptag, rows_all in pools.items():
         for sub, idxs in (("full", list(range(N))), ("safe", keep)):
             rows = [rows_all[b] for b in idxs]
@@ -374,13 +375,13 @@ def _threshold_rounding_fixtures(eng, models_of, pools, Q, N):
                     assert np.float32(t_ge[a]) == s and np.float32(t_gt[a]) == s
                 else:
                     t_ge[a] = t_gt[a] = 0.1
-                e2 = ProgressiveSimilaritySearchEngine(similarity_threshold=t_ge[a], max_candidates_per_level=20)
+                e2 = ProgressiveSimilaritySearchEngine(similarity_threshold=float(t_ge[a]), max_candidates_per_level=20)
                 for j, x in enumerate(e2.progressive_search(Q[a], models, K)):
                     pg_ids[a, j] = int(x.model.model_id[1:])
                     pg_sc[a, j] = float(x.similarity_score)
                 # VideoEnhancedSearchEngine._hierarchical_search (video_search.py:236-264) over the pool's
                 # index vectors: level-0 similarity > threshold, stable sort desc, top K
-                hits = [(v, b) for b, v in enumerate(s0) if v > t_gt[a]]
+                hits = [(v, b) for b, v in enumerate(s0) if v > float(t_gt[a])]
                 hits.sort(key=lambda h: h[0], reverse=True)
                 for j, (v, b) in enumerate(hits[:K]):
                     fr_ids[a, j] = b
@@ -505,6 +506,94 @@ def precomputed_fixtures(hq):
     return out
 
 
+def store_fixtures(hq):
+    """Storage metadata written by the reference's own savers, kept as the JSON text
+    they produced (data), plus the reference's own reading of it:
+    * core/video_storage.py:579-631 `_save_video_metadata` (+ `_save_global_index`) for three videos of 40
+      frames (duplicates across videos), read back by `_load_existing_index` (:633-691); the level-0
+      similarity of every (query, frame) pair by the reference's compare_indices_at_level, keyed by model
+      id (the visiting order is the directory's glob order, so the ranking is rebuilt where the files lie);
+    * rag/video_storage/dual_storage.py:86-121 `_save_metadata` for 12 frames, read back by
+      `_load_existing_metadata` (:51-84)."""
+    import tempfile
+    from pathlib import Path
+    from hilbert_quantization.core import video_storage as VS
+    from hilbert_quantization.core.search_engine import ProgressiveSimilaritySearchEngine
+    from hilbert_quantization.models import ModelMetadata
+    rng = np.random.default_rng(6)
+    C = rng.standard_normal((3 * 40, 64)).cumsum(1) * 0.1
+    C[45] = C[3]
+    C[90] = C[3]
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        st = VS.VideoModelStorage.__new__(VS.VideoModelStorage)
+        st.storage_dir = Path(d)
+        st._global_index_path = Path(d) / "video_index.json"
+        st._video_index, st._model_to_video_map = {}, {}
+        st._video_file_counter, st.max_frames_per_video, st.frame_rate, st.video_codec = 3, 1000, 30.0, "mp4v"
+        for v in range(3):
+            frames = []
+            for i in range(40):
+                md = ModelMetadata(model_name=f"m{40 * v + i}", original_size_bytes=6144, compressed_size_bytes=900,
+                                   compression_ratio=6144 / 900, quantization_timestamp="2025-09-05 12:00:00",
+                                   model_architecture="mlp" if i % 2 else None, additional_info={"layer": i})
+                frames.append(VS.VideoFrameMetadata(
+                    frame_index=i, model_id=f"m{40 * v + i}", original_parameter_count=1536, compression_quality=0.8,
+                    hierarchical_indices=C[40 * v + i], model_metadata=md, frame_timestamp=1000.0 + i,
+                    similarity_features=rng.standard_normal(4) if i % 7 == 0 else None))
+            vm = VS.VideoStorageMetadata(video_path=str(Path(d) / f"video_{v}.mp4"), total_frames=40, frame_rate=30.0,
+                                         video_codec="mp4v", frame_dimensions=(65, 64),
+                                         creation_timestamp="2025-09-05 12:00:00", total_models_stored=40,
+                                         average_compression_ratio=6.8, frame_metadata=frames)
+            st._video_index[vm.video_path] = vm
+            st._save_video_metadata(vm)
+        names = sorted(p.name for p in Path(d).glob("*.json"))
+        out["video_json_names"] = np.array(names)
+        out["video_json_texts"] = np.array([(Path(d) / n).read_text().replace(d, "@STORE@") for n in names])
+        st2 = VS.VideoModelStorage.__new__(VS.VideoModelStorage)
+        st2.storage_dir, st2._video_index, st2._model_to_video_map = Path(d), {}, {}
+        st2._load_existing_index()
+        loaded = {fm.model_id: fm for vm in st2._video_index.values() for fm in vm.frame_metadata}
+        ids = sorted(loaded, key=lambda s: int(s[1:]))
+        out["video_loaded_ids"] = np.array(ids)
+        out["video_loaded_idx"] = np.stack([np.asarray(loaded[m].hierarchical_indices) for m in ids])
+        out["video_loaded_map"] = np.array([[int(st2._model_to_video_map[m][0].rsplit("video_", 1)[1][0]),
+                                             st2._model_to_video_map[m][1]] for m in ids])
+        eng = ProgressiveSimilaritySearchEngine()
+        Q = np.concatenate([C[[3, 50, 100]], C[[7, 60]] + rng.normal(0, 0.05, (2, 64))])
+        out["video_queries"] = Q
+        out["video_sims"] = np.array([[float(eng.compare_indices_at_level(q, loaded[m].hierarchical_indices, 0))
+                                       for m in ids] for q in Q])
+    # RAG dual storage
+    from hilbert_quantization.rag.video_storage import dual_storage as DS
+    from hilbert_quantization.rag.models import DocumentChunk, VideoFrameMetadata as RVF
+    with tempfile.TemporaryDirectory() as d:
+        ds = DS.DualVideoStorageImpl.__new__(DS.DualVideoStorageImpl)
+        ds.metadata_dir = d
+        ds.current_video_index, ds.current_frame_count = 1, 12
+        ds.frame_metadata = []
+        for i in range(12):
+            ch = DocumentChunk(content=f"chunk {i} text " * (i + 1), ipfs_hash=f"Qm{i:044d}", source_path=f"doc{i % 3}.txt",
+                               start_position=100 * i, end_position=100 * i + 50 + i, chunk_sequence=i,
+                               creation_timestamp="2025-09-05T12:00:00", chunk_size=50 + i)
+            ds.frame_metadata.append(RVF(frame_index=i, chunk_id=f"c{i}", ipfs_hash=ch.ipfs_hash,
+                                         source_document=ch.source_path, compression_quality=0.8,
+                                         hierarchical_indices=[], embedding_model="all-MiniLM-L6-v2",
+                                         frame_timestamp=2000.0 + i, chunk_metadata=ch))
+        ds._save_metadata()
+        text = Path(d, "dual_video_metadata.json").read_text()
+        out["dual_json_text"] = np.array(text)
+        ds2 = DS.DualVideoStorageImpl.__new__(DS.DualVideoStorageImpl)
+        ds2.metadata_dir, ds2.current_video_index, ds2.current_frame_count, ds2.frame_metadata = d, 0, 0, []
+        ds2._load_existing_metadata()
+        out["dual_state"] = np.array([ds2.current_video_index, ds2.current_frame_count])
+        out["dual_loaded"] = np.array([[str(f.frame_index), f.chunk_id, f.ipfs_hash, f.source_document,
+                                        repr(f.compression_quality), f.embedding_model, repr(f.frame_timestamp),
+                                        f.chunk_metadata.content, str(f.chunk_metadata.chunk_size)]
+                                       for f in ds2.frame_metadata])
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -514,7 +603,7 @@ def main():
     only = set(filter(None, a.only.split(",")))
     for name, fn in [("mapper", mapper_fixtures), ("index", index_fixtures), ("quant", quant_fixtures),
                      ("search", search_fixtures), ("search_f32", search_f32_fixtures),
-                     ("rag_score", rag_score_fixtures),
+                     ("rag_score", rag_score_fixtures), ("stores", store_fixtures),
                      ("precomputed", precomputed_fixtures)]:
         if only and name not in only:
             continue

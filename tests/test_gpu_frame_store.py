@@ -54,3 +54,77 @@ def test_frame_store_search_vs_oracle(hq_lib, tmp_path):
         pos, sc = O.hierarchical_frame_search(q, Cv, 10, 0.1)
         assert [fm.model_id for fm, _ in res] == [order[p] for p in pos]
         assert [s for _, s in res] == list(sc)
+
+
+def test_frame_store_reference_written_metadata(hq_lib, tmp_path, golden):
+    """The per-video JSON files written by the reference's own _save_video_metadata / _save_global_index
+    (core/video_storage.py:579-631, tests/golden/make_golden.py `stores`), laid out in a directory: the
+    loader reads the same frames, index vectors (bit-exact) and model -> (video, frame) map as the
+    reference's _load_existing_index did, and the level-0 frame search ranks by the reference's own
+    similarities in the directory's glob (visiting) order, ties included (duplicate rows across videos)."""
+    from hq_mi355x.core.frame_store import FrameStoreCorpus
+    g = golden("stores")
+    for name, text in zip(g["video_json_names"], g["video_json_texts"]):
+        (tmp_path / str(name)).write_text(str(text).replace("@STORE@", str(tmp_path)))
+    store = FrameStoreCorpus.from_storage_dir(tmp_path)
+    got = {fm.model_id: (vp, fm) for vp, fm in store.frames}
+    ids = list(g["video_loaded_ids"])
+    assert sorted(got, key=lambda s: int(s[1:])) == ids
+    for k, m in enumerate(ids):
+        vp, fm = got[m]
+        assert fm.hierarchical_indices.tobytes() == g["video_loaded_idx"][k].tobytes()
+        assert int(vp.rsplit("video_", 1)[1][0]) == g["video_loaded_map"][k][0] and fm.frame_index == g["video_loaded_map"][k][1]
+    visit = [fm.model_id for _, fm in store.frames]          # glob order of this directory
+    col = {m: i for i, m in enumerate(ids)}
+    Q = g["video_queries"]
+    res = store.hierarchical_search(Q, 10, 0.1)
+    for a in range(len(Q)):
+        sims = [g["video_sims"][a][col[m]] for m in visit]
+        hits = sorted([(s, m) for s, m in zip(sims, visit) if s > 0.1], key=lambda h: h[0], reverse=True)[:10]
+        assert [fm.model_id for fm, _ in res[a]] == [m for _, m in hits], a
+        np.testing.assert_array_equal([s for _, s in res[a]], [s for s, _ in hits])
+
+
+def test_rag_dual_storage_loader(hq_lib, tmp_path, golden):
+    """RAG dual storage: dual_video_metadata.json written by the reference's own
+    _save_metadata (rag/video_storage/dual_storage.py:86-121) is read back exactly as its
+    _load_existing_metadata does (counters, frame and chunk fields, empty index lists); a broken file
+    keeps the reference's warning-and-continue behaviour; the embedding frames, resident with that
+    metadata, rank query frames by the RAG scorer (spatial locality and original-embedding cosine)
+    like the oracle."""
+    from hq_mi355x.rag.dual_storage import DualStorageCorpus, load_dual_storage_metadata
+    g = golden("stores")
+    (tmp_path / "metadata").mkdir()
+    (tmp_path / "metadata" / "dual_video_metadata.json").write_text(str(g["dual_json_text"]))
+    st = load_dual_storage_metadata(str(tmp_path))
+    assert [st.current_video_index, st.current_frame_count] == list(g["dual_state"])
+    got = [[str(f.frame_index), f.chunk_id, f.ipfs_hash, f.source_document, repr(f.compression_quality),
+            f.embedding_model, repr(f.frame_timestamp), f.chunk_metadata.content, str(f.chunk_metadata.chunk_size)]
+           for f in st.frame_metadata]
+    assert got == [list(r) for r in g["dual_loaded"]]
+    assert all(f.hierarchical_indices == [] for f in st.frame_metadata)
+    assert load_dual_storage_metadata(str(tmp_path / "nowhere")).frame_metadata == []
+    # frames: 12 enhanced 32 x 32 images (RAG index rows appended by the drop-in generator)
+    from hq_mi355x.rag import HierarchicalIndexGenerator
+    rng = np.random.default_rng(12)
+    imgs = rng.standard_normal((12, 32, 32))
+    imgs[5] = imgs[2] + 0.01 * rng.standard_normal((32, 32))
+    gen = HierarchicalIndexGenerator()
+    enh = np.stack([np.asarray(gen.generate_multi_level_indices(im)) for im in imgs])
+    corpus = DualStorageCorpus.from_storage(str(tmp_path), enh)
+    q = enh[[2, 7]]
+    for method in ("spatial", "embedding"):
+        res = corpus.search(q, 4, method)
+        for a in range(2):
+            if method == "spatial":
+                want = np.array([O.rag_spatial_locality_enhanced(q[a], e) for e in enh])
+            else:
+                h = [O.rag_detect_height(e) for e in enh]
+                hq_ = O.rag_detect_height(q[a])
+                want = np.array([O.rag_cosine(q[a][:hq_].ravel(), e[:hc].ravel()[None])[0] for e, hc in zip(enh, h)])
+            order = np.argsort(-want, kind="stable")[:4]
+            assert [f.chunk_id for f, _ in res[a]] == [f"c{i}" for i in order], (method, a)
+            np.testing.assert_allclose([s for _, s in res[a]], want[order], atol=1e-12)
+    (tmp_path / "metadata" / "dual_video_metadata.json").write_text('{"current_video_index": 3, "frame_metadata": [{"x": 1}]}')
+    st = load_dual_storage_metadata(str(tmp_path))   # prints the reference's warning, keeps the counters
+    assert st.current_video_index == 3 and st.frame_metadata == []

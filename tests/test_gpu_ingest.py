@@ -113,3 +113,34 @@ def test_search_batch_failing_query_only_blanks_itself(hq_lib):
         assert [r.model.metadata.model_name for r in got[i]] == [r.model.metadata.model_name for r in want]
         assert [r.similarity_score for r in got[i]] == [r.similarity_score for r in want]
     assert len(bq.quantizer._model_registry) == 30 + 3
+
+
+def test_batched_reconstruct_matches_per_model(hq_lib):
+    """HilbertQuantizer.reconstruct_many (host JPEG decode on threads, one de-normalise
+    and one inverse-Hilbert gather per frame shape) returns exactly reconstruct()'s arrays, model by model,
+    including the reference's quirk of de-normalising with the compressor's LAST (min, max)
+    (core/compressor.py:282-303, core/pipeline.py:183-235); mixed vector lengths; bad payloads raise the
+    per-model errors."""
+    pytest.importorskip("PIL")
+    from hq_mi355x.api import BatchQuantizer, HilbertQuantizer
+    from hq_mi355x.exceptions import ReconstructionError
+    rng = np.random.default_rng(9)
+    sets = _sets(rng)
+    hq = HilbertQuantizer()
+    models = hq.quantize_many(sets, model_ids=[f"r{i}" for i in range(len(sets))])
+    want = [hq.reconstruct(m) for m in models]
+    got = hq.reconstruct_many(models)
+    assert len(got) == len(want)
+    for a, b, p in zip(got, want, sets):
+        assert a.dtype == b.dtype and a.shape == b.shape == p.shape
+        assert a.tobytes() == b.tobytes()
+    got2 = BatchQuantizer().reconstruct_batch(models)   # fresh compressor: u8 / 255 (no state)
+    fresh = HilbertQuantizer()
+    for a, m in zip(got2, models):
+        assert a.tobytes() == fresh.reconstruct(m).tobytes()
+    import dataclasses
+    bad = dataclasses.replace(models[0], compressed_data=b"\x00\x01not a jpeg")
+    with pytest.raises(ReconstructionError, match="Failed to decompress image"):
+        hq.reconstruct_many([models[1], bad])
+    with pytest.raises(ReconstructionError, match="Failed to decompress image"):
+        hq.reconstruct(bad)
