@@ -1223,10 +1223,30 @@ __global__ __launch_bounds__(64) void k_sample_hist(SampleArgs a) {
 // ------------------------------------------------------------------------------------------------
 constexpr float kMarginF = 6e-5f;
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-constexpr int kZ16Row = 64;  // halfs per split row: hi[32] then lo[32]
 constexpr int kPad0 = 3 * kCS;  // pad rows of the f32 copies (hq_seg_pack0_split); k_scan0f reads reach cs + 47
 // rows of the split statistics S32 (SoA groups of 4 rows, padded)
 __host__ __device__ __forceinline__ int64_t pack0_rows(int64_t N) { return ((N + 3) & ~int64_t(3)) + kPad0; }
+// Tiled split fragments Z16 (hq_seg_pack0_split): rows in tiles of 16; tile T = [hi: 64 x 8 halves]
+// [lo: 64 x 8 halves], the 8 halves at (16 g + j) * 8 holding row 16 T + j, k = 8 g .. 8 g + 7 (the A/B
+// operand of lane 16 g + j in v_mfma_f32_16x16x32_f16), so one wave's fragment load is 1 KiB of
+// consecutive bytes (16 tag lookups) instead of 16 rows x 64 B (64 lookups).
+constexpr int kZ16Tile = 1024;  // halves per 16-row tile
+constexpr int kZ16Lo = 512;     // offset of the lo fragments in a tile
+__host__ __device__ __forceinline__ int64_t z16_rows(int64_t N) { return ((N + 15) & ~int64_t(15)) + kPad0; }
+// the hi fragment (8 halves, k = 8 g .. 8 g + 7) of a row
+__host__ __device__ __forceinline__ int64_t z16_frag(int64_t row, int g) {
+  return (row >> 4) * kZ16Tile + ((g << 4) + (row & 15)) * 8;
+}
+// element k (< 32) of a row: hi, and lo at + kZ16Lo
+__host__ __device__ __forceinline__ int64_t z16_elem(int64_t row, int k) { return z16_frag(row, k >> 3) + (k & 7); }
+// sample rows of the split copies: whole tiles, corpus tile t * stride for sample tile t
+__host__ __device__ __forceinline__ int64_t sample_rows_tiled(int64_t N, int64_t stride) {
+  return (((N + 15) >> 4) + stride - 1) / stride * 16;
+}
+__device__ __forceinline__ int64_t sample_row_tiled(int64_t i, int64_t S, int64_t stride) {
+  i = i < S ? i : S - 1;
+  return (((i >> 4) * stride) << 4) + (i & 15);
+}
 
 __device__ __forceinline__ float lower_f32(double x) {  // largest float <= x (x finite or +-inf)
   float f = (float)x;
@@ -1307,10 +1327,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const int q = q0 + 16 * b + j;
     const bool v = q < a.Q;
     const int qq = v ? q : 0;
-    const _Float16* zr = a.Zq16 + (int64_t)qq * kZ16Row + 8 * g;
-    HQ_GUARD(zr, a.Zq16, (int64_t)a.Q * kZ16Row - 39);
+    const _Float16* zr = a.Zq16 + z16_frag(qq, g);
+    HQ_GUARD(zr, a.Zq16, z16_rows(a.Q) * 64 - kZ16Lo - 8);
     qh[b] = *reinterpret_cast<const half8*>(zr);
-    ql[b] = *reinterpret_cast<const half8*>(zr + 32);
+    ql[b] = *reinterpret_cast<const half8*>(zr + kZ16Lo);
     const int64_t gq = (int64_t)(qq >> 2) * 16 + (qq & 3);  // SoA-per-4 statistics
     const float sd = a.Sq32[gq], mn = a.Sq32[gq + 4], ms = a.Sq32[gq + 8];
     const int fl = __float_as_int(a.Sq32[gq + 12]);
@@ -1357,15 +1377,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   struct SStat {
     flt4 sd, mn, ms;  // statistics of rows 4g .. 4g + 3
   };
-  const _Float16* pz = a.Zc16 + (c_begin + j) * kZ16Row + 8 * g;
+  const _Float16* pz = a.Zc16 + z16_frag(c_begin + j, g);  // c_begin: a multiple of 16
   const float* pst = a.Sc32 + (c_begin / 4 + g) * 16 + j;
   auto load_step = [&](CStep& c) {
-    HQ_GUARD(pz, a.Zc16, (a.N + kPad0) * kZ16Row - 39);  // half8 at pz and pz + 32
+    HQ_GUARD(pz, a.Zc16, z16_rows(a.N) * 64 - kZ16Lo - 8);  // half8 at pz and pz + kZ16Lo
     HQ_GUARD(pst, a.Sc32, pack0_rows(a.N) * 4);
     c.f[0] = *reinterpret_cast<const half8*>(pz);
-    c.f[1] = *reinterpret_cast<const half8*>(pz + 32);
+    c.f[1] = *reinterpret_cast<const half8*>(pz + kZ16Lo);
     c.st = *pst;
-    pz += kCS * kZ16Row;
+    pz += kZ16Tile;
     pst += kCS * 4;
   };
   auto expand = [&](const float st, SStat& x) {
@@ -1715,14 +1735,28 @@ struct QEntry {
   int pad0, pad1;
 };
 
-__global__ __launch_bounds__(64) void k_scan0g(Scan0Args a) {
+// wave-local ordering of the queue's LDS accesses (one wave's LDS instructions execute in issue order;
+// this keeps the compiler from moving them across each other)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// WPB waves per workgroup: the WPB waves of a block take WPB consecutive query blocks of ONE chunk and
+// read the same candidate fragments step by step (a barrier per unrolled iteration keeps them within
+// a few steps of each other, so WPB - 1 of the WPB reads of a fragment hit the CU's L1)
+template <int WPB, int PF>
+__global__ __launch_bounds__(64 * WPB) void k_scan0g(Scan0Args a) {
   constexpr int NB = 4;
   constexpr int QW = 16 * NB;
-  __shared__ QEntry qe[kQCap];
-  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  __shared__ QEntry qe_all[WPB][kQCap];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  QEntry* qe = qe_all[WPB > 1 ? threadIdx.x >> 6 : 0];
   const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
-  const int chunk = xcd + 8 * (slot / a.nqb);
-  const int qb = slot % a.nqb;
+  const int nqg = (a.nqb + WPB - 1) / WPB;
+  const int chunk = xcd + 8 * (slot / nqg);
+  const int qb = (slot % nqg) * WPB + (WPB > 1 ? (int)(threadIdx.x >> 6) : 0);
   if (chunk >= a.nchunks) return;
   const int64_t c_begin = (int64_t)chunk * a.chunk_len;
   if (c_begin >= a.N) return;  // chunks past the corpus end (k_scan0f comment)
@@ -1739,24 +1773,29 @@ __global__ __launch_bounds__(64) void k_scan0g(Scan0Args a) {
     const int q = q0 + 16 * b + j;
     const bool v = q < a.Q;
     const int qq = v ? q : 0;
-    const _Float16* zr = a.Zq16 + (int64_t)qq * kZ16Row + 8 * g;
-    HQ_GUARD(zr, a.Zq16, (int64_t)a.Q * kZ16Row - 39);
+    const _Float16* zr = a.Zq16 + z16_frag(qq, g);
+    HQ_GUARD(zr, a.Zq16, z16_rows(a.Q) * 64 - kZ16Lo - 8);
     qh[b] = *reinterpret_cast<const half8*>(zr);
-    ql[b] = *reinterpret_cast<const half8*>(zr + 32);
+    ql[b] = *reinterpret_cast<const half8*>(zr + kZ16Lo);
     gs[b] = v ? qc[q].gs : __builtin_huge_valf();
   }
 
   // wave-uniform bases, per-lane constant offsets (scalar step increments)
-  const char* zb = reinterpret_cast<const char*>(a.Zc16 + c_begin * kZ16Row);
-  const int zoff = (j * kZ16Row + 8 * g) * 2;
+  const char* zb = reinterpret_cast<const char*>(a.Zc16 + (c_begin >> 4) * kZ16Tile);  // c_begin: a multiple of 16
+  const int zoff = lane * 16;  // bytes: the lane's 8 halves of a tile
   struct CStep {
     half8 f[2];
   };
+#ifdef HQ_DIAG
+  const int64_t smul = (a.expt == 5 || a.expt == 6) ? 0 : kZ16Tile * 2;  // timing experiments: step 0 only
+#else
+  constexpr int64_t smul = kZ16Tile * 2;
+#endif
   auto load_step = [&](CStep& c, const int64_t s) {
-    const _Float16* p = reinterpret_cast<const _Float16*>(zb + s * (int64_t)(kCS * kZ16Row * 2) + zoff);
-    HQ_GUARD(p, a.Zc16, (a.N + kPad0) * kZ16Row - 39);
+    const _Float16* p = reinterpret_cast<const _Float16*>(zb + s * smul + zoff);
+    HQ_GUARD(p, a.Zc16, z16_rows(a.N) * 64 - kZ16Lo - 8);
     c.f[0] = *reinterpret_cast<const half8*>(p);
-    c.f[1] = *reinterpret_cast<const half8*>(p + 32);
+    c.f[1] = *reinterpret_cast<const half8*>(p + kZ16Lo);
   };
   auto mfma_half = [&](const int h, const half8* f, flt4* acc) {
     acc[0] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -1812,7 +1851,7 @@ __global__ __launch_bounds__(64) void k_scan0g(Scan0Args a) {
         }
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     // shift the remaining entries down (all reads of a 64-entry block before its writes)
     for (int b0 = n; b0 < qn; b0 += 64) {
       const bool mv = b0 + lane < qn;
@@ -1823,13 +1862,13 @@ __global__ __launch_bounds__(64) void k_scan0g(Scan0Args a) {
         tq = qe[b0 + lane].qi;
         tr = qe[b0 + lane].row;
       }
-      __syncthreads();
+      wave_lds_sync();
       if (mv) {
         qe[b0 - n + lane].g = tg;
         qe[b0 - n + lane].qi = tq;
         qe[b0 - n + lane].row = tr;
       }
-      __syncthreads();
+      wave_lds_sync();
     }
     qn -= n;
   };
@@ -1855,6 +1894,10 @@ __global__ __launch_bounds__(64) void k_scan0g(Scan0Args a) {
   // pre-filter of one half: max of the lane's four rows per block against G* (the compare's lane mask
   // is the ballot); blocks holding a flagged row (f32-unsafe; zero-variance for a query that admits 0.1)
   // are queued regardless
+#ifdef HQ_DIAG
+  if (a.expt == 6)  // timing experiment: nothing is queued
+    for (int b = 0; b < NB; ++b) gs[b] = __builtin_huge_valf();
+#endif
   auto half_step = [&](const int h, const flt4* acc, const int64_t cs) {
     const unsigned long long m0 = __builtin_amdgcn_ballot_w64(max4(acc[0]) >= gs[2 * h]);
     const unsigned long long m1 = __builtin_amdgcn_ballot_w64(max4(acc[1]) >= gs[2 * h + 1]);
@@ -1864,29 +1907,38 @@ __global__ __launch_bounds__(64) void k_scan0g(Scan0Args a) {
     }
   };
 
-  CStep cA, cB, cC;
-  load_step(cA, 0);
-  load_step(cB, 1);
-  flt4 acc0[2], acc1[2];
-  mfma_half(0, cA.f, acc0);
+  // PF + 1 step buffers in rotation: the fragments of step s + PF are requested while step s is computed
+  // (the prefetch index is clamped to the chunk's last step: no read past its rows + 15)
   const int64_t nsteps = (c_end - c_begin + kCS - 1) / kCS;
+  CStep buf[PF + 1];
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load_step(buf[u], u < nsteps ? u : nsteps - 1);
+  flt4 acc0[2], acc1[2];
+  mfma_half(0, buf[0].f, acc0);
+#ifdef HQ_DIAG
+  // timing experiments: 7 = no pre-filter (loads + MFMAs only), 9 = no loads after the prologue
+  const bool x_nofilter = a.expt == 7, x_noload = a.expt == 9;
+#else
+  constexpr bool x_nofilter = false, x_noload = false;
+#endif
   auto body = [&](const int64_t s, const CStep& cur, const CStep& nxt, CStep& nn) {
-    load_step(nn, s + 2);  // padded copies: rows past the chunk are harmless (masked in the drain)
-    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch two steps ahead (the scheduler sinks it otherwise)
+    if (!x_noload) load_step(nn, s + PF < nsteps ? s + PF : nsteps - 1);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch PF steps ahead (the scheduler sinks it otherwise)
     const int64_t cs = c_begin + s * kCS;
     mfma_half(1, cur.f, acc1);
-    half_step(0, acc0, cs);
+    if (!x_nofilter) half_step(0, acc0, cs);
     mfma_half(0, nxt.f, acc0);
-    half_step(1, acc1, cs);
+    if (!x_nofilter) half_step(1, acc1, cs);
   };
   int64_t s = 0;
-  for (; s + 2 < nsteps; s += 3) {
-    body(s, cA, cB, cC);
-    body(s + 1, cB, cC, cA);
-    body(s + 2, cC, cA, cB);
+  for (; s + PF < nsteps; s += PF + 1) {
+#pragma unroll
+    for (int u = 0; u <= PF; ++u) body(s + u, buf[u], buf[(u + 1) % (PF + 1)], buf[(u + PF) % (PF + 1)]);
+    if constexpr (WPB > 1) __builtin_amdgcn_s_barrier();  // same step count in every wave of the block
   }
-  if (s < nsteps) body(s, cA, cB, cC);
-  if (s + 1 < nsteps) body(s + 1, cB, cC, cA);
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (s + u < nsteps) body(s + u, buf[u], buf[(u + 1) % (PF + 1)], buf[(u + PF) % (PF + 1)]);
   while (qn > 0) drain(qn < 64 ? qn : 64);
 }
 
@@ -1912,7 +1964,7 @@ __global__ __launch_bounds__(64) void k_scan0_flagged(Scan0Args a, const int* __
   const QConst c = qc[q];
   if (__float_as_int(c.flag) != 0) return;  // flagged query: dense exact path
   const double* sq = a.Sq + (int64_t)q * a.nseg * 4;
-  const _Float16* zq = a.Zq16 + (int64_t)q * kZ16Row;
+  const _Float16* zq = a.Zq16;
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
     const int row = list[i];
     const double* sc = a.Sc + (int64_t)row * a.nseg * 4;
@@ -1921,10 +1973,12 @@ __global__ __launch_bounds__(64) void k_scan0_flagged(Scan0Args a, const int* __
     if (qs == 0.0 || csd == 0.0) {
       v = const0(qs == 0.0, csd == 0.0, qm, cm, (aux_bits(sq) & aux_bits(sc) & kAuxF32) != 0);
     } else {
-      const _Float16* zc = a.Zc16 + (int64_t)row * kZ16Row;
+      const _Float16* zc = a.Zc16;
       double G = 0.0;
-      for (int k = 0; k < 32; ++k)
-        G = fma((double)zq[k] + (double)zq[32 + k], (double)zc[k] + (double)zc[32 + k], G);
+      for (int k = 0; k < 32; ++k) {
+        const int64_t eq = z16_elem(q, k), ec = z16_elem(row, k);
+        G = fma((double)zq[eq] + (double)zq[eq + kZ16Lo], (double)zc[ec] + (double)zc[ec + kZ16Lo], G);
+      }
       v = approx0(G, a.c1, (0.6 * a.inv_m) * qs, 0.6 * qm, qq, csd, cm, cq);
     }
     const float sv = (float)v;
@@ -2133,9 +2187,9 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
     const int q = q0 + 16 * b + j;
     const bool v = q < a.Q;
     const int qq = v ? q : 0;
-    const _Float16* zr = a.Zq16 + (int64_t)qq * kZ16Row + 8 * g;
+    const _Float16* zr = a.Zq16 + z16_frag(qq, g);
     qh[b] = *reinterpret_cast<const half8*>(zr);
-    ql[b] = *reinterpret_cast<const half8*>(zr + 32);
+    ql[b] = *reinterpret_cast<const half8*>(zr + kZ16Lo);
     const int64_t gq = (int64_t)(qq >> 2) * 16 + (qq & 3);  // SoA-per-4 statistics
     qA[b] = (float)(0.6 * a.inv_m) * a.Sq32[gq];
     qB[b] = 0.6f * a.Sq32[gq + 4];
@@ -2143,12 +2197,12 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
     if (v && __float_as_int(a.Sq32[gq + 12]) == 0) qok |= 1 << b;
   }
   __syncthreads();
-  auto row_of = [&](int64_t i) -> int64_t { return (i < a.S ? i : a.S - 1) * a.stride; };
+  auto row_of = [&](int64_t i) -> int64_t { return sample_row_tiled(i, a.S, a.stride); };
   auto load_frag = [&](int64_t cs, half8* dst) {
-    const _Float16* p = a.Zc16 + row_of(cs + j) * kZ16Row + 8 * g;
-    HQ_GUARD(p, a.Zc16, a.N * kZ16Row - 39);
+    const _Float16* p = a.Zc16 + z16_frag(row_of(cs + j), g);
+    HQ_GUARD(p, a.Zc16, z16_rows(a.N) * 64 - kZ16Lo - 8);
     dst[0] = *reinterpret_cast<const half8*>(p);
-    dst[1] = *reinterpret_cast<const half8*>(p + 32);
+    dst[1] = *reinterpret_cast<const half8*>(p + kZ16Lo);
   };
   half8 cf[2];
   load_frag(c_begin, cf);
@@ -2250,9 +2304,9 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
     const int q = q0 + 16 * b + j;
     const bool v = q < a.Q;
     const int qq = v ? q : 0;
-    const _Float16* zr = a.Zq16 + (int64_t)qq * kZ16Row + 8 * g;
+    const _Float16* zr = a.Zq16 + z16_frag(qq, g);
     qh[b] = *reinterpret_cast<const half8*>(zr);
-    ql[b] = *reinterpret_cast<const half8*>(zr + 32);
+    ql[b] = *reinterpret_cast<const half8*>(zr + kZ16Lo);
     const int64_t gq = (int64_t)(qq >> 2) * 16 + (qq & 3);  // SoA-per-4 statistics
     qA[b] = (float)(0.6 * a.inv_m) * a.Sq32[gq];
     qB[b] = 0.6f * a.Sq32[gq + 4];
@@ -2268,18 +2322,19 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
   float k0[4];
 #pragma unroll
   for (int b = 0; b < 4; ++b) k0[b] = ((qok >> b) & 1) ? 1.35f : -__builtin_huge_valf();
-  auto row_of = [&](int64_t i) -> int64_t { return (i < a.S ? i : a.S - 1) * a.stride; };
+  auto row_of = [&](int64_t i) -> int64_t { return sample_row_tiled(i, a.S, a.stride); };
   auto load_frag = [&](int64_t cs, half8* dst) {
-    const _Float16* p = a.Zc16 + row_of(cs + j) * kZ16Row + 8 * g;
+    const _Float16* p = a.Zc16 + z16_frag(row_of(cs + j), g);
+    HQ_GUARD(p, a.Zc16, z16_rows(a.N) * 64 - kZ16Lo - 8);
     dst[0] = *reinterpret_cast<const half8*>(p);
-    dst[1] = *reinterpret_cast<const half8*>(p + 32);
+    dst[1] = *reinterpret_cast<const half8*>(p + kZ16Lo);
   };
   // statistics: lane (g, j) loads stat (j & 3) (std, mean, msq, flags) of row 4g + (j >> 2) - one dword
   // per lane - and the 16 values of the lane group are broadcast by DPP row_newbcast
   auto load_stats = [&](int64_t cs) -> float {
     const int64_t row = row_of(cs + 4 * g + (j >> 2));
     const float* p = a.Sc32 + (row >> 2) * 16 + (j & 3) * 4 + (row & 3);
-    HQ_GUARD(p, a.Sc32, ((a.N + 3) & ~int64_t(3)) * 4);
+    HQ_GUARD(p, a.Sc32, pack0_rows(a.N) * 4);  // sample tiles may end in pad rows (flag 4: not scored)
     return *p;
   };
   // fragments and statistics are loaded two steps ahead (3-buffer rotation, as in k_scan0f): at 2 waves
@@ -3186,7 +3241,7 @@ static void sample_top_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, i
                                 int64_t& chunk_len) {
   const int64_t sd = opt(OPT_SAMPLE_STRIDE, 16) > 0 ? opt(OPT_SAMPLE_STRIDE, 16) : 16;  // A/B option
   stride = N >= sd * 4096 ? sd : (N / 4096 > 1 ? N / 4096 : 1);
-  S = (N + stride - 1) / stride;
+  S = sample_rows_tiled(N, stride);  // whole 16-row tiles (k_sample_topf)
   nqb = (Q + kQW - 1) / kQW;
   const int waves = opt(OPT_SAMPLE_WAVES, 2048) > 0 ? (int)opt(OPT_SAMPLE_WAVES, 2048) : 2048;
   int64_t target = (waves + nqb - 1) / nqb;
@@ -3221,10 +3276,10 @@ static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
 // below that); chunks of <= 65520 rows (u16 histogram counters), ~1024 waves (a wave has a fixed
 // cost: histogram init and flush)
 static void sample_geometry(int Q, int64_t N, int64_t& stride, int64_t& S, int& nqb, int& nchunks,
-                            int64_t& chunk_len) {
+                            int64_t& chunk_len, bool tiled) {
   const int64_t sd = opt(OPT_SAMPLE_STRIDE, 16) > 0 ? opt(OPT_SAMPLE_STRIDE, 16) : 16;  // A/B option
   stride = N >= sd * 4096 ? sd : (N / 4096 > 1 ? N / 4096 : 1);
-  S = (N + stride - 1) / stride;
+  S = tiled ? sample_rows_tiled(N, stride) : (N + stride - 1) / stride;  // f32 (split) samples: whole tiles
   nqb = (Q + kQW - 1) / kQW;
   const int waves = opt(OPT_SAMPLE_WAVES, 1024) > 0 ? (int)opt(OPT_SAMPLE_WAVES, 1024) : 1024;
   int64_t target = (waves + nqb - 1) / nqb;
@@ -3395,7 +3450,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     sa.Zq = Zq; sa.Sq = Sq; sa.Q = Q; sa.Zc = Zc; sa.Sc = Sc; sa.N = N;
     sa.Zq32 = nullptr; sa.Zc32 = nullptr; sa.Zq16 = Zq16; sa.Zc16 = Zc16; sa.Sq32 = Sq32; sa.Sc32 = Sc32;
     sa.Lp = b.Lp; sa.nseg = b.nseg; sa.P0 = b.P0; sa.inv_m = b.inv_m; sa.c1 = b.c1;
-    sample_geometry(Q, N, sa.stride, sa.S, sa.nqb, sa.nchunks, sa.chunk_len);
+    sample_geometry(Q, N, sa.stride, sa.S, sa.nqb, sa.nchunks, sa.chunk_len, f32);
     sa.hist = hist;
     sa.K = k;
     rc = f32 ? scan0_dispatch<true>(ks, b, &sa, s) : scan0_dispatch<false>(ks, b, &sa, s);
@@ -3419,7 +3474,20 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     hipLaunchKernelGGL(k_flag_rows, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, s, Sc32, N, flag_list,
                        flag_n);
     HQ_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_scan0g, dim3(b.nqb * b.nchunks), dim3(64), 0, s, b);
+    // options scan_wpb: waves per block (1 = one wave per block, each reading its own fragments);
+    // scan_pf: prefetch distance in steps (2, 3, 4)
+    const int pf = (int)opt(OPT_SCAN_PF, 2);
+    if (opt(OPT_SCAN_WPB, 1) == 4) {
+      const dim3 g4((b.nqb + 3) / 4 * b.nchunks);
+      if (pf == 4) hipLaunchKernelGGL((k_scan0g<4, 4>), g4, dim3(256), 0, s, b);
+      else if (pf == 3) hipLaunchKernelGGL((k_scan0g<4, 3>), g4, dim3(256), 0, s, b);
+      else hipLaunchKernelGGL((k_scan0g<4, 2>), g4, dim3(256), 0, s, b);
+    } else {
+      const dim3 g1(b.nqb * b.nchunks);
+      if (pf == 4) hipLaunchKernelGGL((k_scan0g<1, 4>), g1, dim3(64), 0, s, b);
+      else if (pf == 3) hipLaunchKernelGGL((k_scan0g<1, 3>), g1, dim3(64), 0, s, b);
+      else hipLaunchKernelGGL((k_scan0g<1, 2>), g1, dim3(64), 0, s, b);
+    }
     HQ_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_scan0_flagged, dim3(64, (Q + 63) / 64), dim3(64), 0, s, b, (const int*)flag_list,
                        (const int*)flag_n);
@@ -3460,27 +3528,29 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   return HQ_OK;
 }
 
-// Split-f16 level-0 copies for the default scan: Z16 [N + kPad0, 64] = (hi[32], lo[32]) of the
-// level-0 segment zero-padded to 32, and S32 = per-row (std, mean, msq, flag bits: 1 zero variance,
+// Split-f16 level-0 copies for the default scan: Z16 = (hi[32], lo[32]) of the level-0 segment
+// zero-padded to 32 for the rows [0, round_up(N, 16) + kPad0), in the tiled fragment layout (z16_frag),
+// and S32 = per-row (std, mean, msq, flag bits: 1 zero variance,
 // 2 msq outside [2^-60, 2^60], 4 pad row) in SoA groups of 4 rows: group G = rows 4G .. 4G + 3 holds
 // std[4], mean[4], msq[4], flags[4] (16 floats), for the rows [0, round_up(N, 4) + kPad0).  k_scan0f
 // reads up to 31 rows past a step start.
 
 __global__ void k_pack0(const double* __restrict__ Z, const double* __restrict__ S, int64_t N, int Lp, int P0,
                         int nseg, _Float16* __restrict__ Z16, float* __restrict__ S32) {
-  const int64_t rows = pack0_rows(N);
+  const int64_t rows = z16_rows(N);  // >= pack0_rows(N)
   const int64_t total = rows * 32;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = t / 32;
     const int c = (int)(t % 32);
-    if (r < N + kPad0) {
+    {
       const double z = (r < N && c < P0) ? Z[r * Lp + c] : 0.0;
       const _Float16 hi = (_Float16)z;
       const _Float16 lo = (_Float16)(z - (double)hi);
-      Z16[r * kZ16Row + c] = hi;
-      Z16[r * kZ16Row + 32 + c] = lo;
+      const int64_t e = z16_elem(r, c);
+      Z16[e] = hi;
+      Z16[e + kZ16Lo] = lo;
     }
-    if (c == 0) {
+    if (c == 0 && r < pack0_rows(N)) {
       float* o = S32 + (r >> 2) * 16 + (r & 3);
       if (r < N) {
         const double* st = S + r * nseg * 4;
@@ -3580,7 +3650,7 @@ int hq_scan0_geometry(int Q, int64_t N, int* nqb, int* nchunks, int64_t* chunk_l
   if (nqb) *nqb = a;
   if (nchunks) *nchunks = b;
   if (chunk_len) *chunk_len = c;
-  if (z_rows) *z_rows = N + kPad0;
+  if (z_rows) *z_rows = z16_rows(N);
   if (s_rows) *s_rows = pack0_rows(N);
   return HQ_OK;
 }
@@ -3768,7 +3838,7 @@ int hq_seg_pack0_split(const double* Z, const double* S, int64_t N, int L, void*
   seg_info(L, si);
   if (si.nseg == 0) return fail(HQ_E_INVALID, "no level structure for L=%d", L);
   if (si.plen[0] > 32) return fail(HQ_E_UNSUPPORTED, "level-0 segment of %d values (<= 32)", si.plen[0]);
-  int64_t blocks = (pack0_rows(N) * 32 + 255) / 256;
+  int64_t blocks = (z16_rows(N) * 32 + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(k_pack0, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, Z, S, N, si.Lp, si.plen[0],
                      si.nseg, reinterpret_cast<_Float16*>(Z16), S32);

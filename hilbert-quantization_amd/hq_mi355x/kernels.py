@@ -294,7 +294,7 @@ def pack0(p: Prepared, exc=None) -> Prepared:
     t = torch()
     if seg_level0_len(p.L) > 32:
         return p
-    p.Z16 = t.empty((p.N + PAD0, 64), dtype=t.float16, device=p.Z.device)
+    p.Z16 = t.empty(((p.N + 15) // 16 * 16 + PAD0, 64), dtype=t.float16, device=p.Z.device)  # tiled rows
     p.S32 = t.empty(((p.N + 3) // 4 * 4 + PAD0, 4), dtype=t.float32, device=p.Z.device)  # SoA groups of 4 rows
     _chk(_L().hq_seg_pack0_split(ptr(p.Z), ptr(p.S), p.N, p.L, ptr(p.Z16), ptr(p.S32), stream()), exc)
     return p

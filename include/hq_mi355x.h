@@ -54,7 +54,7 @@ const char* hq_last_error(void);
  * e.g. "fused_v" (fused-kernel variant bits), "fused_generic", "chunk_generic", "chunk_exactdiv",
  * "chunk_wpb", "chunk_cpw", "precomp_grid", "precomp_tree_lds", "cos_kernel" (1 register-staged,
  * 2 lockstep), "refine_global", "select_2stage", "sample_kth" (0 = provable bound), "scan_v1" (the
- * LDS-tiled level-0 scan), "scan_variant".  Options are process-wide: set them before launching, not
+ * LDS-tiled level-0 scan), "scan_variant", "scan_wpb" (1 = one wave per level-0 scan block).  Options are process-wide: set them before launching, not
  * while other host threads launch.  hq_reset_option restores the default; hq_get_option returns 1 when
  * the option is set (value in *value), 0 when it is at its default, HQ_E_INVALID for an unknown name.
  * hq_diag_build() = 1 for a `make DIAG=1` library (diagnostics kernels; HQ_<NAME> environment variables
@@ -218,11 +218,14 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
  * a split-f16 product (z = hi + lo, G ~= hi.hi + hi.lo + lo.hi with f32 accumulation, three
  * v_mfma_f32_16x16x32_f16 per 16x16 tile) and the filter and list scores in f32.
  * |approx - exact| <= ~5.5e-6, so callers re-rank with hq_refine_topk at eps >= 2e-5.
- * hq_seg_pack0_split builds, from hq_seg_prepare's Z and S, Z16 [N + 48, 64] f16 (hi[32], lo[32]
- * of the zero-padded level-0 segment) and S32, f32 statistics (std, mean, msq, flag bits) in SoA
+ * hq_seg_pack0_split builds, from hq_seg_prepare's Z and S, Z16: f16 hi[32], lo[32] of the
+ * zero-padded level-0 segment for round_up(N, 16) + 48 rows (128 B per row), in 16-row tiles of 2 KiB:
+ * [hi: 64 x 8][lo: 64 x 8] halves, the 8 at (16 g + j) * 8 being row 16 t + j, values 8 g .. 8 g + 7
+ * (one MFMA operand fragment per lane: a wave loads 1 KiB of consecutive bytes), and S32, f32 statistics (std, mean, msq, flag bits) in SoA
  * groups of 4 rows (std[4], mean[4], msq[4], flags[4]) for round_up(N, 4) + 48 rows (16 B per row);
  * Sq/Sc are the f64 statistics of hq_seg_prepare.  Level-0 segments of up to 32 values, N < 2^31. */
-/* Starting threshold of hq_scan0_topk_split: the K'-th best score of a 1/16 row sample minus the error
+/* Starting threshold of hq_scan0_topk_split: the K'-th best score of a 1/16 sample (every 16th tile of
+ * 16 rows) minus the error
  * margin, K' = 12 (HQ_SAMPLE_KTH; K' = k, a provable lower bound of the k-th best, for corpora below
  * 16 x 4096 rows).  With K' < k a query can end with fewer than k listed candidates although more pass
  * the caller's threshold: its empty slots then carry score +inf (id -1), which hq_refine_topk /

@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
-"""Debug counters of the level-0 scan on the bench corpus (HQ_SCAN_EXPT=3)."""
-# HQ_SCAN_EXPT=3 counters need the diagnostics build (make -C hilbert-quantization_amd/csrc DIAG=1).
+"""The level-0 scan on the bench corpus (cfg3 shape: 1M x 64 level-0 values, 1000 queries), three
+calls, for PMC passes (tools/pmc_kernel.sh).  Argument: level0 (default, the progressive search's scan)
+or overall (the brute-force overall scan)."""
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "hilbert-quantization_amd")]
-os.environ.setdefault("HQ_SCAN_EXPT", "0")
 import torch  # noqa: E402
 from hq_mi355x import kernels as K  # noqa: E402
 from hq_mi355x.core.search_engine import IndexCorpus  # noqa: E402
@@ -19,5 +19,10 @@ del X
 corpus = IndexCorpus(C)
 gq = torch.Generator(device=dev).manual_seed(3)
 qp = corpus.prepare_queries(C[:1000] + 0.01 * torch.randn((1000, 64), generator=gq, device=dev, dtype=torch.float64))
-K.scan_topk(qp, corpus.prep, 0, 28, 0.1 - 2e-5, 1)
+mode = sys.argv[1] if len(sys.argv) > 1 else "level0"
+for _ in range(3):
+    if mode == "overall":
+        K.scan_topk(qp, corpus.prep, 1, 18, -2e-5, 0)
+    else:
+        K.scan_topk(qp, corpus.prep, 0, 28, 0.1 - 2e-5, 1)
 torch.cuda.synchronize()
