@@ -2417,6 +2417,123 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
   }
 }
 
+// f32 sample pass, G-selected form (default): the step loop keeps, per lane (g, j) and query block b,
+// only the step whose four rows 4g .. 4g + 3 hold the largest G (two v_max, one compare and six
+// v_cndmask per block and step: the MFMA work sets the pace, as in k_scan0g), and scores the rows of
+// that step exactly (f32 model) at the end; the stream's kTopT best of those scores go to the pool.  They
+// are real scores of distinct (query, row) pairs, so the K-th best of the union is still a lower bound of
+// the K-th best over the corpus (selecting by G instead of by score only makes it less tight).  Query
+// constants and candidate statistics are read in the epilogue alone.
+__global__ __launch_bounds__(64) void k_sample_topg(SampleArgs a) {
+  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
+  const int chunk = xcd + 8 * (slot / a.nqb);
+  const int qb = slot % a.nqb;
+  if (chunk >= a.nchunks) return;
+  const int64_t c_begin = (int64_t)chunk * a.chunk_len;
+  int64_t c_end = c_begin + a.chunk_len;
+  if (c_end > a.S) c_end = a.S;
+  const int q0 = qb * kQW;
+  half8 qh[4], ql[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int q = q0 + 16 * b + j;
+    const _Float16* zr = a.Zq16 + z16_frag(q < a.Q ? q : 0, g);
+    qh[b] = *reinterpret_cast<const half8*>(zr);
+    ql[b] = *reinterpret_cast<const half8*>(zr + kZ16Lo);
+  }
+  auto row_of = [&](int64_t i) -> int64_t { return sample_row_tiled(i, a.S, a.stride); };
+  auto load_frag = [&](int64_t cs, half8* dst) {
+    const _Float16* p = a.Zc16 + z16_frag(row_of(cs + j), g);
+    HQ_GUARD(p, a.Zc16, z16_rows(a.N) * 64 - kZ16Lo - 8);
+    dst[0] = *reinterpret_cast<const half8*>(p);
+    dst[1] = *reinterpret_cast<const half8*>(p + kZ16Lo);
+  };
+  float bg[4];     // largest max-of-four G so far
+  flt4 bacc[4];    // G of that step's four rows
+  int bcs[4];      // that step (sample index of its first row), -1: none
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    bg[b] = -__builtin_huge_valf();
+    bacc[b] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
+    bcs[b] = -1;
+  }
+  half8 cf[2], cf1[2];
+  load_frag(c_begin, cf);
+  load_frag(c_begin + kCS, cf1);
+  for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
+    half8 cfn[2];
+    load_frag(cs + 2 * kCS, cfn);  // sample indices past S clamp to the last sample row
+    flt4 acc[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[0], qh[b], flt4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[0], ql[b], acc[b], 0, 0, 0);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[1], qh[b], acc[b], 0, 0, 0);
+    if (cs + kCS > c_end) {  // the chunk's last, partial step: rows past c_end never win
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (cs + 4 * g + r >= c_end)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) acc[b][r] = -__builtin_huge_valf();
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const float m = max4(acc[b]);
+      const bool up = m > bg[b];
+      bg[b] = up ? m : bg[b];
+      bacc[b] = up ? acc[b] : bacc[b];
+      bcs[b] = up ? (int)cs : bcs[b];
+    }
+    cf[0] = cf1[0];
+    cf[1] = cf1[1];
+    cf1[0] = cfn[0];
+    cf1[1] = cfn[1];
+  }
+  // epilogue: exact f32 model scores of the selected rows, the stream's kTopT best to the pool
+  const float c1f = (float)a.c1;
+  const int ns = 4 * a.nchunks;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int q = q0 + 16 * b + j;
+    if (q >= a.Q) continue;
+    const int64_t gq = (int64_t)(q >> 2) * 16 + (q & 3);  // SoA-per-4 statistics
+    const float qA = (float)(0.6 * a.inv_m) * a.Sq32[gq], qB = 0.6f * a.Sq32[gq + 4], qQ = a.Sq32[gq + 8];
+    const bool qok = __float_as_int(a.Sq32[gq + 12]) == 0;
+    float top[kTopT];
+#pragma unroll
+    for (int t = 0; t < kTopT; ++t) top[t] = -1.0f;
+    if (qok && bcs[b] >= 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t i = (int64_t)bcs[b] + 4 * g + r;
+        if (i >= c_end) continue;
+        const int64_t row = row_of(i);
+        const float* st = a.Sc32 + (row >> 2) * 16 + (row & 3);
+        HQ_GUARD(st, a.Sc32, pack0_rows(a.N) * 4 - 13);
+        if (__float_as_int(st[12]) != 0) continue;  // flagged / pad row
+        const float G = bacc[b][r];
+        const float num = fmaf(G, qA * st[0], qB * st[4]);
+        float t = num * __builtin_amdgcn_rcpf(qQ + st[8]);
+        t = t > 0.0f ? t : 0.0f;
+        float sc = fmaf(G, c1f, 0.35f) + t;
+        sc = sc < 1.0f ? sc : 1.0f;
+        sc = sc > 0.0f ? sc : 0.0f;  // +0 for -0 and negatives (k_sample_kth orders bit patterns)
+#pragma unroll
+        for (int u = 0; u < kTopT; ++u) {
+          const float hi = fmaxf(top[u], sc);
+          sc = fminf(top[u], sc);
+          top[u] = hi;
+        }
+      }
+    }
+    float* o = a.top + ((int64_t)q * ns + 4 * chunk + g) * kTopT;
+#pragma unroll
+    for (int t = 0; t < kTopT; ++t) o[t] = top[t];
+  }
+}
+
 // per-query starting threshold from the top-T sample pools (one wave per query): the K-th largest
 // value v (bisection on the bit pattern of the non-negative f32 scores, pool held in registers as
 // bits + 1, 0 = empty), th0 = v - margin, or -inf when fewer than K sample scores exist
@@ -3435,7 +3552,11 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     sa.hist = nullptr;
     sa.top = top;
     sa.K = k;
-    hipLaunchKernelGGL(k_sample_topf, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
+    // option sample_variant 1: the full-filter sample pass (k_sample_topf)
+    if (opt(OPT_SAMPLE_VARIANT, 0) == 1)
+      hipLaunchKernelGGL(k_sample_topf, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
+    else
+      hipLaunchKernelGGL(k_sample_topg, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
     HQ_CHECK_LAUNCH();
     const int mg = Q < 8192 ? Q : 8192;
     hipLaunchKernelGGL(k_sample_kth, dim3(mg), dim3(64), 0, s, (const float*)top, 4 * sa.nchunks, Q, sample_kth,

@@ -54,7 +54,8 @@ const char* hq_last_error(void);
  * e.g. "fused_v" (fused-kernel variant bits), "fused_generic", "chunk_generic", "chunk_exactdiv",
  * "chunk_wpb", "chunk_cpw", "precomp_grid", "precomp_tree_lds", "cos_kernel" (1 register-staged,
  * 2 lockstep), "refine_global", "select_2stage", "sample_kth" (0 = provable bound), "scan_v1" (the
- * LDS-tiled level-0 scan), "scan_variant", "scan_wpb" (1 = one wave per level-0 scan block).  Options are process-wide: set them before launching, not
+ * LDS-tiled level-0 scan), "scan_variant", "scan_wpb" (4 = four waves per level-0 scan block), "scan_pf" (prefetch
+ * distance 3 or 4), "sample_variant" (1 = the full-filter sample pass).  Options are process-wide: set them before launching, not
  * while other host threads launch.  hq_reset_option restores the default; hq_get_option returns 1 when
  * the option is set (value in *value), 0 when it is at its default, HQ_E_INVALID for an unknown name.
  * hq_diag_build() = 1 for a `make DIAG=1` library (diagnostics kernels; HQ_<NAME> environment variables
