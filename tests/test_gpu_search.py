@@ -247,9 +247,9 @@ def test_rag_scores(hq_lib, golden):
 
 
 def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, hq_option):
-    """The wave-independent level-0 scan (k_scan0f: sampled thresholds, global threshold exchange,
-    division-free filter, exact constant branches; with and without the sample pass) gives the same exact
-    top-k as the LDS-tiled k_scan (option scan_v1) and as the oracle, on a corpus with a ragged chunk tail, zero-variance level-0 segments on both sides,
+    """The level-0 scan variants (k_scan0g at 1 or 4 waves per block and prefetch distance 2-4, the
+    G-selected or full-filter sample pass or none, the list-based k_scan0f) give the same exact top-k as
+    the LDS-tiled k_scan (option scan_v1) and as the oracle, on a corpus with a ragged chunk tail, zero-variance level-0 segments on both sides,
     duplicate runs across chunks and a query count that is not a multiple of 64."""
     from hq_mi355x.core.search_engine import IndexCorpus
     rng = np.random.default_rng(77)
@@ -264,17 +264,23 @@ def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, hq_option):
     corpus = IndexCorpus(C)
     qp = corpus.prepare_queries(Q)
     res = {}
-    for tag in ("v0", "v0-nosample", "v1"):
-        if tag == "v0-nosample":
-            hq_option("scan_nosample", 1)
-        if tag == "v1":
-            hq_option("scan_nosample", None)
-            hq_option("scan_v1", 1)
+    variants = {  # option settings of each variant (the default k_scan0g + k_sample_topg first)
+        "v0": {},
+        "v0-nosample": {"scan_nosample": 1},
+        "v0-wpb4-pf3": {"scan_wpb": 4, "scan_pf": 3},
+        "v0-pf4": {"scan_pf": 4},
+        "v0-sample-full": {"sample_variant": 1},
+        "v0-list": {"scan_variant": 1},  # k_scan0f
+        "v1": {"scan_v1": 1},
+    }
+    for tag, opts in variants.items():
+        for name in ("scan_nosample", "scan_wpb", "scan_pf", "sample_variant", "scan_variant", "scan_v1"):
+            hq_option(name, opts.get(name))
         for thr, tm in ((0.1, 1), (0.6, 1), (0.1, 2)):
             sc, ids, cnt, _, _ = corpus.exact_topk(qp, 0, 20, thr, tm)
             res[(tag, thr, tm)] = (_np(sc), _np(ids), _np(cnt))
     for key in ((0.1, 1), (0.6, 1), (0.1, 2)):
-        for tag in ("v0-nosample", "v1"):
+        for tag in list(variants)[1:]:
             a, b = res[("v0",) + key], res[(tag,) + key]
             assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]), (tag, key)
             np.testing.assert_array_equal(a[0][a[1] >= 0], b[0][b[1] >= 0])
