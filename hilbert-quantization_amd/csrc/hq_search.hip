@@ -2006,12 +2006,13 @@ __global__ __launch_bounds__(64) void k_pool_select(const float* __restrict__ po
                                                     const int* __restrict__ pool_n, int cap, int Q, int K,
                                                     int64_t id_base, double* __restrict__ out_score,
                                                     int64_t* __restrict__ out_id, const double* __restrict__ th0,
-                                                    double thr0, const QConst* __restrict__ qc) {
+                                                    double thr0, const float* __restrict__ qflag, int qstride) {
   const int lane = threadIdx.x;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
-    // k_scan0g: a flagged query (not scanned) or an overflowing pool -> every slot +inf / -1, which the
-    // exact re-rank reads as unresolved (the caller's dense exact path answers the query)
-    if (qc && (__float_as_int(qc[q].flag) != 0 || pool_n[q] > cap)) {
+    // k_scan0g / k_scanov (qflag: the query's flag word in its constants, qstride floats apart): a flagged
+    // query (not scanned) or an overflowing pool -> every slot +inf / -1, which the exact re-rank reads
+    // as unresolved (the caller's dense exact path answers the query)
+    if (qflag && (__float_as_int(qflag[(int64_t)q * qstride]) != 0 || pool_n[q] > cap)) {
       for (int x = lane; x < K; x += 64) {
         out_score[(int64_t)q * K + x] = __builtin_huge_val();
         out_id[(int64_t)q * K + x] = -1;
@@ -2549,7 +2550,7 @@ __global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top
   const int P = ns * kTopT;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
     if (lane == 0) {
-      gtau[q] = 0ull;
+      if (gtau) gtau[q] = 0ull;
       pool_n[q] = 0;
     }
     const float* p = top + (int64_t)q * P;
@@ -3626,7 +3627,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     hipLaunchKernelGGL(k_pool_select, dim3(mg), dim3(64), 0, s, (const float*)b.pool_s, (const int*)b.pool_i,
                        (const int*)b.pool_n, b.pool_cap, Q, k, id_base, out_score, out_id,
                        top_sample && sample_kth < k ? (const double*)th0 : (const double*)nullptr, b.thr0,
-                       (const QConst*)qc);
+                       qc ? &qc[0].flag : (const float*)nullptr, (int)(sizeof(QConst) / 4));
     HQ_CHECK_LAUNCH();
   }
 #ifdef HQ_DIAG
@@ -3740,6 +3741,690 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
                        out_resolved, count_empty ? 1 : 0, out_redo);
   HQ_CHECK_LAUNCH();
   if (out_det) return hq_rescore(Rq, Zq, Sq, Q, Rc, Zc, Sc, N, L, out_id, k, id_base, out_det, stream);
+  return HQ_OK;
+}
+
+
+// ================================================================================================
+// Overall-mode scan (brute_force_search, search_engine.py:302-338, scoring every candidate with
+// _calculate_overall_similarity :191-230): the approximate overall score of every (query, row) pair
+// from split-f16 contractions of every level segment, per-query pools as in k_scan0g, and the exact
+// re-rank (hq_refine_topk mode 1) on top.
+//   Layout (hq_seg_packov_split): the segments of >= 2 values ("G segments": one contraction each)
+//   are packed in order into K-blocks of 32 values without straddling a block (L = 64: [32 | 8, 3,
+//   20]; L = 32: [16, 4, 11]); each block's normalised values are split hi / lo in the tiled
+//   fragment layout of Z16 (a 16-row tile holds NKB x [hi 512 | lo 512] halves).  One-value segments
+//   always take the reference's constant branch (np.std of one value is 0): they need their value
+//   only.  Statistics Sov32, SoA groups of 4 rows: per G segment (std, mean, msq, zero-std flag)[4],
+//   per one-value segment value[4], row flags[4] (2: a G segment's mean of squares outside [2^-60,
+//   2^60], scored by k_scanov_flagged in f64; 4: pad row).
+//   Query side: one masked copy of the block fragment per G segment (values outside the segment
+//   zeroed), so each contraction D[row][query] is that segment's G alone.
+//   Pre-filter per pair (an upper bound of the f32 model score): a G segment scores at most
+//   be + max(G, 0) ia (k_scan0f's U(G) with sqrt(A^2 G^2 + B^2) <= A |G| + |B|: be = 0.35 + |B| /
+//   (2 sqrt Q), ia = c1 + A / (2 sqrt Q); a zero-variance candidate scores 0.1 <= be; a zero-variance
+//   query segment is bounded by be = 1, ia = 0), a one-value segment 1 when the two values are within
+//   1e-6 plus f32 slack, else 0.  Pairs whose weighted bound reaches the query's threshold are queued
+//   (per pair: the G of every segment) and drained 64 at a time: the f32 model score (k_scan0g's per
+//   level; constant branches decided exactly from the f64 means) and the pool append.
+// ================================================================================================
+constexpr int kOvMaxG = 4, kOvMaxC = 2, kOvMaxKB = 2;
+constexpr int kOvQW = 32;       // queries per wave of k_scanov (two 16-query blocks)
+constexpr int kOvQCap = 128;    // LDS queue entries per wave (< 64 before a ballot adds <= 64)
+
+struct OvLayout {
+  int nseg, ng, nc, nkb, lid;
+  int gseg[kOvMaxG], gkb[kOvMaxG], goff[kOvMaxG], gplen[kOvMaxG], gpoff[kOvMaxG];
+  int cseg[kOvMaxC];
+  float gw[kOvMaxG], gc1[kOvMaxG], gqa[kOvMaxG], cw[kOvMaxC];  // weight 1/(l+1), 0.35/m, 0.6/m
+  float inv_w;  // 1 / sum of weights (f32 model)
+};
+
+// compile-time K-block of each G segment, per supported layout id
+template <int LID> struct OvT;
+template <> struct OvT<0> {  // L = 64: [32 | 8, 3, 20], one one-value segment
+  static constexpr int NKB = 2, NG = 4, NC = 1;
+  static constexpr int kb(int i) { return i == 0 ? 0 : 1; }
+};
+template <> struct OvT<1> {  // L = 32: [16, 4, 11], one one-value segment
+  static constexpr int NKB = 1, NG = 3, NC = 1;
+  static constexpr int kb(int) { return 0; }
+};
+
+static bool ov_layout(int L, OvLayout& o) {
+  SegInfo si;
+  seg_info(L, si);
+  o.nseg = si.nseg;
+  o.ng = o.nc = o.nkb = 0;
+  o.lid = -1;
+  if (si.nseg == 0) return false;
+  int kb = 0, off = 0;
+  for (int s = 0; s < si.nseg; ++s) {
+    if (si.len[s] == 1) {
+      if (o.nc == kOvMaxC) return false;
+      o.cseg[o.nc] = s;
+      o.cw[o.nc] = (float)si.w[s];
+      ++o.nc;
+      continue;
+    }
+    if (si.plen[s] > 32 || o.ng == kOvMaxG) return false;
+    if (o.ng > 0 && off + si.plen[s] > 32) { ++kb; off = 0; }
+    if (kb >= kOvMaxKB) return false;
+    o.gseg[o.ng] = s; o.gkb[o.ng] = kb; o.goff[o.ng] = off; o.gplen[o.ng] = si.plen[s]; o.gpoff[o.ng] = si.poff[s];
+    o.gw[o.ng] = (float)si.w[s];
+    o.gc1[o.ng] = (float)(0.35 * si.inv_m[s]);
+    o.gqa[o.ng] = (float)(0.6 * si.inv_m[s]);
+    ++o.ng;
+    off += si.plen[s];
+  }
+  if (o.ng == 0) return false;
+  o.nkb = kb + 1;
+  o.inv_w = (float)(1.0 / si.wsum);
+  auto match = [&](int nkb, int ng, int nc, auto kbf) {
+    if (o.nkb != nkb || o.ng != ng || o.nc != nc) return false;
+    for (int i = 0; i < ng; ++i)
+      if (o.gkb[i] != kbf(i)) return false;
+    return true;
+  };
+  if (match(OvT<0>::NKB, OvT<0>::NG, OvT<0>::NC, [](int i) { return OvT<0>::kb(i); })) o.lid = 0;
+  else if (match(OvT<1>::NKB, OvT<1>::NG, OvT<1>::NC, [](int i) { return OvT<1>::kb(i); })) o.lid = 1;
+  return o.lid >= 0;
+}
+
+__host__ __device__ __forceinline__ int ov_gsize(int ng, int nc) { return 16 * ng + 4 * nc + 4; }
+// hi fragment (8 halves, k = 8 g .. 8 g + 7) of K-block kb of a row; lo at + kZ16Lo
+__host__ __device__ __forceinline__ int64_t ov_frag(int64_t row, int kb, int nkb, int g) {
+  return ((row >> 4) * nkb + kb) * kZ16Tile + ((g << 4) + (row & 15)) * 8;
+}
+
+__global__ void k_packov(const double* __restrict__ Z, const double* __restrict__ S, int64_t N, int Lp, OvLayout o,
+                         _Float16* __restrict__ Zo, float* __restrict__ So) {
+  const int64_t rows = z16_rows(N);
+  const int per = o.nkb * 32;
+  const int GS = ov_gsize(o.ng, o.nc);
+  const int64_t total = rows * per;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / per;
+    const int c = (int)(t % per), kb = c >> 5, k = c & 31;
+    double z = 0.0;
+    if (r < N)
+      for (int i = 0; i < o.ng; ++i)
+        if (o.gkb[i] == kb && k >= o.goff[i] && k < o.goff[i] + o.gplen[i]) z = Z[r * Lp + o.gpoff[i] + (k - o.goff[i])];
+    const _Float16 hi = (_Float16)z;
+    const _Float16 lo = (_Float16)(z - (double)hi);
+    const int64_t e = ov_frag(r, kb, o.nkb, k >> 3) + (k & 7);
+    Zo[e] = hi;
+    Zo[e + kZ16Lo] = lo;
+    if (c == 0 && r < pack0_rows(N)) {
+      float* gp = So + (r >> 2) * GS + (r & 3);
+      int flag = 4;
+      if (r < N) {
+        flag = 0;
+        for (int i = 0; i < o.ng; ++i) {
+          const double* st = S + (r * o.nseg + o.gseg[i]) * 4;
+          const double mean = st[0], sd = st[1], msq = st[2];
+          gp[16 * i] = (float)sd;
+          gp[16 * i + 4] = (float)mean;
+          gp[16 * i + 8] = (float)msq;
+          gp[16 * i + 12] = __int_as_float(sd == 0.0 ? 1 : 0);
+          if (sd != 0.0 && !(msq >= 0x1p-60 && msq <= 0x1p60)) flag |= 2;
+        }
+        for (int ci = 0; ci < o.nc; ++ci) gp[16 * o.ng + 4 * ci] = (float)S[(r * o.nseg + o.cseg[ci]) * 4];
+      } else {
+        for (int i = 0; i < o.ng; ++i) {
+          gp[16 * i] = 0.0f; gp[16 * i + 4] = 0.0f; gp[16 * i + 8] = 1.0f; gp[16 * i + 12] = __int_as_float(1);
+        }
+        for (int ci = 0; ci < o.nc; ++ci) gp[16 * o.ng + 4 * ci] = 0.0f;
+      }
+      gp[16 * o.ng + 4 * o.nc] = __int_as_float(flag);
+    }
+  }
+}
+
+// per-query constants of the overall scan (k_ov_qconst, from the query's Sov32 statistics and its
+// starting threshold)
+struct QOv {
+  float thl, flag, wthr, tol;          // pool threshold (f32 lower bound), flags, pre-filter bound, 1e-6 + slack
+  float ia[kOvMaxG], be[kOvMaxG];      // pre-filter: level <= be + max(G, 0) ia
+  float qA[kOvMaxG], qB[kOvMaxG], qQ[kOvMaxG], qz[kOvMaxG];  // model constants; qz != 0: zero variance
+  float cv[kOvMaxC], pad[2];           // one-value segments: the query's value
+};
+
+__global__ void k_ov_qconst(const float* __restrict__ Sq, int Q, OvLayout o, const double* __restrict__ th0,
+                            double thr0, QOv* __restrict__ qc) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  const int GS = ov_gsize(o.ng, o.nc);
+  const float* gp = Sq + (int64_t)(q >> 2) * GS + (q & 3);
+  QOv c;
+  double t0 = thr0;
+  if (th0 && th0[q] > t0) t0 = th0[q];
+  c.thl = lower_f32(t0);
+  c.flag = gp[16 * o.ng + 4 * o.nc];
+  // pre-filter bound on the weighted sum, with slack for the f32 evaluation of bound and model
+  c.wthr = t0 > -__builtin_huge_val() ? (c.thl - 1e-4f) / o.inv_w - 1e-4f : -__builtin_huge_valf();
+  for (int i = 0; i < kOvMaxG; ++i) {
+    c.ia[i] = 0.0f; c.be[i] = 0.0f; c.qA[i] = 0.0f; c.qB[i] = 0.0f; c.qQ[i] = 1.0f; c.qz[i] = 1.0f;
+  }
+  for (int i = 0; i < o.ng; ++i) {
+    const float sd = gp[16 * i], mn = gp[16 * i + 4], ms = gp[16 * i + 8];
+    const bool z = __float_as_int(gp[16 * i + 12]) != 0;
+    c.qA[i] = o.gqa[i] * sd;
+    c.qB[i] = 0.6f * mn;
+    c.qQ[i] = ms;
+    c.qz[i] = z ? 1.0f : 0.0f;
+    if (z) {
+      c.ia[i] = 0.0f;
+      c.be[i] = 1.0f;
+    } else {
+      const float h = 0.5f / sqrtf(ms);
+      c.ia[i] = (o.gc1[i] + c.qA[i] * h) * (1.0f + 1e-5f);
+      c.be[i] = (0.35f + fabsf(c.qB[i]) * h) * (1.0f + 1e-5f) + 1e-6f;
+    }
+  }
+  c.tol = 1e-6f;
+  for (int ci = 0; ci < kOvMaxC; ++ci) c.cv[ci] = ci < o.nc ? gp[16 * o.ng + 4 * ci] : 0.0f;
+  c.pad[0] = c.pad[1] = 0.0f;
+  qc[q] = c;
+}
+
+// the f32 model overall score of one pair (G of each G segment given), or -1 when the row is not scored
+// here (flagged: k_scanov_flagged; pad).  Constant branches are decided from the f64 means exactly as
+// const0; the one-value segments compare the f32 values first and fall back to f64 near the edge.
+template <int NG, int NC>
+__device__ __forceinline__ float ov_model(const OvLayout& o, const QOv& c, const float* __restrict__ Sc32, int64_t row,
+                                          const float* G, const double* __restrict__ Sq, const double* __restrict__ Sc,
+                                          int q) {
+  constexpr int GS = 16 * NG + 4 * NC + 4;
+  const float* gp = Sc32 + (row >> 2) * GS + (row & 3);
+  if (__float_as_int(gp[16 * NG + 4 * NC]) != 0) return -1.0f;
+  const double* sq = Sq + (int64_t)q * o.nseg * 4;
+  const double* sc = Sc + row * o.nseg * 4;
+  float tw = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    float lvl;
+    const bool cz = __float_as_int(gp[16 * i + 12]) != 0;
+    if (c.qz[i] != 0.0f || cz) {
+      const int s = o.gseg[i];
+      lvl = (float)const0(c.qz[i] != 0.0f, cz, sq[4 * s], sc[4 * s], (aux_bits(sq + 4 * s) & aux_bits(sc + 4 * s) & kAuxF32) != 0);
+    } else {
+      const float num = fmaf(G[i], c.qA[i] * gp[16 * i], c.qB[i] * gp[16 * i + 4]);
+      float t = num * __builtin_amdgcn_rcpf(c.qQ[i] + gp[16 * i + 8]);
+      t = t > 0.0f ? t : 0.0f;
+      lvl = fmaf(G[i], o.gc1[i], 0.35f) + t;
+      lvl = lvl < 1.0f ? lvl : 1.0f;
+      lvl = lvl > 0.0f ? lvl : 0.0f;
+    }
+    tw = fmaf(o.gw[i], lvl, tw);
+  }
+#pragma unroll
+  for (int ci = 0; ci < NC; ++ci) {
+    const float cv = gp[16 * NG + 4 * ci];
+    const float d = fabsf(c.cv[ci] - cv), sl = 2.5e-7f * (fabsf(c.cv[ci]) + fabsf(cv)) + 1e-12f;
+    float lvl;
+    if (d > 1e-6f + sl) lvl = 0.0f;
+    else if (d < 1e-6f - sl) lvl = 1.0f;
+    else {
+      const int s = o.cseg[ci];
+      lvl = (float)const0(true, true, sq[4 * s], sc[4 * s], (aux_bits(sq + 4 * s) & aux_bits(sc + 4 * s) & kAuxF32) != 0);
+    }
+    tw = fmaf(o.cw[ci], lvl, tw);
+  }
+  float s = tw * o.inv_w;
+  s = s < 1.0f ? s : 1.0f;
+  return s > 0.0f ? s : 0.0f;
+}
+
+struct OvArgs {
+  const _Float16* Zq; const float* Sq32; const double* Sq; int Q;
+  const _Float16* Zc; const float* Sc32; const double* Sc; int64_t N;
+  OvLayout o;
+  const QOv* qc;
+  int64_t chunk_len; int nchunks; int nqb;
+  float* pool_s; int* pool_i; int* pool_n; int pool_cap;
+  int64_t stride, S; float* top;  // sample pass
+  const double* Zq64; const double* Zc64; int Lp;  // k_scanov_flagged: the f64 normalised vectors
+};
+
+struct QEOv {
+  flt4 g;        // G of each G segment
+  int qi, row;   // query within the wave, row
+  int pad0, pad1;
+};
+
+// masked query fragments of one 16-query block: hi / lo of G segment i, values outside it zeroed
+template <class T>
+__device__ __forceinline__ void ov_query_frags(const OvArgs& a, int q, int g, half8* qh, half8* ql) {
+#pragma unroll
+  for (int i = 0; i < T::NG; ++i) {
+    const _Float16* zr = a.Zq + ov_frag(q, T::kb(i), T::NKB, g);
+    half8 h = *reinterpret_cast<const half8*>(zr);
+    half8 l = *reinterpret_cast<const half8*>(zr + kZ16Lo);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * g + e;
+      if (k < a.o.goff[i] || k >= a.o.goff[i] + a.o.gplen[i]) {
+        h[e] = (_Float16)0.0f;
+        l[e] = (_Float16)0.0f;
+      }
+    }
+    qh[i] = h;
+    ql[i] = l;
+  }
+}
+
+// weighted pre-filter bound of the lane's four rows (r) for one query block
+template <class T>
+__device__ __forceinline__ void ov_bound(const flt4* acc, const float* ia, const float* be, const OvLayout& o,
+                                         const float* qv, float tol, const flt4* cvv, float* U) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float u = 0.0f;
+#pragma unroll
+    for (int i = 0; i < T::NG; ++i) u = fmaf(o.gw[i], fmaf(fmaxf(acc[i][r], 0.0f), ia[i], be[i]), u);
+#pragma unroll
+    for (int ci = 0; ci < T::NC; ++ci) {
+      const float d = fabsf(qv[ci] - cvv[ci][r]);
+      u += d <= fmaf(2.5e-7f, fabsf(qv[ci]) + fabsf(cvv[ci][r]), tol) ? o.cw[ci] : 0.0f;
+    }
+    U[r] = u;
+  }
+}
+
+// One wave = 32 queries (two blocks b of 16; lane (g, j) owns queries 16b + j) x one chunk, 16 rows per
+// step (lane group g owns rows 4g + r: the MFMA D layout), NG x 3 MFMAs per block and step.
+template <int LID>
+__global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
+  using T = OvT<LID>;
+  constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, NB = kOvQW / 16, GS = 16 * NG + 4 * NC + 4;
+  __shared__ QEOv qe[kOvQCap];
+  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
+  const int chunk = xcd + 8 * (slot / a.nqb);
+  const int qb = slot % a.nqb;
+  if (chunk >= a.nchunks) return;
+  const int64_t c_begin = (int64_t)chunk * a.chunk_len;
+  if (c_begin >= a.N) return;
+  int64_t c_end = c_begin + a.chunk_len;
+  if (c_end > a.N) c_end = a.N;
+  const int q0 = qb * kOvQW;
+  const OvLayout& o = a.o;
+
+  half8 qh[NB][NG], ql[NB][NG];
+  float ia[NB][NG], be[NB][NG], wt[NB], qv[NB][NC > 0 ? NC : 1], tol[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int q = q0 + 16 * b + j;
+    const bool v = q < a.Q;
+    const int qq = v ? q : 0;
+    ov_query_frags<T>(a, qq, g, qh[b], ql[b]);
+    const QOv& c = a.qc[qq];
+#pragma unroll
+    for (int i = 0; i < NG; ++i) { ia[b][i] = c.ia[i]; be[b][i] = c.be[i]; }
+#pragma unroll
+    for (int ci = 0; ci < NC; ++ci) qv[b][ci] = c.cv[ci];
+    tol[b] = c.tol;
+    wt[b] = (v && __float_as_int(c.flag) == 0) ? c.wthr : __builtin_huge_valf();  // flagged query: dense path
+  }
+
+  const _Float16* zb = a.Zc + (c_begin >> 4) * NKB * kZ16Tile + lane * 8;
+  const float* sb = a.Sc32 + (c_begin >> 2) * GS + 16 * NG;  // one-value segment values of the step's first group
+  struct CStep {
+    half8 f[NKB][2];
+    flt4 cv[NC > 0 ? NC : 1];
+  };
+  const int64_t nsteps = (c_end - c_begin + kCS - 1) / kCS;
+  auto load_step = [&](CStep& c, int64_t s) {
+    s = s < nsteps ? s : nsteps - 1;  // the prefetch stays inside the chunk
+    const _Float16* p = zb + s * (NKB * kZ16Tile);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      c.f[kb][0] = *reinterpret_cast<const half8*>(p + kb * kZ16Tile);
+      c.f[kb][1] = *reinterpret_cast<const half8*>(p + kb * kZ16Tile + kZ16Lo);
+    }
+    const float* sp = sb + (s * 4 + g) * GS;
+#pragma unroll
+    for (int ci = 0; ci < NC; ++ci) c.cv[ci] = *reinterpret_cast<const flt4*>(sp + 4 * ci);
+  };
+
+  int qn = 0;
+  auto drain = [&](const int n) {
+    if (lane < n) {
+      const flt4 eg = qe[lane].g;
+      const int eqi = qe[lane].qi, row = qe[lane].row;
+      const int q = q0 + eqi;
+      const QOv c = a.qc[q];
+      if (row < c_end) {
+        const float G[4] = {eg[0], eg[1], eg[2], eg[3]};
+        const float s = ov_model<NG, NC>(o, c, a.Sc32, row, G, a.Sq, a.Sc, q);
+        if (s >= c.thl) {
+          const int slot = atomicAdd(a.pool_n + q, 1);
+          if (slot < a.pool_cap) {
+            a.pool_s[(int64_t)q * a.pool_cap + slot] = s;
+            a.pool_i[(int64_t)q * a.pool_cap + slot] = row;
+          }
+        }
+      }
+    }
+    wave_lds_sync();
+    for (int b0 = n; b0 < qn; b0 += 64) {
+      const bool mv = b0 + lane < qn;
+      flt4 tg = {0.0f, 0.0f, 0.0f, 0.0f};
+      int tq = 0, tr = 0;
+      if (mv) {
+        tg = qe[b0 + lane].g;
+        tq = qe[b0 + lane].qi;
+        tr = qe[b0 + lane].row;
+      }
+      wave_lds_sync();
+      if (mv) {
+        qe[b0 - n + lane].g = tg;
+        qe[b0 - n + lane].qi = tq;
+        qe[b0 - n + lane].row = tr;
+      }
+      wave_lds_sync();
+    }
+    qn -= n;
+  };
+  // one block of one step: contractions, bound, queue the passing pairs
+  auto block = [&](const int b, const CStep& cur, const int64_t cs) {
+    flt4 acc[NG];
+#pragma unroll
+    for (int i = 0; i < NG; ++i)
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.f[T::kb(i)][0], qh[b][i], flt4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NG; ++i)
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.f[T::kb(i)][0], ql[b][i], acc[i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NG; ++i)
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.f[T::kb(i)][1], qh[b][i], acc[i], 0, 0, 0);
+    float U[4];
+    ov_bound<T>(acc, ia[b], be[b], o, qv[b], tol[b], cur.cv, U);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const unsigned long long m = __builtin_amdgcn_ballot_w64(U[r] >= wt[b]);
+      if (m) {
+        if ((m >> lane) & 1ull) {
+          const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+          flt4 gg = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+          for (int i = 0; i < NG; ++i) gg[i] = acc[i][r];
+          qe[pos].g = gg;
+          qe[pos].qi = 16 * b + j;
+          qe[pos].row = (int)(cs + 4 * g + r);
+        }
+        qn += __popcll(m);
+        if (qn >= 64) {
+          wave_lds_sync();
+          while (qn >= 64) drain(64);  // keeps qn < 64 before each ballot: the queue never exceeds 127
+        }
+      }
+    }
+  };
+
+  CStep cA, cB;
+  load_step(cA, 0);
+  int64_t s = 0;
+  for (; s + 1 < nsteps; s += 2) {
+    load_step(cB, s + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) block(b, cA, c_begin + s * kCS);
+    load_step(cA, s + 2);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) block(b, cB, c_begin + (s + 1) * kCS);
+  }
+  if (s < nsteps)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) block(b, cA, c_begin + s * kCS);
+  wave_lds_sync();
+  while (qn > 0) drain(qn < 64 ? qn : 64);
+}
+
+// Sample pass of the overall scan (as k_sample_topg): 16 queries per wave, whole sample tiles; per lane
+// the step whose four rows hold the largest pre-filter bound is kept and its rows are scored with the
+// model in the epilogue; the stream's kTopT best go to the pool for k_sample_kth.
+template <int LID>
+__global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
+  using T = OvT<LID>;
+  constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, GS = 16 * NG + 4 * NC + 4;
+  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
+  const int chunk = xcd + 8 * (slot / a.nqb);
+  const int qb = slot % a.nqb;
+  if (chunk >= a.nchunks) return;
+  const int64_t c_begin = (int64_t)chunk * a.chunk_len;
+  int64_t c_end = c_begin + a.chunk_len;
+  if (c_end > a.S) c_end = a.S;
+  const OvLayout& o = a.o;
+  const int q = qb * 16 + j;
+  const bool qv_ok = q < a.Q;
+  const int qq = qv_ok ? q : 0;
+  half8 qh[NG], ql[NG];
+  ov_query_frags<T>(a, qq, g, qh, ql);
+  const QOv c = a.qc[qq];
+  auto row_of = [&](int64_t i) -> int64_t { return sample_row_tiled(i, a.S, a.stride); };
+  auto load = [&](int64_t cs, half8 (*f)[2], flt4* cv) {
+    const int64_t row = row_of(cs + j);  // tile-aligned: the step is one corpus tile
+    const _Float16* p = a.Zc + ov_frag(row, 0, NKB, g);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      f[kb][0] = *reinterpret_cast<const half8*>(p + kb * kZ16Tile);
+      f[kb][1] = *reinterpret_cast<const half8*>(p + kb * kZ16Tile + kZ16Lo);
+    }
+    const int64_t r0 = row_of(cs + 4 * g);
+    const float* sp = a.Sc32 + (r0 >> 2) * GS + 16 * NG;
+#pragma unroll
+    for (int ci = 0; ci < NC; ++ci) cv[ci] = *reinterpret_cast<const flt4*>(sp + 4 * ci);
+  };
+  float bu = -__builtin_huge_valf();
+  flt4 bg[NG];
+  int bcs = -1;
+#pragma unroll
+  for (int i = 0; i < NG; ++i) bg[i] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
+  half8 f0[NKB][2], f1[NKB][2];
+  flt4 v0[NC > 0 ? NC : 1], v1[NC > 0 ? NC : 1];
+  load(c_begin, f0, v0);
+  for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
+    load(cs + kCS, f1, v1);
+    flt4 acc[NG];
+#pragma unroll
+    for (int i = 0; i < NG; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[T::kb(i)][0], qh[i], flt4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NG; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[T::kb(i)][0], ql[i], acc[i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NG; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[T::kb(i)][1], qh[i], acc[i], 0, 0, 0);
+    float U[4];
+    float qvv[NC > 0 ? NC : 1];
+#pragma unroll
+    for (int ci = 0; ci < NC; ++ci) qvv[ci] = c.cv[ci];
+    ov_bound<T>(acc, c.ia, c.be, o, qvv, c.tol, v0, U);
+    float m = -__builtin_huge_valf();
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (cs + 4 * g + r < c_end) m = fmaxf(m, U[r]);
+    const bool up = m > bu;
+    bu = up ? m : bu;
+    bcs = up ? (int)cs : bcs;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) bg[i] = up ? acc[i] : bg[i];
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) { f0[kb][0] = f1[kb][0]; f0[kb][1] = f1[kb][1]; }
+#pragma unroll
+    for (int ci = 0; ci < NC; ++ci) v0[ci] = v1[ci];
+  }
+  if (!qv_ok) return;
+  float top[kTopT];
+#pragma unroll
+  for (int t = 0; t < kTopT; ++t) top[t] = -1.0f;
+  if (__float_as_int(c.flag) == 0 && bcs >= 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t i = (int64_t)bcs + 4 * g + r;
+      if (i >= c_end) continue;
+      float G[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s = 0; s < NG; ++s) G[s] = bg[s][r];
+      float sc = ov_model<NG, NC>(o, c, a.Sc32, row_of(i), G, a.Sq, a.Sc, q);
+      if (sc < 0.0f) continue;
+#pragma unroll
+      for (int u = 0; u < kTopT; ++u) {
+        const float hi = fmaxf(top[u], sc);
+        sc = fminf(top[u], sc);
+        top[u] = hi;
+      }
+    }
+  }
+  float* out = a.top + ((int64_t)q * 4 * a.nchunks + 4 * chunk + g) * kTopT;
+#pragma unroll
+  for (int t = 0; t < kTopT; ++t) out[t] = top[t];
+}
+
+// rows of the overall copies with the f32-unsafe flag (row flags bit 2), compacted into list[*count]
+__global__ __launch_bounds__(256) void k_ov_flag_rows(const float* __restrict__ So, int64_t N, int GS, int foff,
+                                                      int* __restrict__ list, int* __restrict__ count) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < N; r += (int64_t)gridDim.x * blockDim.x)
+    if (__float_as_int(So[(r >> 2) * GS + foff + (r & 3)]) & 2) list[atomicAdd(count, 1)] = (int)r;
+}
+
+// the flagged rows against every scanned query (lane = query): the overall score in f64 from the f64
+// normalised vectors (level_sim per segment), appended to the pools when it reaches the threshold
+__global__ __launch_bounds__(64) void k_scanov_flagged(OvArgs a, SegInfo si, const int* __restrict__ list,
+                                                       const int* __restrict__ count) {
+  const int n = *count;
+  const int q = blockIdx.y * 64 + threadIdx.x;
+  if (q >= a.Q || n == 0) return;
+  const QOv c = a.qc[q];
+  if (__float_as_int(c.flag) != 0) return;
+  const double* sq = a.Sq + (int64_t)q * si.nseg * 4;
+  const double* zq = a.Zq64 + (int64_t)q * a.Lp;
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const int row = list[i];
+    const double* sc = a.Sc + (int64_t)row * si.nseg * 4;
+    const double* zc = a.Zc64 + (int64_t)row * a.Lp;
+    double tws = 0.0;
+    for (int s = 0; s < si.nseg; ++s) {
+      double G = 0.0;
+      for (int k = si.poff[s]; k < si.poff[s] + si.plen[s]; ++k) G = fma(zq[k], zc[k], G);
+      const double v = level_sim(G, sq[4 * s], sq[4 * s + 1], sq[4 * s + 2], sc[4 * s], sc[4 * s + 1], sc[4 * s + 2],
+                                 (double)si.len[s], si.inv_m[s], (aux_bits(sq + 4 * s) & aux_bits(sc + 4 * s) & kAuxF32) != 0);
+      tws = tws + v * si.w[s];
+    }
+    double ov = tws / si.wsum;
+    ov = ov < 1.0 ? ov : 1.0;
+    ov = ov > 0.0 ? ov : 0.0;
+    const float sv = (float)ov;
+    if (sv >= c.thl) {
+      const int slot = atomicAdd(a.pool_n + q, 1);
+      if (slot < a.pool_cap) {
+        a.pool_s[(int64_t)q * a.pool_cap + slot] = sv;
+        a.pool_i[(int64_t)q * a.pool_cap + slot] = row;
+      }
+    }
+  }
+}
+
+// grid of k_scanov / k_sampleov: ~waves waves of qw queries, chunks a multiple of 8 (XCD map) and of 16 rows
+static void ov_geometry(int Q, int64_t rows, int qw, int waves, int max_chunks, int& nqb, int& nchunks,
+                        int64_t& chunk_len) {
+  nqb = (Q + qw - 1) / qw;
+  int64_t target = (waves + nqb - 1) / nqb;
+  const int64_t steps = (rows + kCS - 1) / kCS;
+  if (target > steps) target = steps;
+  if (target > max_chunks) target = max_chunks;
+  nchunks = (int)(((target + 7) / 8) * 8);
+  if (nchunks < 8) nchunks = 8;
+  chunk_len = (rows + nchunks - 1) / nchunks;
+  chunk_len = ((chunk_len + kCS - 1) / kCS) * kCS;
+  if (chunk_len < kCS) chunk_len = kCS;
+}
+
+struct OvPlan {
+  int nqb, nchunks, s_nqb, s_nchunks;
+  int64_t chunk_len, s_chunk_len, stride, S;
+  int pool_cap;
+  size_t off_pool_i, off_pool_n, off_th0, off_top, off_qc, off_flag, total;
+};
+
+static OvPlan ov_plan(int Q, int64_t N, int k) {
+  OvPlan p;
+  ov_geometry(Q, N, kOvQW, 3072, 1 << 20, p.nqb, p.nchunks, p.chunk_len);
+  const int64_t sd = opt(OPT_SAMPLE_STRIDE, 16) > 0 ? opt(OPT_SAMPLE_STRIDE, 16) : 16;
+  p.stride = N >= sd * 4096 ? sd : (N / 4096 > 1 ? N / 4096 : 1);
+  p.S = sample_rows_tiled(N, p.stride);
+  ov_geometry(Q, p.S, 16, 4096, 64 * kKthReg / (4 * kTopT), p.s_nqb, p.s_nchunks, p.s_chunk_len);
+  p.pool_cap = p.nchunks * k;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t o = al((size_t)Q * p.pool_cap * 4);
+  p.off_pool_i = 0 + o;
+  o = al(o + (size_t)Q * p.pool_cap * 4);
+  p.off_pool_n = o;
+  o = al(o + (size_t)Q * 4);
+  p.off_th0 = o;
+  o = al(o + (size_t)Q * 8);
+  p.off_top = o;
+  o = al(o + (size_t)Q * 4 * p.s_nchunks * kTopT * 4);
+  p.off_qc = o;
+  o = al(o + (size_t)Q * sizeof(QOv));
+  p.off_flag = o;
+  o = al(o + 256 + (size_t)N * 4);
+  p.total = o;
+  return p;
+}
+
+template <int LID>
+static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k, double thr0, int sample_kth,
+                     int64_t id_base, uint8_t* ws, double* out_score, int64_t* out_id, hipStream_t s) {
+  OvArgs a = a0;
+  const int Q = a.Q;
+  a.pool_cap = p.pool_cap;
+  a.pool_s = reinterpret_cast<float*>(ws);
+  a.pool_i = reinterpret_cast<int*>(ws + p.off_pool_i);
+  a.pool_n = reinterpret_cast<int*>(ws + p.off_pool_n);
+  double* th0 = reinterpret_cast<double*>(ws + p.off_th0);
+  QOv* qc = reinterpret_cast<QOv*>(ws + p.off_qc);
+  int* flag_n = reinterpret_cast<int*>(ws + p.off_flag);
+  int* flag_list = flag_n + 64;
+  a.qc = qc;
+  // sample pass: per-query constants without a threshold, the G-selected sample, K'-th best
+  hipLaunchKernelGGL(k_ov_qconst, dim3((Q + 255) / 256), dim3(256), 0, s, a.Sq32, Q, a.o, (const double*)nullptr,
+                     -__builtin_huge_val(), qc);
+  HQ_CHECK_LAUNCH();
+  OvArgs sa = a;
+  sa.stride = p.stride;
+  sa.S = p.S;
+  sa.nqb = p.s_nqb;
+  sa.nchunks = p.s_nchunks;
+  sa.chunk_len = p.s_chunk_len;
+  sa.top = reinterpret_cast<float*>(ws + p.off_top);
+  hipLaunchKernelGGL(k_sampleov<LID>, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
+  HQ_CHECK_LAUNCH();
+  const int mg = Q < 8192 ? Q : 8192;
+  hipLaunchKernelGGL(k_sample_kth, dim3(mg), dim3(64), 0, s, (const float*)sa.top, 4 * sa.nchunks, Q, sample_kth,
+                     (double)kMarginF, th0, (unsigned long long*)nullptr, a.pool_n, (const float*)nullptr, thr0, 0.0,
+                     (QConst*)nullptr);
+  HQ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_ov_qconst, dim3((Q + 255) / 256), dim3(256), 0, s, a.Sq32, Q, a.o, (const double*)th0, thr0, qc);
+  HQ_CHECK_LAUNCH();
+  // flagged rows (normally none), the scan, the pools' exact top k
+  HQ_CHECK_HIP(hipMemsetAsync(flag_n, 0, sizeof(int), s));
+  const int64_t fb = (a.N + 255) / 256;
+  const int GS = ov_gsize(a.o.ng, a.o.nc);
+  hipLaunchKernelGGL(k_ov_flag_rows, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, s, a.Sc32, a.N, GS,
+                     16 * a.o.ng + 4 * a.o.nc, flag_list, flag_n);
+  HQ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_scanov<LID>, dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  HQ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_scanov_flagged, dim3(64, (Q + 63) / 64), dim3(64), 0, s, a, si, (const int*)flag_list,
+                     (const int*)flag_n);
+  HQ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_pool_select, dim3(mg), dim3(64), 0, s, (const float*)a.pool_s, (const int*)a.pool_i,
+                     (const int*)a.pool_n, a.pool_cap, Q, k, id_base, out_score, out_id,
+                     sample_kth < k ? (const double*)th0 : (const double*)nullptr, thr0, &qc[0].flag,
+                     (int)(sizeof(QOv) / 4));
+  HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
 
@@ -4180,6 +4865,74 @@ int hq_cosine_scores(const float* a, int Q, const float* b, int64_t N, int K, do
   hipLaunchKernelGGL(k_cosine, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, a, Q, b, N, K, out);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
+}
+
+
+/* ---- overall-mode scan (split-f16 copies of every level segment) ------------------------------ */
+int hq_seg_packov_info(int L, int* nkb, int* ng, int* nc, int* group_floats) {
+  OvLayout o;
+  if (L <= 0 || !ov_layout(L, o)) return fail(HQ_E_UNSUPPORTED, "no split overall layout for L=%d", L);
+  if (nkb) *nkb = o.nkb;
+  if (ng) *ng = o.ng;
+  if (nc) *nc = o.nc;
+  if (group_floats) *group_floats = ov_gsize(o.ng, o.nc);
+  return HQ_OK;
+}
+
+int hq_seg_packov_split(const double* Z, const double* S, int64_t N, int L, void* Zo16, float* So32,
+                        hq_stream_t stream) {
+  if (L <= 0 || N < 0) return fail(HQ_E_INVALID, "bad shape N=%lld L=%d", (long long)N, L);
+  if ((N > 0 && (!Z || !S)) || !Zo16 || !So32) return fail(HQ_E_INVALID, "null buffer");
+  if (N >= 0x7FFFFFFF) return fail(HQ_E_UNSUPPORTED, "N=%lld rows (int32 row ids)", (long long)N);
+  OvLayout o;
+  if (!ov_layout(L, o)) return fail(HQ_E_UNSUPPORTED, "no split overall layout for L=%d", L);
+  SegInfo si;
+  seg_info(L, si);
+  int64_t blocks = (z16_rows(N) * o.nkb * 32 + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(k_packov, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, Z, S, N, si.Lp, o,
+                     reinterpret_cast<_Float16*>(Zo16), So32);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
+size_t hq_scanov_workspace_size(int Q, int64_t N, int k) {
+  if (Q <= 0 || N <= 0 || k <= 0) return 256;
+  return ov_plan(Q, N, k).total;
+}
+
+int hq_scanov_topk_split(const void* Zq16, const float* Sq32, const double* Sq, const double* Zq, int Q,
+                         const void* Zc16, const float* Sc32, const double* Sc, const double* Zc, int64_t N, int L,
+                         int k, double threshold, int thr_mode, int64_t id_base, void* workspace,
+                         size_t workspace_bytes, double* out_score, int64_t* out_id, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || L <= 0) return fail(HQ_E_INVALID, "bad shape");
+  if (k <= 0 || k > kMaxTopK) return fail(HQ_E_UNSUPPORTED, "k=%d (1..%d)", k, kMaxTopK);
+  if (Q == 0) return HQ_OK;
+  if (!out_score || !out_id) return fail(HQ_E_INVALID, "null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  if (N == 0) {
+    HQ_CHECK_HIP(hipMemsetAsync(out_id, 0xFF, sizeof(int64_t) * Q * k, s));
+    return HQ_OK;
+  }
+  if (N >= 0x7FFFFFFF) return fail(HQ_E_UNSUPPORTED, "N=%lld rows (int32 row ids)", (long long)N);
+  if (!Zq16 || !Sq32 || !Sq || !Zq || !Zc16 || !Sc32 || !Sc || !Zc || !workspace) return fail(HQ_E_INVALID, "null buffer");
+  if (workspace_bytes < hq_scanov_workspace_size(Q, N, k)) return fail(HQ_E_INVALID, "workspace too small");
+  OvArgs a;
+  if (!ov_layout(L, a.o)) return fail(HQ_E_UNSUPPORTED, "no split overall layout for L=%d", L);
+  SegInfo si;
+  seg_info(L, si);
+  const OvPlan p = ov_plan(Q, N, k);
+  a.Zq = reinterpret_cast<const _Float16*>(Zq16); a.Sq32 = Sq32; a.Sq = Sq; a.Q = Q;
+  a.Zc = reinterpret_cast<const _Float16*>(Zc16); a.Sc32 = Sc32; a.Sc = Sc; a.N = N;
+  a.Zq64 = Zq; a.Zc64 = Zc; a.Lp = si.Lp;
+  a.nqb = p.nqb; a.nchunks = p.nchunks; a.chunk_len = p.chunk_len;
+  a.stride = p.stride; a.S = p.S; a.top = nullptr; a.qc = nullptr;
+  int sample_kth = (int)opt(OPT_SAMPLE_KTH, kSampleKth);
+  if (sample_kth <= 0 || sample_kth > k || p.stride < 16) sample_kth = k;
+  const double thr0 = thr_mode == 0 ? -__builtin_huge_val() : threshold;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
+  if (a.o.lid == 0) return ov_launch<0>(a, p, si, k, thr0, sample_kth, id_base, ws, out_score, out_id, s);
+  return ov_launch<1>(a, p, si, k, thr0, sample_kth, id_base, ws, out_score, out_id, s);
 }
 
 }  // extern "C"

@@ -241,7 +241,7 @@ class Prepared:
     normalised) and stats S [N, nseg, 4] (mean, std, mean of squares, aux).  Built once per corpus.
     f32: some rows are float32 index vectors (aux bit 1; hq_seg_prepare_src / _rows)."""
 
-    __slots__ = ("R", "Z", "S", "L", "N", "nseg", "Lp", "Z16", "S32", "f32", "all32")
+    __slots__ = ("R", "Z", "S", "L", "N", "nseg", "Lp", "Z16", "S32", "Zov16", "Sov32", "f32", "all32")
 
     def __init__(self, R, Z, S, L, f32: bool = False, all32: bool = False):
         self.R, self.Z, self.S, self.L = R, Z, S, int(L)
@@ -251,12 +251,14 @@ class Prepared:
         self.f32 = bool(f32)      # some rows are float32 sources
         self.all32 = bool(all32)  # every row is
         self.Z16 = self.S32 = None  # split-f16 level-0 copies for the level-0 scan (pack0)
+        self.Zov16 = self.Sov32 = None  # split-f16 copies of every level for the overall scan (packov)
 
     def rows(self, sel):
         """Sub-set of rows (device index tensor) as a new Prepared (level-0 copies re-packed on demand)."""
         p = Prepared(self.R.index_select(0, sel), self.Z.index_select(0, sel), self.S.index_select(0, sel), self.L,
                      self.f32, self.all32)
-        return pack0(p) if self.Z16 is not None else p
+        p = pack0(p) if self.Z16 is not None else p
+        return packov(p) if self.Zov16 is not None else p
 
     def unsafe_rows(self):
         """Device bool [N]: float32 rows outside the scans' model (aux bit 2, hq_mi355x.h) -> dense exact path."""
@@ -286,6 +288,31 @@ def seg_prepare(idx, exc=None, src_f32: bool = False, row_f32=None) -> Prepared:
 
 
 PAD0 = 48  # pad rows of the level-0 copies (hq_mi355x.h: hq_seg_pack0_split)
+
+
+@functools.lru_cache(maxsize=None)
+def packov_info(L: int):
+    """(K-blocks, G segments, one-value segments, floats per 4-row statistics group) of the split
+    overall layout (hq_seg_packov_info), or None when the level structure of L has none."""
+    v = [ctypes.c_int() for _ in range(4)]
+    if _lib.load().hq_seg_packov_info(int(L), *[ctypes.byref(x) for x in v]) != 0:
+        return None
+    return tuple(x.value for x in v)
+
+
+def packov(p: Prepared, exc=None) -> Prepared:
+    """Attach the split-f16 copies of every level segment (hq_seg_packov_split) used by the overall
+    (brute-force) scan; level structures without a split layout keep the f64 scan."""
+    t = torch()
+    info = packov_info(p.L)
+    if info is None:
+        return p
+    nkb, _, _, gs = info
+    rows = (p.N + 15) // 16 * 16 + PAD0
+    p.Zov16 = t.empty((rows, nkb * 64), dtype=t.float16, device=p.Z.device)  # tiled: 16-row tiles of nkb x 2 KiB
+    p.Sov32 = t.empty(((p.N + 3) // 4 + PAD0 // 4, gs), dtype=t.float32, device=p.Z.device)  # SoA groups of 4 rows
+    _chk(_L().hq_seg_packov_split(ptr(p.Z), ptr(p.S), p.N, p.L, ptr(p.Zov16), ptr(p.Sov32), stream()), exc)
+    return p
 
 
 def pack0(p: Prepared, exc=None) -> Prepared:
@@ -345,6 +372,15 @@ def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.
         _chk(_L().hq_scan0_topk_split(ptr(q.Z16), ptr(q.S32), ptr(q.S), Q, ptr(c.Z16), ptr(c.S32), ptr(c.S), N, c.L,
                                       k, float(threshold), thr_mode, int(id_base), ptr(ws), ws_bytes, ptr(sc),
                                       ptr(ids), stream()), exc)
+        return sc, ids, best, bid
+    # option scan_v1 (parity tests): the f64 overall scan instead of the split overall scan
+    if (mode == 1 and not need_best and q.Zov16 is not None and c.Zov16 is not None
+            and _lib.get_option("scan_v1") is None):
+        ws_bytes = int(_lib.load().hq_scanov_workspace_size(Q, N, k))
+        ws = _workspace(ws_bytes, dev)
+        _chk(_L().hq_scanov_topk_split(ptr(q.Zov16), ptr(q.Sov32), ptr(q.S), ptr(q.Z), Q, ptr(c.Zov16), ptr(c.Sov32),
+                                       ptr(c.S), ptr(c.Z), N, c.L, k, float(threshold), thr_mode, int(id_base), ptr(ws),
+                                       ws_bytes, ptr(sc), ptr(ids), stream()), exc)
         return sc, ids, best, bid
     _chk(_L().hq_scan_topk(ptr(q.Z), ptr(q.S), Q, ptr(c.Z), ptr(c.S), N, c.L, mode, k, float(threshold), thr_mode,
                            int(id_base), ptr(ws), ws_bytes, ptr(sc), ptr(ids), ptr(best), ptr(bid), stream()), exc)

@@ -239,6 +239,31 @@ int hq_scan0_topk_split(const void* Zq16, const float* Sq32, const double* Sq, i
                         int thr_mode, int64_t id_base, void* workspace, size_t workspace_bytes,
                         double* out_score, int64_t* out_id, hq_stream_t stream);
 
+/* ---- S5 brute force: split-f16 overall scan ----------------------------------------------------
+ * Replaces the per-candidate _calculate_overall_similarity loop of brute_force_search
+ * (core/search_engine.py:302-338, :191-230) with one scan over all levels: approximate overall scores
+ * (|approx - exact| <= ~6e-6) -> per-query top k, re-ranked exactly by hq_refine_topk (mode 1).
+ * hq_seg_packov_info: the layout of L's level segments (K-blocks of 32 values, segments of >= 2 values,
+ * one-value segments, floats per statistics group of 4 rows); HQ_E_UNSUPPORTED when L has none (a
+ * segment longer than 32 values, more than 4 / 2 of either kind, or another block pattern than the
+ * L = 64 and L = 32 structures): callers keep hq_scan_topk.
+ * hq_seg_packov_split builds from hq_seg_prepare's Z and S: Zo16, f16 hi / lo of every segment's
+ * normalised values packed into the K-blocks, round_up(N, 16) + 48 rows of nkb x 128 B in 16-row
+ * tiles of nkb x 2 KiB (hq_seg_pack0_split's fragment order per block), and So32, f32 statistics in
+ * SoA groups of 4 rows (per segment std[4], mean[4], msq[4], zero-std flag[4]; per one-value segment
+ * value[4]; row flags[4]) for (round_up(N, 4) + 48) / 4 groups.
+ * hq_scanov_topk_split: Zq/Zc are hq_seg_prepare's f64 Z (rows with an f32-unsafe statistic are scored
+ * from them in f64); the starting threshold comes from a 1/16 tile sample (K' = 12, as
+ * hq_scan0_topk_split: short lists carry +inf, which hq_refine_topk reports as unresolved).       */
+int hq_seg_packov_info(int L, int* nkb, int* ng, int* nc, int* group_floats);
+int hq_seg_packov_split(const double* Z, const double* S, int64_t N, int L, void* Zo16, float* So32,
+                        hq_stream_t stream);
+size_t hq_scanov_workspace_size(int Q, int64_t N, int k);
+int hq_scanov_topk_split(const void* Zq16, const float* Sq32, const double* Sq, const double* Zq, int Q,
+                         const void* Zc16, const float* Sc32, const double* Sc, const double* Zc, int64_t N, int L,
+                         int k, double threshold, int thr_mode, int64_t id_base, void* workspace,
+                         size_t workspace_bytes, double* out_score, int64_t* out_id, hq_stream_t stream);
+
 /* ---- S5/S6: exact re-rank of a scan list -----------------------------------------------------
  * cand_score/cand_id: Q x kp list from hq_scan_topk (approximate, sorted).  Re-scores every listed
  * candidate exactly (as hq_level_scores), applies the threshold test exactly and writes the exact

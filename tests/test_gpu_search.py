@@ -544,3 +544,41 @@ def test_rag_cosine_float64_kept(hq_lib):
     A = rng.standard_normal((5, 3, 64))
     got = [S.compare_multi_level_indices(A[0], A[i]) for i in range(5)]
     np.testing.assert_allclose(got, O.rag_multi_level_similarity(A[0], A), atol=1e-14)
+
+
+@pytest.mark.parametrize("N,L", [(70_003, 64), (3_001, 64), (20_000, 32)])
+def test_overall_split_scan_matches_f64_scan(hq_lib, hq_option, N, L):
+    """The split-f16 overall scan (hq_scanov_topk_split: segment-packed contractions, pre-filter bound,
+    pools) + exact re-rank gives the same brute-force top-k as the f64 k_scan (option scan_v1) and as the
+    oracle, and leaves (almost) every query resolved: corpus with zero-variance segments, duplicates, and
+    one-value segments equal to / within 1e-6 of / just past 1e-6 from the query's."""
+    from hq_mi355x import kernels as K_
+    from hq_mi355x.core.search_engine import IndexCorpus
+    rng = np.random.default_rng(N + L)
+    C = rng.standard_normal((N, L))
+    segs = O.segment_bounds(L)
+    one = [s for s, e in segs if e - s == 1]
+    s1, e1 = segs[1]
+    C[::7, s1:e1] = 0.25                           # zero-variance segment on every 7th row
+    C[N // 2: N // 2 + 40] = C[11]                  # duplicates
+    Q = np.concatenate([C[[11, 12, 13, 500]] + 0.0, C[1000:1100] + rng.normal(0, 0.01, (100, L))])
+    Q[2, s1:e1] = 0.25                             # zero-variance query segment (both-constant pairs)
+    for o in one:                                  # one-value segments: equal, 5e-7 apart, 2e-6 apart
+        C[20:40, o] = Q[0, o]
+        C[40:60, o] = Q[0, o] + 5e-7
+        C[60:80, o] = Q[0, o] + 2e-6
+    corpus = IndexCorpus(C)
+    assert corpus.prep.Zov16 is not None
+    qp = corpus.prepare_queries(Q)
+    k = 10
+    got = [_np(x) for x in corpus.exact_topk(qp, 1, k)[:3]]
+    sc, ids, _, _ = K_.scan_topk(qp, corpus.prep, 1, k + corpus.SLACK, -corpus.EPS, 0)
+    _, _, _, res = K_.refine_topk(qp, corpus.prep, 1, sc, ids, k, 0.0, 0, corpus.EPS)
+    assert int(_np(res).sum()) >= len(Q) - 2        # the dense fallback stays an exception
+    hq_option("scan_v1", 1)
+    ref = [_np(x) for x in corpus.exact_topk(qp, 1, k)[:3]]
+    assert np.array_equal(got[1], ref[1]) and np.array_equal(got[0], ref[0])
+    for a in (0, 1, 2, 3, 50):
+        rid, rsc, _ = O.brute_force_search(Q[a], C, k)
+        assert list(got[1][a]) == list(rid), a
+        np.testing.assert_allclose(got[0][a], rsc, atol=TOL)
