@@ -3884,10 +3884,10 @@ __global__ void k_packov(const double* __restrict__ Z, const double* __restrict_
 // per-query constants of the overall scan (k_ov_qconst, from the query's Sov32 statistics and its
 // starting threshold)
 struct QOv {
-  float thl, flag, wthr, tol;          // pool threshold (f32 lower bound), flags, pre-filter bound, 1e-6 + slack
-  float ia[kOvMaxG], be[kOvMaxG];      // pre-filter: level <= be + max(G, 0) ia
+  float thl, flag, wthr, bsum;         // pool threshold (f32 lower bound), flags, pre-filter bound, sum w be
+  float wia[kOvMaxG], tolq[kOvMaxC], pad[2];  // pre-filter: w level <= w be + max(G, 0) w ia; one-value tolerance
   float qA[kOvMaxG], qB[kOvMaxG], qQ[kOvMaxG], qz[kOvMaxG];  // model constants; qz != 0: zero variance
-  float cv[kOvMaxC], pad[2];           // one-value segments: the query's value
+  float cv[kOvMaxC], pad2[2];          // one-value segments: the query's value
 };
 
 __global__ void k_ov_qconst(const float* __restrict__ Sq, int Q, OvLayout o, const double* __restrict__ th0,
@@ -3904,8 +3904,10 @@ __global__ void k_ov_qconst(const float* __restrict__ Sq, int Q, OvLayout o, con
   // pre-filter bound on the weighted sum, with slack for the f32 evaluation of bound and model
   c.wthr = t0 > -__builtin_huge_val() ? (c.thl - 1e-4f) / o.inv_w - 1e-4f : -__builtin_huge_valf();
   for (int i = 0; i < kOvMaxG; ++i) {
-    c.ia[i] = 0.0f; c.be[i] = 0.0f; c.qA[i] = 0.0f; c.qB[i] = 0.0f; c.qQ[i] = 1.0f; c.qz[i] = 1.0f;
+    c.wia[i] = 0.0f; c.qA[i] = 0.0f; c.qB[i] = 0.0f; c.qQ[i] = 1.0f; c.qz[i] = 1.0f;
   }
+  c.bsum = 0.0f;
+  c.pad[0] = c.pad[1] = 0.0f;
   for (int i = 0; i < o.ng; ++i) {
     const float sd = gp[16 * i], mn = gp[16 * i + 4], ms = gp[16 * i + 8];
     const bool z = __float_as_int(gp[16 * i + 12]) != 0;
@@ -3913,18 +3915,20 @@ __global__ void k_ov_qconst(const float* __restrict__ Sq, int Q, OvLayout o, con
     c.qB[i] = 0.6f * mn;
     c.qQ[i] = ms;
     c.qz[i] = z ? 1.0f : 0.0f;
-    if (z) {
-      c.ia[i] = 0.0f;
-      c.be[i] = 1.0f;
-    } else {
+    float ia = 0.0f, be = 1.0f;
+    if (!z) {
       const float h = 0.5f / sqrtf(ms);
-      c.ia[i] = (o.gc1[i] + c.qA[i] * h) * (1.0f + 1e-5f);
-      c.be[i] = (0.35f + fabsf(c.qB[i]) * h) * (1.0f + 1e-5f) + 1e-6f;
+      ia = (o.gc1[i] + c.qA[i] * h) * (1.0f + 1e-5f);
+      be = (0.35f + fabsf(c.qB[i]) * h) * (1.0f + 1e-5f) + 1e-6f;
     }
+    c.wia[i] = o.gw[i] * ia * (1.0f + 1e-6f);
+    c.bsum += o.gw[i] * be * (1.0f + 1e-6f);
   }
-  c.tol = 1e-6f;
-  for (int ci = 0; ci < kOvMaxC; ++ci) c.cv[ci] = ci < o.nc ? gp[16 * o.ng + 4 * ci] : 0.0f;
-  c.pad[0] = c.pad[1] = 0.0f;
+  for (int ci = 0; ci < kOvMaxC; ++ci) {
+    c.cv[ci] = ci < o.nc ? gp[16 * o.ng + 4 * ci] : 0.0f;
+    c.tolq[ci] = 1e-6f + 2.5e-7f * fabsf(c.cv[ci]);
+  }
+  c.pad2[0] = c.pad2[1] = 0.0f;
   qc[q] = c;
 }
 
@@ -4014,19 +4018,20 @@ __device__ __forceinline__ void ov_query_frags(const OvArgs& a, int q, int g, ha
   }
 }
 
-// weighted pre-filter bound of the lane's four rows (r) for one query block
+// weighted pre-filter bound of the lane's four rows (r) for one query block: two VALU per G segment
+// (weights folded into wia / bsum per query), four per one-value segment
 template <class T>
-__device__ __forceinline__ void ov_bound(const flt4* acc, const float* ia, const float* be, const OvLayout& o,
-                                         const float* qv, float tol, const flt4* cvv, float* U) {
+__device__ __forceinline__ void ov_bound(const flt4* acc, const float* wia, float bsum, const OvLayout& o,
+                                         const float* qv, const float* tolq, const flt4* cvv, float* U) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    float u = 0.0f;
+    float u = bsum;
 #pragma unroll
-    for (int i = 0; i < T::NG; ++i) u = fmaf(o.gw[i], fmaf(fmaxf(acc[i][r], 0.0f), ia[i], be[i]), u);
+    for (int i = 0; i < T::NG; ++i) u = fmaf(fmaxf(acc[i][r], 0.0f), wia[i], u);
 #pragma unroll
     for (int ci = 0; ci < T::NC; ++ci) {
       const float d = fabsf(qv[ci] - cvv[ci][r]);
-      u += d <= fmaf(2.5e-7f, fabsf(qv[ci]) + fabsf(cvv[ci][r]), tol) ? o.cw[ci] : 0.0f;
+      u += d <= fmaf(2.5e-7f, fabsf(cvv[ci][r]), tolq[ci]) ? o.cw[ci] : 0.0f;
     }
     U[r] = u;
   }
@@ -4052,7 +4057,7 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
   const OvLayout& o = a.o;
 
   half8 qh[NB][NG], ql[NB][NG];
-  float ia[NB][NG], be[NB][NG], wt[NB], qv[NB][NC > 0 ? NC : 1], tol[NB];
+  float wia[NB][NG], bsum[NB], wt[NB], qv[NB][NC > 0 ? NC : 1], tolq[NB][NC > 0 ? NC : 1];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int q = q0 + 16 * b + j;
@@ -4061,10 +4066,10 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
     ov_query_frags<T>(a, qq, g, qh[b], ql[b]);
     const QOv& c = a.qc[qq];
 #pragma unroll
-    for (int i = 0; i < NG; ++i) { ia[b][i] = c.ia[i]; be[b][i] = c.be[i]; }
+    for (int i = 0; i < NG; ++i) wia[b][i] = c.wia[i];
+    bsum[b] = c.bsum;
 #pragma unroll
-    for (int ci = 0; ci < NC; ++ci) qv[b][ci] = c.cv[ci];
-    tol[b] = c.tol;
+    for (int ci = 0; ci < NC; ++ci) { qv[b][ci] = c.cv[ci]; tolq[b][ci] = c.tolq[ci]; }
     wt[b] = (v && __float_as_int(c.flag) == 0) ? c.wthr : __builtin_huge_valf();  // flagged query: dense path
   }
 
@@ -4140,7 +4145,7 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
     for (int i = 0; i < NG; ++i)
       acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.f[T::kb(i)][1], qh[b][i], acc[i], 0, 0, 0);
     float U[4];
-    ov_bound<T>(acc, ia[b], be[b], o, qv[b], tol[b], cur.cv, U);
+    ov_bound<T>(acc, wia[b], bsum[b], o, qv[b], tolq[b], cur.cv, U);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const unsigned long long m = __builtin_amdgcn_ballot_w64(U[r] >= wt[b]);
@@ -4237,10 +4242,7 @@ __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
 #pragma unroll
     for (int i = 0; i < NG; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[T::kb(i)][1], qh[i], acc[i], 0, 0, 0);
     float U[4];
-    float qvv[NC > 0 ? NC : 1];
-#pragma unroll
-    for (int ci = 0; ci < NC; ++ci) qvv[ci] = c.cv[ci];
-    ov_bound<T>(acc, c.ia, c.be, o, qvv, c.tol, v0, U);
+    ov_bound<T>(acc, c.wia, c.bsum, o, c.cv, c.tolq, v0, U);
     float m = -__builtin_huge_valf();
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -4350,7 +4352,9 @@ struct OvPlan {
 
 static OvPlan ov_plan(int Q, int64_t N, int k) {
   OvPlan p;
-  ov_geometry(Q, N, kOvQW, 3072, 1 << 20, p.nqb, p.nchunks, p.chunk_len);
+  // one round of waves: k_scanov holds 2 waves per SIMD (> 168 VGPRs); option ov_waves for A/B
+  const int w = opt(OPT_OV_WAVES, 2048) > 0 ? (int)opt(OPT_OV_WAVES, 2048) : 2048;
+  ov_geometry(Q, N, kOvQW, w, 1 << 20, p.nqb, p.nchunks, p.chunk_len);
   const int64_t sd = opt(OPT_SAMPLE_STRIDE, 16) > 0 ? opt(OPT_SAMPLE_STRIDE, 16) : 16;
   p.stride = N >= sd * 4096 ? sd : (N / 4096 > 1 ? N / 4096 : 1);
   p.S = sample_rows_tiled(N, p.stride);
