@@ -3755,9 +3755,10 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
 //   20]; L = 32: [16, 4, 11]); each block's normalised values are split hi / lo in the tiled
 //   fragment layout of Z16 (a 16-row tile holds NKB x [hi 512 | lo 512] halves).  One-value segments
 //   always take the reference's constant branch (np.std of one value is 0): they need their value
-//   only.  Statistics Sov32, SoA groups of 4 rows: per G segment (std, mean, msq, zero-std flag)[4],
-//   per one-value segment value[4], row flags[4] (2: a G segment's mean of squares outside [2^-60,
-//   2^60], scored by k_scanov_flagged in f64; 4: pad row).
+//   only.  Statistics Sov32 in groups of 4 rows: per one-value segment value[4] and row flags[4] (2: a
+//   G segment's mean of squares outside [2^-60, 2^60], scored by k_scanov_flagged in f64; 4: pad row)
+//   for the scan's per-step loads, then per row its record (std, mean, msq, zero-std flag) per G
+//   segment for the drain (one 16-byte load per segment).
 //   Query side: one masked copy of the block fragment per G segment (values outside the segment
 //   zeroed), so each contraction D[row][query] is that segment's G alone.
 //   Pre-filter per pair (an upper bound of the f32 model score): a G segment scores at most
@@ -3831,7 +3832,10 @@ static bool ov_layout(int L, OvLayout& o) {
   return o.lid >= 0;
 }
 
-__host__ __device__ __forceinline__ int ov_gsize(int ng, int nc) { return 16 * ng + 4 * nc + 4; }
+__host__ __device__ __forceinline__ int ov_gsize(int ng, int nc) { return 16 * ng + 4 * nc + 8; }
+// in a statistics group: one-value segment ci at 4 ci, the row flags at 4 nc, the rows' bound offsets at
+// 4 nc + 4, row r's record of G segment i at 4 nc + 8 + 4 (r ng + i)
+__host__ __device__ __forceinline__ int ov_rec(int ng, int nc, int r, int i) { return 4 * nc + 8 + 4 * (r * ng + i); }
 // hi fragment (8 halves, k = 8 g .. 8 g + 7) of K-block kb of a row; lo at + kZ16Lo
 __host__ __device__ __forceinline__ int64_t ov_frag(int64_t row, int kb, int nkb, int g) {
   return ((row >> 4) * nkb + kb) * kZ16Tile + ((g << 4) + (row & 15)) * 8;
@@ -3856,27 +3860,34 @@ __global__ void k_packov(const double* __restrict__ Z, const double* __restrict_
     Zo[e] = hi;
     Zo[e + kZ16Lo] = lo;
     if (c == 0 && r < pack0_rows(N)) {
-      float* gp = So + (r >> 2) * GS + (r & 3);
+      float* gp = So + (r >> 2) * GS;
+      const int rr = (int)(r & 3);
       int flag = 4;
+      float roff = 0.0f;
       if (r < N) {
         flag = 0;
         for (int i = 0; i < o.ng; ++i) {
           const double* st = S + (r * o.nseg + o.gseg[i]) * 4;
           const double mean = st[0], sd = st[1], msq = st[2];
-          gp[16 * i] = (float)sd;
-          gp[16 * i + 4] = (float)mean;
-          gp[16 * i + 8] = (float)msq;
-          gp[16 * i + 12] = __int_as_float(sd == 0.0 ? 1 : 0);
+          // a zero-variance segment scores 0.1 (or the query's constant branch), <= be - 0.25 (be >= 0.35)
+          if (sd == 0.0) roff -= 0.25f * o.gw[i];
+          float* rec = gp + ov_rec(o.ng, o.nc, rr, i);
+          rec[0] = (float)sd;
+          rec[1] = (float)mean;
+          rec[2] = (float)msq;
+          rec[3] = __int_as_float(sd == 0.0 ? 1 : 0);
           if (sd != 0.0 && !(msq >= 0x1p-60 && msq <= 0x1p60)) flag |= 2;
         }
-        for (int ci = 0; ci < o.nc; ++ci) gp[16 * o.ng + 4 * ci] = (float)S[(r * o.nseg + o.cseg[ci]) * 4];
+        for (int ci = 0; ci < o.nc; ++ci) gp[4 * ci + rr] = (float)S[(r * o.nseg + o.cseg[ci]) * 4];
       } else {
         for (int i = 0; i < o.ng; ++i) {
-          gp[16 * i] = 0.0f; gp[16 * i + 4] = 0.0f; gp[16 * i + 8] = 1.0f; gp[16 * i + 12] = __int_as_float(1);
+          float* rec = gp + ov_rec(o.ng, o.nc, rr, i);
+          rec[0] = 0.0f; rec[1] = 0.0f; rec[2] = 1.0f; rec[3] = __int_as_float(1);
         }
-        for (int ci = 0; ci < o.nc; ++ci) gp[16 * o.ng + 4 * ci] = 0.0f;
+        for (int ci = 0; ci < o.nc; ++ci) gp[4 * ci + rr] = 0.0f;
       }
-      gp[16 * o.ng + 4 * o.nc] = __int_as_float(flag);
+      gp[4 * o.nc + rr] = __int_as_float(flag);
+      gp[4 * o.nc + 4 + rr] = roff;
     }
   }
 }
@@ -3890,17 +3901,20 @@ struct QOv {
   float cv[kOvMaxC], pad2[2];          // one-value segments: the query's value
 };
 
+static_assert(sizeof(QOv) % 16 == 0, "QOv copies as flt4");
+
 __global__ void k_ov_qconst(const float* __restrict__ Sq, int Q, OvLayout o, const double* __restrict__ th0,
                             double thr0, QOv* __restrict__ qc) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= Q) return;
   const int GS = ov_gsize(o.ng, o.nc);
-  const float* gp = Sq + (int64_t)(q >> 2) * GS + (q & 3);
+  const float* gp = Sq + (int64_t)(q >> 2) * GS;
+  const int rr = q & 3;
   QOv c;
   double t0 = thr0;
   if (th0 && th0[q] > t0) t0 = th0[q];
   c.thl = lower_f32(t0);
-  c.flag = gp[16 * o.ng + 4 * o.nc];
+  c.flag = gp[4 * o.nc + rr];
   // pre-filter bound on the weighted sum, with slack for the f32 evaluation of bound and model
   c.wthr = t0 > -__builtin_huge_val() ? (c.thl - 1e-4f) / o.inv_w - 1e-4f : -__builtin_huge_valf();
   for (int i = 0; i < kOvMaxG; ++i) {
@@ -3909,8 +3923,9 @@ __global__ void k_ov_qconst(const float* __restrict__ Sq, int Q, OvLayout o, con
   c.bsum = 0.0f;
   c.pad[0] = c.pad[1] = 0.0f;
   for (int i = 0; i < o.ng; ++i) {
-    const float sd = gp[16 * i], mn = gp[16 * i + 4], ms = gp[16 * i + 8];
-    const bool z = __float_as_int(gp[16 * i + 12]) != 0;
+    const float* rec = gp + ov_rec(o.ng, o.nc, rr, i);
+    const float sd = rec[0], mn = rec[1], ms = rec[2];
+    const bool z = __float_as_int(rec[3]) != 0;
     c.qA[i] = o.gqa[i] * sd;
     c.qB[i] = 0.6f * mn;
     c.qQ[i] = ms;
@@ -3925,7 +3940,7 @@ __global__ void k_ov_qconst(const float* __restrict__ Sq, int Q, OvLayout o, con
     c.bsum += o.gw[i] * be * (1.0f + 1e-6f);
   }
   for (int ci = 0; ci < kOvMaxC; ++ci) {
-    c.cv[ci] = ci < o.nc ? gp[16 * o.ng + 4 * ci] : 0.0f;
+    c.cv[ci] = ci < o.nc ? gp[4 * ci + rr] : 0.0f;
     c.tolq[ci] = 1e-6f + 2.5e-7f * fabsf(c.cv[ci]);
   }
   c.pad2[0] = c.pad2[1] = 0.0f;
@@ -3939,22 +3954,27 @@ template <int NG, int NC>
 __device__ __forceinline__ float ov_model(const OvLayout& o, const QOv& c, const float* __restrict__ Sc32, int64_t row,
                                           const float* G, const double* __restrict__ Sq, const double* __restrict__ Sc,
                                           int q) {
-  constexpr int GS = 16 * NG + 4 * NC + 4;
-  const float* gp = Sc32 + (row >> 2) * GS + (row & 3);
-  if (__float_as_int(gp[16 * NG + 4 * NC]) != 0) return -1.0f;
+  constexpr int GS = 16 * NG + 4 * NC + 8;
+  const float* gp = Sc32 + (row >> 2) * GS;
+  const int rr = (int)(row & 3);
+  if (__float_as_int(gp[4 * NC + rr]) != 0) return -1.0f;
   const double* sq = Sq + (int64_t)q * o.nseg * 4;
   const double* sc = Sc + row * o.nseg * 4;
   float tw = 0.0f;
 #pragma unroll
   for (int i = 0; i < NG; ++i) {
     float lvl;
-    const bool cz = __float_as_int(gp[16 * i + 12]) != 0;
-    if (c.qz[i] != 0.0f || cz) {
-      const int s = o.gseg[i];
-      lvl = (float)const0(c.qz[i] != 0.0f, cz, sq[4 * s], sc[4 * s], (aux_bits(sq + 4 * s) & aux_bits(sc + 4 * s) & kAuxF32) != 0);
+    const flt4 rec = *reinterpret_cast<const flt4*>(gp + ov_rec(NG, NC, rr, i));  // std, mean, msq, zero-std
+    const bool cz = __float_as_int(rec[3]) != 0, qz = c.qz[i] != 0.0f;
+    if (qz || cz) {
+      lvl = 0.1f;  // one side constant (search_engine.py:147-148)
+      if (qz && cz) {
+        const int s = o.gseg[i];
+        lvl = (float)const0(true, true, sq[4 * s], sc[4 * s], (aux_bits(sq + 4 * s) & aux_bits(sc + 4 * s) & kAuxF32) != 0);
+      }
     } else {
-      const float num = fmaf(G[i], c.qA[i] * gp[16 * i], c.qB[i] * gp[16 * i + 4]);
-      float t = num * __builtin_amdgcn_rcpf(c.qQ[i] + gp[16 * i + 8]);
+      const float num = fmaf(G[i], c.qA[i] * rec[0], c.qB[i] * rec[1]);
+      float t = num * __builtin_amdgcn_rcpf(c.qQ[i] + rec[2]);
       t = t > 0.0f ? t : 0.0f;
       lvl = fmaf(G[i], o.gc1[i], 0.35f) + t;
       lvl = lvl < 1.0f ? lvl : 1.0f;
@@ -3964,7 +3984,7 @@ __device__ __forceinline__ float ov_model(const OvLayout& o, const QOv& c, const
   }
 #pragma unroll
   for (int ci = 0; ci < NC; ++ci) {
-    const float cv = gp[16 * NG + 4 * ci];
+    const float cv = gp[4 * ci + rr];
     const float d = fabsf(c.cv[ci] - cv), sl = 2.5e-7f * (fabsf(c.cv[ci]) + fabsf(cv)) + 1e-12f;
     float lvl;
     if (d > 1e-6f + sl) lvl = 0.0f;
@@ -4022,10 +4042,10 @@ __device__ __forceinline__ void ov_query_frags(const OvArgs& a, int q, int g, ha
 // (weights folded into wia / bsum per query), four per one-value segment
 template <class T>
 __device__ __forceinline__ void ov_bound(const flt4* acc, const float* wia, float bsum, const OvLayout& o,
-                                         const float* qv, const float* tolq, const flt4* cvv, float* U) {
+                                         const float* qv, const float* tolq, const flt4* cvv, const flt4 ro, float* U) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    float u = bsum;
+    float u = bsum + ro[r];  // rows with zero-variance G segments: their smaller bound
 #pragma unroll
     for (int i = 0; i < T::NG; ++i) u = fmaf(fmaxf(acc[i][r], 0.0f), wia[i], u);
 #pragma unroll
@@ -4042,8 +4062,9 @@ __device__ __forceinline__ void ov_bound(const flt4* acc, const float* wia, floa
 template <int LID>
 __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
   using T = OvT<LID>;
-  constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, NB = kOvQW / 16, GS = 16 * NG + 4 * NC + 4;
+  constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, NB = kOvQW / 16, GS = 16 * NG + 4 * NC + 8;
   __shared__ QEOv qe[kOvQCap];
+  __shared__ QOv qs[kOvQW];  // the wave's query constants (the drain reads them per entry)
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
   const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
   const int chunk = xcd + 8 * (slot / a.nqb);
@@ -4055,6 +4076,15 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
   if (c_end > a.N) c_end = a.N;
   const int q0 = qb * kOvQW;
   const OvLayout& o = a.o;
+  {
+    constexpr int W4 = (int)(sizeof(QOv) / 16);
+    for (int x = lane; x < kOvQW * W4; x += 64) {
+      const int qi = x / W4, f = x % W4;
+      const int q = q0 + qi < a.Q ? q0 + qi : 0;
+      reinterpret_cast<flt4*>(&qs[qi])[f] = reinterpret_cast<const flt4*>(&a.qc[q])[f];
+    }
+    wave_lds_sync();
+  }
 
   half8 qh[NB][NG], ql[NB][NG];
   float wia[NB][NG], bsum[NB], wt[NB], qv[NB][NC > 0 ? NC : 1], tolq[NB][NC > 0 ? NC : 1];
@@ -4074,10 +4104,11 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
   }
 
   const _Float16* zb = a.Zc + (c_begin >> 4) * NKB * kZ16Tile + lane * 8;
-  const float* sb = a.Sc32 + (c_begin >> 2) * GS + 16 * NG;  // one-value segment values of the step's first group
+  const float* sb = a.Sc32 + (c_begin >> 2) * GS;  // one-value segment values of the step's first group
   struct CStep {
     half8 f[NKB][2];
     flt4 cv[NC > 0 ? NC : 1];
+    flt4 ro;
   };
   const int64_t nsteps = (c_end - c_begin + kCS - 1) / kCS;
   auto load_step = [&](CStep& c, int64_t s) {
@@ -4091,6 +4122,7 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
     const float* sp = sb + (s * 4 + g) * GS;
 #pragma unroll
     for (int ci = 0; ci < NC; ++ci) c.cv[ci] = *reinterpret_cast<const flt4*>(sp + 4 * ci);
+    c.ro = *reinterpret_cast<const flt4*>(sp + 4 * NC + 4);
   };
 
   int qn = 0;
@@ -4099,7 +4131,7 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
       const flt4 eg = qe[lane].g;
       const int eqi = qe[lane].qi, row = qe[lane].row;
       const int q = q0 + eqi;
-      const QOv c = a.qc[q];
+      const QOv& c = qs[eqi];
       if (row < c_end) {
         const float G[4] = {eg[0], eg[1], eg[2], eg[3]};
         const float s = ov_model<NG, NC>(o, c, a.Sc32, row, G, a.Sq, a.Sc, q);
@@ -4145,7 +4177,7 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
     for (int i = 0; i < NG; ++i)
       acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.f[T::kb(i)][1], qh[b][i], acc[i], 0, 0, 0);
     float U[4];
-    ov_bound<T>(acc, wia[b], bsum[b], o, qv[b], tolq[b], cur.cv, U);
+    ov_bound<T>(acc, wia[b], bsum[b], o, qv[b], tolq[b], cur.cv, cur.ro, U);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const unsigned long long m = __builtin_amdgcn_ballot_w64(U[r] >= wt[b]);
@@ -4194,7 +4226,7 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
 template <int LID>
 __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
   using T = OvT<LID>;
-  constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, GS = 16 * NG + 4 * NC + 4;
+  constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, GS = 16 * NG + 4 * NC + 8;
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
   const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
   const int chunk = xcd + 8 * (slot / a.nqb);
@@ -4211,7 +4243,7 @@ __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
   ov_query_frags<T>(a, qq, g, qh, ql);
   const QOv c = a.qc[qq];
   auto row_of = [&](int64_t i) -> int64_t { return sample_row_tiled(i, a.S, a.stride); };
-  auto load = [&](int64_t cs, half8 (*f)[2], flt4* cv) {
+  auto load = [&](int64_t cs, half8 (*f)[2], flt4* cv, flt4& ro) {
     const int64_t row = row_of(cs + j);  // tile-aligned: the step is one corpus tile
     const _Float16* p = a.Zc + ov_frag(row, 0, NKB, g);
 #pragma unroll
@@ -4220,9 +4252,10 @@ __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
       f[kb][1] = *reinterpret_cast<const half8*>(p + kb * kZ16Tile + kZ16Lo);
     }
     const int64_t r0 = row_of(cs + 4 * g);
-    const float* sp = a.Sc32 + (r0 >> 2) * GS + 16 * NG;
+    const float* sp = a.Sc32 + (r0 >> 2) * GS;
 #pragma unroll
     for (int ci = 0; ci < NC; ++ci) cv[ci] = *reinterpret_cast<const flt4*>(sp + 4 * ci);
+    ro = *reinterpret_cast<const flt4*>(sp + 4 * NC + 4);
   };
   float bu = -__builtin_huge_valf();
   flt4 bg[NG];
@@ -4230,10 +4263,10 @@ __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
 #pragma unroll
   for (int i = 0; i < NG; ++i) bg[i] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
   half8 f0[NKB][2], f1[NKB][2];
-  flt4 v0[NC > 0 ? NC : 1], v1[NC > 0 ? NC : 1];
-  load(c_begin, f0, v0);
+  flt4 v0[NC > 0 ? NC : 1], v1[NC > 0 ? NC : 1], ro0, ro1;
+  load(c_begin, f0, v0, ro0);
   for (int64_t cs = c_begin; cs < c_end; cs += kCS) {
-    load(cs + kCS, f1, v1);
+    load(cs + kCS, f1, v1, ro1);
     flt4 acc[NG];
 #pragma unroll
     for (int i = 0; i < NG; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[T::kb(i)][0], qh[i], flt4{0, 0, 0, 0}, 0, 0, 0);
@@ -4242,7 +4275,7 @@ __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
 #pragma unroll
     for (int i = 0; i < NG; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[T::kb(i)][1], qh[i], acc[i], 0, 0, 0);
     float U[4];
-    ov_bound<T>(acc, c.wia, c.bsum, o, c.cv, c.tolq, v0, U);
+    ov_bound<T>(acc, c.wia, c.bsum, o, c.cv, c.tolq, v0, ro0, U);
     float m = -__builtin_huge_valf();
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -4256,6 +4289,7 @@ __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
     for (int kb = 0; kb < NKB; ++kb) { f0[kb][0] = f1[kb][0]; f0[kb][1] = f1[kb][1]; }
 #pragma unroll
     for (int ci = 0; ci < NC; ++ci) v0[ci] = v1[ci];
+    ro0 = ro1;
   }
   if (!qv_ok) return;
   float top[kTopT];
@@ -4288,7 +4322,7 @@ __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
 __global__ __launch_bounds__(256) void k_ov_flag_rows(const float* __restrict__ So, int64_t N, int GS, int foff,
                                                       int* __restrict__ list, int* __restrict__ count) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < N; r += (int64_t)gridDim.x * blockDim.x)
-    if (__float_as_int(So[(r >> 2) * GS + foff + (r & 3)]) & 2) list[atomicAdd(count, 1)] = (int)r;
+    if (__float_as_int(So[(r >> 2) * GS + foff + (r & 3)]) & 2) list[atomicAdd(count, 1)] = (int)r;  // foff = 4 nc
 }
 
 // the flagged rows against every scanned query (lane = query): the overall score in f64 from the f64
@@ -4417,7 +4451,7 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
   const int64_t fb = (a.N + 255) / 256;
   const int GS = ov_gsize(a.o.ng, a.o.nc);
   hipLaunchKernelGGL(k_ov_flag_rows, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, s, a.Sc32, a.N, GS,
-                     16 * a.o.ng + 4 * a.o.nc, flag_list, flag_n);
+                     4 * a.o.nc, flag_list, flag_n);
   HQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_scanov<LID>, dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   HQ_CHECK_LAUNCH();

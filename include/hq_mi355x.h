@@ -250,8 +250,8 @@ int hq_scan0_topk_split(const void* Zq16, const float* Sq32, const double* Sq, i
  * hq_seg_packov_split builds from hq_seg_prepare's Z and S: Zo16, f16 hi / lo of every segment's
  * normalised values packed into the K-blocks, round_up(N, 16) + 48 rows of nkb x 128 B in 16-row
  * tiles of nkb x 2 KiB (hq_seg_pack0_split's fragment order per block), and So32, f32 statistics in
- * SoA groups of 4 rows (per segment std[4], mean[4], msq[4], zero-std flag[4]; per one-value segment
- * value[4]; row flags[4]) for (round_up(N, 4) + 48) / 4 groups.
+ * groups of 4 rows (per one-value segment value[4], row flags[4], pre-filter offsets[4], then per row
+ * and segment (std, mean, msq, zero-std flag)) for (round_up(N, 4) + 48) / 4 groups.
  * hq_scanov_topk_split: Zq/Zc are hq_seg_prepare's f64 Z (rows with an f32-unsafe statistic are scored
  * from them in f64); the starting threshold comes from a 1/16 tile sample (K' = 12, as
  * hq_scan0_topk_split: short lists carry +inf, which hq_refine_topk reports as unresolved).       */
