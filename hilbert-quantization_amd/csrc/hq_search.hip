@@ -3771,7 +3771,7 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
 // ================================================================================================
 constexpr int kOvMaxG = 4, kOvMaxC = 2, kOvMaxKB = 2;
 constexpr int kOvQW = 32;       // queries per wave of k_scanov (two 16-query blocks)
-constexpr int kOvQCap = 128;    // LDS queue entries per wave (< 64 before a ballot adds <= 64)
+constexpr int kOvQCap = 64 + 64 * 4;  // LDS queue entries per wave (< 64 before a block adds <= 256)
 
 struct OvLayout {
   int nseg, ng, nc, nkb, lid;
@@ -3893,7 +3893,7 @@ __global__ void k_packov(const double* __restrict__ Z, const double* __restrict_
 }
 
 // per-query constants of the overall scan (k_ov_qconst, from the query's Sov32 statistics and its
-// starting threshold)
+// starting threshold); QOvD: the model's part, cached in LDS by k_scanov
 struct QOv {
   float thl, flag, wthr, bsum;         // pool threshold (f32 lower bound), flags, pre-filter bound, sum w be
   float wia[kOvMaxG], tolq[kOvMaxC], pad[2];  // pre-filter: w level <= w be + max(G, 0) w ia; one-value tolerance
@@ -3901,7 +3901,10 @@ struct QOv {
   float cv[kOvMaxC], pad2[2];          // one-value segments: the query's value
 };
 
-static_assert(sizeof(QOv) % 16 == 0, "QOv copies as flt4");
+struct QOvD {
+  float qA[kOvMaxG], qB[kOvMaxG], qQ[kOvMaxG], qz[kOvMaxG];
+  float cv[kOvMaxC], thl, pad;
+};
 
 __global__ void k_ov_qconst(const float* __restrict__ Sq, int Q, OvLayout o, const double* __restrict__ th0,
                             double thr0, QOv* __restrict__ qc) {
@@ -3950,8 +3953,13 @@ __global__ void k_ov_qconst(const float* __restrict__ Sq, int Q, OvLayout o, con
 // the f32 model overall score of one pair (G of each G segment given), or -1 when the row is not scored
 // here (flagged: k_scanov_flagged; pad).  Constant branches are decided from the f64 means exactly as
 // const0; the one-value segments compare the f32 values first and fall back to f64 near the edge.
-template <int NG, int NC>
-__device__ __forceinline__ float ov_model(const OvLayout& o, const QOv& c, const float* __restrict__ Sc32, int64_t row,
+// the reference's both-constant branch from the f64 means (out of line: rare)
+__device__ __noinline__ float ov_const0(const double* __restrict__ sq, const double* __restrict__ sc) {
+  return (float)const0(true, true, sq[0], sc[0], (aux_bits(sq) & aux_bits(sc) & kAuxF32) != 0);
+}
+
+template <int NG, int NC, class QC>
+__device__ __forceinline__ float ov_model(const OvLayout& o, const QC& c, const float* __restrict__ Sc32, int64_t row,
                                           const float* G, const double* __restrict__ Sq, const double* __restrict__ Sc,
                                           int q) {
   constexpr int GS = 16 * NG + 4 * NC + 8;
@@ -3968,10 +3976,7 @@ __device__ __forceinline__ float ov_model(const OvLayout& o, const QOv& c, const
     const bool cz = __float_as_int(rec[3]) != 0, qz = c.qz[i] != 0.0f;
     if (qz || cz) {
       lvl = 0.1f;  // one side constant (search_engine.py:147-148)
-      if (qz && cz) {
-        const int s = o.gseg[i];
-        lvl = (float)const0(true, true, sq[4 * s], sc[4 * s], (aux_bits(sq + 4 * s) & aux_bits(sc + 4 * s) & kAuxF32) != 0);
-      }
+      if (qz && cz) lvl = ov_const0(sq + 4 * o.gseg[i], sc + 4 * o.gseg[i]);
     } else {
       const float num = fmaf(G[i], c.qA[i] * rec[0], c.qB[i] * rec[1]);
       float t = num * __builtin_amdgcn_rcpf(c.qQ[i] + rec[2]);
@@ -3989,10 +3994,7 @@ __device__ __forceinline__ float ov_model(const OvLayout& o, const QOv& c, const
     float lvl;
     if (d > 1e-6f + sl) lvl = 0.0f;
     else if (d < 1e-6f - sl) lvl = 1.0f;
-    else {
-      const int s = o.cseg[ci];
-      lvl = (float)const0(true, true, sq[4 * s], sc[4 * s], (aux_bits(sq + 4 * s) & aux_bits(sc + 4 * s) & kAuxF32) != 0);
-    }
+    else lvl = ov_const0(sq + 4 * o.cseg[ci], sc + 4 * o.cseg[ci]);
     tw = fmaf(o.cw[ci], lvl, tw);
   }
   float s = tw * o.inv_w;
@@ -4011,11 +4013,6 @@ struct OvArgs {
   const double* Zq64; const double* Zc64; int Lp;  // k_scanov_flagged: the f64 normalised vectors
 };
 
-struct QEOv {
-  flt4 g;        // G of each G segment
-  int qi, row;   // query within the wave, row
-  int pad0, pad1;
-};
 
 // masked query fragments of one 16-query block: hi / lo of G segment i, values outside it zeroed
 template <class T>
@@ -4059,12 +4056,13 @@ __device__ __forceinline__ void ov_bound(const flt4* acc, const float* wia, floa
 
 // One wave = 32 queries (two blocks b of 16; lane (g, j) owns queries 16b + j) x one chunk, 16 rows per
 // step (lane group g owns rows 4g + r: the MFMA D layout), NG x 3 MFMAs per block and step.
-template <int LID>
-__global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
+template <int LID, int OCC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_scanov(OvArgs a) {
   using T = OvT<LID>;
   constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, NB = kOvQW / 16, GS = 16 * NG + 4 * NC + 8;
-  __shared__ QEOv qe[kOvQCap];
-  __shared__ QOv qs[kOvQW];  // the wave's query constants (the drain reads them per entry)
+  __shared__ flt4 qg[kOvQCap];  // queue: G of each G segment ...
+  __shared__ int qk[kOvQCap];   // ... and (row - c_begin) << 5 | query within the wave
+  __shared__ QOvD qs[kOvQW];    // the wave's model constants (the drain reads them per entry)
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
   const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
   const int chunk = xcd + 8 * (slot / a.nqb);
@@ -4076,15 +4074,18 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
   if (c_end > a.N) c_end = a.N;
   const int q0 = qb * kOvQW;
   const OvLayout& o = a.o;
-  {
-    constexpr int W4 = (int)(sizeof(QOv) / 16);
-    for (int x = lane; x < kOvQW * W4; x += 64) {
-      const int qi = x / W4, f = x % W4;
-      const int q = q0 + qi < a.Q ? q0 + qi : 0;
-      reinterpret_cast<flt4*>(&qs[qi])[f] = reinterpret_cast<const flt4*>(&a.qc[q])[f];
-    }
-    wave_lds_sync();
+  if (lane < kOvQW) {
+    const QOv& c = a.qc[q0 + lane < a.Q ? q0 + lane : 0];
+    QOvD d;
+#pragma unroll
+    for (int i = 0; i < kOvMaxG; ++i) { d.qA[i] = c.qA[i]; d.qB[i] = c.qB[i]; d.qQ[i] = c.qQ[i]; d.qz[i] = c.qz[i]; }
+#pragma unroll
+    for (int ci = 0; ci < kOvMaxC; ++ci) d.cv[ci] = c.cv[ci];
+    d.thl = c.thl;
+    d.pad = 0.0f;
+    qs[lane] = d;
   }
+  wave_lds_sync();
 
   half8 qh[NB][NG], ql[NB][NG];
   float wia[NB][NG], bsum[NB], wt[NB], qv[NB][NC > 0 ? NC : 1], tolq[NB][NC > 0 ? NC : 1];
@@ -4126,12 +4127,14 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
   };
 
   int qn = 0;
+  // drain the first n <= 64 entries (one per lane): f32 model score, pool append; then shift the rest down
   auto drain = [&](const int n) {
     if (lane < n) {
-      const flt4 eg = qe[lane].g;
-      const int eqi = qe[lane].qi, row = qe[lane].row;
+      const flt4 eg = qg[lane];
+      const int key = qk[lane], eqi = key & 31;
+      const int64_t row = c_begin + (key >> 5);
       const int q = q0 + eqi;
-      const QOv& c = qs[eqi];
+      const QOvD& c = qs[eqi];
       if (row < c_end) {
         const float G[4] = {eg[0], eg[1], eg[2], eg[3]};
         const float s = ov_model<NG, NC>(o, c, a.Sc32, row, G, a.Sq, a.Sc, q);
@@ -4139,7 +4142,7 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
           const int slot = atomicAdd(a.pool_n + q, 1);
           if (slot < a.pool_cap) {
             a.pool_s[(int64_t)q * a.pool_cap + slot] = s;
-            a.pool_i[(int64_t)q * a.pool_cap + slot] = row;
+            a.pool_i[(int64_t)q * a.pool_cap + slot] = (int)row;
           }
         }
       }
@@ -4148,23 +4151,15 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
     for (int b0 = n; b0 < qn; b0 += 64) {
       const bool mv = b0 + lane < qn;
       flt4 tg = {0.0f, 0.0f, 0.0f, 0.0f};
-      int tq = 0, tr = 0;
-      if (mv) {
-        tg = qe[b0 + lane].g;
-        tq = qe[b0 + lane].qi;
-        tr = qe[b0 + lane].row;
-      }
+      int tk = 0;
+      if (mv) { tg = qg[b0 + lane]; tk = qk[b0 + lane]; }
       wave_lds_sync();
-      if (mv) {
-        qe[b0 - n + lane].g = tg;
-        qe[b0 - n + lane].qi = tq;
-        qe[b0 - n + lane].row = tr;
-      }
+      if (mv) { qg[b0 - n + lane] = tg; qk[b0 - n + lane] = tk; }
       wave_lds_sync();
     }
     qn -= n;
   };
-  // one block of one step: contractions, bound, queue the passing pairs
+  // one block of one step: contractions, bound, queue the passing pairs (drained once per step)
   auto block = [&](const int b, const CStep& cur, const int64_t cs) {
     flt4 acc[NG];
 #pragma unroll
@@ -4187,17 +4182,20 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
           flt4 gg = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
           for (int i = 0; i < NG; ++i) gg[i] = acc[i][r];
-          qe[pos].g = gg;
-          qe[pos].qi = 16 * b + j;
-          qe[pos].row = (int)(cs + 4 * g + r);
+          qg[pos] = gg;
+          qk[pos] = (int)((cs - c_begin + 4 * g + r) << 5) | (16 * b + j);
         }
         qn += __popcll(m);
-        if (qn >= 64) {
-          wave_lds_sync();
-          while (qn >= 64) drain(64);  // keeps qn < 64 before each ballot: the queue never exceeds 127
-        }
       }
     }
+    if (qn >= 64) {  // keeps qn < 64 before each block: the queue never exceeds 63 + 4 x 64
+      wave_lds_sync();
+      while (qn >= 64) drain(64);
+    }
+  };
+  auto step = [&](const CStep& cur, const int64_t s) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) block(b, cur, c_begin + s * kCS);
   };
 
   CStep cA, cB;
@@ -4206,16 +4204,12 @@ __global__ __launch_bounds__(64) void k_scanov(OvArgs a) {
   for (; s + 1 < nsteps; s += 2) {
     load_step(cB, s + 1);
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int b = 0; b < NB; ++b) block(b, cA, c_begin + s * kCS);
+    step(cA, s);
     load_step(cA, s + 2);
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int b = 0; b < NB; ++b) block(b, cB, c_begin + (s + 1) * kCS);
+    step(cB, s + 1);
   }
-  if (s < nsteps)
-#pragma unroll
-    for (int b = 0; b < NB; ++b) block(b, cA, c_begin + s * kCS);
+  if (s < nsteps) step(cA, s);
   wave_lds_sync();
   while (qn > 0) drain(qn < 64 ? qn : 64);
 }
@@ -4386,9 +4380,14 @@ struct OvPlan {
 
 static OvPlan ov_plan(int Q, int64_t N, int k) {
   OvPlan p;
-  // one round of waves: k_scanov holds 2 waves per SIMD (> 168 VGPRs); option ov_waves for A/B
-  const int w = opt(OPT_OV_WAVES, 2048) > 0 ? (int)opt(OPT_OV_WAVES, 2048) : 2048;
+  // one round of waves at the kernel's occupancy (OvOcc: 3 waves per SIMD, 168 VGPRs; option ov_occ 2)
+  const int occ = opt(OPT_OV_OCC, 3) == 2 ? 2 : 3;
+  int w = opt(OPT_OV_WAVES, 0) > 0 ? (int)opt(OPT_OV_WAVES, 0) : 1024 * occ;
   ov_geometry(Q, N, kOvQW, w, 1 << 20, p.nqb, p.nchunks, p.chunk_len);
+  while (p.chunk_len > (int64_t(1) << 26)) {  // queue keys hold (row - chunk start) << 5
+    w *= 2;
+    ov_geometry(Q, N, kOvQW, w, 1 << 20, p.nqb, p.nchunks, p.chunk_len);
+  }
   const int64_t sd = opt(OPT_SAMPLE_STRIDE, 16) > 0 ? opt(OPT_SAMPLE_STRIDE, 16) : 16;
   p.stride = N >= sd * 4096 ? sd : (N / 4096 > 1 ? N / 4096 : 1);
   p.S = sample_rows_tiled(N, p.stride);
@@ -4453,7 +4452,8 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
   hipLaunchKernelGGL(k_ov_flag_rows, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, s, a.Sc32, a.N, GS,
                      4 * a.o.nc, flag_list, flag_n);
   HQ_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_scanov<LID>, dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  if (opt(OPT_OV_OCC, 3) == 2) hipLaunchKernelGGL((k_scanov<LID, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  else hipLaunchKernelGGL((k_scanov<LID, 3>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   HQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_scanov_flagged, dim3(64, (Q + 63) / 64), dim3(64), 0, s, a, si, (const int*)flag_list,
                      (const int*)flag_n);
