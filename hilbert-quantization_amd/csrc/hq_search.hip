@@ -1721,12 +1721,17 @@ __global__ void k_scan_qprep(const float* __restrict__ Sq32, int Q, double thr0,
   pool_n[q] = 0;
 }
 
+// max of an accumulator in two instructions.  Inline asm: the compiler's hazard recognizer does not see
+// its reads, so the operand must NOT be an MFMA result issued shortly before (the VALU read of an MFMA
+// destination needs wait states): k_scan0g reads accumulators at least six MFMAs after they were
+// written (one mfma_half in between).  max4_fresh is the compiler-visible form for fresh results.
 __device__ __forceinline__ float max4(const flt4 v) {
   float t, r;
   asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(t) : "v"(v.x), "v"(v.y), "v"(v.z));
   asm volatile("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(t), "v"(v.w));
   return r;
 }
+__device__ __forceinline__ float max4_fresh(const flt4 v) { return fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)); }
 
 constexpr int kQCap = 256;  // LDS queue entries per wave (a half-step adds at most 128)
 struct QEntry {
@@ -2481,7 +2486,7 @@ __global__ __launch_bounds__(64) void k_sample_topg(SampleArgs a) {
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      const float m = max4(acc[b]);
+      const float m = max4_fresh(acc[b]);
       const bool up = m > bg[b];
       bg[b] = up ? m : bg[b];
       bacc[b] = up ? acc[b] : bacc[b];
@@ -4035,6 +4040,11 @@ __device__ __forceinline__ void ov_query_frags(const OvArgs& a, int q, int g, ha
   }
 }
 
+// max(x, 0) in one instruction (fmaxf adds a canonicalising v_max of x with itself).  A builtin, not
+// inline asm: the hazard recognizer does not see an asm statement's reads, and a VALU read of an MFMA
+// result needs wait states (an asm v_max right after the MFMA read the stale register).
+__device__ __forceinline__ float relu_f32(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 3.0e38f); }
+
 // weighted pre-filter bound of the lane's four rows (r) for one query block: two VALU per G segment
 // (weights folded into wia / bsum per query), four per one-value segment
 template <class T>
@@ -4044,11 +4054,12 @@ __device__ __forceinline__ void ov_bound(const flt4* acc, const float* wia, floa
   for (int r = 0; r < 4; ++r) {
     float u = bsum + ro[r];  // rows with zero-variance G segments: their smaller bound
 #pragma unroll
-    for (int i = 0; i < T::NG; ++i) u = fmaf(fmaxf(acc[i][r], 0.0f), wia[i], u);
+    for (int i = 0; i < T::NG; ++i) u = fmaf(relu_f32(acc[i][r]), wia[i], u);
 #pragma unroll
     for (int ci = 0; ci < T::NC; ++ci) {
       const float d = fabsf(qv[ci] - cvv[ci][r]);
-      u += d <= fmaf(2.5e-7f, fabsf(cvv[ci][r]), tolq[ci]) ? o.cw[ci] : 0.0f;
+      const float uc = u + o.cw[ci];
+      u = d <= fmaf(2.5e-7f, fabsf(cvv[ci][r]), tolq[ci]) ? uc : u;
     }
     U[r] = u;
   }
@@ -4380,8 +4391,9 @@ struct OvPlan {
 
 static OvPlan ov_plan(int Q, int64_t N, int k) {
   OvPlan p;
-  // one round of waves at the kernel's occupancy (OvOcc: 3 waves per SIMD, 168 VGPRs; option ov_occ 2)
-  const int occ = opt(OPT_OV_OCC, 3) == 2 ? 2 : 3;
+  // one round of waves at the kernel's occupancy (2 waves per SIMD, 185 VGPRs; option ov_occ 3: the
+  // 168-VGPR build with a few spills, measured equal)
+  const int occ = opt(OPT_OV_OCC, 2) == 3 ? 3 : 2;
   int w = opt(OPT_OV_WAVES, 0) > 0 ? (int)opt(OPT_OV_WAVES, 0) : 1024 * occ;
   ov_geometry(Q, N, kOvQW, w, 1 << 20, p.nqb, p.nchunks, p.chunk_len);
   while (p.chunk_len > (int64_t(1) << 26)) {  // queue keys hold (row - chunk start) << 5
@@ -4452,8 +4464,8 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
   hipLaunchKernelGGL(k_ov_flag_rows, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, s, a.Sc32, a.N, GS,
                      4 * a.o.nc, flag_list, flag_n);
   HQ_CHECK_LAUNCH();
-  if (opt(OPT_OV_OCC, 3) == 2) hipLaunchKernelGGL((k_scanov<LID, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
-  else hipLaunchKernelGGL((k_scanov<LID, 3>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  if (opt(OPT_OV_OCC, 2) == 3) hipLaunchKernelGGL((k_scanov<LID, 3>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  else hipLaunchKernelGGL((k_scanov<LID, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   HQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_scanov_flagged, dim3(64, (Q + 63) / 64), dim3(64), 0, s, a, si, (const int*)flag_list,
                      (const int*)flag_n);

@@ -575,6 +575,10 @@ def test_overall_split_scan_matches_f64_scan(hq_lib, hq_option, N, L):
     sc, ids, _, _ = K_.scan_topk(qp, corpus.prep, 1, k + corpus.SLACK, -corpus.EPS, 0)
     _, _, _, res = K_.refine_topk(qp, corpus.prep, 1, sc, ids, k, 0.0, 0, corpus.EPS)
     assert int(_np(res).sum()) >= len(Q) - 2        # the dense fallback stays an exception
+    hq_option("ov_occ", 3)                         # the 3-waves-per-SIMD build of k_scanov
+    occ3 = [_np(x) for x in corpus.exact_topk(qp, 1, k)[:3]]
+    assert np.array_equal(got[1], occ3[1]) and np.array_equal(got[0], occ3[0])
+    hq_option("ov_occ", None)
     hq_option("scan_v1", 1)
     ref = [_np(x) for x in corpus.exact_topk(qp, 1, k)[:3]]
     assert np.array_equal(got[1], ref[1]) and np.array_equal(got[0], ref[0])
