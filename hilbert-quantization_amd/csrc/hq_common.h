@@ -107,6 +107,24 @@ constexpr GroupLut<NS> make_group_lut() {
   return t;
 }
 
+// Scatter LUT of the chunk kernels: for every 2x2 group j (Hilbert positions 4j .. 4j + 3) the LDS byte
+// offsets of its four values in the row-major n x n float image, two per dword (value m of the group in
+// dword 2j + (m >> 1), bits 16 (m & 1) ..): one mask or shift per value gives the store address.
+template <int NS>
+struct AddrLut {
+  uint32_t v[NS * NS / 2];
+};
+template <int NS>
+constexpr AddrLut<NS> make_addr_lut() {
+  AddrLut<NS> t{};
+  for (uint32_t d = 0; d < (uint32_t)(NS * NS); ++d) {
+    uint32_t x = 0, y = 0;
+    d2xy(NS, d, x, y);
+    t.v[d >> 1] |= (4u * (y * NS + x)) << (16 * (d & 1u));
+  }
+  return t;
+}
+
 __host__ __device__ inline uint32_t xy2d(uint32_t n, uint32_t x, uint32_t y) {
   // _xy_to_hilbert_index (:68-90); the rotate uses the loop's s, values wrap in uint32 which only
   // disturbs bits at or above s — never looked at again (SURVEY.md §8a note).
@@ -354,7 +372,8 @@ __device__ __forceinline__ int wsum64i(int v) {
 }
 // Fast form of qz: with d = fl(x - mn) >= 0 (shared by both forms), the reference's
 // y = fl(fl(d / rng) * 255) = Y (1+e1)(1+e2) and y' = fl(fl(d * fl(1/rng)) * 255) = Y (1+e3)(1+e4)(1+e5)
-// with Y = 255 d / rng <= 255 and |ei| <= 2^-24, so |y - y'| <= 255 * 5 * 2^-24 < 7.7e-5.  Hence
+// with Y = 255 d / rng <= 255 and |ei| <= 2^-24, so |y - y'| <= 255 * 5 * 2^-24 < 7.7e-5 (with the
+// hardware reciprocal, 1 ulp: |e3| <= 2^-23 and |y - y'| <= 255 * 6 * 2^-24 < 9.2e-5).  Hence
 // trunc(y') == trunc(y) whenever frac(y') lies in [1e-4, 1 - 1e-4] (frac is exact: y' - floor(y')
 // for y' < 2^23); otherwise `slow` is set and the caller recomputes that element with the exact
 // division.

@@ -283,8 +283,8 @@ __global__ __launch_bounds__(64) void k_chunk(const __half* __restrict__ src, in
 // chip, tools/ubench/hbm_shapes.hip).  Each lane loads 16-byte runs of the f16 stream (two float4
 // groups = two 2x2 image blocks) and scatters them into the wave's LDS image with the compile-time
 // group LUT; the traditional index and the 16-byte frame stores follow k_chunk.
-__device__ constexpr GroupLut<32> kLut32 = make_group_lut<32, false>();
-__device__ constexpr GroupLut<64> kLut64 = make_group_lut<64, false>();
+__device__ constexpr AddrLut<32> kAddr32 = make_addr_lut<32>();
+__device__ constexpr AddrLut<64> kAddr64 = make_addr_lut<64>();
 
 __device__ __forceinline__ float2 h2f(uint32_t w) {
   return make_float2(__half2float(__ushort_as_half((unsigned short)(w & 0xFFFFu))),
@@ -313,10 +313,10 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
   float* img = img_all[wv];
   float* rowv = rowv_all[wv];
   const int64_t c0 = ((int64_t)blockIdx.x * WPB + wv) * CPW;
-  const uint32_t* lut = NS == 32 ? kLut32.v : kLut64.v;
+  const uint32_t* alut = NS == 32 ? kAddr32.v : kAddr64.v;
   // CPW chunks per wave, all loaded up front (more bytes in flight per wave)
   uint4 raw_all[CPW][NU];
-  uint32_t ent[2 * NU];
+  uint32_t ent[4 * NU];  // LDS byte offsets of the lane's 8 NU values, two per dword (AddrLut)
 #pragma unroll
   for (int k = 0; k < CPW; ++k)
 #pragma unroll
@@ -333,8 +333,11 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
       }
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
-    ent[2 * u] = lut[2 * (lane + 64 * u)];
-    ent[2 * u + 1] = lut[2 * (lane + 64 * u) + 1];
+    const uint4 e = reinterpret_cast<const uint4*>(alut)[lane + 64 * u];  // values 8 (lane + 64 u) ..
+    ent[4 * u] = e.x;
+    ent[4 * u + 1] = e.y;
+    ent[4 * u + 2] = e.z;
+    ent[4 * u + 3] = e.w;
   }
 #pragma unroll
   for (int k = 0; k < CPW; ++k) {
@@ -350,14 +353,13 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
       const float2 a = h2f(h ? raw[u].z : raw[u].x), b = h2f(h ? raw[u].w : raw[u].y);
       lmin = fminf(lmin, fminf(fminf(a.x, a.y), fminf(b.x, b.y)));
       lmax = fmaxf(lmax, fmaxf(fmaxf(a.x, a.y), fmaxf(b.x, b.y)));
-      // element m -> slot b = (code >> 2m) & 3 of the 2x2 block (forward LUT): four b32 LDS stores,
-      // no data-dependent selects
-      const uint32_t e = ent[2 * u + h], off = e & 0xFFFFu, code = e >> 16;
-      auto at = [&](uint32_t b) { return img + off + (b & 1u) + (b >> 1) * NS; };
-      *at(code & 3u) = a.x;
-      *at((code >> 2) & 3u) = a.y;
-      *at((code >> 4) & 3u) = b.x;
-      *at((code >> 6) & 3u) = b.y;
+      // four b32 LDS stores at the group's precomputed byte offsets (one mask or shift each)
+      const uint32_t e0 = ent[4 * u + 2 * h], e1 = ent[4 * u + 2 * h + 1];
+      auto at = [&](uint32_t byte_off) { return reinterpret_cast<float*>(reinterpret_cast<char*>(img) + byte_off); };
+      *at(e0 & 0xFFFFu) = a.x;
+      *at(e0 >> 16) = a.y;
+      *at(e1 & 0xFFFFu) = b.x;
+      *at(e1 >> 16) = b.y;
     }
   }
   __syncthreads();
@@ -399,7 +401,9 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
   if (live) {
   const bool flat = mx == mn;
   const float rng = mx - mn;
-  const float rcp = 1.0f / rng;
+  // hardware reciprocal (1 ulp; the fast form's bound with it: qfast, hq_common.h); f16 data gives
+  // rng >= 2^-24 or a flat frame, so 1 / rng stays finite
+  const float rcp = __builtin_amdgcn_rcpf(rng);
   uint8_t* dst = frame_out + c * FB;
   // one quantized byte: reciprocal form with an exact fallback per cell position (qfast, hq_common.h)
   // — the IEEE division runs only where some lane's value lies within 1e-3 of a level edge
@@ -439,10 +443,11 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk_np(const uint16_t* __restric
         word = __builtin_amdgcn_cvt_pk_u8_f32(fb.y, 3, word);
         const float xs[4] = {f.x, f.y, f.z, f.w};
         const bool sl[4] = {fabsf(ta.x) > 0.4999f, fabsf(ta.y) > 0.4999f, fabsf(tb.x) > 0.4999f, fabsf(tb.y) > 0.4999f};
+        if (__builtin_amdgcn_ballot_w64(sl[0] | sl[1] | sl[2] | sl[3]))  // one branch per four cells
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
-          if (__builtin_amdgcn_ballot_w64(sl[m]))
-            if (sl[m]) word = (word & ~(0xFFu << (8 * m))) | (q8(xs[m], mn, rng) << (8 * m));
+          for (int m = 0; m < 4; ++m)
+            if (__builtin_amdgcn_ballot_w64(sl[m]))
+              if (sl[m]) word = (word & ~(0xFFu << (8 * m))) | (q8(xs[m], mn, rng) << (8 * m));
         w[k] = word;
       } else {
         w[k] = qb(f.x) | (qb(f.y) << 8) | (qb(f.z) << 16) | (qb(f.w) << 24);

@@ -375,6 +375,7 @@ class ProgressiveSimilaritySearchEngine(*_bases("interfaces", "SimilaritySearchE
     def __init__(self, similarity_threshold: float = 0.1, max_candidates_per_level: int = 100):
         self.similarity_threshold = similarity_threshold
         self.max_candidates_per_level = max_candidates_per_level
+        self._pool_cache = None  # (index arrays of the last uniform pool, their resident IndexCorpus)
 
     # ---- structure -----------------------------------------------------------------------------
     def _parse_index_structure(self, indices, total_space: int) -> List[LevelConfig]:
@@ -388,6 +389,20 @@ class ProgressiveSimilaritySearchEngine(*_bases("interfaces", "SimilaritySearchE
     def _corpus(self, rows) -> IndexCorpus:
         C, flags = _stack_rows(rows)
         return IndexCorpus(C, row_f32=flags)
+
+    def _pool_corpus(self, pool) -> IndexCorpus:
+        """The resident corpus of a candidate pool, re-used while the pool holds the same index arrays
+        in the same order (the reference re-scores every candidate per call; re-uploading and
+        re-preparing the pool per query was O(pool) host and PCIe work).  The arrays are kept
+        referenced, so an identity match is a match; a QuantizedModel's hierarchical_indices are never
+        written after creation (the reference's pipeline builds a new array per model)."""
+        arrays = [c.hierarchical_indices for c in pool]
+        hit = self._pool_cache
+        if hit is not None and len(hit[0]) == len(arrays) and all(a is b for a, b in zip(hit[0], arrays)):
+            return hit[1]
+        corpus = self._corpus(arrays)
+        self._pool_cache = (arrays, corpus)
+        return corpus
 
     def _scores_at_level(self, q: np.ndarray, cands: Sequence[np.ndarray], level: int) -> np.ndarray:
         """compare_indices_at_level(q, c, level) for every candidate, on the GPU."""
@@ -480,7 +495,7 @@ class ProgressiveSimilaritySearchEngine(*_bases("interfaces", "SimilaritySearchE
             return []
         q = _idx(query_indices)
         if self._uniform(q, candidate_pool):
-            corpus = self._corpus([c.hierarchical_indices for c in candidate_pool])
+            corpus = self._pool_corpus(candidate_pool)
             ids, ov, lv = corpus.brute_force(q[None], min(max_results, len(candidate_pool)))
             return self._results(candidate_pool, to_np(ids)[0], to_np(ov)[0], to_np(lv)[0], with_error=False)
         ov, lv = self._overall_many(q, [c.hierarchical_indices for c in candidate_pool])
@@ -495,7 +510,7 @@ class ProgressiveSimilaritySearchEngine(*_bases("interfaces", "SimilaritySearchE
         if not self._parse_index_structure(q, len(q)):
             return []
         if self._uniform(q, candidate_pool):
-            corpus = self._corpus([c.hierarchical_indices for c in candidate_pool])
+            corpus = self._pool_corpus(candidate_pool)
             ids, ov, lv, cnt = corpus.progressive(q[None], max_results, self.similarity_threshold,
                                                   self.max_candidates_per_level)
             return self._results(candidate_pool, to_np(ids)[0], to_np(ov)[0], to_np(lv)[0], int(to_np(cnt)[0]))
@@ -512,7 +527,7 @@ class ProgressiveSimilaritySearchEngine(*_bases("interfaces", "SimilaritySearchE
         if not qs or any(len(q) != L for q in qs) or L == 0 or not self._parse_index_structure(qs[0], L) \
                 or not self._uniform(qs[0], candidate_pool):
             return [self.progressive_search(q, candidate_pool, max_results) for q in qs]
-        corpus = self._corpus([c.hierarchical_indices for c in candidate_pool])
+        corpus = self._pool_corpus(candidate_pool)
         Qa, qflags = _stack_rows(qs)
         ids, ov, lv, cnt = corpus.progressive(Qa if qflags is None else (Qa, qflags), max_results,
                                               self.similarity_threshold,

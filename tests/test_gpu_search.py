@@ -586,3 +586,33 @@ def test_overall_split_scan_matches_f64_scan(hq_lib, hq_option, N, L):
         rid, rsc, _ = O.brute_force_search(Q[a], C, k)
         assert list(got[1][a]) == list(rid), a
         np.testing.assert_allclose(got[0][a], rsc, atol=TOL)
+
+
+def test_dropin_pool_corpus_reused_per_pool(hq_lib):
+    """ProgressiveSimilaritySearchEngine keeps the resident corpus of the last uniform pool: the same
+    pool (same index arrays, same order) re-uses it; a pool with one model replaced, or re-ordered, is
+    re-uploaded, and every call still equals the oracle."""
+    from hq_mi355x.core import ProgressiveSimilaritySearchEngine
+    from hq_mi355x.models import ModelMetadata, QuantizedModel
+    C = _corpus(400, 64, 21)
+    pool = [QuantizedModel(b"x", (8, 8), 1, 0.8, C[i], ModelMetadata(f"m{i}", 1, 1, 1.0, "t")) for i in range(len(C))]
+    eng = ProgressiveSimilaritySearchEngine(0.1, 20)
+    rng = np.random.default_rng(5)
+
+    def check(p, q):
+        r = eng.brute_force_search(q, p, 10)
+        M = np.stack([m.hierarchical_indices for m in p])
+        rid, rsc, _ = O.brute_force_search(q, M, 10)
+        pos = {id(m): i for i, m in enumerate(p)}
+        assert [pos[id(x.model)] for x in r] == list(rid)
+
+    q = C[7] + rng.normal(0, 0.01, 64)
+    check(pool, q)
+    first = eng._pool_cache[1]
+    check(pool, C[9] + 0.0)
+    assert eng._pool_cache[1] is first                        # same pool: no re-upload
+    pool2 = list(pool)
+    pool2[3] = QuantizedModel(b"x", (8, 8), 1, 0.8, C[7] + 1e-3, ModelMetadata("new", 1, 1, 1.0, "t"))
+    check(pool2, q)
+    assert eng._pool_cache[1] is not first                    # a replaced model: new corpus
+    check(pool2[::-1], q)                                     # re-ordered: new corpus, ids follow the order

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes (one rocprofv3 run per pass) for one kernel of tools/scan_debug.py:
-#   tools/pmc_kernel.sh <kernel-name-substring> <outdir> [level0|overall]
+#   tools/pmc_kernel.sh <kernel-name-substring> <outdir> [level0|overall|chunk]
 # P1 issue/wait split, P2 instruction mix + MFMA busy, P3 L2 hits/misses + clock, P4 LDS + L1.
 set -u
 K=${1:-k_scan0g}
@@ -15,7 +15,9 @@ P4="SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_
 i=0
 for P in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $P -d $OUT/p$i -o p$i --output-format csv -- python3 tools/scan_debug.py $MODE > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -3 $OUT/p$i.log; exit 1; }
+  DRV="tools/scan_debug.py $MODE"
+  [ "$MODE" = "chunk" ] && DRV="tools/chunk_debug.py"
+  timeout -s KILL 120 rocprofv3 --pmc $P -d $OUT/p$i -o p$i --output-format csv -- python3 $DRV > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -3 $OUT/p$i.log; exit 1; }
 done
 python3 - "$K" "$OUT" <<'PY'
 import csv, glob, sys
