@@ -78,6 +78,69 @@ __global__ __launch_bounds__(256) void k_cos_prepare(const float* __restrict__ X
   }
 }
 
+// ---- tiled fragment layout (default) ------------------------------------------------------------------
+// Fragment (16-row tile t, K step kb, plane p) = 512 halves (1 KiB) at ((t KB + kb) 2 + p) 512, KB = Kp / 32;
+// lane 16 g + j holds row 16 t + j, k = 32 kb + 8 g .. + 7 — exactly the v_mfma_f32_16x16x32_f16 A / B
+// operand, so one fragment is one contiguous 1 KiB wave load (16 B per lane) and, staged in LDS
+// lane-linearly, one bank-conflict-free ds_read_b128.
+__device__ __forceinline__ int64_t cos_frag(int64_t t, int kb, int KB, int p) {
+  return ((t * KB + kb) * 2 + p) * 512;
+}
+
+__global__ __launch_bounds__(256) void k_cos_prepare_tiled(const float* __restrict__ X, int64_t N, int64_t ld, int K,
+                                                           int Kp, int64_t rows_out, _Float16* __restrict__ X16,
+                                                           double* __restrict__ inv) {
+  // one wave per row; lane c writes the 8-value chunks c, c + 64, ... (16 B per plane each)
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int KB = Kp / kCosK, C = Kp / 8;
+  for (int64_t r = w0; r < rows_out; r += nw) {
+    const int64_t t = r >> 4;
+    const int j = (int)(r & 15);
+    auto put = [&](int c, const h8& hi, const h8& lo) {
+      const int kb = c >> 2, g = c & 3;
+      _Float16* f = X16 + cos_frag(t, kb, KB, 0) + 8 * (16 * g + j);
+      *reinterpret_cast<h8*>(f) = hi;
+      *reinterpret_cast<h8*>(f + 512) = lo;
+    };
+    if (r >= N) {  // pad rows: zeros, inv 0
+      const h8 z = {};
+      for (int c = lane; c < C; c += 64) put(c, z, z);
+      if (lane == 0) inv[r] = 0.0;
+      continue;
+    }
+    const float* x = X + r * ld;
+    float amax = 0.0f;
+    double ss = 0.0;
+    for (int k = lane; k < K; k += 64) {
+      const float v = x[k];
+      amax = fmaxf(amax, fabsf(v));
+      ss = fma((double)v, (double)v, ss);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+      ss += __shfl_xor(ss, o, 64);
+    }
+    int e = 0;
+    if (amax > 0.0f) frexpf(amax, &e);  // amax = m 2^e, m in [0.5, 1)
+    const float s = ldexpf(1.0f, -e);   // s x in (-1, 1)
+    for (int c = lane; c < C; c += 64) {
+      h8 hi, lo;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = 8 * c + u;
+        const float v = k < K ? x[k] * s : 0.0f;
+        const _Float16 h = (_Float16)v;
+        hi[u] = h;
+        lo[u] = (_Float16)(v - (float)h);
+      }
+      put(c, hi, lo);
+    }
+    if (lane == 0) inv[r] = ss > 0.0 ? 1.0 / ((double)s * sqrt(ss)) : 0.0;
+  }
+}
+
 // ---- GEMM + epilogue ---------------------------------------------------------------------------------
 struct CosArgs {
   const _Float16* A;  // queries [Qp, 2, Kp]
@@ -390,6 +453,186 @@ __global__ __launch_bounds__(TN * 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
     }
 }
 
+// Tiled-layout kernel (default).  Workgroup = 8 waves (2 per SIMD), tile 128 queries x 128 FT frames; wave
+// w owns frames 16 FT w .. + 16 FT - 1 against all 128 queries (8 x FT accumulator tiles).  Only the query
+// operand goes through LDS (16 fragments = 16 KiB per K step, two stages, register-staged: each wave loads
+// and stores two of them), read by all 8 waves; every frame fragment is used by exactly one wave of the
+// workgroup, so it goes straight from global memory into that wave's VGPRs (contiguous 1 KiB loads, two
+// K steps ahead) and never touches LDS.  Per K step and wave: 16 ds_read_b128 + 2 ds_write_b128, 2 + 2 FT
+// global loads, 24 FT MFMAs; one block barrier.  Per output the MFMA sequence is k_cos_g3's (per K step
+// hi.hi, hi.lo, lo.hi), so the scores are bit-identical to it.
+template <int FT, int PP>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_cos_t(CosArgs a, int64_t ftiles) {
+  __shared__ __attribute__((aligned(16))) _Float16 sA[2][16 * 512];
+  constexpr int QT = 8, TN = 8 * 16 * FT;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t blk = blockIdx.x;
+  const int64_t xcd = blk & 7, slot = blk >> 3;
+  const int qt = (int)(slot % a.qtiles);
+  const int64_t nt = xcd + 8 * (slot / a.qtiles);
+  if (nt >= a.ntiles) return;
+  const int KB = a.Kp / kCosK;
+  const int64_t qt0 = (int64_t)qt * QT;
+  // this thread's two query pieces per step: fragment f = wv + 8 i -> query tile f >> 1, plane f & 1
+  const _Float16* srcA[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int f = wv + 8 * i;
+    srcA[i] = a.A + cos_frag(qt0 + (f >> 1), 0, KB, f & 1) + 8 * lane;
+  }
+  const _Float16* srcB[FT];
+#pragma unroll
+  for (int j = 0; j < FT; ++j) {
+    int64_t t = nt * (TN / 16) + wv * FT + j;
+    if (t > ftiles - 1) t = ftiles - 1;  // the last frame tile may pass the padded rows
+    srcB[j] = a.B + cos_frag(t, 0, KB, 0) + 8 * lane;
+  }
+  h8 ra[2];
+  h8 rb0[FT][2], rb1[FT][2], rb2[FT][2];  // frame fragments of steps s, s + 1, s + 2 (a ring, unrolled by 3)
+  auto loadA = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ra[i] = *reinterpret_cast<const h8*>(srcA[i] + (int64_t)kb * 1024);
+  };
+  auto loadB = [&](int kb, h8 (&d)[FT][2]) {
+#pragma unroll
+    for (int j = 0; j < FT; ++j) {
+      d[j][0] = *reinterpret_cast<const h8*>(srcB[j] + (int64_t)kb * 1024);
+      d[j][1] = *reinterpret_cast<const h8*>(srcB[j] + (int64_t)kb * 1024 + 512);
+    }
+  };
+  auto storeA = [&](int st) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<h8*>(&sA[st][(wv + 8 * i) * 512 + 8 * lane]) = ra[i];
+  };
+  f4 acc[QT][FT];
+#pragma unroll
+  for (int i = 0; i < QT; ++i)
+#pragma unroll
+    for (int j = 0; j < FT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // one K step: b = frame fragments of step s, nb = the ring slot that receives step s + 2
+  auto step = [&](int s, const h8 (&b)[FT][2], h8 (&nb)[FT][2]) {
+    const int st = s & 1;
+    // query pieces of step s + 1 into the other stage (read by every wave in step s - 1, which ended at
+    // the last barrier), then the loads for step s + 2: query pieces first, so the wait for them at the
+    // next step leaves the frame fragments of s + 2 in flight
+    // (branch-free: past the end the loads repeat the last step and the store fills a stage nobody reads
+    // again — a conditional load would make the compiler's vmcnt merge wait for the new loads too)
+    storeA(st ^ 1);
+    const int nk = s + 2 < KB ? s + 2 : KB - 1;
+    loadA(nk);
+    loadB(nk, nb);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PP) {
+      // memory phase: every query fragment of the step into registers, then publish; compute phase: 24 FT
+      // MFMAs while the SIMD's other wave runs its memory phase
+      h8 af[QT][2];
+#pragma unroll
+      for (int i = 0; i < QT; ++i) {
+        af[i][0] = *reinterpret_cast<const h8*>(&sA[st][(2 * i) * 512 + 8 * lane]);
+        af[i][1] = *reinterpret_cast<const h8*>(&sA[st][(2 * i + 1) * 512 + 8 * lane]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < QT; ++i)
+#pragma unroll
+        for (int j = 0; j < FT; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][0], b[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][0], b[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][1], b[j][0], acc[i][j], 0, 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < QT; ++i) {
+        const h8 ah = *reinterpret_cast<const h8*>(&sA[st][(2 * i) * 512 + 8 * lane]);
+        const h8 al = *reinterpret_cast<const h8*>(&sA[st][(2 * i + 1) * 512 + 8 * lane]);
+#pragma unroll
+        for (int j = 0; j < FT; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, b[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, b[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, b[j][0], acc[i][j], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  };
+
+  loadA(0);
+  loadB(0, rb0);
+  storeA(0);
+  loadA(KB > 1 ? 1 : 0);
+  loadB(KB > 1 ? 1 : 0, rb1);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  // ping-pong: waves w and w + 4 share a SIMD; group 1 (waves 4-7) runs one barrier phase behind group 0,
+  // so each SIMD alternates one wave's memory phase with the other's MFMAs.  A stage is read in the memory
+  // phases of step s (group 0 at phase 2s, group 1 at 2s + 1) and rewritten in those of step s + 1 (2s + 2,
+  // 2s + 3); each memory phase ends with lgkmcnt(0) + barrier, so no write overtakes a read and every write
+  // is published before its first reader.  Group 0 takes one extra barrier at the end: equal counts.
+  const int grp = __builtin_amdgcn_readfirstlane(wv >> 2);
+  if (PP && grp) asm volatile("s_barrier" ::: "memory");
+  int s = 0;
+  for (; s + 3 <= KB; s += 3) {
+    step(s, rb0, rb2);
+    step(s + 1, rb1, rb0);
+    step(s + 2, rb2, rb1);
+  }
+  if (s < KB) step(s, rb0, rb2);
+  if (s + 1 < KB) step(s + 1, rb1, rb0);
+  if (PP && !grp) asm volatile("s_barrier" ::: "memory");
+  // epilogue: lane holds queries 16 i + 4 (lane >> 4) + r, frames 16 j + (lane & 15) of its wave's columns;
+  // the inverse norms are loaded once (ia / ib cover the padded rows; a frame column past them is clamped
+  // for the load and never stored)
+  const int64_t q0 = qt0 * 16, n0 = nt * TN + (int64_t)wv * 16 * FT;
+  const int64_t nrows = ftiles * 16;
+  double ic[FT];
+#pragma unroll
+  for (int j = 0; j < FT; ++j) {
+    const int64_t n = n0 + 16 * j + (lane & 15);
+    ic[j] = a.ib[n < nrows ? n : nrows - 1];
+  }
+#pragma unroll
+  for (int i = 0; i < QT; ++i) {
+    const int64_t qb = q0 + 16 * i + 4 * (lane >> 4);
+    const double4 iq4 = *reinterpret_cast<const double4*>(a.ia + qb);
+    const double iqv[4] = {iq4.x, iq4.y, iq4.z, iq4.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t q = qb + r;
+      if (q >= a.Q) continue;
+      const double iq = iqv[r];
+#pragma unroll
+      for (int j = 0; j < FT; ++j) {
+        const int64_t n = n0 + 16 * j + (lane & 15);
+        if (n >= a.N) continue;
+        const double cs = (double)acc[i][j][r] * iq * ic[j];
+        const double v = (iq != 0.0 && ic[j] != 0.0) ? (cs + 1.0) / 2.0 : 0.0;
+        __builtin_nontemporal_store(v, a.out + q * a.N + n);  // write-once scores
+      }
+    }
+  }
+}
+
+template <int FT, int PP>
+static int launch_t(CosArgs a, hipStream_t s) {
+  constexpr int TN = 8 * 16 * FT;
+  const int64_t np_rows = a.ntiles * kCosT;
+  a.qtiles = (int)(hq_cos_padded_rows(a.Q) / 128);
+  a.ntiles = (np_rows + TN - 1) / TN;
+  const int64_t nt8 = ((a.ntiles + 7) / 8) * 8;
+  const int64_t blocks = nt8 * a.qtiles;
+  if (blocks > 0x7FFFFFFF) return fail(HQ_E_UNSUPPORTED, "too many tiles");
+  auto kern = k_cos_t<FT, PP>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), 0, s, a, np_rows / 16);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
 template <int TN, int PP, bool NTS = true>
 static int launch_g3(CosArgs a, hipStream_t s) {
   const int64_t np_rows = a.ntiles * kCosT;
@@ -436,7 +679,10 @@ int hq_cos_prepare(const float* X, int64_t N, int64_t ld, int K, void* X16, doub
   const int64_t rows = hq_cos_padded_rows(N);
   int64_t blocks = (rows + 3) / 4;
   if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(k_cos_prepare, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, X, N, ld, K, Kp, rows,
+  // the row-major layout only for the superseded A/B kernels (option cos_kernel 1-3)
+  const int64_t ek = opt(OPT_COS_KERNEL, 0);
+  auto kern = ek >= 1 && ek <= 3 ? k_cos_prepare : k_cos_prepare_tiled;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, X, N, ld, K, Kp, rows,
                      reinterpret_cast<_Float16*>(X16), inv);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
@@ -462,8 +708,10 @@ int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* 
   const int64_t ek = opt(OPT_COS_KERNEL, 0);
   if (ek == 1) return launch_cos<128>(a, (hipStream_t)stream);
   if (ek == 2) return launch_g3<256, 0>(a, (hipStream_t)stream);
-  if (ek == 3) return launch_g3<256, 1, false>(a, (hipStream_t)stream);
-  return launch_g3<256, 1>(a, (hipStream_t)stream);
+  if (ek == 3) return launch_g3<256, 1>(a, (hipStream_t)stream);
+  if (ek == 4) return launch_t<2, 0>(a, (hipStream_t)stream);
+  if (ek == 5) return launch_t<1, 1>(a, (hipStream_t)stream);
+  return launch_t<2, 1>(a, (hipStream_t)stream);
 }
 
 }  // extern "C"

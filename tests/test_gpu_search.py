@@ -329,20 +329,25 @@ def test_cosine_mfma_vs_reference_golden(hq_lib, golden):
 
 @pytest.mark.parametrize("Q,N,K", [(130, 300, 1024), (257, 700, 4096), (1, 257, 32), (5, 40, 64)])
 def test_cosine_dma_kernels_match_regstage(hq_lib, Q, N, K, hq_option):
-    """The default LDS-DMA ping-pong kernel (k_cos_g3<256, 1>: 256-frame tiles, swizzled LDS, staggered
-    wave groups), its lockstep form and the register-staged baseline (k_cos_mfma, 128-frame tiles) run
-    the same MFMA sequence per output, so their scores are bit-identical; ragged last frame tile (N not
-    a multiple of 256) and 1- and 2-step K loops (K = 32, 64: the prologue / drain paths) included."""
+    """The default tiled-layout kernel (k_cos_t: frame fragments straight into VGPRs, query fragments
+    through LDS), the LDS-DMA ping-pong kernel (k_cos_g3<256, 1>: swizzled row-major LDS, staggered wave
+    groups), its lockstep form and the register-staged baseline (k_cos_mfma, 128-frame tiles) run the same
+    MFMA sequence per output, so their scores are bit-identical; ragged last frame tile (N not a multiple
+    of 256) and 1- and 2-step K loops (K = 32, 64: the prologue / drain paths) included.  The layout of
+    the prepared rows follows the kernel option, so each kernel prepares its own operands."""
     import torch
     from hq_mi355x import kernels as K_
     rng = np.random.default_rng(11 + Q + N)
     A = rng.standard_normal((Q, K)).astype(np.float32)
     B = rng.standard_normal((N, K)).astype(np.float32)
-    pa, pb = K_.cos_prepare(torch.from_numpy(A).cuda()), K_.cos_prepare(torch.from_numpy(B).cuda())
-    got = _np(K_.cosine_scores_mfma(pa, pb))
-    for kern, code in (("lockstep", 2), ("regstage", 1)):
+
+    def run():
+        pa, pb = K_.cos_prepare(torch.from_numpy(A).cuda()), K_.cos_prepare(torch.from_numpy(B).cuda())
+        return _np(K_.cosine_scores_mfma(pa, pb))
+    got = run()
+    for kern, code in (("tiled lockstep", 4), ("tiled 128 x 128", 5), ("ping-pong", 3), ("lockstep", 2), ("regstage", 1)):
         hq_option("cos_kernel", code)
-        np.testing.assert_array_equal(got, _np(K_.cosine_scores_mfma(pa, pb)), err_msg=kern)
+        np.testing.assert_array_equal(got, run(), err_msg=kern)
 
 
 @pytest.mark.parametrize("L", [64, 32, 256])
