@@ -32,6 +32,7 @@ namespace hq {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
 
 constexpr int kCosT = 128;                 // tile rows (queries) = tile cols (frames)
 constexpr int kCosK = 32;                  // K per step
@@ -461,9 +462,12 @@ __global__ __launch_bounds__(TN * 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
 // K steps ahead) and never touches LDS.  Per K step and wave: 16 ds_read_b128 + 2 ds_write_b128, 2 + 2 FT
 // global loads, 24 FT MFMAs; one block barrier.  Per output the MFMA sequence is k_cos_g3's (per K step
 // hi.hi, hi.lo, lo.hi), so the scores are bit-identical to it.
-template <int FT, int PP>
+template <int FT, int PP, int D, int EP>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_cos_t(CosArgs a, int64_t ftiles) {
-  __shared__ __attribute__((aligned(16))) _Float16 sA[2][16 * 512];
+  // two query stages (32 KiB); after the K loop the epilogue stages one 16-query row block per wave here
+  constexpr int kSm = 2 * 16 * 512 * 2 > 8 * 16 * 16 * FT * 8 ? 2 * 16 * 512 * 2 : 8 * 16 * 16 * FT * 8;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kSm];
+  _Float16(*sA)[16 * 512] = reinterpret_cast<_Float16(*)[16 * 512]>(smem);
   constexpr int QT = 8, TN = 8 * 16 * FT;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t blk = blockIdx.x;
@@ -519,9 +523,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     // (branch-free: past the end the loads repeat the last step and the store fills a stage nobody reads
     // again — a conditional load would make the compiler's vmcnt merge wait for the new loads too)
     storeA(st ^ 1);
-    const int nk = s + 2 < KB ? s + 2 : KB - 1;
-    loadA(nk);
-    loadB(nk, nb);
+    loadA(s + 2 < KB ? s + 2 : KB - 1);
+    loadB(s + D < KB ? s + D : KB - 1, nb);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (PP) {
       // memory phase: every query fragment of the step into registers, then publish; compute phase: 24 FT
@@ -567,7 +570,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   loadB(0, rb0);
   storeA(0);
   loadA(KB > 1 ? 1 : 0);
-  loadB(KB > 1 ? 1 : 0, rb1);
+  if (D == 2) loadB(KB > 1 ? 1 : 0, rb1);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   // ping-pong: waves w and w + 4 share a SIMD; group 1 (waves 4-7) runs one barrier phase behind group 0,
   // so each SIMD alternates one wave's memory phase with the other's MFMAs.  A stage is read in the memory
@@ -577,13 +580,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int grp = __builtin_amdgcn_readfirstlane(wv >> 2);
   if (PP && grp) asm volatile("s_barrier" ::: "memory");
   int s = 0;
-  for (; s + 3 <= KB; s += 3) {
-    step(s, rb0, rb2);
-    step(s + 1, rb1, rb0);
-    step(s + 2, rb2, rb1);
+  if constexpr (D == 2) {  // frame fragments two steps ahead: a ring of three
+    for (; s + 3 <= KB; s += 3) {
+      step(s, rb0, rb2);
+      step(s + 1, rb1, rb0);
+      step(s + 2, rb2, rb1);
+    }
+    if (s < KB) step(s, rb0, rb2);
+    if (s + 1 < KB) step(s + 1, rb1, rb0);
+  } else {  // one step ahead: a ring of two
+    for (; s + 2 <= KB; s += 2) {
+      step(s, rb0, rb1);
+      step(s + 1, rb1, rb0);
+    }
+    if (s < KB) step(s, rb0, rb1);
   }
-  if (s < KB) step(s, rb0, rb2);
-  if (s + 1 < KB) step(s + 1, rb1, rb0);
   if (PP && !grp) asm volatile("s_barrier" ::: "memory");
   // epilogue: lane holds queries 16 i + 4 (lane >> 4) + r, frames 16 j + (lane & 15) of its wave's columns;
   // the inverse norms are loaded once (ia / ib cover the padded rows; a frame column past them is clamped
@@ -596,6 +607,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     const int64_t n = n0 + 16 * j + (lane & 15);
     ic[j] = a.ib[n < nrows ? n : nrows - 1];
   }
+  // EP 1 (even N): each 16-query row block goes through the wave's LDS slice (16 x 16 FT f64, row-major)
+  // and leaves as 16-byte stores of two adjacent frames; EP 0 (or odd N, whose rows are not all 16-byte
+  // aligned): 8-byte stores straight from the accumulator layout
+  const bool wide = EP == 1 && (a.N & 1) == 0;
+  double* stage = reinterpret_cast<double*>(smem) + wv * 16 * 16 * FT;
 #pragma unroll
   for (int i = 0; i < QT; ++i) {
     const int64_t qb = q0 + 16 * i + 4 * (lane >> 4);
@@ -604,21 +620,40 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t q = qb + r;
-      if (q >= a.Q) continue;
       const double iq = iqv[r];
 #pragma unroll
       for (int j = 0; j < FT; ++j) {
         const int64_t n = n0 + 16 * j + (lane & 15);
-        if (n >= a.N) continue;
         const double cs = (double)acc[i][j][r] * iq * ic[j];
         const double v = (iq != 0.0 && ic[j] != 0.0) ? (cs + 1.0) / 2.0 : 0.0;
-        __builtin_nontemporal_store(v, a.out + q * a.N + n);  // write-once scores
+        if constexpr (EP == 2) {  // diagnostics: no stores (wrong output; A/B of the epilogue's cost)
+          if (v == -1.0) a.out[0] = v;
+        } else if (wide) {
+          stage[(4 * (lane >> 4) + r) * 16 * FT + 16 * j + (lane & 15)] = v;
+        } else if (q < a.Q && n < a.N) {
+          __builtin_nontemporal_store(v, a.out + q * a.N + n);  // write-once scores
+        }
+      }
+    }
+    if (wide) {
+      // 16 rows x 8 FT pairs of frames; lane c takes pairs c, c + 64, ...
+#pragma unroll
+      for (int u = 0; u < (16 * 8 * FT + 63) / 64; ++u) {
+        const int c = lane + 64 * u;
+        if (c >= 16 * 8 * FT) break;
+        const int row = c / (8 * FT), pr = c % (8 * FT);
+        const int64_t q = q0 + 16 * i + row, n = n0 + 2 * pr;
+        const d2v v2 = *reinterpret_cast<const d2v*>(stage + row * 16 * FT + 2 * pr);
+        if (q < a.Q) {
+          if (n + 1 < a.N) __builtin_nontemporal_store(v2, reinterpret_cast<d2v*>(a.out + q * a.N + n));
+          else if (n < a.N) __builtin_nontemporal_store(v2.x, a.out + q * a.N + n);
+        }
       }
     }
   }
 }
 
-template <int FT, int PP>
+template <int FT, int PP, int D = 2, int EP = 0>
 static int launch_t(CosArgs a, hipStream_t s) {
   constexpr int TN = 8 * 16 * FT;
   const int64_t np_rows = a.ntiles * kCosT;
@@ -627,7 +662,7 @@ static int launch_t(CosArgs a, hipStream_t s) {
   const int64_t nt8 = ((a.ntiles + 7) / 8) * 8;
   const int64_t blocks = nt8 * a.qtiles;
   if (blocks > 0x7FFFFFFF) return fail(HQ_E_UNSUPPORTED, "too many tiles");
-  auto kern = k_cos_t<FT, PP>;
+  auto kern = k_cos_t<FT, PP, D, EP>;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), 0, s, a, np_rows / 16);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
@@ -709,9 +744,18 @@ int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* 
   if (ek == 1) return launch_cos<128>(a, (hipStream_t)stream);
   if (ek == 2) return launch_g3<256, 0>(a, (hipStream_t)stream);
   if (ek == 3) return launch_g3<256, 1>(a, (hipStream_t)stream);
+  // tiled-layout forms: 4 lockstep 128 x 256, 5 ping-pong 128 x 128, 6 ping-pong 128 x 256
+  // with frame fragments two steps ahead, 7 the same one step ahead, 8 the default with 16-byte score
+  // stores through LDS
   if (ek == 4) return launch_t<2, 0>(a, (hipStream_t)stream);
   if (ek == 5) return launch_t<1, 1>(a, (hipStream_t)stream);
-  return launch_t<2, 1>(a, (hipStream_t)stream);
+  if (ek == 6) return launch_t<2, 1, 2>(a, (hipStream_t)stream);
+  if (ek == 7) return launch_t<2, 1, 1>(a, (hipStream_t)stream);
+  if (ek == 8) return launch_t<3, 1, 1, 1>(a, (hipStream_t)stream);
+#ifdef HQ_DIAG
+  if (ek == 90) return launch_t<3, 1, 1, 2>(a, (hipStream_t)stream);  // no score stores (wrong output)
+#endif
+  return launch_t<3, 1, 1>(a, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -329,8 +329,9 @@ def test_cosine_mfma_vs_reference_golden(hq_lib, golden):
 
 @pytest.mark.parametrize("Q,N,K", [(130, 300, 1024), (257, 700, 4096), (1, 257, 32), (5, 40, 64)])
 def test_cosine_dma_kernels_match_regstage(hq_lib, Q, N, K, hq_option):
-    """The default tiled-layout kernel (k_cos_t: frame fragments straight into VGPRs, query fragments
-    through LDS), the LDS-DMA ping-pong kernel (k_cos_g3<256, 1>: swizzled row-major LDS, staggered wave
+    """The default tiled-layout kernel (k_cos_t<3, 1, 1>: 128 x 384 tiles, frame fragments straight into
+    VGPRs one step ahead, query fragments through LDS, ping-pong wave groups), its other tile / prefetch /
+    epilogue forms, the LDS-DMA ping-pong kernel (k_cos_g3<256, 1>: swizzled row-major LDS, staggered wave
     groups), its lockstep form and the register-staged baseline (k_cos_mfma, 128-frame tiles) run the same
     MFMA sequence per output, so their scores are bit-identical; ragged last frame tile (N not a multiple
     of 256) and 1- and 2-step K loops (K = 32, 64: the prologue / drain paths) included.  The layout of
@@ -345,7 +346,9 @@ def test_cosine_dma_kernels_match_regstage(hq_lib, Q, N, K, hq_option):
         pa, pb = K_.cos_prepare(torch.from_numpy(A).cuda()), K_.cos_prepare(torch.from_numpy(B).cuda())
         return _np(K_.cosine_scores_mfma(pa, pb))
     got = run()
-    for kern, code in (("tiled lockstep", 4), ("tiled 128 x 128", 5), ("ping-pong", 3), ("lockstep", 2), ("regstage", 1)):
+    for kern, code in (("tiled lockstep 128 x 256", 4), ("tiled 128 x 128", 5), ("tiled 128 x 256", 6),
+                       ("tiled 128 x 256, one step ahead", 7), ("tiled, 16-byte stores", 8), ("ping-pong", 3),
+                       ("lockstep", 2), ("regstage", 1)):
         hq_option("cos_kernel", code)
         np.testing.assert_array_equal(got, run(), err_msg=kern)
 

@@ -12,7 +12,7 @@ from collections import defaultdict
 
 def short(name):
     for key in ("k_fused_np", "k_fused_fast", "k_fused", "k_scan0", "k_sample_hist", "k_hist_tau", "k_scan", "k_seg_prepare", "k_refine", "k_merge", "k_chunk_np", "k_chunk", "k_precomp",
-                "k_progressive_final", "k_rescore", "k_level_scores", "k_cos_glds", "k_cos_g3", "k_cos_mfma", "k_cos_prepare"):
+                "k_progressive_final", "k_rescore", "k_level_scores", "k_cos_glds", "k_cos_g3", "k_cos_t", "k_cos_mfma", "k_cos_prepare"):
         if key in name:
             if key == "k_fused_fast":
                 return "k_fused" + name.split("k_fused_fast<")[1].split(",")[0]
