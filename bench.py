@@ -512,6 +512,7 @@ def main():
         # alternates the batches over n HIP streams: 2 / 3 streams measured 1.43M / 0.7-1.05M vs 2.07M QPS
         # on one (two batches' scans contend for the CUs), so one stream is the default
         nstreams = int(os.environ.get("HQ_SEARCH_STREAMS", "1"))
+        depth = int(os.environ.get("HQ_SEARCH_DEPTH", "2"))  # batches in flight (A/B knob; 3 measured equal)
         streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
         pend, nsub = [], [0]
 
@@ -520,7 +521,7 @@ def main():
             nsub[0] += 1
             with torch.cuda.stream(st):
                 pend.append((st, engine.progressive_submit(queries, 10, 0.1, 20)))
-            if len(pend) > 1:
+            if len(pend) >= depth:
                 drain(1)
 
         def drain(n=None):
@@ -540,7 +541,7 @@ def main():
             "corpus_per_gpu": Nc, "corpus_total": Nc * world, "queries": Qn, "steps": args.search_steps,
             "ms_per_step": swall / args.search_steps * 1e3, "index_prepare_s": prep_s,
             "mode": "progressive (level-0 split-f16 MFMA scan top-28 >= 0.1 - eps, exact re-rank to top-20, "
-                    "overall re-score, top-10); up to 2 batches in flight (submit / finish)",
+                    f"overall re-score, top-10); up to {depth} batches in flight (submit / finish)",
             "roofline": {"bound": "mfma", "achieved": flops / skern / 1e12, "peak": FP16_MATRIX_PEAK_TFS,
                          "unit": "TFLOP/s", "frac": flops / skern / 1e12 / FP16_MATRIX_PEAK_TFS,
                          "note": "3 x 2*Q*N*32 f16 MFMA flops of the split level-0 contraction per step / step "

@@ -3482,7 +3482,7 @@ static int scan0_dispatch(int ks, const Scan0Args& b, const SampleArgs* sa, hipS
 static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const _Float16* Zq16, const float* Sq32,
                      int Q, const double* Zc, const double* Sc, const _Float16* Zc16, const float* Sc32, int64_t N,
                      const SegInfo& si, int k, double threshold, int thr_mode, int64_t id_base, void* workspace,
-                     double* out_score, int64_t* out_id, hipStream_t s) {
+                     double* out_score, int64_t* out_id, hipStream_t s, const int* corpus_flags = nullptr) {
 #ifndef HQ_DIAG
   if (!f32) return fail(HQ_E_UNSUPPORTED, "the f64 level-0 scan exists only in DIAG builds");
 #endif
@@ -3596,11 +3596,16 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
       hipLaunchKernelGGL(k_scan_qprep, dim3((Q + 255) / 256), dim3(256), 0, s, Sq32, Q, b.thr0, b.inv_m, qc, b.pool_n);
       HQ_CHECK_LAUNCH();
     }
-    HQ_CHECK_HIP(hipMemsetAsync(flag_n, 0, sizeof(int), s));
-    const int64_t fb = (N + 255) / 256;
-    hipLaunchKernelGGL(k_flag_rows, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, s, Sc32, N, flag_list,
-                       flag_n);
-    HQ_CHECK_LAUNCH();
+    if (corpus_flags) {  // the corpus's flagged rows listed once (hq_seg_flag_rows): [count, rows...]
+      flag_n = const_cast<int*>(corpus_flags);
+      flag_list = flag_n + 1;
+    } else {
+      HQ_CHECK_HIP(hipMemsetAsync(flag_n, 0, sizeof(int), s));
+      const int64_t fb = (N + 255) / 256;
+      hipLaunchKernelGGL(k_flag_rows, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, s, Sc32, N, flag_list,
+                         flag_n);
+      HQ_CHECK_LAUNCH();
+    }
     // options scan_wpb: waves per block (1 = one wave per block, each reading its own fragments);
     // scan_pf: prefetch distance in steps (2, 3, 4)
     const int pf = (int)opt(OPT_SCAN_PF, 2);
@@ -4702,10 +4707,30 @@ int hq_seg_pack0_split(const double* Z, const double* S, int64_t N, int L, void*
   return HQ_OK;
 }
 
+int hq_seg_flag_rows(const float* S32, int64_t N, int* flags, hq_stream_t stream) {
+  if (N < 0) return fail(HQ_E_INVALID, "bad shape N=%lld", (long long)N);
+  if (!flags || (N > 0 && !S32)) return fail(HQ_E_INVALID, "null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  HQ_CHECK_HIP(hipMemsetAsync(flags, 0, sizeof(int), s));
+  if (N == 0) return HQ_OK;
+  const int64_t fb = (N + 255) / 256;
+  hipLaunchKernelGGL(k_flag_rows, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, s, S32, N, flags + 1, flags);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
+}
+
 int hq_scan0_topk_split(const void* Zq16, const float* Sq32, const double* Sq, int Q, const void* Zc16,
                         const float* Sc32, const double* Sc, int64_t N, int L, int k, double threshold, int thr_mode,
                         int64_t id_base, void* workspace, size_t workspace_bytes, double* out_score,
                         int64_t* out_id, hq_stream_t stream) {
+  return hq_scan0_topk_split_fl(Zq16, Sq32, Sq, Q, Zc16, Sc32, Sc, N, L, k, threshold, thr_mode, id_base, workspace,
+                                workspace_bytes, out_score, out_id, nullptr, stream);
+}
+
+int hq_scan0_topk_split_fl(const void* Zq16, const float* Sq32, const double* Sq, int Q, const void* Zc16,
+                           const float* Sc32, const double* Sc, int64_t N, int L, int k, double threshold,
+                           int thr_mode, int64_t id_base, void* workspace, size_t workspace_bytes, double* out_score,
+                           int64_t* out_id, const int* corpus_flags, hq_stream_t stream) {
   if (Q < 0 || N < 0 || L <= 0) return fail(HQ_E_INVALID, "bad shape");
   if (k <= 0 || k > kMaxTopK) return fail(HQ_E_UNSUPPORTED, "k=%d (1..%d)", k, kMaxTopK);
   if (Q == 0) return HQ_OK;
@@ -4724,7 +4749,7 @@ int hq_scan0_topk_split(const void* Zq16, const float* Sq32, const double* Sq, i
   if (ks < 1 || ks > 8) return fail(HQ_E_UNSUPPORTED, "level-0 segment of %d values (1..32)", si.plen[0]);
   return scan0_run(true, ks, nullptr, Sq, reinterpret_cast<const _Float16*>(Zq16), Sq32, Q, nullptr, Sc,
                    reinterpret_cast<const _Float16*>(Zc16), Sc32, N, si, k, threshold, thr_mode, id_base, workspace,
-                   out_score, out_id, s);
+                   out_score, out_id, s, corpus_flags);
 }
 
 int hq_rescore(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc, const double* Zc,

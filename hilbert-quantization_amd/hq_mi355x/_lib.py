@@ -78,6 +78,8 @@ SIGNATURES = {
     "hq_seg_level0_len": (_i, [_i]),
     "hq_seg_pack0_split": (_i, [_p, _p, _i64, _i, _p, _p, _p]),
     "hq_scan0_topk_split": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _d, _i, _i64, _p, _sz, _p, _p, _p]),
+    "hq_seg_flag_rows": (_i, [_p, _i64, _p, _p]),
+    "hq_scan0_topk_split_fl": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _d, _i, _i64, _p, _sz, _p, _p, _p, _p]),
     "hq_seg_packov_info": (_i, [_i, _p, _p, _p, _p]),
     "hq_seg_packov_split": (_i, [_p, _p, _i64, _i, _p, _p, _p]),
     "hq_scanov_workspace_size": (_sz, [_i, _i64, _i]),

@@ -129,7 +129,7 @@ class IndexCorpus:
             raise ValueError("IndexCorpus expects a 2-D [N, L] array of index vectors")
         self.N, self.L = int(x.shape[0]), int(x.shape[1])
         self.id_base = int(id_base)
-        self.prep = K.packov(K.pack0(K.seg_prepare(x, src_f32=f32, row_f32=None if f32 else row_f32)))
+        self.prep = K.flag_rows(K.packov(K.pack0(K.seg_prepare(x, src_f32=f32, row_f32=None if f32 else row_f32))))
         self.nseg = self.prep.nseg
         # float32 rows outside the scans' model (values whose squares under/overflow in float32): the
         # whole corpus then takes the dense exact path (one host sync, at build time, f32 corpora only)
@@ -145,7 +145,8 @@ class IndexCorpus:
             q = q.view(1, -1)
         if q.shape[1] != self.L:
             raise ValueError(f"query index length {q.shape[1]} != corpus index length {self.L}")
-        return K.packov(K.pack0(K.seg_prepare(q, src_f32=f32, row_f32=None if f32 else row_f32)))
+        # the overall (brute-force) layout is attached by the first overall scan of the batch (scan_topk)
+        return K.pack0(K.seg_prepare(q, src_f32=f32, row_f32=None if f32 else row_f32))
 
     def _fused_ok(self, mode: int) -> bool:
         """The fused scans hold the contracted columns in registers: <= 256 padded values (hq_scan_topk)."""

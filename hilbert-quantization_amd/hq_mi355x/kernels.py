@@ -241,7 +241,7 @@ class Prepared:
     normalised) and stats S [N, nseg, 4] (mean, std, mean of squares, aux).  Built once per corpus.
     f32: some rows are float32 index vectors (aux bit 1; hq_seg_prepare_src / _rows)."""
 
-    __slots__ = ("R", "Z", "S", "L", "N", "nseg", "Lp", "Z16", "S32", "Zov16", "Sov32", "f32", "all32")
+    __slots__ = ("R", "Z", "S", "L", "N", "nseg", "Lp", "Z16", "S32", "F0", "Zov16", "Sov32", "f32", "all32")
 
     def __init__(self, R, Z, S, L, f32: bool = False, all32: bool = False):
         self.R, self.Z, self.S, self.L = R, Z, S, int(L)
@@ -251,6 +251,7 @@ class Prepared:
         self.f32 = bool(f32)      # some rows are float32 sources
         self.all32 = bool(all32)  # every row is
         self.Z16 = self.S32 = None  # split-f16 level-0 copies for the level-0 scan (pack0)
+        self.F0 = None  # a corpus's flagged rows of the level-0 copies, listed once (flag_rows)
         self.Zov16 = self.Sov32 = None  # split-f16 copies of every level for the overall scan (packov)
 
     def rows(self, sel):
@@ -327,6 +328,17 @@ def pack0(p: Prepared, exc=None) -> Prepared:
     return p
 
 
+def flag_rows(p: Prepared, exc=None) -> Prepared:
+    """List a corpus's flagged level-0 rows once (hq_seg_flag_rows: int32 [1 + N], count first), so the
+    level-0 scan of every query batch skips that pass over the statistics."""
+    if p.S32 is None:
+        return p
+    t = torch()
+    p.F0 = t.empty(1 + p.N, dtype=t.int32, device=p.Z.device)
+    _chk(_L().hq_seg_flag_rows(ptr(p.S32), p.N, ptr(p.F0), stream()), exc)
+    return p
+
+
 def level_scores(q: Prepared, c: Prepared, level: int, exc=None):
     """Dense EXACT [Q, N] level (>= 0) or overall (level = -1) scores (reference operation order)."""
     t = torch()
@@ -369,11 +381,13 @@ def scan_topk(q: Prepared, c: Prepared, mode: int, k: int, threshold: float = 0.
     # option scan_v1 (parity tests): the LDS-tiled k_scan instead of the split-f16 level-0 scan
     if (mode == 0 and not need_best and q.Z16 is not None and c.Z16 is not None
             and (q.f32 or c.f32 or _lib.get_option("scan_v1") is None)):
-        _chk(_L().hq_scan0_topk_split(ptr(q.Z16), ptr(q.S32), ptr(q.S), Q, ptr(c.Z16), ptr(c.S32), ptr(c.S), N, c.L,
-                                      k, float(threshold), thr_mode, int(id_base), ptr(ws), ws_bytes, ptr(sc),
-                                      ptr(ids), stream()), exc)
+        _chk(_L().hq_scan0_topk_split_fl(ptr(q.Z16), ptr(q.S32), ptr(q.S), Q, ptr(c.Z16), ptr(c.S32), ptr(c.S), N,
+                                         c.L, k, float(threshold), thr_mode, int(id_base), ptr(ws), ws_bytes,
+                                         ptr(sc), ptr(ids), None if c.F0 is None else ptr(c.F0), stream()), exc)
         return sc, ids, best, bid
     # option scan_v1 (parity tests): the f64 overall scan instead of the split overall scan
+    if mode == 1 and not need_best and q.Zov16 is None and c.Zov16 is not None and _lib.get_option("scan_v1") is None:
+        packov(q, exc)  # query batches get the overall layout only when an overall scan needs it
     if (mode == 1 and not need_best and q.Zov16 is not None and c.Zov16 is not None
             and _lib.get_option("scan_v1") is None):
         ws_bytes = int(_lib.load().hq_scanov_workspace_size(Q, N, k))

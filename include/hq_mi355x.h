@@ -238,6 +238,15 @@ int hq_scan0_topk_split(const void* Zq16, const float* Sq32, const double* Sq, i
                         const float* Sc32, const double* Sc, int64_t N, int L, int k, double threshold,
                         int thr_mode, int64_t id_base, void* workspace, size_t workspace_bytes,
                         double* out_score, int64_t* out_id, hq_stream_t stream);
+/* hq_seg_flag_rows: the rows of a split copy (S32 of hq_seg_pack0_split) whose zero-variance / f32-unsafe
+ *   flag is set, listed once per corpus into flags [1 + N] int32: flags[0] = count, then the rows (any
+ *   order).  hq_scan0_topk_split_fl: hq_scan0_topk_split with that list of the corpus (the plain entry
+ *   lists the flagged rows on every call: one memset and one pass over S32 per query batch).           */
+int hq_seg_flag_rows(const float* S32, int64_t N, int* flags, hq_stream_t stream);
+int hq_scan0_topk_split_fl(const void* Zq16, const float* Sq32, const double* Sq, int Q, const void* Zc16,
+                           const float* Sc32, const double* Sc, int64_t N, int L, int k, double threshold,
+                           int thr_mode, int64_t id_base, void* workspace, size_t workspace_bytes,
+                           double* out_score, int64_t* out_id, const int* corpus_flags, hq_stream_t stream);
 
 /* ---- S5 brute force: split-f16 overall scan ----------------------------------------------------
  * Replaces the per-candidate _calculate_overall_similarity loop of brute_force_search
