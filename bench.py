@@ -313,9 +313,9 @@ def bench_frames(args, world, rank, dev):
            "value": Qn * Nf * world * steps / wall, "unit": "pairs/sec", "queries": Qn, "frames_per_gpu": Nf,
            "K": Kd, "steps": steps, "ms_per_step": wall / steps * 1e3, "scaling": "weak",
            "roofline": {"bound": "mfma", "achieved": flops / kern / 1e12, "peak": peak, "unit": "TFLOP/s",
-                        "frac": flops / kern / 1e12 / peak, "traffic": load_traffic("k_cos_g3"),
+                        "frac": flops / kern / 1e12 / peak, "traffic": load_traffic("k_cos_t"),
                         "note": "algorithmic 2*Q*N*K f32 dot flops per step; peak = dense f16 MFMA / 3 (split-f16: "
-                                "hi.hi + hi.lo + lo.hi); traffic = HBM bytes per k_cos_g3 launch (PMC)"}}
+                                "hi.hi + hi.lo + lo.hi); traffic = HBM bytes per k_cos_t launch (PMC)"}}
     del corpus, Qf
     if rank == 0 and world == 1 and not args.no_cpu:
         from oracle import hq_oracle as O
