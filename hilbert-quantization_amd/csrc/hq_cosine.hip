@@ -9,20 +9,20 @@
 // for bit (DESIGN.md §4.5 has the error budget).
 //
 // Layout (hq_cos_prepare, once per corpus / query batch): every row x is scaled by a power of two s
-// (max |s x| in [0.5, 1)) and split as hi = f16(s x), lo = f16(s x - hi) into a row of Kp = K rounded
-// up to 32 halves each: X16 [rows, 2, Kp] (hi row then lo row), plus inv[row] = 1 / (s |x|) (f64 norm
-// of the original values; 0 for a zero row).  dot(a, b) = (hi_a.hi_b + hi_a.lo_b + lo_a.hi_b) / (s_a
-// s_b) + O(2^-22 |a||b|).
+// (max |s x| in [0.5, 1)) and split as hi = f16(s x), lo = f16(s x - hi), Kp = K rounded up to 32, stored
+// as 1 KiB MFMA operand fragments (16-row tile, K step of 32, plane hi / lo: see cos_frag), plus inv[row] =
+// 1 / (s |x|) (f64 norm of the original values; 0 for a zero row).  dot(a, b) = (hi_a.hi_b + hi_a.lo_b +
+// lo_a.hi_b) / (s_a s_b) + O(2^-22 |a||b|).
 //
-// GEMM (default k_cos_g3<256, 1>): workgroup = 8 waves, tile 128 queries x 256 frames, each wave 64 x 64
-// = 4 x 4 tiles of v_mfma_f32_16x16x32_f16 x 3 (hi.hi, hi.lo, lo.hi), K steps of 32.  Operands go HBM ->
-// LDS by global_load_lds_dwordx4 (LDS-DMA, no staging registers) into three stages, two steps ahead,
-// XOR-swizzled on the source address so the fragment reads are bank-conflict free.  Ping-pong: the two
-// waves of every SIMD run one barrier phase apart, one issuing its reads + DMA while the other runs
-// its MFMAs.  XCD-aware block order: the query tiles of one frame tile run back to back on one XCD, so
-// the frame tile is read from HBM once per XCD L2.  Epilogue: (acc * inv_q * inv_c + 1) / 2, f64
-// stores.  A/B baselines: k_cos_g3<256, 0> (same staging, waves in lockstep) and k_cos_mfma (register
-// staged, two buffers, 128 x 128).
+// GEMM (default k_cos_t<3, 1, 1>): workgroup = 8 waves, tile 128 queries x 384 frames, wave w = all 128
+// queries x frames 48 w .. + 47 (8 x 3 tiles of v_mfma_f32_16x16x32_f16 x 3: hi.hi, hi.lo, lo.hi), K steps
+// of 32.  Query fragments go through LDS (register-staged, two stages, read by every wave); frame
+// fragments, each used by one wave only, go straight from global memory into that wave's VGPRs one K step
+// ahead.  Ping-pong: the two waves of every SIMD run one barrier phase apart (memory phase / 72 MFMAs).
+// XCD-aware block order: the query tiles of one frame tile run back to back on one XCD, so the frame tile
+// is read from HBM once.  Epilogue: (acc * inv_q * inv_c + 1) / 2, f64 stores.  A/B forms (option
+// cos_kernel): the LDS-DMA kernel k_cos_g3 (ping-pong / lockstep) and the register-staged
+// k_cos_mfma on the row-major layout, and other k_cos_t tiles / prefetch distances / epilogues.
 #include "hq_common.h"
 
 #include <stdlib.h>
@@ -88,57 +88,63 @@ __device__ __forceinline__ int64_t cos_frag(int64_t t, int kb, int KB, int p) {
   return ((t * KB + kb) * 2 + p) * 512;
 }
 
-__global__ __launch_bounds__(256) void k_cos_prepare_tiled(const float* __restrict__ X, int64_t N, int64_t ld, int K,
-                                                           int Kp, int64_t rows_out, _Float16* __restrict__ X16,
-                                                           double* __restrict__ inv) {
-  // one wave per row; lane c writes the 8-value chunks c, c + 64, ... (16 B per plane each)
-  const int lane = threadIdx.x & 63;
-  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int KB = Kp / kCosK, C = Kp / 8;
-  for (int64_t r = w0; r < rows_out; r += nw) {
-    const int64_t t = r >> 4;
-    const int j = (int)(r & 15);
-    auto put = [&](int c, const h8& hi, const h8& lo) {
-      const int kb = c >> 2, g = c & 3;
-      _Float16* f = X16 + cos_frag(t, kb, KB, 0) + 8 * (16 * g + j);
-      *reinterpret_cast<h8*>(f) = hi;
-      *reinterpret_cast<h8*>(f + 512) = lo;
-    };
-    if (r >= N) {  // pad rows: zeros, inv 0
-      const h8 z = {};
-      for (int c = lane; c < C; c += 64) put(c, z, z);
-      if (lane == 0) inv[r] = 0.0;
-      continue;
+__global__ __launch_bounds__(1024) void k_cos_prepare_tiled(const float* __restrict__ X, int64_t N, int64_t ld, int K,
+                                                            int Kp, int64_t rows_out, _Float16* __restrict__ X16,
+                                                            double* __restrict__ inv) {
+  // one 16-wave workgroup per 16-row tile: wave w takes row w's statistics in k_cos_prepare's lane-strided
+  // order (same scale and inverse-norm bits), then the waves split the tile's K steps; per K step lane
+  // 16 g + j converts row j's values 8 g .. 8 g + 7, so every fragment leaves as one contiguous 1 KiB wave
+  // store per plane
+  __shared__ float sc[16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, j = lane & 15, g = lane >> 4;
+  const int KB = Kp / kCosK;
+  for (int64_t t = blockIdx.x; t < rows_out / 16; t += gridDim.x) {
+    const int64_t r0 = 16 * t + wv;
+    if (r0 >= N) {  // pad rows: zeros (scale 0), inv 0
+      if (lane == 0) {
+        sc[wv] = 0.0f;
+        inv[r0] = 0.0;
+      }
+    } else {
+      const float* x = X + r0 * ld;
+      float amax = 0.0f;
+      double ss = 0.0;
+      for (int k = lane; k < K; k += 64) {
+        const float v = x[k];
+        amax = fmaxf(amax, fabsf(v));
+        ss = fma((double)v, (double)v, ss);
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+        ss += __shfl_xor(ss, o, 64);
+      }
+      int e = 0;
+      if (amax > 0.0f) frexpf(amax, &e);  // amax = m 2^e, m in [0.5, 1)
+      const float s = ldexpf(1.0f, -e);   // s x in (-1, 1)
+      if (lane == 0) {
+        sc[wv] = s;
+        inv[r0] = ss > 0.0 ? 1.0 / ((double)s * sqrt(ss)) : 0.0;
+      }
     }
-    const float* x = X + r * ld;
-    float amax = 0.0f;
-    double ss = 0.0;
-    for (int k = lane; k < K; k += 64) {
-      const float v = x[k];
-      amax = fmaxf(amax, fabsf(v));
-      ss = fma((double)v, (double)v, ss);
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      amax = fmaxf(amax, __shfl_xor(amax, o, 64));
-      ss += __shfl_xor(ss, o, 64);
-    }
-    int e = 0;
-    if (amax > 0.0f) frexpf(amax, &e);  // amax = m 2^e, m in [0.5, 1)
-    const float s = ldexpf(1.0f, -e);   // s x in (-1, 1)
-    for (int c = lane; c < C; c += 64) {
+    __syncthreads();
+    const int64_t r = 16 * t + j;
+    const float my_s = sc[j];
+    const float* x = X + (r < N ? r : 0) * ld;
+    for (int kb = wv; kb < KB; kb += 16) {
       h8 hi, lo;
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int k = 8 * c + u;
-        const float v = k < K ? x[k] * s : 0.0f;
+        const int k = kCosK * kb + 8 * g + u;
+        const float v = (r < N && k < K) ? x[k] * my_s : 0.0f;
         const _Float16 h = (_Float16)v;
         hi[u] = h;
         lo[u] = (_Float16)(v - (float)h);
       }
-      put(c, hi, lo);
+      _Float16* f = X16 + cos_frag(t, kb, KB, 0) + 8 * lane;
+      *reinterpret_cast<h8*>(f) = hi;
+      *reinterpret_cast<h8*>(f + 512) = lo;
     }
-    if (lane == 0) inv[r] = ss > 0.0 ? 1.0 / ((double)s * sqrt(ss)) : 0.0;
+    __syncthreads();  // sc is rewritten by the next tile
   }
 }
 
@@ -712,13 +718,18 @@ int hq_cos_prepare(const float* X, int64_t N, int64_t ld, int K, void* X16, doub
   if (!X || !X16 || !inv) return fail(HQ_E_INVALID, "null buffer");
   const int Kp = hq_cos_padded_k(K);
   const int64_t rows = hq_cos_padded_rows(N);
-  int64_t blocks = (rows + 3) / 4;
-  if (blocks > 65536) blocks = 65536;
-  // the row-major layout only for the superseded A/B kernels (option cos_kernel 1-3)
+  // the row-major layout only for the superseded A/B kernels (option cos_kernel 1-3): one wave per row;
+  // the tiled layout: one wave per 16-row tile
   const int64_t ek = opt(OPT_COS_KERNEL, 0);
-  auto kern = ek >= 1 && ek <= 3 ? k_cos_prepare : k_cos_prepare_tiled;
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, X, N, ld, K, Kp, rows,
-                     reinterpret_cast<_Float16*>(X16), inv);
+  const bool rowmajor = ek >= 1 && ek <= 3;
+  int64_t blocks = rowmajor ? (rows + 3) / 4 : rows / 16;
+  if (blocks > 65536) blocks = 65536;
+  if (rowmajor)
+    hipLaunchKernelGGL(k_cos_prepare, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, X, N, ld, K, Kp, rows,
+                       reinterpret_cast<_Float16*>(X16), inv);
+  else
+    hipLaunchKernelGGL(k_cos_prepare_tiled, dim3((unsigned)blocks), dim3(1024), 0, (hipStream_t)stream, X, N, ld, K, Kp,
+                       rows, reinterpret_cast<_Float16*>(X16), inv);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }

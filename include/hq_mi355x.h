@@ -386,9 +386,12 @@ int hq_precomputed_similarity(const float* q_avgs, const float* q_norm, const fl
 /* ---- S7 dense frame similarity on the matrix cores ------------------------------------------
  * replaces rag/search/engine.py:622-660 (_calculate_embedding_cosine_similarity) for Q query x N
  * frame pairs of K values (e.g. 64 x 64 images, K = 4096).
- * hq_cos_prepare: f32 rows X [N, K] (row stride ld) -> split-f16 rows X16 [hq_cos_padded_rows(N), 2,
- *   hq_cos_padded_k(K)] (power-of-two scaled hi / lo halves) and inv [padded rows] = 1 / (scale |x|)
- *   (0 for a zero row).  Prepare a corpus once, each query batch per call.
+ * hq_cos_prepare: f32 rows X [N, K] (row stride ld) -> split-f16 copies X16 of hq_cos_padded_rows(N) x 2 x
+ *   hq_cos_padded_k(K) halves (power-of-two scaled hi / lo halves in 1 KiB MFMA operand fragments: 16-row
+ *   tile t, K step kb of 32, plane p at ((t KB + kb) 2 + p) x 512 halves, lane 16 g + j = row 16 t + j,
+ *   k = 32 kb + 8 g .. + 7; the superseded kernels of option cos_kernel 1-3 use rows [N, 2, Kp]) and
+ *   inv [padded rows] = 1 / (scale |x|) (0 for a zero row).  Prepare a corpus once, each query batch per
+ *   call, under the same cos_kernel option as the scoring call.
  * hq_cos_scores_mfma: out [Q, N] f64 = (cos + 1) / 2 (0 when a norm is 0), split-f16 MFMA contraction
  *   (v_mfma_f32_16x16x32_f16 x 3), within 1e-5 of the reference's float32 BLAS result.          */
 int hq_cos_padded_k(int K);
