@@ -98,12 +98,16 @@ __global__ __launch_bounds__(1024) void k_cos_prepare_tiled(const float* __restr
   __shared__ float sc[16];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, j = lane & 15, g = lane >> 4;
   const int KB = Kp / kCosK;
+  // blockIdx.y: one of gridDim.y parts of the K steps (small batches: more workgroups per tile, each
+  // recomputing the tile's statistics)
+  const int per = (KB + gridDim.y - 1) / gridDim.y;
+  const int kb0 = blockIdx.y * per, kb1 = kb0 + per < KB ? kb0 + per : KB;
   for (int64_t t = blockIdx.x; t < rows_out / 16; t += gridDim.x) {
     const int64_t r0 = 16 * t + wv;
     if (r0 >= N) {  // pad rows: zeros (scale 0), inv 0
       if (lane == 0) {
         sc[wv] = 0.0f;
-        inv[r0] = 0.0;
+        if (blockIdx.y == 0) inv[r0] = 0.0;
       }
     } else {
       const float* x = X + r0 * ld;
@@ -123,14 +127,14 @@ __global__ __launch_bounds__(1024) void k_cos_prepare_tiled(const float* __restr
       const float s = ldexpf(1.0f, -e);   // s x in (-1, 1)
       if (lane == 0) {
         sc[wv] = s;
-        inv[r0] = ss > 0.0 ? 1.0 / ((double)s * sqrt(ss)) : 0.0;
+        if (blockIdx.y == 0) inv[r0] = ss > 0.0 ? 1.0 / ((double)s * sqrt(ss)) : 0.0;
       }
     }
     __syncthreads();
     const int64_t r = 16 * t + j;
     const float my_s = sc[j];
     const float* x = X + (r < N ? r : 0) * ld;
-    for (int kb = wv; kb < KB; kb += 16) {
+    for (int kb = kb0 + wv; kb < kb1; kb += 16) {
       h8 hi, lo;
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -724,12 +728,15 @@ int hq_cos_prepare(const float* X, int64_t N, int64_t ld, int K, void* X16, doub
   const bool rowmajor = ek >= 1 && ek <= 3;
   int64_t blocks = rowmajor ? (rows + 3) / 4 : rows / 16;
   if (blocks > 65536) blocks = 65536;
+  // tiled: split the K steps over up to 8 workgroups per tile while there are fewer than 1024 tiles
+  int parts = 1;
+  while (!rowmajor && parts < 8 && blocks * parts < 1024 && (Kp / kCosK) / (2 * parts) >= 16) parts *= 2;
   if (rowmajor)
     hipLaunchKernelGGL(k_cos_prepare, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, X, N, ld, K, Kp, rows,
                        reinterpret_cast<_Float16*>(X16), inv);
   else
-    hipLaunchKernelGGL(k_cos_prepare_tiled, dim3((unsigned)blocks), dim3(1024), 0, (hipStream_t)stream, X, N, ld, K, Kp,
-                       rows, reinterpret_cast<_Float16*>(X16), inv);
+    hipLaunchKernelGGL(k_cos_prepare_tiled, dim3((unsigned)blocks, (unsigned)parts), dim3(1024), 0, (hipStream_t)stream,
+                       X, N, ld, K, Kp, rows, reinterpret_cast<_Float16*>(X16), inv);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
