@@ -2547,6 +2547,7 @@ constexpr int kKthReg = 32;  // pool entries per lane: 4 * 256 chunks * kTopT / 
 
 // Also clears the scan's per-query published threshold and pool count (gtau, pool_n; top-T mode has no
 // histogram, so no memset runs before the scan).
+template <int R>
 __global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top, int ns, int Q, int K, double margin,
                                                    double* __restrict__ th0, unsigned long long* __restrict__ gtau,
                                                    int* __restrict__ pool_n, const float* __restrict__ Sq32, double thr0,
@@ -2559,9 +2560,9 @@ __global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top
       pool_n[q] = 0;
     }
     const float* p = top + (int64_t)q * P;
-    uint32_t u[kKthReg];
+    uint32_t u[R];
 #pragma unroll
-    for (int e = 0; e < kKthReg; ++e) {
+    for (int e = 0; e < R; ++e) {
       const int x = lane + 64 * e;
       const float v = x < P ? p[x] : -1.0f;
       u[e] = v >= 0.0f ? __float_as_uint(v) + 1u : 0u;
@@ -2569,7 +2570,7 @@ __global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top
     auto count_ge = [&](uint32_t t) {  // entries with u >= t (t >= 1): DPP sum, no LDS round trips
       int c = 0;
 #pragma unroll
-      for (int e = 0; e < kKthReg; ++e) c += u[e] >= t ? 1 : 0;
+      for (int e = 0; e < R; ++e) c += u[e] >= t ? 1 : 0;
       return wsum64i(c);
     };
     double t = -__builtin_huge_val();
@@ -2586,6 +2587,23 @@ __global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top
       if (qc) qc[q] = qconst_of(Sq32, q, t > thr0 ? t : thr0, inv_m, 0.0f);
     }
   }
+}
+
+// the pool held in registers: R = 8 / 16 / 32 entries per lane (ns * kTopT <= 64 R; the geometry caps it
+// at 64 kKthReg), so a smaller pool makes every bisection step cheaper
+static void launch_kth(int mg, hipStream_t s, const float* top, int ns, int Q, int K, double margin, double* th0,
+                       unsigned long long* gtau, int* pool_n, const float* Sq32, double thr0, double inv_m,
+                       QConst* qc) {
+  const int P = ns * kTopT;
+  if (P <= 64 * 8)
+    hipLaunchKernelGGL(k_sample_kth<8>, dim3(mg), dim3(64), 0, s, top, ns, Q, K, margin, th0, gtau, pool_n, Sq32, thr0,
+                       inv_m, qc);
+  else if (P <= 64 * 16)
+    hipLaunchKernelGGL(k_sample_kth<16>, dim3(mg), dim3(64), 0, s, top, ns, Q, K, margin, th0, gtau, pool_n, Sq32,
+                       thr0, inv_m, qc);
+  else
+    hipLaunchKernelGGL(k_sample_kth<kKthReg>, dim3(mg), dim3(64), 0, s, top, ns, Q, K, margin, th0, gtau, pool_n, Sq32,
+                       thr0, inv_m, qc);
 }
 
 #ifdef HQ_DIAG
@@ -3175,14 +3193,14 @@ __device__ __forceinline__ double overall_from_levels(const double* lv, const in
 // ...), then every (candidate, level) score is one task over the 256 threads in level-major order (the
 // long level-0 tasks all in the first round), wave 0 adds each candidate's levels in the reference's
 // order and typing, ranks and writes.  Needed tasks: level 0 only for mode 0 without odet.
-template <bool SM = false>
-__global__ __launch_bounds__(256) void k_refine_lds(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si, int mode,
-                                                    const double* __restrict__ cs, const int64_t* __restrict__ cid,
-                                                    int kp, int k, double thr, int thr_mode, double eps,
-                                                    int64_t id_base, double* __restrict__ os,
-                                                    int64_t* __restrict__ oid, int* __restrict__ ocnt,
-                                                    int* __restrict__ ores, int count_empty, int* __restrict__ oredo,
-                                                    double* __restrict__ odet, int expt) {
+#define HQ_REFINE_ARGS                                                                                        \
+  VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si, int mode, const double *__restrict__ cs,                  \
+      const int64_t *__restrict__ cid, int kp, int k, double thr, int thr_mode, double eps, int64_t id_base,     \
+      double *__restrict__ os, int64_t *__restrict__ oid, int *__restrict__ ocnt, int *__restrict__ ores,        \
+      int count_empty, int *__restrict__ oredo, double *__restrict__ odet, int expt
+#define HQ_REFINE_PASS Qs, Q, Cs, N, si, mode, cs, cid, kp, k, thr, thr_mode, eps, id_base, os, oid, ocnt, ores, count_empty, oredo, odet, expt
+template <bool SM>
+__device__ __forceinline__ void refine_lds_body(HQ_REFINE_ARGS) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   __shared__ int64_t srow[kMaxTopK + 1];  // source row per staged row (-1: empty)
   __shared__ int t32s[kMaxTopK * kMaxSeg];
@@ -3293,6 +3311,17 @@ __global__ __launch_bounds__(256) void k_refine_lds(VecSet Qs, int Q, VecSet Cs,
     }
     __syncthreads();
   }
+}
+
+// segments of <= 128 values: at most 128 VGPRs (4 waves per SIMD), so four workgroups per CU keep a
+// 1000-query batch in one round (152 VGPRs allowed three per CU: 768 resident queries, the rest a second
+// round of the whole latency chain)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_refine_lds_sm(HQ_REFINE_ARGS) {
+  refine_lds_body<true>(HQ_REFINE_PASS);
+}
+// longer segments (out-of-line pairwise levels): the register-heavy general form
+__global__ __launch_bounds__(256) void k_refine_lds(HQ_REFINE_ARGS) {
+  refine_lds_body<false>(HQ_REFINE_PASS);
 }
 
 // S7: (cos + 1) / 2, 0 if a norm is 0 (rag/search/engine.py:622-660, 1025-1051)
@@ -3565,8 +3594,8 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
       hipLaunchKernelGGL(k_sample_topg, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
     HQ_CHECK_LAUNCH();
     const int mg = Q < 8192 ? Q : 8192;
-    hipLaunchKernelGGL(k_sample_kth, dim3(mg), dim3(64), 0, s, (const float*)top, 4 * sa.nchunks, Q, sample_kth,
-                       (double)kMarginF, th0, b.gtau, b.pool_n, Sq32, b.thr0, b.inv_m, qc);
+    launch_kth(mg, s, (const float*)top, 4 * sa.nchunks, Q, sample_kth, (double)kMarginF, th0, b.gtau, b.pool_n, Sq32,
+               b.thr0, b.inv_m, qc);
     HQ_CHECK_LAUNCH();
     b.th0 = th0;
   }
@@ -3728,14 +3757,14 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
   const int expt = 0;
 #endif
   if (lds <= 96 * 1024 && L % 2 == 0 && !opt_on(OPT_REFINE_GLOBAL)) {  // 16-B pieces: L even
-    const void* fn = sm ? (const void*)k_refine_lds<true> : (const void*)k_refine_lds<false>;
+    const void* fn = sm ? (const void*)k_refine_lds_sm : (const void*)k_refine_lds;
     HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (sm)
-      hipLaunchKernelGGL(k_refine_lds<true>, dim3(grid), dim3(256), lds, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc},
+      hipLaunchKernelGGL(k_refine_lds_sm, dim3(grid), dim3(256), lds, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc},
                          N, si, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
                          out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, expt);
     else
-      hipLaunchKernelGGL(k_refine_lds<false>, dim3(grid), dim3(256), lds, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc},
+      hipLaunchKernelGGL(k_refine_lds, dim3(grid), dim3(256), lds, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc},
                          N, si, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
                          out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, expt);
     HQ_CHECK_LAUNCH();
@@ -4456,9 +4485,8 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
   hipLaunchKernelGGL(k_sampleov<LID>, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
   HQ_CHECK_LAUNCH();
   const int mg = Q < 8192 ? Q : 8192;
-  hipLaunchKernelGGL(k_sample_kth, dim3(mg), dim3(64), 0, s, (const float*)sa.top, 4 * sa.nchunks, Q, sample_kth,
-                     (double)kMarginF, th0, (unsigned long long*)nullptr, a.pool_n, (const float*)nullptr, thr0, 0.0,
-                     (QConst*)nullptr);
+  launch_kth(mg, s, (const float*)sa.top, 4 * sa.nchunks, Q, sample_kth, (double)kMarginF, th0,
+             (unsigned long long*)nullptr, a.pool_n, (const float*)nullptr, thr0, 0.0, (QConst*)nullptr);
   HQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_ov_qconst, dim3((Q + 255) / 256), dim3(256), 0, s, a.Sq32, Q, a.o, (const double*)th0, thr0, qc);
   HQ_CHECK_LAUNCH();
