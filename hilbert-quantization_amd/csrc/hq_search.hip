@@ -3650,7 +3650,8 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
       else hipLaunchKernelGGL((k_scan0g<1, 2>), g1, dim3(64), 0, s, b);
     }
     HQ_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_scan0_flagged, dim3(64, (Q + 63) / 64), dim3(64), 0, s, b, (const int*)flag_list,
+    // flagged rows are rare (usually none): 8 workgroups per 64-query block loop over them
+    hipLaunchKernelGGL(k_scan0_flagged, dim3(8, (Q + 63) / 64), dim3(64), 0, s, b, (const int*)flag_list,
                        (const int*)flag_n);
     HQ_CHECK_LAUNCH();
   } else {

@@ -122,6 +122,8 @@ def test_validation_paths_of_batched_entries(lib):
     assert lib.hq_cos_scores_mfma(None, None, 3, None, None, 5, 64, None, None) == _lib.HQ_E_INVALID  # null
     assert lib.hq_cos_prepare(None, 4, 10, 16, None, None, None) == _lib.HQ_E_INVALID                # ld < K
     assert lib.hq_cos_prepare(None, 0, 16, 16, None, None, None) == _lib.HQ_OK
+    assert lib.hq_seg_flag_rows(None, -1, None, None) == _lib.HQ_E_INVALID                           # bad N
+    assert lib.hq_seg_flag_rows(None, 5, None, None) == _lib.HQ_E_INVALID                            # null
     rc = lib.hq_precomputed_index(0, 1, None, 1, 64, 10, 3, 6, 2, None, 64, None)
     assert rc == _lib.HQ_E_NOT_POW2 and _lib.last_error() == "Dimension must be a power of 2, got 3"
     assert lib.hq_precomputed_index(0, 1, None, 1, 64, 10, 256, 6, 2, None, 64, None) == _lib.HQ_E_UNSUPPORTED
