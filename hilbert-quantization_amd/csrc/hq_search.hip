@@ -1751,10 +1751,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 // WPB waves per workgroup: the WPB waves of a block take WPB consecutive query blocks of ONE chunk and
 // read the same candidate fragments step by step (a barrier per unrolled iteration keeps them within
 // a few steps of each other, so WPB - 1 of the WPB reads of a fragment hit the CU's L1)
-template <int WPB, int PF>
-__global__ __launch_bounds__(64 * WPB) void k_scan0g(Scan0Args a) {
-  constexpr int NB = 4;
-  constexpr int QW = 16 * NB;
+// NB 16-query blocks per wave (4: 64 queries; 8: 128 queries, half the corpus fragment loads per MFMA at
+// more VGPRs), processed as NB / 2 parts of two blocks, software-pipelined: part p's MFMAs are issued
+// before part p - 1's pre-filter reads its accumulators
+template <int WPB, int PF, int NB = 4>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 8 ? 3 : 1))) void k_scan0g(Scan0Args a) {
+  constexpr int QW = 16 * NB, NP = NB / 2;
   __shared__ QEntry qe_all[WPB][kQCap];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   QEntry* qe = qe_all[WPB > 1 ? threadIdx.x >> 6 : 0];
@@ -1802,7 +1804,7 @@ __global__ __launch_bounds__(64 * WPB) void k_scan0g(Scan0Args a) {
     c.f[0] = *reinterpret_cast<const half8*>(p);
     c.f[1] = *reinterpret_cast<const half8*>(p + kZ16Lo);
   };
-  auto mfma_half = [&](const int h, const half8* f, flt4* acc) {
+  auto mfma_part = [&](const int h, const half8* f, flt4* acc) {
     acc[0] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
     acc[1] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -1877,7 +1879,7 @@ __global__ __launch_bounds__(64 * WPB) void k_scan0g(Scan0Args a) {
     }
     qn -= n;
   };
-  // enqueue the lane blocks of one half whose pre-filter passed (masks m0, m1: blocks 2h, 2h + 1)
+  // enqueue the lane blocks of one part whose pre-filter passed (masks m0, m1: blocks 2h, 2h + 1)
   auto enqueue = [&](const int h, const flt4* acc, const unsigned long long m0, const unsigned long long m1,
                      const int64_t cs) {
     const int c0 = __popcll(m0);
@@ -1903,7 +1905,7 @@ __global__ __launch_bounds__(64 * WPB) void k_scan0g(Scan0Args a) {
   if (a.expt == 6)  // timing experiment: nothing is queued
     for (int b = 0; b < NB; ++b) gs[b] = __builtin_huge_valf();
 #endif
-  auto half_step = [&](const int h, const flt4* acc, const int64_t cs) {
+  auto part_step = [&](const int h, const flt4* acc, const int64_t cs) {
     const unsigned long long m0 = __builtin_amdgcn_ballot_w64(max4(acc[0]) >= gs[2 * h]);
     const unsigned long long m1 = __builtin_amdgcn_ballot_w64(max4(acc[1]) >= gs[2 * h + 1]);
     if (m0 | m1) {
@@ -1918,8 +1920,8 @@ __global__ __launch_bounds__(64 * WPB) void k_scan0g(Scan0Args a) {
   CStep buf[PF + 1];
 #pragma unroll
   for (int u = 0; u < PF; ++u) load_step(buf[u], u < nsteps ? u : nsteps - 1);
-  flt4 acc0[2], acc1[2];
-  mfma_half(0, buf[0].f, acc0);
+  flt4 acc[NP][2];
+  mfma_part(0, buf[0].f, acc[0]);
 #ifdef HQ_DIAG
   // timing experiments: 7 = no pre-filter (loads + MFMAs only), 9 = no loads after the prologue
   const bool x_nofilter = a.expt == 7, x_noload = a.expt == 9;
@@ -1930,10 +1932,13 @@ __global__ __launch_bounds__(64 * WPB) void k_scan0g(Scan0Args a) {
     if (!x_noload) load_step(nn, s + PF < nsteps ? s + PF : nsteps - 1);
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch PF steps ahead (the scheduler sinks it otherwise)
     const int64_t cs = c_begin + s * kCS;
-    mfma_half(1, cur.f, acc1);
-    if (!x_nofilter) half_step(0, acc0, cs);
-    mfma_half(0, nxt.f, acc0);
-    if (!x_nofilter) half_step(1, acc1, cs);
+#pragma unroll
+    for (int p = 1; p < NP; ++p) {
+      mfma_part(p, cur.f, acc[p]);
+      if (!x_nofilter) part_step(p - 1, acc[p - 1], cs);
+    }
+    mfma_part(0, nxt.f, acc[0]);
+    if (!x_nofilter) part_step(NP - 1, acc[NP - 1], cs);
   };
   int64_t s = 0;
   for (; s + PF < nsteps; s += PF + 1) {
@@ -3376,7 +3381,9 @@ static void scan_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& chu
 // k_scan0: ~16 resident waves per CU-pair of rounds; nchunks multiple of 8 (XCD mapping), <= 512
 static void scan0_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& chunk_len, int qw = kQW) {
   nqb = (Q + qw - 1) / qw;
-  int64_t target = (4096 * (kQW / qw) + nqb - 1) / nqb;
+  // ~4096 waves of 64 queries (4 per SIMD); 128-query waves (k_scan0g<.., 8>, 3 per SIMD): one round of 3072
+  const int64_t waves = qw <= kQW ? 4096LL * (kQW / qw) : 3072;
+  int64_t target = (waves + nqb - 1) / nqb;
   int64_t max_chunks = (N + kCS - 1) / kCS;
   if (target > max_chunks) target = max_chunks;
   if (target > 512) target = 512;
@@ -3417,6 +3424,8 @@ static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
   int64_t chunk_len, chunk_len2;
   scan0_geometry(Q, N, nqb, nchunks, chunk_len);
   scan0_geometry(Q, N, nqb2, nchunks2, chunk_len2, 32);
+  if (nchunks2 > nchunks) nchunks = nchunks2;
+  scan0_geometry(Q, N, nqb2, nchunks2, chunk_len2, 128);
   if (nchunks2 > nchunks) nchunks = nchunks2;
   // lists / pools + global thresholds + sample histogram + starting thresholds + pool counts + sample tops
   return (size_t)nchunks * Q * k * 16 + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 8 + (size_t)Q * 4 +
@@ -3535,7 +3544,9 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   }
   b.dbg = dbg;
 #endif
-  scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len);
+  // option scan_nb 8: 128-query waves (k_scan0g<1, PF, 8>) and their geometry
+  const int scan_nb = f32 && opt(OPT_SCAN_NB, 4) == 8 && opt(OPT_SCAN_WPB, 1) != 4 ? 8 : 4;
+  scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len, 16 * scan_nb);
   uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
   b.ws_score = reinterpret_cast<double*>(ws);
   b.ws_id = reinterpret_cast<int64_t*>(ws + (size_t)b.nchunks * Q * k * 8);
@@ -3645,7 +3656,8 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
       else hipLaunchKernelGGL((k_scan0g<4, 2>), g4, dim3(256), 0, s, b);
     } else {
       const dim3 g1(b.nqb * b.nchunks);
-      if (pf == 4) hipLaunchKernelGGL((k_scan0g<1, 4>), g1, dim3(64), 0, s, b);
+      if (scan_nb == 8) hipLaunchKernelGGL((k_scan0g<1, 2, 8>), g1, dim3(64), 0, s, b);
+      else if (pf == 4) hipLaunchKernelGGL((k_scan0g<1, 4>), g1, dim3(64), 0, s, b);
       else if (pf == 3) hipLaunchKernelGGL((k_scan0g<1, 3>), g1, dim3(64), 0, s, b);
       else hipLaunchKernelGGL((k_scan0g<1, 2>), g1, dim3(64), 0, s, b);
     }
