@@ -3425,8 +3425,10 @@ static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
   scan0_geometry(Q, N, nqb, nchunks, chunk_len);
   scan0_geometry(Q, N, nqb2, nchunks2, chunk_len2, 32);
   if (nchunks2 > nchunks) nchunks = nchunks2;
-  scan0_geometry(Q, N, nqb2, nchunks2, chunk_len2, 128);
-  if (nchunks2 > nchunks) nchunks = nchunks2;
+  if (opt(OPT_SCAN_NB, 4) == 8) {  // the 128-query scan's geometry (A/B option) only when selected
+    scan0_geometry(Q, N, nqb2, nchunks2, chunk_len2, 128);
+    if (nchunks2 > nchunks) nchunks = nchunks2;
+  }
   // lists / pools + global thresholds + sample histogram + starting thresholds + pool counts + sample tops
   return (size_t)nchunks * Q * k * 16 + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 8 + (size_t)Q * 4 +
          sample_top_bytes(Q, N) + (size_t)Q * sizeof(QConst) + (size_t)N * 4 + 1024;
