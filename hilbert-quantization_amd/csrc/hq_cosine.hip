@@ -472,7 +472,9 @@ __global__ __launch_bounds__(TN * 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
 // K steps ahead) and never touches LDS.  Per K step and wave: 16 ds_read_b128 + 2 ds_write_b128, 2 + 2 FT
 // global loads, 24 FT MFMAs; one block barrier.  Per output the MFMA sequence is k_cos_g3's (per K step
 // hi.hi, hi.lo, lo.hi), so the scores are bit-identical to it.
-template <int FT, int PP, int D, int EP>
+// X: diagnostics only (wrong scores; make DIAG=1): 1 no MFMAs, 2 no barriers in the K loop, 3 no frame
+// loads after the prologue, 4 no query staging after the prologue, 5 no query fragment reads
+template <int FT, int PP, int D, int EP, int X = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_cos_t(CosArgs a, int64_t ftiles) {
   // two query stages (32 KiB); after the K loop the epilogue stages one 16-query row block per wave here
   constexpr int kSm = 2 * 16 * 512 * 2 > 8 * 16 * 16 * FT * 8 ? 2 * 16 * 512 * 2 : 8 * 16 * 16 * FT * 8;
@@ -532,9 +534,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     // next step leaves the frame fragments of s + 2 in flight
     // (branch-free: past the end the loads repeat the last step and the store fills a stage nobody reads
     // again — a conditional load would make the compiler's vmcnt merge wait for the new loads too)
-    storeA(st ^ 1);
-    loadA(s + 2 < KB ? s + 2 : KB - 1);
-    loadB(s + D < KB ? s + D : KB - 1, nb);
+    if constexpr (X != 4) {
+      storeA(st ^ 1);
+      loadA(s + 2 < KB ? s + 2 : KB - 1);
+    }
+    if constexpr (X != 3) loadB(s + D < KB ? s + D : KB - 1, nb);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (PP) {
       // memory phase: every query fragment of the step into registers, then publish; compute phase: 24 FT
@@ -542,22 +546,35 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       h8 af[QT][2];
 #pragma unroll
       for (int i = 0; i < QT; ++i) {
-        af[i][0] = *reinterpret_cast<const h8*>(&sA[st][(2 * i) * 512 + 8 * lane]);
-        af[i][1] = *reinterpret_cast<const h8*>(&sA[st][(2 * i + 1) * 512 + 8 * lane]);
+        if constexpr (X == 5) {  // diagnostics: no fragment reads
+          af[i][0] = b[i % FT][0];
+          af[i][1] = b[i % FT][1];
+        } else {
+          af[i][0] = *reinterpret_cast<const h8*>(&sA[st][(2 * i) * 512 + 8 * lane]);
+          af[i][1] = *reinterpret_cast<const h8*>(&sA[st][(2 * i + 1) * 512 + 8 * lane]);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if constexpr (X == 2) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (X == 1) {  // keep the fragments live without the matrix cores
 #pragma unroll
-      for (int i = 0; i < QT; ++i)
+        for (int i = 0; i < QT; ++i)
 #pragma unroll
-        for (int j = 0; j < FT; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][0], b[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][0], b[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][1], b[j][0], acc[i][j], 0, 0, 0);
-        }
+          for (int j = 0; j < FT; ++j) acc[i][j][0] += (float)af[i][0][0] + (float)af[i][1][0] + (float)b[j][0][0] + (float)b[j][1][0];
+      } else {
+#pragma unroll
+        for (int i = 0; i < QT; ++i)
+#pragma unroll
+          for (int j = 0; j < FT; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][0], b[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][0], b[j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][1], b[j][0], acc[i][j], 0, 0, 0);
+          }
+      }
       __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_barrier" ::: "memory");
+      if constexpr (X != 2) asm volatile("s_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     } else {
 #pragma unroll
@@ -578,6 +595,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 
   loadA(0);
   loadB(0, rb0);
+  if constexpr (X == 3) loadB(0, rb2);
   storeA(0);
   loadA(KB > 1 ? 1 : 0);
   if (D == 2) loadB(KB > 1 ? 1 : 0, rb1);
@@ -663,7 +681,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   }
 }
 
-template <int FT, int PP, int D = 2, int EP = 0>
+template <int FT, int PP, int D = 2, int EP = 0, int X = 0>
 static int launch_t(CosArgs a, hipStream_t s) {
   constexpr int TN = 8 * 16 * FT;
   const int64_t np_rows = a.ntiles * kCosT;
@@ -672,7 +690,7 @@ static int launch_t(CosArgs a, hipStream_t s) {
   const int64_t nt8 = ((a.ntiles + 7) / 8) * 8;
   const int64_t blocks = nt8 * a.qtiles;
   if (blocks > 0x7FFFFFFF) return fail(HQ_E_UNSUPPORTED, "too many tiles");
-  auto kern = k_cos_t<FT, PP, D, EP>;
+  auto kern = k_cos_t<FT, PP, D, EP, X>;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), 0, s, a, np_rows / 16);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
@@ -772,6 +790,13 @@ int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* 
   if (ek == 8) return launch_t<3, 1, 1, 1>(a, (hipStream_t)stream);
 #ifdef HQ_DIAG
   if (ek == 90) return launch_t<3, 1, 1, 2>(a, (hipStream_t)stream);  // no score stores (wrong output)
+  // diagnostics (wrong output): 91 no MFMAs, 92 no K-loop barriers, 93 no frame loads, 94 no query
+  // staging, 95 no query fragment reads
+  if (ek == 91) return launch_t<3, 1, 1, 0, 1>(a, (hipStream_t)stream);
+  if (ek == 92) return launch_t<3, 1, 1, 0, 2>(a, (hipStream_t)stream);
+  if (ek == 93) return launch_t<3, 1, 1, 0, 3>(a, (hipStream_t)stream);
+  if (ek == 94) return launch_t<3, 1, 1, 0, 4>(a, (hipStream_t)stream);
+  if (ek == 95) return launch_t<3, 1, 1, 0, 5>(a, (hipStream_t)stream);
 #endif
   return launch_t<3, 1, 1>(a, (hipStream_t)stream);
 }
