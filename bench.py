@@ -545,7 +545,8 @@ def main():
             "roofline": {"bound": "mfma", "achieved": flops / skern / 1e12, "peak": FP16_MATRIX_PEAK_TFS,
                          "unit": "TFLOP/s", "frac": flops / skern / 1e12 / FP16_MATRIX_PEAK_TFS,
                          "note": "3 x 2*Q*N*32 f16 MFMA flops of the split level-0 contraction per step / step "
-                                 "time; the scan is bound by the per-pair f32 filter on the VALUs (DESIGN.md)"},
+                                 "time (the whole pipeline: sample pass, scan, pool select, exact re-rank, final); the scan kernel "
+                                 "alone keeps the matrix cores ~57% busy (DESIGN.md §4.2)"},
             "self_match_rate": float((ids[:, 0].cpu() == torch.arange(Qn)).float().mean()),
         }
         # the other two cfg3 modes: brute-force overall top-10 (core/search_engine.py:302-338,
