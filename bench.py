@@ -210,6 +210,35 @@ def cpu_baseline_quantize_loops(dim, seconds):
             "structure": "reference-shaped (per-element Python loops, BASELINE.md §3 item 1)"}
 
 
+def cpu_baseline_precomputed(dim, seconds):
+    """The pre-computed index leg on one host core: the reference-shaped port (oracle/hq_loops.py:
+    per-cell map, one np.mean per square) and the vectorised oracle (hq_oracle.precomputed_index over a
+    256-embedding batch, one np.mean per square across the batch)."""
+    from oracle import hq_loops as HL
+    from oracle import hq_oracle as O
+    rng = np.random.default_rng(1)
+    n = O.optimal_dimensions(dim)[0]
+    P = rng.standard_normal((256, dim)).astype(np.float32)
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds / 2:
+        HL.precomputed_one(P[done % 256], n)
+        done += 1
+    dt = time.perf_counter() - t0
+    res = {"value": done / dt, "unit": "embeddings/sec", "cores": 1, "kind": "port",
+           "sample": f"{done} x {dim}-d f32 embeddings through the reference-shaped port (oracle/hq_loops.py "
+                     f"precomputed_one: per-cell map, one np.mean per square, 2,610 squares) in {dt:.1f}s",
+           "structure": "reference-shaped (per-square loop, core/precomputed_hilbert_index.py:65-212)"}
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds / 2:
+        O.precomputed_index(O.map_to_2d(O.pad_parameters(P, n), n))
+        done += len(P)
+    dt = time.perf_counter() - t0
+    res["vectorised"] = {"value": done / dt, "unit": "embeddings/sec", "cores": 1, "kind": "port",
+                         "sample": f"{done} x {dim}-d f32 embeddings, oracle map_to_2d + precomputed_index "
+                                   f"(NumPy, 256-embedding batches, single thread) in {dt:.1f}s"}
+    return res
+
+
 def cpu_baseline_search_loops(C, Q, seconds):
     """Reference-shaped search: the per-candidate Python loop of core/search_engine.py:232-388 (both level
     structures re-parsed per comparison) over a 10k-row slice, extrapolated linearly to 1M rows."""
@@ -620,6 +649,8 @@ def main():
                                               f"core ({w} processes), linear in corpus size"}
         if "stream" in rec:
             rec["stream"]["cpu_baseline"] = cpu_baseline_stream(args.cpu_seconds / 2)
+        if "precomputed" in rec:
+            rec["precomputed"]["cpu_baseline"] = cpu_baseline_precomputed(d, args.cpu_seconds / 2)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -112,6 +112,20 @@ def quantize_one(p: np.ndarray, n: int, L: int) -> np.ndarray:
     return u8
 
 
+def precomputed_one(p: np.ndarray, n: int, max_levels: int = 6, min_square_size: int = 2) -> np.ndarray:
+    """pad -> map_to_2d -> create_precomputed_index for one model (api.py:162-173): per level, one
+    float(np.mean(square)) per grid square then per overlapping square, each stored as float32
+    (core/precomputed_hilbert_index.py:65-212)."""
+    padded = np.zeros(n * n, dtype=p.dtype)
+    padded[:len(p)] = p
+    img = map_to_2d(padded, n)
+    out: List[np.float32] = []
+    for g, s in O.precomputed_levels(n, max_levels, min_square_size):
+        for (x0, y0) in O.precomputed_squares(n, g, s):
+            out.append(np.float32(float(np.mean(img[y0:y0 + s, x0:x0 + s]))))
+    return np.array(out, dtype=np.float32)
+
+
 def compare_at_level(q: np.ndarray, c: np.ndarray, level: int) -> float:
     """One (query, candidate) comparison; both level structures are re-parsed per call (:129-130)."""
     ql = O.parse_index_structure(len(q))

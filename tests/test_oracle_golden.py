@@ -299,6 +299,10 @@ def test_precomputed_index_golden(golden, name):
     assert np.array_equal(np.array(xy, dtype=np.int64).reshape(-1, 2), g[f"xy_{name}"].reshape(-1, 2))
     # storage accounting (:98): averages bytes + 16 per coordinate pair
     assert int(g[f"bytes_{name}"]) == sum(4 * c + 16 * c for (_, _, c, _) in meta)
+    if name in ("n16", "n64", "pad1536", "const32"):
+        # the reference-shaped port bench.py times as the precomputed leg's cpu_baseline
+        from oracle import hq_loops as HL
+        assert HL.precomputed_one(O.map_from_2d(img), n).tobytes() == g[f"avg_{name}"].tobytes()
 
 
 def test_precomputed_similarity_golden(golden):
