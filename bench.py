@@ -393,10 +393,32 @@ def bench_ingest(args):
         for i in range(S):
             hq.quantize(sets[i], model_id=f"s{i}")
         ds = time.perf_counter() - t1
-    return {"metric": "QuantizedModels/sec ingest (1024-d, JPEG payload + pre-computed index, HilbertQuantizer semantics)",
-            "value": M / dt, "unit": "models/sec", "models": M, "seconds": dt,
-            "per_model_path": {"value": S / ds, "unit": "models/sec", "sample": f"{S} x HilbertQuantizer.quantize"},
-            "note": "host-bound: the JPEG codec (PIL, SURVEY §8f row 2) runs on host threads"}
+    res = {"metric": "QuantizedModels/sec ingest (1024-d, JPEG payload + pre-computed index, HilbertQuantizer semantics)",
+           "value": M / dt, "unit": "models/sec", "models": M, "seconds": dt,
+           "per_model_path": {"value": S / ds, "unit": "models/sec", "sample": f"{S} x HilbertQuantizer.quantize"},
+           "note": "host-bound: the JPEG codec (PIL, SURVEY §8f row 2) runs on host threads"}
+    if not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline_ingest(sets, hq.compression_quality, args.cpu_seconds / 4)
+    return res
+
+
+def cpu_baseline_ingest(sets, quality, seconds):
+    """One host core, one model at a time, reference-shaped: per-cell map + streaming tree + u8 normalise
+    (oracle/hq_loops.py quantize_one), the same PIL JPEG encode, and the per-square pre-computed index
+    (hq_loops.precomputed_one) — the work HilbertQuantizer.quantize does per model (api.py:98-173)."""
+    from hq_mi355x.core.compressor import encode_jpeg
+    from oracle import hq_loops as HL
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        p = sets[done % len(sets)]
+        encode_jpeg(HL.quantize_one(p, 32, 32), quality)
+        HL.precomputed_one(p, 32)
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "models/sec", "cores": 1, "kind": "port",
+            "sample": f"{done} x 1024-d models: reference-shaped map + streaming index + u8 normalise, PIL JPEG, "
+                      f"per-square pre-computed index (oracle/hq_loops.py), single thread, {dt:.1f}s",
+            "structure": "reference-shaped (per-element / per-square loops, BASELINE.md §3 item 1)"}
 
 
 STREAM_CHUNK = 1024
