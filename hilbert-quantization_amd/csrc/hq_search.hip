@@ -1678,7 +1678,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 //     statistics for flagged rows) and the pool append;
 //   * candidate fragments / statistics addressed from a wave-uniform base (scalar step increments).
 // Flagged candidate rows (zero variance, f32-unsafe) are skipped by the scan and scored by
-// k_scan0_flagged from the f64 statistics (k_flag_rows lists them per call; normally none).  Flagged queries
+// k_pool_select from the f64 statistics before it reads the pools (the corpus's list from hq_seg_flag_rows,
+// or k_flag_rows per call; normally none).  Flagged queries
 // (zero variance / f32-unsafe) never enter the scan: k_pool_select marks their lists unresolved and the
 // caller answers them on the dense exact path.  A pool that would overflow its capacity marks its query
 // unresolved the same way.
@@ -1833,7 +1834,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
       for (int r = 0; r < 4; ++r) {
         const int row = erow + r;
         const int f = __float_as_int(fl[r]);
-        if (row >= c_end || f != 0) continue;  // past the chunk; flagged rows: k_scan0_flagged
+        if (row >= c_end || f != 0) continue;  // past the chunk; flagged rows: k_pool_select
         const float G = eg[r];
         float s = -__builtin_huge_valf();
         {
@@ -1962,42 +1963,32 @@ __global__ __launch_bounds__(256) void k_flag_rows(const float* __restrict__ S32
   }
 }
 
-// the flagged rows against every scanned query (lane = query): the f64 statistics as k_scan0f's insert
+// one flagged row against one scanned query: the f64 statistics as k_scan0f's insert
 // path (const0 for zero variance, approx0 with G from the split copies otherwise), appended to the pools
 // when the score reaches the query's list threshold
-__global__ __launch_bounds__(64) void k_scan0_flagged(Scan0Args a, const int* __restrict__ list,
-                                                      const int* __restrict__ count) {
-  const QConst* qc = reinterpret_cast<const QConst*>(a.qconst);
-  const int n = *count;
-  const int q = blockIdx.y * 64 + threadIdx.x;
-  if (q >= a.Q || n == 0) return;
-  const QConst c = qc[q];
-  if (__float_as_int(c.flag) != 0) return;  // flagged query: dense exact path
+__device__ __forceinline__ void flagged_pair(const Scan0Args& a, const QConst& c, int q, int row) {
   const double* sq = a.Sq + (int64_t)q * a.nseg * 4;
   const _Float16* zq = a.Zq16;
-  for (int i = blockIdx.x; i < n; i += gridDim.x) {
-    const int row = list[i];
-    const double* sc = a.Sc + (int64_t)row * a.nseg * 4;
-    const double qm = sq[0], qs = sq[1], qq = sq[2], cm = sc[0], csd = sc[1], cq = sc[2];
-    double v;
-    if (qs == 0.0 || csd == 0.0) {
-      v = const0(qs == 0.0, csd == 0.0, qm, cm, (aux_bits(sq) & aux_bits(sc) & kAuxF32) != 0);
-    } else {
-      const _Float16* zc = a.Zc16;
-      double G = 0.0;
-      for (int k = 0; k < 32; ++k) {
-        const int64_t eq = z16_elem(q, k), ec = z16_elem(row, k);
-        G = fma((double)zq[eq] + (double)zq[eq + kZ16Lo], (double)zc[ec] + (double)zc[ec + kZ16Lo], G);
-      }
-      v = approx0(G, a.c1, (0.6 * a.inv_m) * qs, 0.6 * qm, qq, csd, cm, cq);
+  const double* sc = a.Sc + (int64_t)row * a.nseg * 4;
+  const double qm = sq[0], qs = sq[1], qq = sq[2], cm = sc[0], csd = sc[1], cq = sc[2];
+  double v;
+  if (qs == 0.0 || csd == 0.0) {
+    v = const0(qs == 0.0, csd == 0.0, qm, cm, (aux_bits(sq) & aux_bits(sc) & kAuxF32) != 0);
+  } else {
+    const _Float16* zc = a.Zc16;
+    double G = 0.0;
+    for (int k = 0; k < 32; ++k) {
+      const int64_t eq = z16_elem(q, k), ec = z16_elem(row, k);
+      G = fma((double)zq[eq] + (double)zq[eq + kZ16Lo], (double)zc[ec] + (double)zc[ec + kZ16Lo], G);
     }
-    const float sv = (float)v;
-    if (sv >= c.thl) {
-      const int slot = atomicAdd(a.pool_n + q, 1);
-      if (slot < a.pool_cap) {
-        a.pool_s[(int64_t)q * a.pool_cap + slot] = sv;
-        a.pool_i[(int64_t)q * a.pool_cap + slot] = row;
-      }
+    v = approx0(G, a.c1, (0.6 * a.inv_m) * qs, 0.6 * qm, qq, csd, cm, cq);
+  }
+  const float sv = (float)v;
+  if (sv >= c.thl) {
+    const int slot = atomicAdd(a.pool_n + q, 1);
+    if (slot < a.pool_cap) {
+      a.pool_s[(int64_t)q * a.pool_cap + slot] = sv;
+      a.pool_i[(int64_t)q * a.pool_cap + slot] = row;
     }
   }
 }
@@ -2016,13 +2007,28 @@ __global__ __launch_bounds__(64) void k_pool_select(const float* __restrict__ po
                                                     const int* __restrict__ pool_n, int cap, int Q, int K,
                                                     int64_t id_base, double* __restrict__ out_score,
                                                     int64_t* __restrict__ out_id, const double* __restrict__ th0,
-                                                    double thr0, const float* __restrict__ qflag, int qstride) {
+                                                    double thr0, const float* __restrict__ qflag, int qstride,
+                                                    Scan0Args fa, const int* __restrict__ flist,
+                                                    const int* __restrict__ fcount) {
   const int lane = threadIdx.x;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    // fcount != null (k_scan0g): the corpus's flagged rows against this query first (lanes over the
+    // rows), appended to the pool before it is read; pool_n is then read with an
+    // L1-bypassing load (the appends are L2 atomics)
+    if (fcount) {
+      const QConst* qc = reinterpret_cast<const QConst*>(fa.qconst);
+      const int n = *fcount;
+      if (n > 0 && __float_as_int(qc[q].flag) == 0) {
+        const QConst c = qc[q];
+        for (int i = lane; i < n; i += 64) flagged_pair(fa, c, q, flist[i]);
+      }
+      __syncthreads();
+    }
+    const int pn = fcount ? __hip_atomic_load(pool_n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : pool_n[q];
     // k_scan0g / k_scanov (qflag: the query's flag word in its constants, qstride floats apart): a flagged
     // query (not scanned) or an overflowing pool -> every slot +inf / -1, which the exact re-rank reads
     // as unresolved (the caller's dense exact path answers the query)
-    if (qflag && (__float_as_int(qflag[(int64_t)q * qstride]) != 0 || pool_n[q] > cap)) {
+    if (qflag && (__float_as_int(qflag[(int64_t)q * qstride]) != 0 || pn > cap)) {
       for (int x = lane; x < K; x += 64) {
         out_score[(int64_t)q * K + x] = __builtin_huge_val();
         out_id[(int64_t)q * K + x] = -1;
@@ -2030,9 +2036,9 @@ __global__ __launch_bounds__(64) void k_pool_select(const float* __restrict__ po
       continue;
     }
 #ifdef HQ_DIAG
-    const int T = (int)diag_bound(pool_n[q], (int64_t)cap + 1, __LINE__);
+    const int T = (int)diag_bound(pn, (int64_t)cap + 1, __LINE__);
 #else
-    const int T = pool_n[q];
+    const int T = pn;
 #endif
     const float* ps = pool_s + (int64_t)q * cap;
     const int* pi = pool_i + (int64_t)q * cap;
@@ -3664,10 +3670,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
       else hipLaunchKernelGGL((k_scan0g<1, 2>), g1, dim3(64), 0, s, b);
     }
     HQ_CHECK_LAUNCH();
-    // flagged rows are rare (usually none): 8 workgroups per 64-query block loop over them
-    hipLaunchKernelGGL(k_scan0_flagged, dim3(8, (Q + 63) / 64), dim3(64), 0, s, b, (const int*)flag_list,
-                       (const int*)flag_n);
-    HQ_CHECK_LAUNCH();
+    // flagged rows are rare (usually none): scored inside k_pool_select, before it reads the pools
   } else {
 #ifdef HQ_DIAG
     rc = f32 ? scan0_dispatch<true>(ks, b, nullptr, s) : scan0_dispatch<false>(ks, b, nullptr, s);
@@ -3681,7 +3684,9 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     hipLaunchKernelGGL(k_pool_select, dim3(mg), dim3(64), 0, s, (const float*)b.pool_s, (const int*)b.pool_i,
                        (const int*)b.pool_n, b.pool_cap, Q, k, id_base, out_score, out_id,
                        top_sample && sample_kth < k ? (const double*)th0 : (const double*)nullptr, b.thr0,
-                       qc ? &qc[0].flag : (const float*)nullptr, (int)(sizeof(QConst) / 4));
+                       qc ? &qc[0].flag : (const float*)nullptr, (int)(sizeof(QConst) / 4), b,
+                       queue_scan ? (const int*)flag_list : (const int*)nullptr,
+                       queue_scan ? (const int*)flag_n : (const int*)nullptr);
     HQ_CHECK_LAUNCH();
   }
 #ifdef HQ_DIAG
@@ -4521,7 +4526,7 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
   hipLaunchKernelGGL(k_pool_select, dim3(mg), dim3(64), 0, s, (const float*)a.pool_s, (const int*)a.pool_i,
                      (const int*)a.pool_n, a.pool_cap, Q, k, id_base, out_score, out_id,
                      sample_kth < k ? (const double*)th0 : (const double*)nullptr, thr0, &qc[0].flag,
-                     (int)(sizeof(QOv) / 4));
+                     (int)(sizeof(QOv) / 4), Scan0Args{}, (const int*)nullptr, (const int*)nullptr);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
