@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--n-emb", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=1536)
     ap.add_argument("--corpus", type=int, default=1_000_000)
+    ap.add_argument("--corpus-total", type=int, default=8_000_000,
+                    help="cfg4 strong scaling: one global corpus of this many rows, shard_range over the ranks (0: off)")
     ap.add_argument("--queries", type=int, default=1000)
     ap.add_argument("--search-steps", type=int, default=20)
     ap.add_argument("--no-search", action="store_true")
@@ -482,6 +484,81 @@ def cpu_baseline_stream(seconds):
                       f"in {dt:.1f}s"}
 
 
+def bench_search_strong(args, world, rank, dev):
+    """Config 4 as BASELINE.json names it: ONE global 8M-frame corpus (L = 64 index vectors of seed-4
+    embeddings, generated 1M rows at a time exactly as tests/test_gpu_fullsize.py::test_cfg4_full_size_8_shards
+    builds it), each rank holding its shard_range of the rows (strong scaling: N = 1 answers the whole 8M
+    corpus on one GPU), the cfg3 query batch (global rows 0..999 + N(0, 0.01), seed 3), progressive top-10,
+    the per-shard records merged after one all-gather (hq_allgather_topk over RCCL at N > 1)."""
+    from hq_mi355x import kernels as K
+    from hq_mi355x.core.search_engine import IndexCorpus
+    from hq_mi355x.distributed import ShardedIndexCorpus, shard_range
+    Nt, Qn, per = args.corpus_total, args.queries, 1_000_000
+    a, b = shard_range(Nt, rank, world)
+    C = torch.empty((b - a, 64), dtype=torch.float64, device=dev)
+    Q = None
+    g = torch.Generator(device=dev).manual_seed(4)
+    Xc = torch.empty((per, args.dim), device=dev, dtype=torch.float32)
+    t0 = time.perf_counter()
+    for j in range((Nt + per - 1) // per):
+        r0, r1 = j * per, min(Nt, (j + 1) * per)
+        torch.randn((r1 - r0, args.dim), generator=g, out=Xc[: r1 - r0])  # every rank draws the same stream
+        lo, hi = max(a, r0), min(b, r1)
+        if lo < hi or j == 0:
+            _, blk, _ = K.map_index_quantize(Xc[: r1 - r0], 64, 64)
+            if j == 0:
+                gq = torch.Generator(device=dev).manual_seed(3)
+                Q = blk[:Qn] + 0.01 * torch.randn((Qn, 64), generator=gq, device=dev, dtype=torch.float64)
+            if lo < hi:
+                C[lo - a:hi - a] = blk[lo - r0:hi - r0]
+            del blk
+    del Xc
+    comm = None
+    if world > 1:
+        if os.environ.get("HQ_BENCH_BACKEND", "nccl") == "nccl":
+            from hq_mi355x.rccl import Communicator
+            comm = Communicator.from_process_group()
+        engine = ShardedIndexCorpus(C, id_base=a, n_total=Nt, comm=comm)
+    else:
+        engine = IndexCorpus(C)
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t0
+    pend = []
+
+    def run():
+        pend.append(engine.progressive_submit(Q, 10, 0.1, 20))
+        if len(pend) >= 2:
+            engine.progressive_finish(pend.pop(0))
+
+    def drain():
+        while pend:
+            engine.progressive_finish(pend.pop(0))
+
+    steps = max(2, args.search_steps)
+    wall, kern = timed(run, steps, 1, world, drain)
+    ids, ov, _, cnt = engine.progressive(Q, 10, 0.1, 20)
+    ids_h = ids.cpu().numpy()
+    res = {"metric": "queries/sec@top-10 over the 8M-frame cfg4 corpus (strong scaling)",
+           "value": Qn * steps / wall, "unit": "queries/sec", "scaling": "strong", "corpus_total": Nt,
+           "corpus_this_rank": b - a, "ranks": world, "queries": Qn, "steps": steps,
+           "ms_per_step": wall / steps * 1e3, "build_s": build_s,
+           "self_match_rate": float((ids[:, 0].cpu() == torch.arange(Qn)).float().mean()),
+           "ids_checksum": int((ids_h.astype(np.int64) * (np.arange(ids_h.size).reshape(ids_h.shape) % 7919 + 1)).sum()),
+           "data": "8M x 1536-d N(0,1) embeddings (torch seed 4, 1M-row blocks) -> fused map + streaming index (L=64)",
+           "roofline": {"bound": "mfma", "achieved": 3 * 2.0 * Qn * (b - a) * 32 / kern / 1e12,
+                        "peak": FP16_MATRIX_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": 3 * 2.0 * Qn * (b - a) * 32 / kern / 1e12 / FP16_MATRIX_PEAK_TFS,
+                        "note": "this rank's split-f16 level-0 contraction flops per step / step time"}}
+    if comm is not None:
+        x = torch.zeros((Qn, 21, 3 + engine.local.nseg), dtype=torch.float64, device=dev)
+        _, ak = timed(lambda: comm.all_gather(x), 20, 3, world)
+        res["allgather"] = {"ms": ak * 1e3, "bytes_per_rank": x.numel() * 8, "ranks": world,
+                            "path": "hq_allgather_topk (ncclAllGather over xGMI)"}
+    del engine, C, Q
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     args = parse()
     # multi-core CPU baseline first: worker processes are forked before anything initialises the GPU
@@ -611,14 +688,22 @@ def main():
         ov_flops, ov_peak, ov_pname = ((3 * 2.0 * pairs * 32 * ovinfo[0], FP16_MATRIX_PEAK_TFS, "dense F16 MFMA")
                                        if ovinfo else (2.0 * pairs * Lp, FP64_MATRIX_PEAK_TFS, "FP64 matrix (spec)"))
         modes = {}
+        l0_flops = 3 * 2.0 * pairs * 32
         for mode, fn, flops, peak, pname in (
                 ("overall", lambda: engine.brute_force(queries, 10), ov_flops, ov_peak, ov_pname),
-                ("level0", lambda: engine.frame_search(queries, 10, 0.1), 3 * 2.0 * pairs * 32, FP16_MATRIX_PEAK_TFS,
+                ("level0", lambda: engine.frame_search(queries, 10, 0.1), l0_flops, FP16_MATRIX_PEAK_TFS,
+                 "dense F16 MFMA"),
+                # the reference engine's default max_candidates_per_level (core/search_engine.py:31,
+                # core/video_search.py:48) and SearchConfig's (config.py:181): long pools on the scan path
+                ("m100", lambda: engine.progressive(queries, 10, 0.1, 100), l0_flops, FP16_MATRIX_PEAK_TFS,
+                 "dense F16 MFMA"),
+                ("m1000", lambda: engine.progressive(queries, 10, 0.1, 1000), l0_flops, FP16_MATRIX_PEAK_TFS,
                  "dense F16 MFMA")):
             msteps = max(2, args.search_steps // 2)
             mw, mk = timed(fn, msteps, 1, world)
             modes[mode] = {
                 "value": Qn * msteps / mw, "unit": "queries/sec", "steps": msteps, "ms_per_step": mw / msteps * 1e3,
+                "max_candidates_per_level": {"m100": 100, "m1000": 1000}.get(mode),
                 "roofline": {"bound": "mfma", "achieved": flops / mk / 1e12, "peak": peak, "unit": "TFLOP/s",
                              "frac": flops / mk / 1e12 / peak,
                              "note": f"algorithmic contraction flops per step ({('3 x 2*Q*N*32*K-blocks split f16' if ovinfo else '2*Q*N*Lp f64') if mode == 'overall' else '3 x 2*Q*N*32 split f16'}) / "
@@ -630,6 +715,11 @@ def main():
             _, ak = timed(lambda: comm.all_gather(x), 20, 3, world)
             rec["search"]["allgather"] = {"ms": ak * 1e3, "bytes_per_rank": x.numel() * 8, "ranks": world,
                                           "path": "hq_allgather_topk (ncclAllGather over xGMI)"}
+            comm.close()
+        if args.corpus_total > 0:
+            del engine
+            torch.cuda.empty_cache()
+            rec["search"]["strong"] = bench_search_strong(args, world, rank, dev)
 
     if not args.no_precomputed:
         rec["precomputed"] = bench_precomputed(args, X, world)

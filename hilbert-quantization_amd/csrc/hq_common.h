@@ -49,7 +49,7 @@ enum Opt {
   OPT_COS_KERNEL,
   OPT_SAMPLE_STRIDE, OPT_SAMPLE_WAVES, OPT_SAMPLE_KTH, OPT_SAMPLE_VARIANT,
   OPT_SCAN_V1, OPT_SCAN_NOSAMPLE, OPT_SCAN_EXPT, OPT_SCAN_VARIANT, OPT_SCAN_WPB, OPT_SCAN_PF, OPT_SCAN_NB, OPT_OV_WAVES, OPT_OV_OCC,
-  OPT_REFINE_GLOBAL, OPT_REFINE_EXPT, OPT_SEG_PREPARE_FLAT, OPT_SELECT_2STAGE,
+  OPT_REFINE_GLOBAL, OPT_REFINE_EXPT, OPT_SEG_PREPARE_FLAT, OPT_SELECT_2STAGE, OPT_LEVEL_SCORES_V1,
   OPT_COUNT
 };
 int64_t opt(Opt id, int64_t dflt);
@@ -111,7 +111,7 @@ constexpr GroupLut<NS> make_group_lut() {
 // offsets of its four values in the row-major n x n float image, two per dword (value m of the group in
 // dword 2j + (m >> 1), bits 16 (m & 1) ..): one mask or shift per value gives the store address.
 template <int NS>
-struct AddrLut {
+struct alignas(16) AddrLut {  // read as uint4 by k_chunk_np
   uint32_t v[NS * NS / 2];
 };
 template <int NS>

@@ -396,6 +396,38 @@ __global__ __launch_bounds__(256) void k_level_scores(VecSet Qs, int Q, VecSet C
   }
 }
 
+// Dense exact level scores with coalesced candidate rows (level >= 0, segments of <= 128 values): a block
+// of kLsTile threads stages the level segment of kLsTile consecutive candidate rows into LDS (consecutive
+// threads read consecutive values of a row: 256-B runs instead of one row per thread), then thread t
+// scores candidate c0 + t against the block's kLsQ queries from LDS.  The same exact_level code on other
+// addresses (the candidate's normalised values recomputed as (x - mean) / std, the f64 operations
+// k_seg_prepare stored in Z), so the scores are bit-identical to k_level_scores.
+constexpr int kLsTile = 128, kLsQ = 4;
+__global__ __launch_bounds__(kLsTile) void k_level_scores_lds(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si,
+                                                              int level, double* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) double lsm[];
+  const int m = si.len[level], src = si.src[level], pitch = m | 1;  // odd pitch: conflict-free row reads
+  const int64_t c0 = (int64_t)blockIdx.x * kLsTile;
+  const int q0 = blockIdx.y * kLsQ;
+  const int tid = threadIdx.x;
+  const int nrow = N - c0 < kLsTile ? (int)(N - c0) : kLsTile;
+  for (int e = tid; e < nrow * m; e += kLsTile) {
+    const int r = e / m, k = e - r * m;
+    lsm[r * pitch + k] = Cs.raw[(c0 + r) * si.L + src + k];
+  }
+  __syncthreads();
+  if (tid >= nrow) return;
+  const int64_t c = c0 + tid;
+  const double* rc = lsm + tid * pitch;
+  const double* sc = Cs.S + (c * si.nseg + level) * 4;
+  for (int qi = 0; qi < kLsQ && q0 + qi < Q; ++qi) {
+    const int64_t q = q0 + qi;
+    int t32;
+    out[q * N + c] = exact_level<true>(Qs.raw + q * si.L + src, Qs.Z + q * si.Lp + si.poff[level],
+                                       Qs.S + (q * si.nseg + level) * 4, rc, nullptr, sc, m, &t32);
+  }
+}
+
 // exact overall + per-level for selected (query, candidate) pairs; ids are global, id_base subtracted.
 // G lanes per pair (G >= nseg): lane s computes level s, the pair's first lane adds them up in level
 // order with the reference's typing (exact_pair's sum), so the 5-7 level scores run in parallel.
@@ -1722,17 +1754,14 @@ __global__ void k_scan_qprep(const float* __restrict__ Sq32, int Q, double thr0,
   pool_n[q] = 0;
 }
 
-// max of an accumulator in two instructions.  Inline asm: the compiler's hazard recognizer does not see
-// its reads, so the operand must NOT be an MFMA result issued shortly before (the VALU read of an MFMA
-// destination needs wait states): k_scan0g reads accumulators at least six MFMAs after they were
-// written (one mfma_half in between).  max4_fresh is the compiler-visible form for fresh results.
+// max of an accumulator in two instructions: IEEE-2019 maximum (v_maximum3_f32 on gfx950; the accumulators
+// are never NaN, so it equals fmaxf here).  Compiler-visible, so the MFMA -> VALU read hazard of a fresh
+// accumulator gets its wait states from the compiler (fmaxf / fmed3 forms add a v_max canonicalisation of
+// each operand in IEEE mode; an inline-asm v_max3 hides the read from the hazard recognizer, the fault
+// class of commit ee0b4c1).
 __device__ __forceinline__ float max4(const flt4 v) {
-  float t, r;
-  asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(t) : "v"(v.x), "v"(v.y), "v"(v.z));
-  asm volatile("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(t), "v"(v.w));
-  return r;
+  return __builtin_elementwise_maximum(__builtin_elementwise_maximum(v.x, v.y), __builtin_elementwise_maximum(v.z, v.w));
 }
-__device__ __forceinline__ float max4_fresh(const flt4 v) { return fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)); }
 
 constexpr int kQCap = 256;  // LDS queue entries per wave (a half-step adds at most 128)
 struct QEntry {
@@ -2003,8 +2032,9 @@ constexpr int kPoolReg = 16;
 // from the sample's K'-th best (K' < K, see k_sample_kth) is not a provable lower bound of the K-th
 // best: a query whose pool then holds fewer than K entries while th0 > thr0 may miss pairs below th0,
 // so its empty slots are marked with score +inf (id -1), which hq_refine_topk reads as "unresolved".
-__global__ __launch_bounds__(64) void k_pool_select(const float* __restrict__ pool_s, const int* __restrict__ pool_i,
-                                                    const int* __restrict__ pool_n, int cap, int Q, int K,
+// pool_s / pool_i / pool_n are plain pointers (no const, no __restrict__): flagged_pair appends to the same
+// pools through fa.pool_* before they are read
+__global__ __launch_bounds__(64) void k_pool_select(float* pool_s, int* pool_i, int* pool_n, int cap, int Q, int K,
                                                     int64_t id_base, double* __restrict__ out_score,
                                                     int64_t* __restrict__ out_id, const double* __restrict__ th0,
                                                     double thr0, const float* __restrict__ qflag, int qstride,
@@ -2299,7 +2329,6 @@ __global__ __launch_bounds__(64) void k_sample_histf(SampleArgs a) {
 // No LDS, no atomics: occupancy is set by VGPRs alone.  Output: top[(q * nstreams + 4 chunk + g) *
 // kTopT + t], every entry of every existing query written (-1 = empty).
 constexpr int kTopT = 2;
-constexpr int kSampleKth = 12;
 
 __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
@@ -2497,7 +2526,7 @@ __global__ __launch_bounds__(64) void k_sample_topg(SampleArgs a) {
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      const float m = max4_fresh(acc[b]);
+      const float m = max4(acc[b]);
       const bool up = m > bg[b];
       bg[b] = up ? m : bg[b];
       bacc[b] = up ? acc[b] : bacc[b];
@@ -2707,6 +2736,83 @@ __device__ __forceinline__ bool wave_better(double s, int64_t id, double s2, int
   return id >= 0 && (id2 < 0 || s > s2 || (s == s2 && id < id2));
 }
 
+// survivors of query q (one wave, no barrier inside: callers synchronise before reading sel): the global
+// top-M of the R lists merged on (score desc, id asc) into sel[] as (list r << 16) | slot; if none passed,
+// the first arg-max of the level-0 score (sel[0] = r << 16, *fb_id = its id).  Returns the count.
+__device__ int final_survivors(int R, int Q, int M, int q, const double* __restrict__ s0,
+                               const int64_t* __restrict__ ids, const double* __restrict__ best,
+                               const int64_t* __restrict__ best_id, int* sel, int64_t* fb_id) {
+  const int lane = threadIdx.x & 63;
+  // ---- R-way merge: lane r < R follows list r's head ----
+  int h = 0;
+  double hs = -__builtin_huge_val();
+  int64_t hid = -1;
+  auto load_head = [&]() {
+    hs = -__builtin_huge_val();
+    hid = -1;
+    if (lane < R && h < M) {
+      const int64_t o = ((int64_t)lane * Q + q) * M + h;
+      hid = ids[o];
+      if (hid >= 0) hs = s0[o];
+    }
+  };
+  load_head();
+  int n = 0;
+  if (R == 1) {
+    // one list: it is already the (score desc, id asc) order; its valid entries come first
+    for (int i = lane; i < M; i += 64) {
+      const bool v = ids[(int64_t)q * M + i] >= 0;
+      const unsigned long long m = __ballot(v);
+      n += __popcll(m);
+      if (v) sel[i] = i;
+    }
+    n = __builtin_amdgcn_readfirstlane(n);
+  }
+  for (; R > 1 && n < M; ++n) {
+    double bs = hs;
+    int64_t bid = hid;
+    int bl = lane;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double s2 = __shfl_xor(bs, o, 64);
+      const int64_t i2 = __shfl_xor(bid, o, 64);
+      const int l2 = __shfl_xor(bl, o, 64);
+      if (wave_better(s2, i2, bs, bid)) { bs = s2; bid = i2; bl = l2; }
+    }
+    if (bid < 0) break;
+    const int hb = __shfl(h, bl, 64);
+    if (lane == 0) sel[n] = (bl << 16) | hb;
+    if (lane == bl) {
+      h = hb + 1;
+      load_head();
+    }
+  }
+  *fb_id = -1;
+  if (n == 0) {
+    // none passed the threshold: keep the first arg-max of the level-0 score (:295-298)
+    double bs = -__builtin_huge_val();
+    int64_t bid = -1;
+    int bl = lane;
+    if (lane < R) {
+      bid = best_id[(int64_t)lane * Q + q];
+      if (bid >= 0) bs = best[(int64_t)lane * Q + q];
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double s2 = __shfl_xor(bs, o, 64);
+      const int64_t i2 = __shfl_xor(bid, o, 64);
+      const int l2 = __shfl_xor(bl, o, 64);
+      if (wave_better(s2, i2, bs, bid)) { bs = s2; bid = i2; bl = l2; }
+    }
+    if (bid >= 0) {
+      n = 1;
+      *fb_id = bid;
+      if (lane == 0) sel[0] = bl << 16;
+    }
+  }
+  return n;
+}
+
 __global__ __launch_bounds__(64) void k_progressive_final(int R, int Q, int M, int W, const double* __restrict__ s0,
                                                           const int64_t* __restrict__ ids,
                                                           const double* __restrict__ det,
@@ -2718,77 +2824,10 @@ __global__ __launch_bounds__(64) void k_progressive_final(int R, int Q, int M, i
   __shared__ int sel[kMaxFinal];  // survivor i -> (list r << 16) | slot
   const int lane = threadIdx.x;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
-    // ---- R-way merge: lane r < R follows list r's head ----
-    int h = 0;
-    double hs = -__builtin_huge_val();
-    int64_t hid = -1;
-    auto load_head = [&]() {
-      hs = -__builtin_huge_val();
-      hid = -1;
-      if (lane < R && h < M) {
-        const int64_t o = ((int64_t)lane * Q + q) * M + h;
-        hid = ids[o];
-        if (hid >= 0) hs = s0[o];
-      }
-    };
-    load_head();
-    int n = 0;
-    if (R == 1) {
-      // one list: it is already the (score desc, id asc) order; its valid entries come first
-      for (int i = lane; i < M; i += 64) {
-        const bool v = ids[(int64_t)q * M + i] >= 0;
-        const unsigned long long m = __ballot(v);
-        n += __popcll(m);
-        if (v) sel[i] = i;
-      }
-      n = __builtin_amdgcn_readfirstlane(n);
-    }
-    for (; R > 1 && n < M; ++n) {
-      double bs = hs;
-      int64_t bid = hid;
-      int bl = lane;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const double s2 = __shfl_xor(bs, o, 64);
-        const int64_t i2 = __shfl_xor(bid, o, 64);
-        const int l2 = __shfl_xor(bl, o, 64);
-        if (wave_better(s2, i2, bs, bid)) { bs = s2; bid = i2; bl = l2; }
-      }
-      if (bid < 0) break;
-      const int hb = __shfl(h, bl, 64);
-      if (lane == 0) sel[n] = (bl << 16) | hb;
-      if (lane == bl) {
-        h = hb + 1;
-        load_head();
-      }
-    }
+    int64_t fb_id;
+    const int n = final_survivors(R, Q, M, q, s0, ids, best, best_id, sel, &fb_id);
     __syncthreads();
-    const double* rowbase = det;
-    int64_t fb_id = -1;
-    if (n == 0) {
-      // none passed the threshold: keep the first arg-max of the level-0 score (:295-298)
-      double bs = -__builtin_huge_val();
-      int64_t bid = -1;
-      int bl = lane;
-      if (lane < R) {
-        bid = best_id[(int64_t)lane * Q + q];
-        if (bid >= 0) bs = best[(int64_t)lane * Q + q];
-      }
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const double s2 = __shfl_xor(bs, o, 64);
-        const int64_t i2 = __shfl_xor(bid, o, 64);
-        const int l2 = __shfl_xor(bl, o, 64);
-        if (wave_better(s2, i2, bs, bid)) { bs = s2; bid = i2; bl = l2; }
-      }
-      if (bid >= 0) {
-        n = 1;
-        fb_id = bid;
-        rowbase = best_det;
-        if (lane == 0) sel[0] = bl << 16;
-      }
-      __syncthreads();
-    }
+    const double* rowbase = fb_id >= 0 ? best_det : det;
     // ---- stable sort of the survivors by overall score ----
     const int outn = n < K ? n : K;
     // row of survivor i in rowbase: list rows (r Q + q) M + slot, or the fallback's best row r Q + q
@@ -3335,6 +3374,352 @@ __global__ __launch_bounds__(256) void k_refine_lds(HQ_REFINE_ARGS) {
   refine_lds_body<false>(HQ_REFINE_PASS);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Long candidate lists (k > 64): the reference engine's default max_candidates_per_level = 100
+// (core/search_engine.py:31, core/video_search.py:48) and SearchConfig's 1000 (config.py:181).  Same
+// contracts as k_pool_select / k_refine_lds / k_progressive_final, one 256-thread workgroup per query,
+// the orderings done as bitonic sorts in LDS instead of one entry per lane.
+// ------------------------------------------------------------------------------------------------
+constexpr int kMaxTopKBig = 1024;  // list entries (k + slack) of the long-list path
+constexpr int kSortCap = 4096;     // pool keys sorted whole in LDS (32 KiB); larger pools are cut first
+constexpr int kRefTile = 64;       // candidate rows staged per round of the long-list re-rank
+
+__device__ __forceinline__ int pow2_at_least(int n) {
+  int p = 2;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+// ascending bitonic sort of n (a power of two) LDS entries; first(a, b): entry a ranks before entry b.
+// All threads of the workgroup call it (the entries must be visible: a barrier before the call).
+template <class First, class Swap>
+__device__ __forceinline__ void lds_bitonic(int n, First first, Swap swp) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int size = 2; size <= n; size <<= 1)
+    for (int st = size >> 1; st > 0; st >>= 1) {
+      for (int t = tid; t < (n >> 1); t += nt) {
+        const int lo = 2 * t - (t & (st - 1)), hi = lo + st;
+        if (first(hi, lo) == ((lo & size) == 0)) swp(lo, hi);
+      }
+      __syncthreads();
+    }
+}
+
+// pool entry -> 64-bit key, ascending = (score desc, row asc): scores are >= 0, so their f32 bit
+// patterns order like the values; rows are unique within a pool, so keys are unique
+__device__ __forceinline__ uint64_t pool_key(float s, int row) {
+  return ((uint64_t)(0x7FFFFFFFu - __float_as_uint(s)) << 32) | (uint32_t)row;
+}
+
+// k_pool_select for K > 64: the query's pool (<= kSortCap entries) is sorted whole; a larger pool is first
+// cut at its K-th key (bisection over the 64-bit keys in memory) and the K survivors are sorted.
+__global__ __launch_bounds__(256) void k_pool_sort(float* pool_s, int* pool_i, int* pool_n, int cap, int Q, int K,
+                                                   int64_t id_base, double* __restrict__ out_score,
+                                                   int64_t* __restrict__ out_id, const double* __restrict__ th0,
+                                                   double thr0, const float* __restrict__ qflag, int qstride,
+                                                   Scan0Args fa, const int* __restrict__ flist,
+                                                   const int* __restrict__ fcount) {
+  __shared__ uint64_t key[kSortCap];
+  __shared__ int red[4];
+  __shared__ int nsel;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  auto bsum = [&](int v) -> int {
+    v = wsum64i(v);
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    const int r = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    return r;
+  };
+  for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    if (fcount) {  // the corpus's flagged rows against this query first (k_pool_select)
+      const QConst* qc = reinterpret_cast<const QConst*>(fa.qconst);
+      const int n = *fcount;
+      if (n > 0 && __float_as_int(qc[q].flag) == 0) {
+        const QConst c = qc[q];
+        for (int i = tid; i < n; i += 256) flagged_pair(fa, c, q, flist[i]);
+      }
+      __syncthreads();
+    }
+    const int pn = fcount ? __hip_atomic_load(pool_n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : pool_n[q];
+    if (qflag && (__float_as_int(qflag[(int64_t)q * qstride]) != 0 || pn > cap)) {
+      for (int x = tid; x < K; x += 256) {
+        out_score[(int64_t)q * K + x] = __builtin_huge_val();
+        out_id[(int64_t)q * K + x] = -1;
+      }
+      continue;
+    }
+    const int T = pn < cap ? pn : cap;
+    const float* ps = pool_s + (int64_t)q * cap;
+    const int* pi = pool_i + (int64_t)q * cap;
+    const int k = T < K ? T : K;
+    int n2;
+    if (T <= kSortCap) {
+      n2 = pow2_at_least(T);
+      for (int x = tid; x < n2; x += 256) key[x] = x < T ? pool_key(ps[x], pi[x]) : ~0ull;
+    } else {
+      uint64_t lo = 0ull, hi = ~0ull;  // smallest key with count(key <= lo) >= K
+      while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        int c = 0;
+        for (int x = tid; x < T; x += 256) c += pool_key(ps[x], pi[x]) <= mid ? 1 : 0;
+        if (bsum(c) >= K) hi = mid; else lo = mid + 1;
+      }
+      if (tid == 0) nsel = 0;
+      __syncthreads();
+      for (int x = tid; x < T; x += 256) {
+        const uint64_t kk = pool_key(ps[x], pi[x]);
+        if (kk <= lo) key[atomicAdd(&nsel, 1)] = kk;  // exactly K entries
+      }
+      n2 = pow2_at_least(K);
+      __syncthreads();
+      for (int x = K + tid; x < n2; x += 256) key[x] = ~0ull;
+    }
+    __syncthreads();
+    lds_bitonic(n2, [&](int a, int b) { return key[a] < key[b]; },
+                [&](int a, int b) { const uint64_t t = key[a]; key[a] = key[b]; key[b] = t; });
+    const bool trunc = th0 != nullptr && th0[q] > thr0;
+    for (int x = tid; x < K; x += 256) {
+      if (x < k) {
+        const uint64_t kk = key[x];
+        out_score[(int64_t)q * K + x] = (double)__uint_as_float(0x7FFFFFFFu - (uint32_t)(kk >> 32));
+        out_id[(int64_t)q * K + x] = (int64_t)(uint32_t)kk + id_base;
+      } else {
+        out_score[(int64_t)q * K + x] = trunc ? __builtin_huge_val() : -__builtin_huge_val();
+        out_id[(int64_t)q * K + x] = -1;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// pool select launcher: one wave per query up to 64 entries, the LDS sort above beyond
+static void launch_pool_select(int K, hipStream_t s, int Q, float* pool_s, int* pool_i, int* pool_n, int cap,
+                               int64_t id_base, double* out_score, int64_t* out_id, const double* th0, double thr0,
+                               const float* qflag, int qstride, const Scan0Args& fa, const int* flist,
+                               const int* fcount) {
+  const int mg = Q < 8192 ? Q : 8192;
+  if (K <= kMaxTopK)
+    hipLaunchKernelGGL(k_pool_select, dim3(mg), dim3(64), 0, s, pool_s, pool_i, pool_n, cap, Q, K, id_base, out_score,
+                       out_id, th0, thr0, qflag, qstride, fa, flist, fcount);
+  else
+    hipLaunchKernelGGL(k_pool_sort, dim3(mg), dim3(256), 0, s, pool_s, pool_i, pool_n, cap, Q, K, id_base, out_score,
+                       out_id, th0, thr0, qflag, qstride, fa, flist, fcount);
+}
+
+// k_refine_lds for kp > 64 (same contract, arithmetic and outputs).  Pass 1 stages the listed candidates'
+// rows in tiles of tb (LDS-DMA), scores the levels the ranking needs (level 0 in mode 0 without odet...
+// every level in mode 1), applies the threshold test and keeps (score, id) per list entry in LDS; the
+// entries are bitonic-sorted by (score desc, id asc).  Pass 2 (odet) re-stages the rows of the ranked
+// output entries and writes their [overall, level..] records with the same exact_level code.
+template <bool SM>
+__device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  __shared__ int64_t srow[kRefTile];
+  __shared__ int t32s[kRefTile * kMaxSeg];
+  __shared__ double se[kMaxTopKBig];
+  __shared__ int64_t sid[kMaxTopKBig];
+  __shared__ int red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int RW = refine_rw(si), QW = refine_qw(si), W = 1 + si.nseg;
+  double* rq = sm;                          // query row: raw, Z, S
+  double* rows = sm + QW;                   // tb x RW candidate rows: raw, S
+  double* lvs = rows + (int64_t)tb * RW;    // tb x W: overall, levels
+  const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)sm;
+  const int nlev1 = mode == 0 ? 1 : si.nseg;
+  const int n2 = pow2_at_least(kp);
+  // stage the rows srow[0 .. nt) (and the query with the first tile), score levels [0, nlev) of each
+  auto stage_score = [&](int nt, int nlev, bool with_query, int64_t qrow) {
+    if (with_query && wave == 0) {
+      dma_seg(Qs.raw + qrow * si.L, lbase, 8 * si.L, lane);
+      dma_seg(Qs.Z + qrow * si.Lp, lbase + 8u * si.L, 8 * si.Lp, lane);
+      dma_seg(Qs.S + qrow * si.nseg * 4, lbase + 8u * (si.L + si.Lp), 32 * si.nseg, lane);
+    }
+    for (int r = wave; r < nt; r += 4) {
+      const int64_t i = srow[r];
+      if (i < 0) continue;
+      const uint32_t d0 = lbase + 8u * (uint32_t)(QW + r * RW);
+      dma_seg(Cs.raw + i * si.L, d0, 8 * si.L, lane);
+      dma_seg(Cs.S + i * si.nseg * 4, d0 + 8u * si.L, 32 * si.nseg, lane);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = tid; t < nlev * nt; t += 256) {
+      const int sg = t / nt, p = t - sg * nt;
+      double v = 0.0;
+      int f32 = 0;
+      if (srow[p] >= 0) {
+        const double* rc = rows + (int64_t)p * RW;
+        v = exact_level<SM>(rq + si.src[sg], rq + si.L + si.poff[sg], rq + si.L + si.Lp + 4 * sg, rc + si.src[sg],
+                            nullptr, rc + si.L + 4 * sg, si.len[sg], &f32);
+      }
+      lvs[(int64_t)p * W + 1 + sg] = v;
+      t32s[p * kMaxSeg + sg] = f32;
+    }
+    __syncthreads();
+  };
+  for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    const int64_t base = (int64_t)q * kp;
+    // ---- pass 1: exact ranking score of every list entry ----
+    for (int t0 = 0; t0 < kp; t0 += tb) {
+      const int nt = kp - t0 < tb ? kp - t0 : tb;
+      if (tid < nt) {
+        const int64_t id = cid[base + t0 + tid];
+        const int64_t c = id - id_base;
+        srow[tid] = (id >= 0 && c >= 0 && c < N) ? c : -1;
+      }
+      __syncthreads();
+      stage_score(nt, nlev1, t0 == 0, q);
+      if (tid < nt) {
+        double e = -__builtin_huge_val();
+        int64_t id = -1;
+        if (srow[tid] >= 0) {
+          const double* lv = lvs + (int64_t)tid * W;
+          e = mode == 0 ? lv[1] : overall_from_levels(lv + 1, t32s + tid * kMaxSeg, si.nseg);
+          const bool pass = mode == 0 ? typed_pass(e, t32s[tid * kMaxSeg], thr, thr_mode)
+                                      : (thr_mode == 0 || (thr_mode == 1 ? e >= thr : e > thr));
+          if (pass) id = cid[base + t0 + tid];
+          else e = -__builtin_huge_val();
+        }
+        se[t0 + tid] = e;
+        sid[t0 + tid] = id;
+      }
+      __syncthreads();
+    }
+    for (int x = kp + tid; x < n2; x += 256) {
+      se[x] = -__builtin_huge_val();
+      sid[x] = -1;
+    }
+    int nv = 0;
+    for (int x = tid; x < kp; x += 256) nv += sid[x] >= 0 ? 1 : 0;
+    nv = wsum64i(nv);
+    if (lane == 0) red[wave] = nv;
+    __syncthreads();
+    const int n = red[0] + red[1] + red[2] + red[3];
+    // ---- rank: (score desc, id asc), invalid entries last ----
+    lds_bitonic(n2,
+                [&](int a, int b) {
+                  const int64_t ia = sid[a], ib = sid[b];
+                  if (ib < 0) return ia >= 0;
+                  return ia >= 0 && (se[a] > se[b] || (se[a] == se[b] && ia < ib));
+                },
+                [&](int a, int b) {
+                  const double te = se[a];
+                  se[a] = se[b];
+                  se[b] = te;
+                  const int64_t ti = sid[a];
+                  sid[a] = sid[b];
+                  sid[b] = ti;
+                });
+    const int cnt = n < k ? n : k;
+    for (int x = tid; x < k; x += 256) {
+      os[(int64_t)q * k + x] = x < cnt ? se[x] : -__builtin_huge_val();
+      oid[(int64_t)q * k + x] = x < cnt ? sid[x] : -1;
+      if (odet && x >= cnt)
+        for (int w = 0; w < W; ++w) odet[((int64_t)q * k + x) * W + w] = 0.0;
+    }
+    if (tid == 0) {
+      const double kth = n >= k ? se[k - 1] : -__builtin_huge_val();
+      ocnt[q] = cnt;
+      const bool full = cid[base + kp - 1] >= 0;
+      // an empty last slot with score +inf: the scan's list may be incomplete (k_pool_select)
+      const bool trunc = !full && cs[base + kp - 1] == __builtin_huge_val();
+      int res = trunc ? 0 : 1;
+      if (full) {
+        const double bound = cs[base + kp - 1] + eps;
+        if (n >= k) res = bound < kth;
+        else if (thr_mode == 0) res = 0;
+        else res = thr_mode == 1 ? (bound < thr_low(thr)) : (bound <= thr_low(thr));
+      }
+      ores[q] = res;
+      if (oredo && (res == 0 || (count_empty && cnt == 0))) atomicAdd(oredo, 1);
+    }
+    // ---- pass 2: [overall, level..] records of the output entries ----
+    for (int r0 = 0; odet && r0 < cnt; r0 += tb) {
+      const int nt = cnt - r0 < tb ? cnt - r0 : tb;
+      __syncthreads();
+      if (tid < nt) srow[tid] = sid[r0 + tid] - id_base;
+      __syncthreads();
+      stage_score(nt, si.nseg, false, q);
+      if (tid < nt) {
+        double* lv = lvs + (int64_t)tid * W;
+        lv[0] = overall_from_levels(lv + 1, t32s + tid * kMaxSeg, si.nseg);
+        for (int w = 0; w < W; ++w) odet[((int64_t)q * k + r0 + tid) * W + w] = lv[w];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_refine_big_sm(HQ_REFINE_ARGS, int tb) { refine_big_body<true>(HQ_REFINE_PASS, tb); }
+__global__ __launch_bounds__(256) void k_refine_big(HQ_REFINE_ARGS, int tb) { refine_big_body<false>(HQ_REFINE_PASS, tb); }
+
+// k_progressive_final for M > 64: wave 0 selects the survivors (final_survivors), the workgroup sorts them
+// by (overall desc, survivor position asc) — the reference's stable sort — in LDS
+__global__ __launch_bounds__(256) void k_progressive_final_big(int R, int Q, int M, int W,
+                                                               const double* __restrict__ s0,
+                                                               const int64_t* __restrict__ ids,
+                                                               const double* __restrict__ det,
+                                                               const double* __restrict__ best,
+                                                               const int64_t* __restrict__ best_id,
+                                                               const double* __restrict__ best_det, int K,
+                                                               int64_t* __restrict__ out_id,
+                                                               double* __restrict__ out_det,
+                                                               int* __restrict__ out_count) {
+  __shared__ int sel[kMaxTopKBig];
+  __shared__ double ovs[kMaxTopKBig];
+  __shared__ int pos[kMaxTopKBig];
+  __shared__ int sn;
+  __shared__ int64_t sfb;
+  const int tid = threadIdx.x;
+  for (int q = blockIdx.x; q < Q; q += gridDim.x) {
+    if (tid < 64) {
+      int64_t fb;
+      const int n = final_survivors(R, Q, M, q, s0, ids, best, best_id, sel, &fb);
+      if (tid == 0) {
+        sn = n;
+        sfb = fb;
+      }
+    }
+    __syncthreads();
+    const int n = sn;
+    const int64_t fb_id = sfb;
+    const double* rowbase = fb_id >= 0 ? best_det : det;
+    auto row_of = [&](int v) -> int64_t {
+      const int64_t rq = (int64_t)(v >> 16) * Q + q;
+      return fb_id >= 0 ? rq : rq * M + (v & 0xFFFF);
+    };
+    const int n2 = pow2_at_least(n);
+    for (int i = tid; i < n2; i += 256) {
+      ovs[i] = i < n ? rowbase[row_of(sel[i]) * W] : -__builtin_huge_val();
+      pos[i] = i;
+    }
+    __syncthreads();
+    lds_bitonic(n2, [&](int a, int b) { return ovs[a] > ovs[b] || (ovs[a] == ovs[b] && pos[a] < pos[b]); },
+                [&](int a, int b) {
+                  const double to = ovs[a];
+                  ovs[a] = ovs[b];
+                  ovs[b] = to;
+                  const int tp = pos[a];
+                  pos[a] = pos[b];
+                  pos[b] = tp;
+                });
+    const int outn = n < K ? n : K;
+    for (int r = tid; r < K; r += 256) {
+      if (r < outn) {
+        const int64_t oi = row_of(sel[pos[r]]);
+        out_id[(int64_t)q * K + r] = fb_id >= 0 ? fb_id : ids[oi];
+        for (int w = 0; w < W; ++w) out_det[((int64_t)q * K + r) * W + w] = rowbase[oi * W + w];
+      } else {
+        out_id[(int64_t)q * K + r] = -1;
+        for (int w = 0; w < W; ++w) out_det[((int64_t)q * K + r) * W + w] = 0.0;
+      }
+    }
+    if (tid == 0) out_count[q] = outn;
+    __syncthreads();
+  }
+}
+
 // S7: (cos + 1) / 2, 0 if a norm is 0 (rag/search/engine.py:622-660, 1025-1051)
 __global__ __launch_bounds__(256) void k_cosine(const float* __restrict__ A, int Q, const float* __restrict__ B,
                                                 int64_t N, int K, double* __restrict__ out) {
@@ -3425,6 +3810,51 @@ static size_t sample_top_bytes(int Q, int64_t N) {
   return (size_t)Q * 4 * nchunks * kTopT * 4;
 }
 
+// K' of the sampled starting threshold (a stride-s sample): the smallest K' with P(Binomial(k, 1/s) >= K')
+// <= 1e-7, the chance that the sample holds K' of the corpus's k best pairs — only then can a pool end with
+// fewer than k entries although more pass the caller's threshold (k_pool_select marks such a pool and the
+// dense exact path answers the query).  k = 28 (the M = 20 headline): 12; k = 108: 24; k = 1008: 107.
+static int sample_kprime(int k, int64_t stride) {
+  if (stride <= 1 || k <= 1) return k;
+  const double p = 1.0 / (double)stride, lp = log(p), lq = log1p(-p), lk = lgamma((double)k + 1.0);
+  double tail = 0.0;
+  for (int i = k; i >= 1; --i) {
+    tail += exp(lk - lgamma((double)i + 1.0) - lgamma((double)(k - i) + 1.0) + i * lp + (k - i) * lq);
+    if (tail > 1e-7) return i + 1 <= k ? i + 1 : k;
+  }
+  return 1;
+}
+
+// K' actually used: option sample_kth (0 = k, a provable bound) or the rule above; dense samples (stride
+// below 16, small corpora) always k
+static int scan_kprime(int k, int64_t stride) {
+  int kp = (int)opt(OPT_SAMPLE_KTH, -1);
+  if (kp < 0) kp = sample_kprime(k, stride);
+  if (kp <= 0 || kp > k || stride < 16) kp = k;
+  return kp;
+}
+
+// per-query pool capacity: k <= 64 keeps nchunks x k entries (a pool then never overflows); a long list
+// (k > 64) is sized from the sample: ~stride x K' entries pass its starting threshold, capacity 3x that plus
+// 1024 as a power of two, at most the corpus (an overflowing pool marks its query for the dense path)
+static int pool_cap_for(int nchunks, int k, int64_t N, int64_t stride, int kprime) {
+  if (k <= kMaxTopK) return nchunks * k;
+  const int64_t want = 3 * stride * (int64_t)kprime + 1024;
+  int64_t c = 4096;
+  while (c < want && c < (int64_t(1) << 22)) c <<= 1;
+  const int64_t n64 = (N + 63) / 64 * 64;
+  return (int)(c < n64 ? c : n64);
+}
+
+static size_t scan0_lists_bytes(int Q, int64_t N, int k, int nchunks) {
+  if (k <= kMaxTopK) return (size_t)nchunks * Q * k * 16;
+  int64_t stride, S, chunk_len;
+  int nqb, sn;
+  sample_top_geometry(Q, N, stride, S, nqb, sn, chunk_len);
+  const size_t b = (size_t)Q * pool_cap_for(nchunks, k, N, stride, scan_kprime(k, stride)) * 8;
+  return (b + 255) & ~(size_t)255;
+}
+
 static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
   int nqb, nchunks, nqb2, nchunks2;
   int64_t chunk_len, chunk_len2;
@@ -3436,7 +3866,7 @@ static size_t scan0_ws_bytes(int Q, int64_t N, int k) {
     if (nchunks2 > nchunks) nchunks = nchunks2;
   }
   // lists / pools + global thresholds + sample histogram + starting thresholds + pool counts + sample tops
-  return (size_t)nchunks * Q * k * 16 + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 8 + (size_t)Q * 4 +
+  return scan0_lists_bytes(Q, N, k, nchunks) + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 8 + (size_t)Q * 4 +
          sample_top_bytes(Q, N) + (size_t)Q * sizeof(QConst) + (size_t)N * 4 + 1024;
 }
 
@@ -3560,14 +3990,17 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   b.ws_id = reinterpret_cast<int64_t*>(ws + (size_t)b.nchunks * Q * k * 8);
   // [lists / pools][gtau Q x 8][hist Q x kBins x 4][pool_n Q x 4][th0 Q x 8][sample tops]: the zeroed
   // regions are adjacent, so one memset clears them
-  const size_t lists = (size_t)b.nchunks * Q * k * 16;
+  const size_t lists = scan0_lists_bytes(Q, N, k, b.nchunks);
   b.gtau = reinterpret_cast<unsigned long long*>(ws + lists);
   unsigned int* hist = reinterpret_cast<unsigned int*>(ws + lists + (size_t)Q * 8);
   b.pool_n = reinterpret_cast<int*>(ws + lists + (size_t)Q * 8 + (size_t)Q * kBins * 4);
   double* th0 = reinterpret_cast<double*>(ws + lists + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 4);
   b.th0 = nullptr;
-  // f32 path: per-query pools in the list area (cap = nchunks * k entries, never overflows)
-  b.pool_cap = b.nchunks * k;
+  // f32 path: per-query pools in the list area (pool_cap_for: nchunks * k entries for k <= 64)
+  int64_t s_stride, s_S, s_len;
+  int s_nqb, s_nch;
+  sample_top_geometry(Q, N, s_stride, s_S, s_nqb, s_nch, s_len);
+  b.pool_cap = pool_cap_for(b.nchunks, k, N, s_stride, scan_kprime(k, s_stride));
   b.pool_s = reinterpret_cast<float*>(ws);
   b.pool_i = reinterpret_cast<int*>(ws + (size_t)Q * b.pool_cap * 4);
   // option scan_nosample: no sample pass, the scan starts from the caller's threshold
@@ -3578,8 +4011,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
 #endif
   // K' of the starting threshold: the sample's K'-th best (statistical for K' < k: pools left short are
   // marked for the exact path, k_pool_select); option sample_kth = 0 -> k (a provable bound)
-  int sample_kth = (int)opt(OPT_SAMPLE_KTH, kSampleKth);
-  if (sample_kth <= 0 || sample_kth > k) sample_kth = k;
+  int sample_kth = scan_kprime(k, s_stride);
   float* top = reinterpret_cast<float*>(ws + lists + (size_t)Q * 8 + (size_t)Q * kBins * 4 + (size_t)Q * 4 +
                                         (size_t)Q * 8);
   // k_scan0g (default; option scan_variant 1 = the list-based k_scan0f): per-query constants after the
@@ -3602,7 +4034,6 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     sa.Zq32 = nullptr; sa.Zc32 = nullptr; sa.Zq16 = Zq16; sa.Zc16 = Zc16; sa.Sq32 = Sq32; sa.Sc32 = Sc32;
     sa.Lp = b.Lp; sa.nseg = b.nseg; sa.P0 = b.P0; sa.inv_m = b.inv_m; sa.c1 = b.c1;
     sample_top_geometry(Q, N, sa.stride, sa.S, sa.nqb, sa.nchunks, sa.chunk_len);
-    if (sa.stride < 16) sample_kth = k;  // dense samples (small corpora): the provable bound is tight enough
     sa.hist = nullptr;
     sa.top = top;
     sa.K = k;
@@ -3680,9 +4111,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
   }
   if (rc) return rc;
   if (f32) {
-    const int mg = Q < 8192 ? Q : 8192;
-    hipLaunchKernelGGL(k_pool_select, dim3(mg), dim3(64), 0, s, (const float*)b.pool_s, (const int*)b.pool_i,
-                       (const int*)b.pool_n, b.pool_cap, Q, k, id_base, out_score, out_id,
+    launch_pool_select(k, s, Q, b.pool_s, b.pool_i, b.pool_n, b.pool_cap, id_base, out_score, out_id,
                        top_sample && sample_kth < k ? (const double*)th0 : (const double*)nullptr, b.thr0,
                        qc ? &qc[0].flag : (const float*)nullptr, (int)(sizeof(QConst) / 4), b,
                        queue_scan ? (const int*)flag_list : (const int*)nullptr,
@@ -3769,8 +4198,28 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
   const hipStream_t s = (hipStream_t)stream;
   const int grid = Q < 8192 ? Q : 8192;
   if (out_redo) HQ_CHECK_HIP(hipMemsetAsync(out_redo, 0, sizeof(int), s));
-  const size_t lds = ((size_t)refine_qw(si) + (size_t)kp * refine_rw(si) + (size_t)kp * (1 + si.nseg)) * 8;
   const bool sm = seg_small(si);
+  if (kp > kMaxTopK) {  // long lists: tiles of tb staged candidate rows (<= 96 KiB of dynamic LDS)
+    if (L % 2) return fail(HQ_E_UNSUPPORTED, "long candidate lists need an even index length (L=%d)", L);
+    const size_t per = ((size_t)refine_rw(si) + (size_t)(1 + si.nseg)) * 8;
+    int tb = (int)((96 * 1024 - (size_t)refine_qw(si) * 8) / per);
+    if (tb > kRefTile) tb = kRefTile;
+    if (tb < 4) return fail(HQ_E_UNSUPPORTED, "index rows too long for the long-list re-rank (L=%d)", L);
+    const size_t lb = (size_t)refine_qw(si) * 8 + (size_t)tb * per;
+    const void* fn = sm ? (const void*)k_refine_big_sm : (const void*)k_refine_big;
+    HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb));
+    if (sm)
+      hipLaunchKernelGGL(k_refine_big_sm, dim3(grid), dim3(256), lb, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
+                         mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
+                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, tb);
+    else
+      hipLaunchKernelGGL(k_refine_big, dim3(grid), dim3(256), lb, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
+                         mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
+                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, tb);
+    HQ_CHECK_LAUNCH();
+    return HQ_OK;
+  }
+  const size_t lds = ((size_t)refine_qw(si) + (size_t)kp * refine_rw(si) + (size_t)kp * (1 + si.nseg)) * 8;
 #ifdef HQ_DIAG
   const int expt = (int)opt(OPT_REFINE_EXPT, 0);  // diagnostics build only
 #else
@@ -4458,7 +4907,7 @@ static OvPlan ov_plan(int Q, int64_t N, int k) {
   p.stride = N >= sd * 4096 ? sd : (N / 4096 > 1 ? N / 4096 : 1);
   p.S = sample_rows_tiled(N, p.stride);
   ov_geometry(Q, p.S, 16, 4096, 64 * kKthReg / (4 * kTopT), p.s_nqb, p.s_nchunks, p.s_chunk_len);
-  p.pool_cap = p.nchunks * k;
+  p.pool_cap = pool_cap_for(p.nchunks, k, N, p.stride, scan_kprime(k, p.stride));
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   size_t o = al((size_t)Q * p.pool_cap * 4);
   p.off_pool_i = 0 + o;
@@ -4523,8 +4972,7 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
   hipLaunchKernelGGL(k_scanov_flagged, dim3(64, (Q + 63) / 64), dim3(64), 0, s, a, si, (const int*)flag_list,
                      (const int*)flag_n);
   HQ_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_pool_select, dim3(mg), dim3(64), 0, s, (const float*)a.pool_s, (const int*)a.pool_i,
-                     (const int*)a.pool_n, a.pool_cap, Q, k, id_base, out_score, out_id,
+  launch_pool_select(k, s, Q, a.pool_s, a.pool_i, a.pool_n, a.pool_cap, id_base, out_score, out_id,
                      sample_kth < k ? (const double*)th0 : (const double*)nullptr, thr0, &qc[0].flag,
                      (int)(sizeof(QOv) / 4), Scan0Args{}, (const int*)nullptr, (const int*)nullptr);
   HQ_CHECK_LAUNCH();
@@ -4614,6 +5062,15 @@ int hq_level_scores(const double* Rq, const double* Zq, const double* Sq, int Q,
   if (!Rq || !Zq || !Sq || !Rc || !Zc || !Sc || !scores) return fail(HQ_E_INVALID, "null buffer");
   SegInfo si;
   seg_info(L, si);
+  if (level >= 0 && level < si.nseg && si.len[level] <= 128 && !opt_on(OPT_LEVEL_SCORES_V1) &&
+      (N + kLsTile - 1) / kLsTile < (int64_t(1) << 31) && (Q + kLsQ - 1) / kLsQ < 65536) {
+    const size_t lds = (size_t)kLsTile * (si.len[level] | 1) * 8;
+    hipLaunchKernelGGL(k_level_scores_lds, dim3((unsigned)((N + kLsTile - 1) / kLsTile), (Q + kLsQ - 1) / kLsQ),
+                       dim3(kLsTile), lds, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si, level,
+                       scores);
+    HQ_CHECK_LAUNCH();
+    return HQ_OK;
+  }
   const int64_t total = (int64_t)Q * N;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
@@ -4632,7 +5089,7 @@ int hq_refine_topk(const double* Rq, const double* Zq, const double* Sq, int Q, 
                    int kp, int k, double threshold, int thr_mode, double eps, int64_t id_base, double* out_score,
                    int64_t* out_id, int* out_count, int* out_resolved, int count_empty, int* out_redo,
                    hq_stream_t stream) {
-  if (Q < 0 || N < 0 || L <= 0 || kp <= 0 || kp > kMaxTopK || k <= 0 || k > kp)
+  if (Q < 0 || N < 0 || L <= 0 || kp <= 0 || kp > kMaxTopKBig || k <= 0 || k > kp)
     return fail(HQ_E_INVALID, "bad sizes kp=%d k=%d", kp, k);
   if (Q == 0) return HQ_OK;
   if (!Rq || !Zq || !Sq || !cand_score || !cand_id || !out_score || !out_id || !out_count || !out_resolved ||
@@ -4647,7 +5104,7 @@ int hq_refine_rescore_topk(const double* Rq, const double* Zq, const double* Sq,
                            const int64_t* cand_id, int kp, int k, double threshold, int thr_mode, double eps,
                            int64_t id_base, double* out_score, int64_t* out_id, int* out_count, int* out_resolved,
                            int count_empty, int* out_redo, double* out_det, hq_stream_t stream) {
-  if (Q < 0 || N < 0 || L <= 0 || kp <= 0 || kp > kMaxTopK || k <= 0 || k > kp)
+  if (Q < 0 || N < 0 || L <= 0 || kp <= 0 || kp > kMaxTopKBig || k <= 0 || k > kp)
     return fail(HQ_E_INVALID, "bad sizes kp=%d k=%d", kp, k);
   if (Q == 0) return HQ_OK;
   if (!Rq || !Zq || !Sq || !cand_score || !cand_id || !out_score || !out_id || !out_count || !out_resolved ||
@@ -4658,6 +5115,7 @@ int hq_refine_rescore_topk(const double* Rq, const double* Zq, const double* Sq,
 }
 
 size_t hq_scan_workspace_size(int Q, int64_t N, int k) {
+  if (k > kMaxTopK) return scan0_ws_bytes(Q, N, k);  // long lists: the split level-0 scan only
   int nqb, nchunks;
   int64_t chunk_len;
   scan_geometry(Q, N, nqb, nchunks, chunk_len);
@@ -4780,7 +5238,7 @@ int hq_scan0_topk_split_fl(const void* Zq16, const float* Sq32, const double* Sq
                            int thr_mode, int64_t id_base, void* workspace, size_t workspace_bytes, double* out_score,
                            int64_t* out_id, const int* corpus_flags, hq_stream_t stream) {
   if (Q < 0 || N < 0 || L <= 0) return fail(HQ_E_INVALID, "bad shape");
-  if (k <= 0 || k > kMaxTopK) return fail(HQ_E_UNSUPPORTED, "k=%d (1..%d)", k, kMaxTopK);
+  if (k <= 0 || k > kMaxTopKBig) return fail(HQ_E_UNSUPPORTED, "k=%d (1..%d)", k, kMaxTopKBig);
   if (Q == 0) return HQ_OK;
   if (!out_score || !out_id) return fail(HQ_E_INVALID, "null buffer");
   hipStream_t s = (hipStream_t)stream;
@@ -4832,15 +5290,19 @@ int hq_rescore(const double* Rq, const double* Zq, const double* Sq, int Q, cons
 int hq_progressive_final(int R, int Q, int M, int nseg, const double* s0, const int64_t* ids, const double* det,
                          const double* best, const int64_t* best_id, const double* best_det, int K,
                          int64_t* out_id, double* out_det, int* out_count, hq_stream_t stream) {
-  if (R <= 0 || R > 16 || Q < 0 || M <= 0 || M > kMaxFinal || K <= 0 || nseg < 0 || nseg >= kMaxSeg)
+  if (R <= 0 || R > 16 || Q < 0 || M <= 0 || M > kMaxTopKBig || K <= 0 || nseg < 0 || nseg >= kMaxSeg)
     return fail(HQ_E_INVALID, "bad sizes R=%d Q=%d M=%d K=%d", R, Q, M, K);
   if (Q == 0) return HQ_OK;
   if (!s0 || !ids || !det || !best || !best_id || !best_det || !out_id || !out_det || !out_count)
     return fail(HQ_E_INVALID, "null buffer");
   const int W = 1 + nseg;
   const int grid = Q < 8192 ? Q : 8192;
-  hipLaunchKernelGGL(k_progressive_final, dim3(grid), dim3(64), 0, (hipStream_t)stream, R, Q, M, W, s0, ids, det,
-                     best, best_id, best_det, K, out_id, out_det, out_count);
+  if (M <= kMaxTopK)
+    hipLaunchKernelGGL(k_progressive_final, dim3(grid), dim3(64), 0, (hipStream_t)stream, R, Q, M, W, s0, ids, det,
+                       best, best_id, best_det, K, out_id, out_det, out_count);
+  else
+    hipLaunchKernelGGL(k_progressive_final_big, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, Q, M, W, s0, ids,
+                       det, best, best_id, best_det, K, out_id, out_det, out_count);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
@@ -5029,7 +5491,7 @@ int hq_scanov_topk_split(const void* Zq16, const float* Sq32, const double* Sq, 
                          int k, double threshold, int thr_mode, int64_t id_base, void* workspace,
                          size_t workspace_bytes, double* out_score, int64_t* out_id, hq_stream_t stream) {
   if (Q < 0 || N < 0 || L <= 0) return fail(HQ_E_INVALID, "bad shape");
-  if (k <= 0 || k > kMaxTopK) return fail(HQ_E_UNSUPPORTED, "k=%d (1..%d)", k, kMaxTopK);
+  if (k <= 0 || k > kMaxTopKBig) return fail(HQ_E_UNSUPPORTED, "k=%d (1..%d)", k, kMaxTopKBig);
   if (Q == 0) return HQ_OK;
   if (!out_score || !out_id) return fail(HQ_E_INVALID, "null buffer");
   hipStream_t s = (hipStream_t)stream;
@@ -5050,8 +5512,7 @@ int hq_scanov_topk_split(const void* Zq16, const float* Sq32, const double* Sq, 
   a.Zq64 = Zq; a.Zc64 = Zc; a.Lp = si.Lp;
   a.nqb = p.nqb; a.nchunks = p.nchunks; a.chunk_len = p.chunk_len;
   a.stride = p.stride; a.S = p.S; a.top = nullptr; a.qc = nullptr;
-  int sample_kth = (int)opt(OPT_SAMPLE_KTH, kSampleKth);
-  if (sample_kth <= 0 || sample_kth > k || p.stride < 16) sample_kth = k;
+  const int sample_kth = scan_kprime(k, p.stride);
   const double thr0 = thr_mode == 0 ? -__builtin_huge_val() : threshold;
   uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
   if (a.o.lid == 0) return ov_launch<0>(a, p, si, k, thr0, sample_kth, id_base, ws, out_score, out_id, s);

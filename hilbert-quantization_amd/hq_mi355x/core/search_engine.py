@@ -22,7 +22,8 @@ from .._dev import is_tensor, to_dev, to_np, torch
 from ..models import QuantizedModel, SearchResult
 from .._compat import bases as _bases
 
-MAX_FUSED_K = 64
+MAX_FUSED_K = 64     # list length of the f64 scans (hq_scan_topk)
+MAX_SPLIT_K = 1024   # list length of the split-f16 scans (k > 64: LDS-sorted pools, tiled re-rank)
 
 
 @dataclass
@@ -154,6 +155,15 @@ class IndexCorpus:
             return K.seg_level0_len(self.L) <= 256
         return self.prep.Lp <= 256
 
+    def _max_list(self, mode: int) -> int:
+        """Longest scan list (k + SLACK) the scan for `mode` takes: the split-f16 scans (level-0 copies for
+        mode 0, the overall layout for mode 1) up to MAX_SPLIT_K, the f64 scans up to MAX_FUSED_K."""
+        if self.L % 2 or K._lib.get_option("scan_v1") is not None:
+            return MAX_FUSED_K
+        if (mode == 0 and self.prep.Z16 is not None) or (mode == 1 and self.prep.Zov16 is not None):
+            return MAX_SPLIT_K
+        return MAX_FUSED_K
+
     def _forced(self, qp):
         """Device bool [Q] of queries that must take the dense exact path (float32 outside the model)."""
         t = torch()
@@ -215,7 +225,7 @@ class IndexCorpus:
         best = t.full((Q,), -float("inf"), dtype=t.float64, device=dev)
         bid = t.full((Q,), -1, dtype=t.int64, device=dev)
         kp = k + self.SLACK
-        if kp > MAX_FUSED_K or self.dense_only or not self._fused_ok(mode):
+        if kp > self._max_list(mode) or self.dense_only or not self._fused_ok(mode):
             sc, ids, b, bi = self._dense(qp, t.arange(Q, device=dev), mode, k, thr, thr_mode)
             cnt = (ids >= 0).sum(1).to(t.int32)
             return sc, ids, cnt, b, bi
@@ -270,7 +280,7 @@ class IndexCorpus:
             ids, ov, lv = self.brute_force(queries, min(K_out, max(self.N, 1)))
             cnt = (ids >= 0).sum(dim=1).to(t.int32)
             return PendingSearch(done=(ids, ov, lv, cnt))
-        if M + self.SLACK > MAX_FUSED_K or self.dense_only or not self._fused_ok(0):
+        if M + self.SLACK > self._max_list(0) or self.dense_only or not self._fused_ok(0):
             s0, ids, cnt, best, bid = self.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)
             oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
             return PendingSearch(done=(oid, odet[..., 0], odet[..., 1:], ocnt))

@@ -133,7 +133,7 @@ class ShardedIndexCorpus:
         if self.n_total <= M:
             return ["done", self.brute_force(queries, max_results)]
         qp = c.prepare_queries(queries)
-        if M + c.SLACK > 64 or c.dense_only or not c._fused_ok(0):  # the dense exact path per shard (list length / f32 model)
+        if M + c.SLACK > c._max_list(0) or c.dense_only or not c._fused_ok(0):  # the dense exact path per shard (list length / f32 model)
             t = torch()
             Q = qp.N
             s0, ids, _, best, bid = c.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)

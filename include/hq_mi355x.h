@@ -53,7 +53,8 @@ const char* hq_last_error(void);
  * hq_set_option selects an alternative form of a kernel (same results, checked by the parity tests):
  * e.g. "fused_v" (fused-kernel variant bits), "fused_generic", "chunk_generic", "chunk_exactdiv",
  * "chunk_wpb", "chunk_cpw", "precomp_grid", "precomp_tree_lds", "cos_kernel" (1 register-staged,
- * 2 lockstep), "refine_global", "select_2stage", "sample_kth" (0 = provable bound), "scan_v1" (the
+ * 2 lockstep), "refine_global", "select_2stage", "level_scores_v1" (the one-thread-per-pair dense scorer),
+ * "sample_kth" (0 = provable bound), "scan_v1" (the
  * LDS-tiled level-0 scan), "scan_variant", "scan_wpb" (4 = four waves per level-0 scan block), "scan_pf" (prefetch
  * distance 3 or 4), "sample_variant" (1 = the full-filter sample pass).  Options are process-wide: set them before launching, not
  * while other host threads launch.  hq_reset_option restores the default; hq_get_option returns 1 when
@@ -70,7 +71,9 @@ int hq_diag_build(void);
 int hq_diag_violations(int64_t* count, int* first_line);
 /* Launch geometry of the level-0 scan k_scan0f (host only): query blocks of 64, corpus chunks (a multiple
  * of 8: XCD map) of chunk_len rows (a multiple of 16), and the row counts of the split copies it reads
- * (Z16: z_rows = N + 48, S32: s_rows = round_up(N, 4) + 48).  Exported for the bounds test.          */
+ * (Z16: z_rows = round_up(N, 16) + 48 rows of 64 halves in the tiled fragment layout, S32: s_rows =
+ * round_up(N, 4) + 48).  A C caller of hq_seg_pack0_split allocates z_rows x 64 halves and s_rows x 4
+ * floats; hq_scan0_geometry(1, N, ...) returns both.  Exported for the bounds test.                 */
 int hq_scan0_geometry(int Q, int64_t N, int* nqb, int* nchunks, int64_t* chunk_len, int64_t* z_rows,
                       int64_t* s_rows);
 
@@ -227,8 +230,11 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
  * Sq/Sc are the f64 statistics of hq_seg_prepare.  Level-0 segments of up to 32 values, N < 2^31. */
 /* Starting threshold of hq_scan0_topk_split: the K'-th best score of a 1/16 sample (every 16th tile of
  * 16 rows) minus the error
- * margin, K' = 12 (HQ_SAMPLE_KTH; K' = k, a provable lower bound of the k-th best, for corpora below
- * 16 x 4096 rows).  With K' < k a query can end with fewer than k listed candidates although more pass
+ * margin, K' = the smallest count with P(Binomial(k, 1/16) >= K') <= 1e-7 (12 at k = 28, 24 at k = 108,
+ * 107 at k = 1008; option sample_kth overrides; K' = k, a provable lower bound of the k-th best, for
+ * corpora below 16 x 4096 rows).  k up to 1024: lists longer than 64 (the reference engine's default
+ * max_candidates_per_level = 100, SearchConfig's 1000) are reduced by a per-query LDS sort of the pool,
+ * whose capacity is sized from the sample (an overflowing pool marks its query unresolved).  With K' < k a query can end with fewer than k listed candidates although more pass
  * the caller's threshold: its empty slots then carry score +inf (id -1), which hq_refine_topk /
  * hq_refine_rescore_topk report as unresolved (the caller's dense exact path answers the query).    */
 int hq_seg_level0_len(int L);
@@ -262,8 +268,8 @@ int hq_scan0_topk_split_fl(const void* Zq16, const float* Sq32, const double* Sq
  * groups of 4 rows (per one-value segment value[4], row flags[4], pre-filter offsets[4], then per row
  * and segment (std, mean, msq, zero-std flag)) for (round_up(N, 4) + 48) / 4 groups.
  * hq_scanov_topk_split: Zq/Zc are hq_seg_prepare's f64 Z (rows with an f32-unsafe statistic are scored
- * from them in f64); the starting threshold comes from a 1/16 tile sample (K' = 12, as
- * hq_scan0_topk_split: short lists carry +inf, which hq_refine_topk reports as unresolved).       */
+ * from them in f64); the starting threshold comes from a 1/16 tile sample (K' as
+ * hq_scan0_topk_split: short lists carry +inf, which hq_refine_topk reports as unresolved).  k <= 1024. */
 int hq_seg_packov_info(int L, int* nkb, int* ng, int* nc, int* group_floats);
 int hq_seg_packov_split(const double* Z, const double* S, int64_t N, int L, void* Zo16, float* So32,
                         hq_stream_t stream);
@@ -278,7 +284,8 @@ int hq_scanov_topk_split(const void* Zq16, const float* Sq32, const double* Sq, 
  * candidate exactly (as hq_level_scores), applies the threshold test exactly and writes the exact
  * top-k (score desc, id asc): out_score/out_id Q x k, out_count Q, and out_resolved Q = 1 when the
  * result is provably the exact top-k over the whole corpus given |approx - exact| <= eps (else the
- * caller re-runs that query on the dense exact path).  kp <= 64, k <= kp.  out_redo (device int, may
+ * caller re-runs that query on the dense exact path).  kp <= 1024 (lists longer than 64 are staged in
+ * tiles and ranked by an LDS sort; even L), k <= kp.  out_redo (device int, may
  * be NULL): the number of queries that need the dense path — unresolved, or (count_empty != 0) with
  * no candidate passing — so the caller syncs on one int.                                          */
 int hq_refine_topk(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
@@ -311,7 +318,7 @@ int hq_rescore(const double* Rq, const double* Zq, const double* Sq, int Q, cons
  * best_det (R x Q x (1+nseg)).  Forms the global level-0 top-M, falls back to the global first
  * arg-max when no candidate passed (search_engine.py:295-298), stable-sorts the survivors by the
  * overall score (:386-388) and writes the top K: out_id (Q x K, -1 padded), out_det
- * (Q x K x (1+nseg)), out_count (Q).                                                            */
+ * (Q x K x (1+nseg)), out_count (Q).  M <= 1024, R <= 16.                                        */
 int hq_progressive_final(int R, int Q, int M, int nseg, const double* s0, const int64_t* ids,
                          const double* det, const double* best, const int64_t* best_id,
                          const double* best_det, int K, int64_t* out_id, double* out_det,

@@ -594,6 +594,57 @@ def store_fixtures(hq):
     return out
 
 
+def api_fixtures(hq):
+    """End-to-end HilbertQuantizer (api.py:120-297, core/pipeline.py:71-233, core/compressor.py:43-148):
+    quantize 8 seeded vectors per length with the pre-computed index on, reconstruct each in order (the
+    compressor's instance state: every decompress de-normalises with the LAST compress's min / max),
+    then search the 8 models with 4 queries (each query is itself quantized first, api.py:268)."""
+    import contextlib
+    import io
+    from hilbert_quantization.api import HilbertQuantizer
+    rng = np.random.default_rng(4242)
+    out = {}
+    try:  # 1536 values on 64 x 64 = efficiency 0.375 < the default minimum 0.5: the reference refuses
+        HilbertQuantizer(use_precomputed_indexing=True).quantize(rng.standard_normal(1536).astype(np.float32),
+                                                                 model_id="eff")
+        out["d1536_error"] = np.array("")
+    except Exception as e:  # noqa: BLE001
+        out["d1536_error"] = np.array(f"{type(e).__name__}: {e}")
+    for d in (1024, 3000, 4096):
+        tag = f"d{d}"
+        hqz = HilbertQuantizer(use_precomputed_indexing=True)
+        P = rng.standard_normal((8, d)).astype(np.float32)
+        P[5] = P[2] * 0.5 + 0.01            # a near-duplicate direction
+        P[7] = P[3]                          # an exact duplicate: tie order follows the pool
+        out[f"{tag}_params"] = P
+        with contextlib.redirect_stdout(io.StringIO()):
+            models = [hqz.quantize(P[i], model_id=f"{tag}_m{i}") for i in range(8)]
+            for i, m in enumerate(models):
+                out[f"{tag}_payload_{i}"] = np.frombuffer(m.compressed_data, dtype=np.uint8).copy()
+                out[f"{tag}_hidx_{i}"] = np.asarray(m.hierarchical_indices)
+            out[f"{tag}_dims"] = np.array([m.original_dimensions for m in models], dtype=np.int64)
+            out[f"{tag}_count"] = np.array([m.parameter_count for m in models], dtype=np.int64)
+            out[f"{tag}_quality"] = np.array([m.compression_quality for m in models])
+            comp = hqz.quantization_pipeline.compressor
+            out[f"{tag}_minmax_last"] = np.array([comp._norm_min, comp._norm_max], dtype=np.float64) \
+                if hasattr(comp, "_norm_min") else np.zeros(0)
+            out[f"{tag}_recon"] = np.stack([np.asarray(hqz.reconstruct(m), dtype=np.float32) for m in models])
+            Qs = np.stack([P[2] + rng.normal(0, 0.05, d).astype(np.float32), P[3] + 0.0,
+                           rng.standard_normal(d).astype(np.float32), P[6] * 2.0]).astype(np.float32)
+            out[f"{tag}_queries"] = Qs
+            ids = np.full((4, 8), -1, dtype=np.int64)
+            sc = np.zeros((4, 8))
+            err = np.zeros((4, 8))
+            for a in range(4):
+                r = hqz.search(Qs[a], candidate_models=models, max_results=8)
+                for j, x in enumerate(r):
+                    ids[a, j] = int(x.model.metadata.model_name.rsplit("_m", 1)[1])
+                    sc[a, j] = x.similarity_score
+                    err[a, j] = x.reconstruction_error
+            out[f"{tag}_search_ids"], out[f"{tag}_search_sc"], out[f"{tag}_search_err"] = ids, sc, err
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -604,7 +655,7 @@ def main():
     for name, fn in [("mapper", mapper_fixtures), ("index", index_fixtures), ("quant", quant_fixtures),
                      ("search", search_fixtures), ("search_f32", search_f32_fixtures),
                      ("rag_score", rag_score_fixtures), ("stores", store_fixtures),
-                     ("precomputed", precomputed_fixtures)]:
+                     ("precomputed", precomputed_fixtures), ("api", api_fixtures)]:
         if only and name not in only:
             continue
         d = fn(hq)

@@ -1,0 +1,186 @@
+"""Long candidate lists on the scan path (k + slack > 64): the reference engine's default
+max_candidates_per_level = 100 (core/search_engine.py:31, core/video_search.py:48) and SearchConfig's 1000
+(config.py:181).  The level-0 split scan fills per-query pools, k_pool_sort orders them in LDS, the tiled
+exact re-rank (k_refine_big) proves the list complete, k_progressive_final_big ranks the survivors; results
+are identical (ids, order, scores) to the oracle's reference-order restatement, and only queries the scan
+cannot model (zero-variance queries, nothing passing) take the dense exact path."""
+import numpy as np
+import pytest
+
+from oracle import hq_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-10
+
+
+def _np(x):
+    from hq_mi355x._dev import to_np
+    return to_np(x)
+
+
+def _corpus(n_rows, L, seed):
+    """Streaming-index corpus (cfg3's index shape) with degenerate rows and duplicates (ties)."""
+    rng = np.random.default_rng(seed)
+    d = 1536 if L == 64 else L * L
+    P = rng.standard_normal((n_rows, d)).astype(np.float32)
+    C = O.streaming_index(O.map_from_2d(O.map_to_2d(O.pad_parameters(P, L), L)), L)
+    C[1] = 0.0
+    C[2] = 0.1
+    C[3] = C[17]
+    C[30:34] = C[20]
+    C[n_rows - 5:] = C[40]          # duplicates far apart: ties ordered by id
+    return C
+
+
+def _dense_counter(corpus):
+    """Count the query rows the corpus sends to the dense exact path."""
+    calls = []
+    orig = corpus._dense
+
+    def wrapped(qp, sel, *a, **kw):
+        calls.append(int(sel.numel()))
+        return orig(qp, sel, *a, **kw)
+
+    corpus._dense = wrapped
+    return calls
+
+
+@pytest.mark.parametrize("M", [100, 1000])
+def test_long_list_progressive_matches_oracle(hq_lib, M):
+    from hq_mi355x.core.search_engine import IndexCorpus
+    C = _corpus(40000, 64, 21)
+    rng = np.random.default_rng(22)
+    Q = np.concatenate([C[[20, 3, 40, 1]] + 0.0, C[500:505] + rng.normal(0, 0.01, (5, 64)),
+                        rng.standard_normal((2, 64))])
+    corpus = IndexCorpus(C)
+    assert M + corpus.SLACK <= corpus._max_list(0)  # the scan path, not the dense fallback
+    dense = _dense_counter(corpus)
+    K_out = min(M, 200)
+    ids, ov, lv, cnt = [_np(x) for x in corpus.progressive(Q, K_out, 0.1, M)]
+    # only the zero-variance query (row 1) may need the dense exact path
+    assert sum(dense) <= 1, dense
+    for a in range(len(Q)):
+        rid, rsc, rlv, _ = O.progressive_search(Q[a], C, K_out, 0.1, M)
+        assert cnt[a] == len(rid), a
+        assert list(ids[a][: cnt[a]]) == list(rid), a
+        np.testing.assert_allclose(ov[a][: cnt[a]], rsc, atol=TOL)
+        np.testing.assert_allclose(lv[a][: cnt[a]], rlv, atol=TOL)
+        assert all(ids[a][cnt[a]:] == -1)
+
+
+def test_long_list_fallback_and_threshold(hq_lib):
+    """Nothing passes (threshold 0.999): the first arg-max fallback; a high threshold cutting the list."""
+    from hq_mi355x.core.search_engine import IndexCorpus
+    C = _corpus(20000, 64, 23)
+    rng = np.random.default_rng(24)
+    Q = np.concatenate([rng.standard_normal((2, 64)), C[[100, 20]] + 0.001])
+    corpus = IndexCorpus(C)
+    for thr in (0.999, 0.6):
+        ids, ov, lv, cnt = [_np(x) for x in corpus.progressive(Q, 150, thr, 100)]
+        for a in range(len(Q)):
+            rid, rsc, rlv, _ = O.progressive_search(Q[a], C, 150, thr, 100)
+            assert list(ids[a][: cnt[a]]) == list(rid), (thr, a)
+            np.testing.assert_allclose(ov[a][: cnt[a]], rsc, atol=TOL)
+
+
+def test_long_list_sampled_threshold(hq_lib):
+    """A corpus large enough for the 1/16 sample (stride 16): K' < k (24 at k = 108), pools sized from
+    the sample; queries resolved on the scan path and equal to the oracle."""
+    from hq_mi355x.core.search_engine import IndexCorpus
+    rng = np.random.default_rng(25)
+    N = 70000
+    C = rng.standard_normal((N, 64))
+    C[N - 3:] = C[77]
+    Q = np.concatenate([C[[77, 1000, 5000]] + rng.normal(0, 0.02, (3, 64)), rng.standard_normal((2, 64))])
+    corpus = IndexCorpus(C)
+    dense = _dense_counter(corpus)
+    ids, ov, lv, cnt = [_np(x) for x in corpus.progressive(Q, 100, 0.1, 100)]
+    assert sum(dense) == 0, dense
+    for a in range(len(Q)):
+        rid, rsc, rlv, _ = O.progressive_search(Q[a], C, 100, 0.1, 100)
+        assert list(ids[a][: cnt[a]]) == list(rid), a
+        np.testing.assert_allclose(ov[a][: cnt[a]], rsc, atol=TOL)
+
+
+def test_long_list_brute_force_and_frame_scan(hq_lib):
+    """k > 64 on the overall scan (brute_force_search) and the strict level-0 frame scan."""
+    from hq_mi355x.core.search_engine import IndexCorpus
+    C = _corpus(30000, 64, 26)
+    rng = np.random.default_rng(27)
+    Q = np.concatenate([C[[20, 40]] + 0.0, C[900:903] + rng.normal(0, 0.01, (3, 64))])
+    corpus = IndexCorpus(C)
+    bids, bov, blv = [_np(x) for x in corpus.brute_force(Q, 120)]
+    fids, fsc = [_np(x) for x in corpus.frame_search(Q, 300, 0.1)]
+    for a in range(len(Q)):
+        rid, rsc, rlv = O.brute_force_search(Q[a], C, 120)
+        assert list(bids[a]) == list(rid), a
+        np.testing.assert_allclose(bov[a], rsc, atol=TOL)
+        np.testing.assert_allclose(blv[a], rlv, atol=TOL)
+        rid, rsc = O.hierarchical_frame_search(Q[a], C, 300, 0.1)
+        assert list(fids[a][: len(rid)]) == list(rid), a
+        np.testing.assert_allclose(fsc[a][: len(rid)], rsc, atol=TOL)
+
+
+def test_long_list_sharded_merge_equals_single(hq_lib):
+    """R = 3 shards at M = 100: records merged by hq_progressive_final (M > 64 form) == unsharded."""
+    import torch
+    from hq_mi355x.core.search_engine import IndexCorpus
+    from hq_mi355x.distributed import ShardedIndexCorpus, shard_range
+    C = _corpus(12000, 64, 28)
+    C[9000:9004] = C[10]
+    Q = np.concatenate([C[[10, 20, 11999]], C[[5, 6]] + 0.01])
+    ref = [_np(x) for x in IndexCorpus(C).progressive(Q, 100, 0.1, 100)]
+    recs = []
+    for r in range(3):
+        a, b = shard_range(len(C), r, 3)
+        sh = ShardedIndexCorpus(C[a:b], id_base=a, n_total=len(C))
+        recs.append(sh.local_records(sh.local.prepare_queries(Q), 100, 0.1))
+    oid, ov, lv, cnt = ShardedIndexCorpus.merge(torch.stack(recs, 0), 100, 100)
+    assert np.array_equal(_np(oid), ref[0]) and np.array_equal(_np(cnt), ref[3])
+    np.testing.assert_array_equal(_np(ov), ref[1])
+    np.testing.assert_array_equal(_np(lv), ref[2])
+
+
+@pytest.mark.parametrize("k", [65, 100, 600])
+def test_pool_sort_equals_short_select_order(hq_lib, hq_option, k):
+    """k > 64 through k_pool_sort + k_refine_big: every query whose list is proven complete returns exactly
+    the dense exact select's top-k (hq_level_scores + hq_select_topk: score desc, id asc), and at most one
+    query is left unresolved."""
+    from hq_mi355x import kernels as K
+    from hq_mi355x.core.search_engine import IndexCorpus
+    C = _corpus(25000, 64, 29)
+    rng = np.random.default_rng(30)
+    Q = C[300:340] + rng.normal(0, 0.01, (40, 64))
+    corpus = IndexCorpus(C)
+    qp = corpus.prepare_queries(Q)
+    sc, ids, cnt, res = corpus._scan_refine(qp, 0, k, 0.1, 1)
+    dsc, dids, _, _ = K.select_topk(K.level_scores(qp, corpus.prep, 0), k, 0.1, 1)
+    res, ids, dids = _np(res), _np(ids), _np(dids)
+    assert res.sum() >= len(Q) - 1
+    for a in range(len(Q)):
+        if res[a]:
+            assert list(ids[a]) == list(dids[a]), a
+
+
+@pytest.mark.parametrize("f32", [False, True])
+def test_dense_level_scores_lds_equal_per_pair_kernel(hq_lib, hq_option, f32):
+    """The coalesced dense scorer (k_level_scores_lds: candidate segments staged in LDS) is bit-identical
+    to the one-thread-per-pair kernel (option level_scores_v1) at every level, ragged N and Q, float64
+    and float32 index vectors (incl. zero-variance rows); and equal to the reference goldens' values via
+    the oracle on a sample."""
+    from hq_mi355x.core.search_engine import IndexCorpus
+    C = _corpus(3001, 64, 31)
+    rng = np.random.default_rng(32)
+    Q = np.concatenate([C[[1, 2, 20]] + 0.0, C[100:106] + rng.normal(0, 0.01, (6, 64))])
+    if f32:
+        C, Q = C.astype(np.float32), Q.astype(np.float32)
+    corpus = IndexCorpus(C)
+    for lv in range(corpus.nseg):
+        got = _np(corpus.level_scores(Q, lv))
+        hq_option("level_scores_v1", 1)
+        want = _np(corpus.level_scores(Q, lv))
+        hq_option("level_scores_v1", None)
+        assert np.array_equal(got, want), lv
+        for a in (0, 3, 8):
+            np.testing.assert_array_equal(got[a, :500], O.level_similarity(Q[a], C[:500], lv))
