@@ -1769,6 +1769,12 @@ struct QEntry {
   int qi, row;   // query within the wave, first row (absolute, multiple of 4)
   int pad0, pad1;
 };
+// the hi.hi scan's queue entry: no G (the drain recomputes the split G), 8 B per entry
+struct QEntryHI {
+  int qi, row;
+};
+template <bool HI> struct QEntryOf { using type = QEntry; };
+template <> struct QEntryOf<true> { using type = QEntryHI; };
 
 // wave-local ordering of the queue's LDS accesses (one wave's LDS instructions execute in issue order;
 // this keeps the compiler from moving them across each other)
@@ -1778,18 +1784,58 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ half2v h2(const half8 v, int p) {
+  return p == 0 ? __builtin_shufflevector(v, v, 0, 1) : p == 1 ? __builtin_shufflevector(v, v, 2, 3)
+       : p == 2 ? __builtin_shufflevector(v, v, 4, 5) : __builtin_shufflevector(v, v, 6, 7);
+}
+
+// The split G (hi.hi + hi.lo + lo.hi, f32 accumulation: the three-MFMA contraction, another summation order,
+// the same error bound) of query q against rows row0 .. row0 + 3 of the tiled split copies, by v_dot2_f32_f16
+// (products exact in f32).  k_scan0g's drain: its pre-filter contracted hi.hi only.
+__device__ __forceinline__ flt4 split_g4(const _Float16* __restrict__ Zq16, const _Float16* __restrict__ Zc16, int q,
+                                         int64_t row0) {
+  flt4 G = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 1
+  for (int gg = 0; gg < 4; ++gg) {  // one k-group at a time: 10 fragment loads in flight, few live VGPRs
+    const _Float16* pq = Zq16 + z16_frag(q, gg);
+    const half8 qhv = *reinterpret_cast<const half8*>(pq), qlv = *reinterpret_cast<const half8*>(pq + kZ16Lo);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const _Float16* pc = Zc16 + z16_frag(row0 + r, gg);
+      const half8 chv = *reinterpret_cast<const half8*>(pc), clv = *reinterpret_cast<const half8*>(pc + kZ16Lo);
+      float acc = G[r];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        acc = __builtin_amdgcn_fdot2(h2(qhv, p), h2(chv, p), acc, false);
+        acc = __builtin_amdgcn_fdot2(h2(qhv, p), h2(clv, p), acc, false);
+        acc = __builtin_amdgcn_fdot2(h2(qlv, p), h2(chv, p), acc, false);
+      }
+      G[r] = acc;
+    }
+  }
+  return G;
+}
+
 // WPB waves per workgroup: the WPB waves of a block take WPB consecutive query blocks of ONE chunk and
 // read the same candidate fragments step by step (a barrier per unrolled iteration keeps them within
 // a few steps of each other, so WPB - 1 of the WPB reads of a fragment hit the CU's L1)
 // NB 16-query blocks per wave (4: 64 queries; 8: 128 queries, half the corpus fragment loads per MFMA at
 // more VGPRs), processed as NB / 2 parts of two blocks, software-pipelined: part p's MFMAs are issued
 // before part p - 1's pre-filter reads its accumulators
-template <int WPB, int PF, int NB = 4>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 8 ? 3 : 1))) void k_scan0g(Scan0Args a) {
+// HI (default): the pre-filter contracts hi.hi only (one MFMA per 16 x 16 tile instead of three, the corpus
+// lo fragments are not loaded): |G_split - G_hihi| <= sum |hq lc| + |lq hc| + f32 accumulation
+// < 2^-10 (1.002) m + 1e-5 m, so a lane block passes when max G_hihi >= G* - (1e-3 m + 1e-4); the drain then
+// recomputes each queued block's split G (split_g4) for the filter and the pool score.  HI = false: the
+// three-MFMA form (option scan_split3).
+// OCC: waves per SIMD the register allocation targets (HI form: 92 VGPRs at 5, no spills)
+template <int WPB, int PF, int NB = 4, bool HI = true, int OCC = 5>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 8 ? 3 : (HI ? OCC : 1)))) void k_scan0g(Scan0Args a) {
   constexpr int QW = 16 * NB, NP = NB / 2;
-  __shared__ QEntry qe_all[WPB][kQCap];
+  using QE = typename QEntryOf<HI>::type;
+  __shared__ QE qe_all[WPB][kQCap];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
-  QEntry* qe = qe_all[WPB > 1 ? threadIdx.x >> 6 : 0];
+  QE* qe = qe_all[WPB > 1 ? threadIdx.x >> 6 : 0];
   const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
   const int nqg = (a.nqb + WPB - 1) / WPB;
   const int chunk = xcd + 8 * (slot / nqg);
@@ -1803,8 +1849,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
   const float c1f = (float)a.c1;
   const QConst* qc = reinterpret_cast<const QConst*>(a.qconst);
 
-  half8 qh[NB], ql[NB];
+  half8 qh[NB], ql[HI ? 1 : NB];
   float gs[NB];
+  const float dG = HI ? (float)(1e-3 / a.inv_m) + 1e-4f : 0.0f;  // hi.hi pre-filter slack (above)
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int q = q0 + 16 * b + j;
@@ -1813,15 +1860,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
     const _Float16* zr = a.Zq16 + z16_frag(qq, g);
     HQ_GUARD(zr, a.Zq16, z16_rows(a.Q) * 64 - kZ16Lo - 8);
     qh[b] = *reinterpret_cast<const half8*>(zr);
-    ql[b] = *reinterpret_cast<const half8*>(zr + kZ16Lo);
-    gs[b] = v ? qc[q].gs : __builtin_huge_valf();
+    if constexpr (!HI) ql[b] = *reinterpret_cast<const half8*>(zr + kZ16Lo);
+    gs[b] = v ? qc[q].gs - dG : __builtin_huge_valf();
   }
 
   // wave-uniform bases, per-lane constant offsets (scalar step increments)
   const char* zb = reinterpret_cast<const char*>(a.Zc16 + (c_begin >> 4) * kZ16Tile);  // c_begin: a multiple of 16
   const int zoff = lane * 16;  // bytes: the lane's 8 halves of a tile
   struct CStep {
-    half8 f[2];
+    half8 f[HI ? 1 : 2];
   };
 #ifdef HQ_DIAG
   const int64_t smul = (a.expt == 5 || a.expt == 6) ? 0 : kZ16Tile * 2;  // timing experiments: step 0 only
@@ -1832,26 +1879,31 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
     const _Float16* p = reinterpret_cast<const _Float16*>(zb + s * smul + zoff);
     HQ_GUARD(p, a.Zc16, z16_rows(a.N) * 64 - kZ16Lo - 8);
     c.f[0] = *reinterpret_cast<const half8*>(p);
-    c.f[1] = *reinterpret_cast<const half8*>(p + kZ16Lo);
+    if constexpr (!HI) c.f[HI ? 0 : 1] = *reinterpret_cast<const half8*>(p + kZ16Lo);
   };
   auto mfma_part = [&](const int h, const half8* f, flt4* acc) {
     acc[0] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
     acc[1] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[0], qh[2 * h + u], acc[u], 0, 0, 0);
+    if constexpr (!HI) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[0], ql[2 * h + u], acc[u], 0, 0, 0);
+      for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[0], ql[2 * h + u], acc[u], 0, 0, 0);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[1], qh[2 * h + u], acc[u], 0, 0, 0);
+      for (int u = 0; u < 2; ++u)
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[HI ? 0 : 1], qh[2 * h + u], acc[u], 0, 0, 0);
+    }
   };
 
   int qn = 0;  // queue entries (wave-uniform)
   // drain n <= 64 entries from the front of the queue, then shift the rest down
   auto drain = [&](const int n) {
     if (lane < n) {
-      const flt4 eg = qe[lane].g;
       const int eqi = qe[lane].qi, erow = qe[lane].row;
       const int q = q0 + eqi;
+      flt4 eg;
+      if constexpr (HI) eg = split_g4(a.Zq16, a.Zc16, q, erow);
+      else eg = qe[lane].g;
       const QConst c = qc[q];
       const float* st = a.Sc32 + (int64_t)(erow >> 2) * 16;  // the SoA group of rows row .. row + 3
       HQ_GUARD(st, a.Sc32, pack0_rows(a.N) * 4 - 15);
@@ -1895,13 +1947,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
       flt4 tg = {0.0f, 0.0f, 0.0f, 0.0f};
       int tq = 0, tr = 0;
       if (mv) {
-        tg = qe[b0 + lane].g;
+        if constexpr (!HI) tg = qe[b0 + lane].g;
         tq = qe[b0 + lane].qi;
         tr = qe[b0 + lane].row;
       }
       wave_lds_sync();
       if (mv) {
-        qe[b0 - n + lane].g = tg;
+        if constexpr (!HI) qe[b0 - n + lane].g = tg;
         qe[b0 - n + lane].qi = tq;
         qe[b0 - n + lane].row = tr;
       }
@@ -1916,13 +1968,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
     const unsigned lo0 = __builtin_amdgcn_mbcnt_lo((unsigned)m0, 0u), lo1 = __builtin_amdgcn_mbcnt_lo((unsigned)m1, 0u);
     if ((m0 >> lane) & 1ull) {
       const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m0 >> 32), lo0);
-      qe[pos].g = acc[0];
+      if constexpr (!HI) qe[pos].g = acc[0];
       qe[pos].qi = 32 * h + j;
       qe[pos].row = (int)(cs + 4 * g);
     }
     if ((m1 >> lane) & 1ull) {
       const int pos = qn + c0 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m1 >> 32), lo1);
-      qe[pos].g = acc[1];
+      if constexpr (!HI) qe[pos].g = acc[1];
       qe[pos].qi = 32 * h + 16 + j;
       qe[pos].row = (int)(cs + 4 * g);
     }
@@ -4096,6 +4148,9 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     } else {
       const dim3 g1(b.nqb * b.nchunks);
       if (scan_nb == 8) hipLaunchKernelGGL((k_scan0g<1, 2, 8>), g1, dim3(64), 0, s, b);
+      else if (opt_on(OPT_SCAN_SPLIT3)) hipLaunchKernelGGL((k_scan0g<1, 2, 4, false>), g1, dim3(64), 0, s, b);
+      else if (opt(OPT_SCAN_OCC, 5) == 4) hipLaunchKernelGGL((k_scan0g<1, 2, 4, true, 4>), g1, dim3(64), 0, s, b);
+      else if (opt(OPT_SCAN_OCC, 5) == 6) hipLaunchKernelGGL((k_scan0g<1, 2, 4, true, 6>), g1, dim3(64), 0, s, b);
       else if (pf == 4) hipLaunchKernelGGL((k_scan0g<1, 4>), g1, dim3(64), 0, s, b);
       else if (pf == 3) hipLaunchKernelGGL((k_scan0g<1, 3>), g1, dim3(64), 0, s, b);
       else hipLaunchKernelGGL((k_scan0g<1, 2>), g1, dim3(64), 0, s, b);
@@ -4291,13 +4346,17 @@ struct OvLayout {
 
 // compile-time K-block of each G segment, per supported layout id
 template <int LID> struct OvT;
+// seg(kb, k): the G segment holding value k of K-block kb (segments start at multiples of 4, so a dot2 pair
+// never straddles two; padding values are zero in both copies and may be attributed to either side)
 template <> struct OvT<0> {  // L = 64: [32 | 8, 3, 20], one one-value segment
   static constexpr int NKB = 2, NG = 4, NC = 1;
   static constexpr int kb(int i) { return i == 0 ? 0 : 1; }
+  static constexpr int seg(int b, int k) { return b == 0 ? 0 : (k < 8 ? 1 : (k < 12 ? 2 : 3)); }
 };
 template <> struct OvT<1> {  // L = 32: [16, 4, 11], one one-value segment
   static constexpr int NKB = 1, NG = 3, NC = 1;
   static constexpr int kb(int) { return 0; }
+  static constexpr int seg(int, int k) { return k < 16 ? 0 : (k < 20 ? 1 : 2); }
 };
 
 static bool ov_layout(int L, OvLayout& o) {
@@ -4543,6 +4602,37 @@ __device__ __forceinline__ void ov_query_frags(const OvArgs& a, int q, int g, ha
   }
 }
 
+// the split G (hi.hi + hi.lo + lo.hi, f32 accumulation by v_dot2_f32_f16) of every G segment of query q
+// against one row of the overall layout: k_scanov's drain (its pre-filter contracted hi.hi only)
+template <class T>
+__device__ __forceinline__ void ov_split_g(const _Float16* __restrict__ Zq, const _Float16* __restrict__ Zc, int q,
+                                           int64_t row, float* G) {
+  float g0 = 0.0f, g1 = 0.0f, g2 = 0.0f, g3 = 0.0f;
+#pragma unroll 1
+  for (int t = 0; t < 4 * T::NKB; ++t) {  // one k-group (8 values) at a time: few live VGPRs
+    const int kb = t >> 2, gg = t & 3;
+    const _Float16* pq = Zq + ov_frag(q, kb, T::NKB, gg);
+    const _Float16* pc = Zc + ov_frag(row, kb, T::NKB, gg);
+    const half8 qhv = *reinterpret_cast<const half8*>(pq), qlv = *reinterpret_cast<const half8*>(pq + kZ16Lo);
+    const half8 chv = *reinterpret_cast<const half8*>(pc), clv = *reinterpret_cast<const half8*>(pc + kZ16Lo);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float d = __builtin_amdgcn_fdot2(h2(qhv, p), h2(chv, p), 0.0f, false);
+      d = __builtin_amdgcn_fdot2(h2(qhv, p), h2(clv, p), d, false);
+      d = __builtin_amdgcn_fdot2(h2(qlv, p), h2(chv, p), d, false);
+      const int i = T::seg(kb, 8 * gg + 2 * p);  // partial sums of a pair's six products, then per segment
+      g0 += i == 0 ? d : 0.0f;
+      g1 += i == 1 ? d : 0.0f;
+      g2 += i == 2 ? d : 0.0f;
+      g3 += i == 3 ? d : 0.0f;
+    }
+  }
+  G[0] = g0;
+  if (T::NG > 1) G[1] = g1;
+  if (T::NG > 2) G[2] = g2;
+  if (T::NG > 3) G[3] = g3;
+}
+
 // max(x, 0) in one instruction (fmaxf adds a canonicalising v_max of x with itself).  A builtin, not
 // inline asm: the hazard recognizer does not see an asm statement's reads, and a VALU read of an MFMA
 // result needs wait states (an asm v_max right after the MFMA read the stale register).
@@ -4569,12 +4659,15 @@ __device__ __forceinline__ void ov_bound(const flt4* acc, const float* wia, floa
 }
 
 // One wave = 32 queries (two blocks b of 16; lane (g, j) owns queries 16b + j) x one chunk, 16 rows per
-// step (lane group g owns rows 4g + r: the MFMA D layout), NG x 3 MFMAs per block and step.
-template <int LID, int OCC>
+// step (lane group g owns rows 4g + r: the MFMA D layout), NG MFMAs (HI: hi.hi only) or NG x 3 (split) per
+// block and step.  HI: the bound takes G_hihi, each segment's slack |G_split - G_hihi| < 1e-3 m + 1e-4 (as
+// k_scan0g) folded into bsum (relu(G + d) <= relu(G) + d), and the drain recomputes the split G of every
+// queued pair (ov_split_g) for the model score; the queue then holds the (row, query) key only.
+template <int LID, int OCC, bool HI = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_scanov(OvArgs a) {
   using T = OvT<LID>;
   constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, NB = kOvQW / 16, GS = 16 * NG + 4 * NC + 8;
-  __shared__ flt4 qg[kOvQCap];  // queue: G of each G segment ...
+  __shared__ flt4 qg[HI ? 1 : kOvQCap];  // queue: G of each G segment (split form) ...
   __shared__ int qk[kOvQCap];   // ... and (row - c_begin) << 5 | query within the wave
   __shared__ QOvD qs[kOvQW];    // the wave's model constants (the drain reads them per entry)
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
@@ -4601,18 +4694,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
   }
   wave_lds_sync();
 
-  half8 qh[NB][NG], ql[NB][NG];
+  half8 qh[NB][NG], ql[HI ? 1 : NB][NG];
   float wia[NB][NG], bsum[NB], wt[NB], qv[NB][NC > 0 ? NC : 1], tolq[NB][NC > 0 ? NC : 1];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int q = q0 + 16 * b + j;
     const bool v = q < a.Q;
     const int qq = v ? q : 0;
-    ov_query_frags<T>(a, qq, g, qh[b], ql[b]);
+    half8 lo_unused[NG];
+    ov_query_frags<T>(a, qq, g, qh[b], HI ? lo_unused : ql[HI ? 0 : b]);
     const QOv& c = a.qc[qq];
 #pragma unroll
     for (int i = 0; i < NG; ++i) wia[b][i] = c.wia[i];
     bsum[b] = c.bsum;
+    if constexpr (HI) {
+#pragma unroll
+      for (int i = 0; i < NG; ++i) bsum[b] = fmaf(wia[b][i], 1e-3f * (float)o.gplen[i] + 1e-4f, bsum[b]);
+    }
 #pragma unroll
     for (int ci = 0; ci < NC; ++ci) { qv[b][ci] = c.cv[ci]; tolq[b][ci] = c.tolq[ci]; }
     wt[b] = (v && __float_as_int(c.flag) == 0) ? c.wthr : __builtin_huge_valf();  // flagged query: dense path
@@ -4621,7 +4719,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
   const _Float16* zb = a.Zc + (c_begin >> 4) * NKB * kZ16Tile + lane * 8;
   const float* sb = a.Sc32 + (c_begin >> 2) * GS;  // one-value segment values of the step's first group
   struct CStep {
-    half8 f[NKB][2];
+    half8 f[NKB][HI ? 1 : 2];
     flt4 cv[NC > 0 ? NC : 1];
     flt4 ro;
   };
@@ -4632,7 +4730,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
       c.f[kb][0] = *reinterpret_cast<const half8*>(p + kb * kZ16Tile);
-      c.f[kb][1] = *reinterpret_cast<const half8*>(p + kb * kZ16Tile + kZ16Lo);
+      if constexpr (!HI) c.f[kb][HI ? 0 : 1] = *reinterpret_cast<const half8*>(p + kb * kZ16Tile + kZ16Lo);
     }
     const float* sp = sb + (s * 4 + g) * GS;
 #pragma unroll
@@ -4644,13 +4742,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
   // drain the first n <= 64 entries (one per lane): f32 model score, pool append; then shift the rest down
   auto drain = [&](const int n) {
     if (lane < n) {
-      const flt4 eg = qg[lane];
       const int key = qk[lane], eqi = key & 31;
       const int64_t row = c_begin + (key >> 5);
       const int q = q0 + eqi;
       const QOvD& c = qs[eqi];
       if (row < c_end) {
-        const float G[4] = {eg[0], eg[1], eg[2], eg[3]};
+        float G[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if constexpr (HI) {
+          ov_split_g<T>(a.Zq, a.Zc, q, row, G);
+        } else {
+          const flt4 eg = qg[lane];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) G[i] = eg[i];
+        }
         const float s = ov_model<NG, NC>(o, c, a.Sc32, row, G, a.Sq, a.Sc, q);
         if (s >= c.thl) {
           const int slot = atomicAdd(a.pool_n + q, 1);
@@ -4666,9 +4770,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
       const bool mv = b0 + lane < qn;
       flt4 tg = {0.0f, 0.0f, 0.0f, 0.0f};
       int tk = 0;
-      if (mv) { tg = qg[b0 + lane]; tk = qk[b0 + lane]; }
+      if (mv) {
+        if constexpr (!HI) tg = qg[b0 + lane];
+        tk = qk[b0 + lane];
+      }
       wave_lds_sync();
-      if (mv) { qg[b0 - n + lane] = tg; qk[b0 - n + lane] = tk; }
+      if (mv) {
+        if constexpr (!HI) qg[b0 - n + lane] = tg;
+        qk[b0 - n + lane] = tk;
+      }
       wave_lds_sync();
     }
     qn -= n;
@@ -4679,12 +4789,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
 #pragma unroll
     for (int i = 0; i < NG; ++i)
       acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.f[T::kb(i)][0], qh[b][i], flt4{0, 0, 0, 0}, 0, 0, 0);
+    if constexpr (!HI) {
 #pragma unroll
-    for (int i = 0; i < NG; ++i)
-      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.f[T::kb(i)][0], ql[b][i], acc[i], 0, 0, 0);
+      for (int i = 0; i < NG; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.f[T::kb(i)][0], ql[HI ? 0 : b][i], acc[i], 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < NG; ++i)
-      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.f[T::kb(i)][1], qh[b][i], acc[i], 0, 0, 0);
+      for (int i = 0; i < NG; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.f[T::kb(i)][HI ? 0 : 1], qh[b][i], acc[i], 0, 0, 0);
+    }
     float U[4];
     ov_bound<T>(acc, wia[b], bsum[b], o, qv[b], tolq[b], cur.cv, cur.ro, U);
 #pragma unroll
@@ -4693,10 +4805,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
       if (m) {
         if ((m >> lane) & 1ull) {
           const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-          flt4 gg = {0.0f, 0.0f, 0.0f, 0.0f};
+          if constexpr (!HI) {
+            flt4 gg = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-          for (int i = 0; i < NG; ++i) gg[i] = acc[i][r];
-          qg[pos] = gg;
+            for (int i = 0; i < NG; ++i) gg[i] = acc[i][r];
+            qg[pos] = gg;
+          }
           qk[pos] = (int)((cs - c_begin + 4 * g + r) << 5) | (16 * b + j);
         }
         qn += __popcll(m);
@@ -4730,8 +4844,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
 
 // Sample pass of the overall scan (as k_sample_topg): 16 queries per wave, whole sample tiles; per lane
 // the step whose four rows hold the largest pre-filter bound is kept and its rows are scored with the
-// model in the epilogue; the stream's kTopT best go to the pool for k_sample_kth.
-template <int LID>
+// model in the epilogue; the stream's kTopT best go to the pool for k_sample_kth.  HI (default): the step
+// loop contracts hi.hi only (the kept step is a heuristic choice: any choice leaves the sample's scores real
+// scores of distinct pairs) and the epilogue recomputes the kept rows' split G (ov_split_g) for the model.
+template <int LID, bool HI = true>
 __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
   using T = OvT<LID>;
   constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, GS = 16 * NG + 4 * NC + 8;
@@ -4757,7 +4873,7 @@ __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
       f[kb][0] = *reinterpret_cast<const half8*>(p + kb * kZ16Tile);
-      f[kb][1] = *reinterpret_cast<const half8*>(p + kb * kZ16Tile + kZ16Lo);
+      if constexpr (!HI) f[kb][1] = *reinterpret_cast<const half8*>(p + kb * kZ16Tile + kZ16Lo);
     }
     const int64_t r0 = row_of(cs + 4 * g);
     const float* sp = a.Sc32 + (r0 >> 2) * GS;
@@ -4778,10 +4894,12 @@ __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
     flt4 acc[NG];
 #pragma unroll
     for (int i = 0; i < NG; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[T::kb(i)][0], qh[i], flt4{0, 0, 0, 0}, 0, 0, 0);
+    if constexpr (!HI) {
 #pragma unroll
-    for (int i = 0; i < NG; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[T::kb(i)][0], ql[i], acc[i], 0, 0, 0);
+      for (int i = 0; i < NG; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[T::kb(i)][0], ql[i], acc[i], 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < NG; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[T::kb(i)][1], qh[i], acc[i], 0, 0, 0);
+      for (int i = 0; i < NG; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[T::kb(i)][1], qh[i], acc[i], 0, 0, 0);
+    }
     float U[4];
     ov_bound<T>(acc, c.wia, c.bsum, o, c.cv, c.tolq, v0, ro0, U);
     float m = -__builtin_huge_valf();
@@ -4794,7 +4912,10 @@ __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
 #pragma unroll
     for (int i = 0; i < NG; ++i) bg[i] = up ? acc[i] : bg[i];
 #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) { f0[kb][0] = f1[kb][0]; f0[kb][1] = f1[kb][1]; }
+    for (int kb = 0; kb < NKB; ++kb) {
+      f0[kb][0] = f1[kb][0];
+      if constexpr (!HI) f0[kb][1] = f1[kb][1];
+    }
 #pragma unroll
     for (int ci = 0; ci < NC; ++ci) v0[ci] = v1[ci];
     ro0 = ro1;
@@ -4809,8 +4930,12 @@ __global__ __launch_bounds__(64) void k_sampleov(OvArgs a) {
       const int64_t i = (int64_t)bcs + 4 * g + r;
       if (i >= c_end) continue;
       float G[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if constexpr (HI) {
+        ov_split_g<T>(a.Zq, a.Zc, q, row_of(i), G);
+      } else {
 #pragma unroll
-      for (int s = 0; s < NG; ++s) G[s] = bg[s][r];
+        for (int s = 0; s < NG; ++s) G[s] = bg[s][r];
+      }
       float sc = ov_model<NG, NC>(o, c, a.Sc32, row_of(i), G, a.Sq, a.Sc, q);
       if (sc < 0.0f) continue;
 #pragma unroll
@@ -4894,9 +5019,9 @@ struct OvPlan {
 
 static OvPlan ov_plan(int Q, int64_t N, int k) {
   OvPlan p;
-  // one round of waves at the kernel's occupancy (2 waves per SIMD, 185 VGPRs; option ov_occ 3: the
-  // 168-VGPR build with a few spills, measured equal)
-  const int occ = opt(OPT_OV_OCC, 2) == 3 ? 3 : 2;
+  // one round of waves at the kernel's occupancy (the hi.hi form: 4 waves per SIMD, 128 VGPRs; option
+  // ov_occ 2 / 3)
+  const int occ = (int)opt(OPT_OV_OCC, 4) == 2 ? 2 : ((int)opt(OPT_OV_OCC, 4) == 3 ? 3 : 4);
   int w = opt(OPT_OV_WAVES, 0) > 0 ? (int)opt(OPT_OV_WAVES, 0) : 1024 * occ;
   ov_geometry(Q, N, kOvQW, w, 1 << 20, p.nqb, p.nchunks, p.chunk_len);
   while (p.chunk_len > (int64_t(1) << 26)) {  // queue keys hold (row - chunk start) << 5
@@ -4951,7 +5076,8 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
   sa.nchunks = p.s_nchunks;
   sa.chunk_len = p.s_chunk_len;
   sa.top = reinterpret_cast<float*>(ws + p.off_top);
-  hipLaunchKernelGGL(k_sampleov<LID>, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
+  if (opt_on(OPT_SCANOV_SPLIT3)) hipLaunchKernelGGL((k_sampleov<LID, false>), dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
+  else hipLaunchKernelGGL((k_sampleov<LID, true>), dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
   HQ_CHECK_LAUNCH();
   const int mg = Q < 8192 ? Q : 8192;
   launch_kth(mg, s, (const float*)sa.top, 4 * sa.nchunks, Q, sample_kth, (double)kMarginF, th0,
@@ -4966,8 +5092,18 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
   hipLaunchKernelGGL(k_ov_flag_rows, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, s, a.Sc32, a.N, GS,
                      4 * a.o.nc, flag_list, flag_n);
   HQ_CHECK_LAUNCH();
-  if (opt(OPT_OV_OCC, 2) == 3) hipLaunchKernelGGL((k_scanov<LID, 3>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
-  else hipLaunchKernelGGL((k_scanov<LID, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  // default: the hi.hi form at 4 waves per SIMD (option ov_occ 2 / 3); option scanov_split3: the split form
+  const int oocc = (int)opt(OPT_OV_OCC, 4);
+  if (opt_on(OPT_SCANOV_SPLIT3)) {
+    if (oocc == 3) hipLaunchKernelGGL((k_scanov<LID, 3, false>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((k_scanov<LID, 2, false>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  } else if (oocc == 2) {
+    hipLaunchKernelGGL((k_scanov<LID, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  } else if (oocc == 3) {
+    hipLaunchKernelGGL((k_scanov<LID, 3>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((k_scanov<LID, 4>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  }
   HQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_scanov_flagged, dim3(64, (Q + 63) / 64), dim3(64), 0, s, a, si, (const int*)flag_list,
                      (const int*)flag_n);

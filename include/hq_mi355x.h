@@ -54,6 +54,9 @@ const char* hq_last_error(void);
  * e.g. "fused_v" (fused-kernel variant bits), "fused_generic", "chunk_generic", "chunk_exactdiv",
  * "chunk_wpb", "chunk_cpw", "precomp_grid", "precomp_tree_lds", "cos_kernel" (1 register-staged,
  * 2 lockstep), "refine_global", "select_2stage", "level_scores_v1" (the one-thread-per-pair dense scorer),
+ * "scan_split3" (the level-0 scan's pre-filter on the three-MFMA split contraction instead of hi.hi),
+ * "scan_occ" (4 / 5 / 6: the level-0 scan's register target in waves per SIMD), "scanov_split3" (the
+ * overall scan's pre-filter on the split contraction), "ov_occ" (2 / 3 / 4: the overall scan's target),
  * "sample_kth" (0 = provable bound), "scan_v1" (the
  * LDS-tiled level-0 scan), "scan_variant", "scan_wpb" (4 = four waves per level-0 scan block), "scan_pf" (prefetch
  * distance 3 or 4), "sample_variant" (1 = the full-filter sample pass).  Options are process-wide: set them before launching, not
