@@ -384,6 +384,16 @@ __device__ __forceinline__ double thr_low(double thr) {
   return t32 < thr ? t32 : thr;
 }
 
+// Sort keys of all-float32 searches (thr_mode | kThrKey32 on the re-rank, flag 1 of hq_progressive_final_ex):
+// the reference sorts a list mixing numpy float32 scores and Python-float scores (constant branches, clamps;
+// core/search_engine.py:291, :387), and NumPy 2 (NEP 50) compares the two in float32, so float32(0.1) ties a
+// Python 0.1 and the stable sort keeps their pool order.  The Python floats there are the constant-branch
+// values and their weighted means, which float32 rounding keeps distinct, so ranking by the float32-rounded
+// value reproduces Python's order exactly.  A list is then proven complete when float32(last approximate
+// + eps) < float32(k-th exact): an unlisted pair's key is at most the former.
+constexpr int kThrKey32 = 8;
+__device__ __forceinline__ double key_of(double x, bool k32) { return k32 ? (double)(float)x : x; }
+
 // dense Q x N exact scores (drop-in path and rare exact fallbacks)
 template <bool SM = false>
 __global__ __launch_bounds__(256) void k_level_scores(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si, int level,
@@ -2521,7 +2531,10 @@ __global__ __launch_bounds__(64) void k_sample_topf(SampleArgs a) {
 // that step exactly (f32 model) at the end; the stream's kTopT best of those scores go to the pool.  They
 // are real scores of distinct (query, row) pairs, so the K-th best of the union is still a lower bound of
 // the K-th best over the corpus (selecting by G instead of by score only makes it less tight).  Query
-// constants and candidate statistics are read in the epilogue alone.
+// constants and candidate statistics are read in the epilogue alone.  HI (default): the step loop
+// contracts hi.hi only (the kept step is a heuristic choice) and the epilogue recomputes the kept rows'
+// split G (split_g4) for the model score.
+template <bool HI = true>
 __global__ __launch_bounds__(64) void k_sample_topg(SampleArgs a) {
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
   const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
@@ -2538,14 +2551,14 @@ __global__ __launch_bounds__(64) void k_sample_topg(SampleArgs a) {
     const int q = q0 + 16 * b + j;
     const _Float16* zr = a.Zq16 + z16_frag(q < a.Q ? q : 0, g);
     qh[b] = *reinterpret_cast<const half8*>(zr);
-    ql[b] = *reinterpret_cast<const half8*>(zr + kZ16Lo);
+    if constexpr (!HI) ql[b] = *reinterpret_cast<const half8*>(zr + kZ16Lo);
   }
   auto row_of = [&](int64_t i) -> int64_t { return sample_row_tiled(i, a.S, a.stride); };
   auto load_frag = [&](int64_t cs, half8* dst) {
     const _Float16* p = a.Zc16 + z16_frag(row_of(cs + j), g);
     HQ_GUARD(p, a.Zc16, z16_rows(a.N) * 64 - kZ16Lo - 8);
     dst[0] = *reinterpret_cast<const half8*>(p);
-    dst[1] = *reinterpret_cast<const half8*>(p + kZ16Lo);
+    if constexpr (!HI) dst[1] = *reinterpret_cast<const half8*>(p + kZ16Lo);
   };
   float bg[4];     // largest max-of-four G so far
   flt4 bacc[4];    // G of that step's four rows
@@ -2565,10 +2578,12 @@ __global__ __launch_bounds__(64) void k_sample_topg(SampleArgs a) {
     flt4 acc[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[0], qh[b], flt4{0, 0, 0, 0}, 0, 0, 0);
+    if constexpr (!HI) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[0], ql[b], acc[b], 0, 0, 0);
+      for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[0], ql[b], acc[b], 0, 0, 0);
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[1], qh[b], acc[b], 0, 0, 0);
+      for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cf[1], qh[b], acc[b], 0, 0, 0);
+    }
     if (cs + kCS > c_end) {  // the chunk's last, partial step: rows past c_end never win
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -2585,9 +2600,11 @@ __global__ __launch_bounds__(64) void k_sample_topg(SampleArgs a) {
       bcs[b] = up ? (int)cs : bcs[b];
     }
     cf[0] = cf1[0];
-    cf[1] = cf1[1];
     cf1[0] = cfn[0];
-    cf1[1] = cfn[1];
+    if constexpr (!HI) {
+      cf[1] = cf1[1];
+      cf1[1] = cfn[1];
+    }
   }
   // epilogue: exact f32 model scores of the selected rows, the stream's kTopT best to the pool
   const float c1f = (float)a.c1;
@@ -2603,6 +2620,8 @@ __global__ __launch_bounds__(64) void k_sample_topg(SampleArgs a) {
 #pragma unroll
     for (int t = 0; t < kTopT; ++t) top[t] = -1.0f;
     if (qok && bcs[b] >= 0) {
+      flt4 Gs = bacc[b];
+      if constexpr (HI) Gs = split_g4(a.Zq16, a.Zc16, q, row_of((int64_t)bcs[b] + 4 * g));  // 4 consecutive rows
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t i = (int64_t)bcs[b] + 4 * g + r;
@@ -2611,7 +2630,7 @@ __global__ __launch_bounds__(64) void k_sample_topg(SampleArgs a) {
         const float* st = a.Sc32 + (row >> 2) * 16 + (row & 3);
         HQ_GUARD(st, a.Sc32, pack0_rows(a.N) * 4 - 13);
         if (__float_as_int(st[12]) != 0) continue;  // flagged / pad row
-        const float G = bacc[b][r];
+        const float G = Gs[r];
         const float num = fmaf(G, qA * st[0], qB * st[4]);
         float t = num * __builtin_amdgcn_rcpf(qQ + st[8]);
         t = t > 0.0f ? t : 0.0f;
@@ -2793,7 +2812,7 @@ __device__ __forceinline__ bool wave_better(double s, int64_t id, double s2, int
 // the first arg-max of the level-0 score (sel[0] = r << 16, *fb_id = its id).  Returns the count.
 __device__ int final_survivors(int R, int Q, int M, int q, const double* __restrict__ s0,
                                const int64_t* __restrict__ ids, const double* __restrict__ best,
-                               const int64_t* __restrict__ best_id, int* sel, int64_t* fb_id) {
+                               const int64_t* __restrict__ best_id, int* sel, int64_t* fb_id, bool k32) {
   const int lane = threadIdx.x & 63;
   // ---- R-way merge: lane r < R follows list r's head ----
   int h = 0;
@@ -2805,7 +2824,7 @@ __device__ int final_survivors(int R, int Q, int M, int q, const double* __restr
     if (lane < R && h < M) {
       const int64_t o = ((int64_t)lane * Q + q) * M + h;
       hid = ids[o];
-      if (hid >= 0) hs = s0[o];
+      if (hid >= 0) hs = key_of(s0[o], k32);
     }
   };
   load_head();
@@ -2847,7 +2866,7 @@ __device__ int final_survivors(int R, int Q, int M, int q, const double* __restr
     int bl = lane;
     if (lane < R) {
       bid = best_id[(int64_t)lane * Q + q];
-      if (bid >= 0) bs = best[(int64_t)lane * Q + q];
+      if (bid >= 0) bs = key_of(best[(int64_t)lane * Q + q], k32);
     }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -2872,12 +2891,13 @@ __global__ __launch_bounds__(64) void k_progressive_final(int R, int Q, int M, i
                                                           const int64_t* __restrict__ best_id,
                                                           const double* __restrict__ best_det, int K,
                                                           int64_t* __restrict__ out_id, double* __restrict__ out_det,
-                                                          int* __restrict__ out_count) {
+                                                          int* __restrict__ out_count, int flags) {
   __shared__ int sel[kMaxFinal];  // survivor i -> (list r << 16) | slot
   const int lane = threadIdx.x;
+  const bool k32 = (flags & 1) != 0;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
     int64_t fb_id;
-    const int n = final_survivors(R, Q, M, q, s0, ids, best, best_id, sel, &fb_id);
+    const int n = final_survivors(R, Q, M, q, s0, ids, best, best_id, sel, &fb_id, k32);
     __syncthreads();
     const double* rowbase = fb_id >= 0 ? best_det : det;
     // ---- stable sort of the survivors by overall score ----
@@ -2890,10 +2910,10 @@ __global__ __launch_bounds__(64) void k_progressive_final(int R, int Q, int M, i
     // stable rank of survivor i: ranks from register copies of the overall scores (n <= 64 here:
     // M <= 64 on the fused path; larger n re-reads the rows)
     double ovl = -__builtin_huge_val();
-    if (lane < n) ovl = rowbase[row_of(sel[lane]) * W];
+    if (lane < n) ovl = key_of(rowbase[row_of(sel[lane]) * W], k32);
     for (int i = lane; i < n; i += 64) {
       const int64_t oi = row_of(sel[i]);
-      const double ovi = rowbase[oi * W];
+      const double ovi = key_of(rowbase[oi * W], k32);
       int rank = 0;
       if (n <= 64) {
         for (int jj = 0; jj < n; ++jj) {
@@ -2902,7 +2922,7 @@ __global__ __launch_bounds__(64) void k_progressive_final(int R, int Q, int M, i
         }
       } else {
         for (int jj = 0; jj < n; ++jj) {
-          const double ovj = rowbase[row_of(sel[jj]) * W];
+          const double ovj = key_of(rowbase[row_of(sel[jj]) * W], k32);
           rank += (ovj > ovi || (ovj == ovi && jj < i)) ? 1 : 0;
         }
       }
@@ -3173,6 +3193,8 @@ __global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int6
   __shared__ double es[kMaxTopK];
   __shared__ int64_t ei[kMaxTopK];
   const int lane = threadIdx.x;
+  const bool k32 = (thr_mode & kThrKey32) != 0;
+  thr_mode &= kThrKey32 - 1;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
     const int64_t base = (int64_t)q * kp;
     if (lane < kp) {
@@ -3194,14 +3216,15 @@ __global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int6
     __syncthreads();
     // rank of each valid entry by (score desc, id asc) among the valid ones (kp <= 64: one lane each)
     const double e = lane < kp ? es[lane] : -__builtin_huge_val();
+    const double ek = key_of(e, k32);
     const int64_t id = lane < kp ? ei[lane] : -1;
     const bool valid = id >= 0;
     const int n = __popcll(__ballot(valid));
     int rank = 0;
     for (int o = 0; o < kp; ++o) {
-      const double so = rl_f64(e, o);
+      const double so = rl_f64(ek, o);
       const long long io = __double_as_longlong(rl_f64(__longlong_as_double((long long)id), o));
-      rank += (io >= 0 && (so > e || (so == e && io < id))) ? 1 : 0;
+      rank += (io >= 0 && (so > ek || (so == ek && io < id))) ? 1 : 0;
     }
     const int cnt = n < k ? n : k;
     if (valid && rank < k) {
@@ -3223,7 +3246,7 @@ __global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int6
       int res = trunc ? 0 : 1;
       if (full) {
         const double bound = cs[base + kp - 1] + eps;
-        if (n >= k) res = bound < kth;
+        if (n >= k) res = k32 ? (float)bound < (float)kth : bound < kth;
         else if (thr_mode == 0) res = 0;
         else res = thr_mode == 1 ? (bound < thr_low(thr)) : (bound <= thr_low(thr));
       }
@@ -3313,6 +3336,8 @@ __device__ __forceinline__ void refine_lds_body(HQ_REFINE_ARGS) {
   double* lvs = rows + (int64_t)kp * RW;      // kp x W: overall, levels
   const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)sm;
   const int nlev = (mode == 0 && !odet) ? 1 : si.nseg;
+  const bool k32 = (thr_mode & kThrKey32) != 0;
+  thr_mode &= kThrKey32 - 1;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
     const int64_t base = (int64_t)q * kp;
     if (tid < nr) {
@@ -3374,11 +3399,12 @@ __device__ __forceinline__ void refine_lds_body(HQ_REFINE_ARGS) {
       }
       const bool valid = id >= 0;
       const int n = __popcll(__ballot(valid));
+      const double ek = key_of(e, k32);
       int rank = 0;
       for (int o = 0; o < kp; ++o) {
-        const double so = rl_f64(e, o);
+        const double so = rl_f64(ek, o);
         const long long io = __double_as_longlong(rl_f64(__longlong_as_double((long long)id), o));
-        rank += (io >= 0 && (so > e || (so == e && io < id))) ? 1 : 0;
+        rank += (io >= 0 && (so > ek || (so == ek && io < id))) ? 1 : 0;
       }
       const int cnt = n < k ? n : k;
       if (valid && rank < k) {
@@ -3403,7 +3429,7 @@ __device__ __forceinline__ void refine_lds_body(HQ_REFINE_ARGS) {
         int res = trunc ? 0 : 1;
         if (full) {
           const double bound = cs[base + kp - 1] + eps;
-          if (n >= k) res = bound < kth;
+          if (n >= k) res = k32 ? (float)bound < (float)kth : bound < kth;
           else if (thr_mode == 0) res = 0;
           else res = thr_mode == 1 ? (bound < thr_low(thr)) : (bound <= thr_low(thr));
         }
@@ -3580,6 +3606,8 @@ __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
   const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)sm;
   const int nlev1 = mode == 0 ? 1 : si.nseg;
   const int n2 = pow2_at_least(kp);
+  const bool k32 = (thr_mode & kThrKey32) != 0;
+  thr_mode &= kThrKey32 - 1;
   // stage the rows srow[0 .. nt) (and the query with the first tile), score levels [0, nlev) of each
   auto stage_score = [&](int nt, int nlev, bool with_query, int64_t qrow) {
     if (with_query && wave == 0) {
@@ -3653,7 +3681,8 @@ __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
                 [&](int a, int b) {
                   const int64_t ia = sid[a], ib = sid[b];
                   if (ib < 0) return ia >= 0;
-                  return ia >= 0 && (se[a] > se[b] || (se[a] == se[b] && ia < ib));
+                  const double ka = key_of(se[a], k32), kb = key_of(se[b], k32);
+                  return ia >= 0 && (ka > kb || (ka == kb && ia < ib));
                 },
                 [&](int a, int b) {
                   const double te = se[a];
@@ -3679,7 +3708,7 @@ __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
       int res = trunc ? 0 : 1;
       if (full) {
         const double bound = cs[base + kp - 1] + eps;
-        if (n >= k) res = bound < kth;
+        if (n >= k) res = k32 ? (float)bound < (float)kth : bound < kth;
         else if (thr_mode == 0) res = 0;
         else res = thr_mode == 1 ? (bound < thr_low(thr)) : (bound <= thr_low(thr));
       }
@@ -3717,17 +3746,18 @@ __global__ __launch_bounds__(256) void k_progressive_final_big(int R, int Q, int
                                                                const double* __restrict__ best_det, int K,
                                                                int64_t* __restrict__ out_id,
                                                                double* __restrict__ out_det,
-                                                               int* __restrict__ out_count) {
+                                                               int* __restrict__ out_count, int flags) {
   __shared__ int sel[kMaxTopKBig];
   __shared__ double ovs[kMaxTopKBig];
   __shared__ int pos[kMaxTopKBig];
   __shared__ int sn;
   __shared__ int64_t sfb;
   const int tid = threadIdx.x;
+  const bool k32 = (flags & 1) != 0;
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
     if (tid < 64) {
       int64_t fb;
-      const int n = final_survivors(R, Q, M, q, s0, ids, best, best_id, sel, &fb);
+      const int n = final_survivors(R, Q, M, q, s0, ids, best, best_id, sel, &fb, k32);
       if (tid == 0) {
         sn = n;
         sfb = fb;
@@ -3743,7 +3773,7 @@ __global__ __launch_bounds__(256) void k_progressive_final_big(int R, int Q, int
     };
     const int n2 = pow2_at_least(n);
     for (int i = tid; i < n2; i += 256) {
-      ovs[i] = i < n ? rowbase[row_of(sel[i]) * W] : -__builtin_huge_val();
+      ovs[i] = i < n ? key_of(rowbase[row_of(sel[i]) * W], k32) : -__builtin_huge_val();
       pos[i] = i;
     }
     __syncthreads();
@@ -4092,8 +4122,10 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     // option sample_variant 1: the full-filter sample pass (k_sample_topf)
     if (opt(OPT_SAMPLE_VARIANT, 0) == 1)
       hipLaunchKernelGGL(k_sample_topf, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
+    else if (opt_on(OPT_SCAN_SPLIT3))
+      hipLaunchKernelGGL(k_sample_topg<false>, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
     else
-      hipLaunchKernelGGL(k_sample_topg, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
+      hipLaunchKernelGGL(k_sample_topg<true>, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
     HQ_CHECK_LAUNCH();
     const int mg = Q < 8192 ? Q : 8192;
     launch_kth(mg, s, (const float*)top, 4 * sa.nchunks, Q, sample_kth, (double)kMarginF, th0, b.gtau, b.pool_n, Sq32,
@@ -5426,6 +5458,13 @@ int hq_rescore(const double* Rq, const double* Zq, const double* Sq, int Q, cons
 int hq_progressive_final(int R, int Q, int M, int nseg, const double* s0, const int64_t* ids, const double* det,
                          const double* best, const int64_t* best_id, const double* best_det, int K,
                          int64_t* out_id, double* out_det, int* out_count, hq_stream_t stream) {
+  return hq_progressive_final_ex(R, Q, M, nseg, s0, ids, det, best, best_id, best_det, K, out_id, out_det, out_count,
+                                 0, stream);
+}
+
+int hq_progressive_final_ex(int R, int Q, int M, int nseg, const double* s0, const int64_t* ids, const double* det,
+                            const double* best, const int64_t* best_id, const double* best_det, int K,
+                            int64_t* out_id, double* out_det, int* out_count, int flags, hq_stream_t stream) {
   if (R <= 0 || R > 16 || Q < 0 || M <= 0 || M > kMaxTopKBig || K <= 0 || nseg < 0 || nseg >= kMaxSeg)
     return fail(HQ_E_INVALID, "bad sizes R=%d Q=%d M=%d K=%d", R, Q, M, K);
   if (Q == 0) return HQ_OK;
@@ -5435,10 +5474,10 @@ int hq_progressive_final(int R, int Q, int M, int nseg, const double* s0, const 
   const int grid = Q < 8192 ? Q : 8192;
   if (M <= kMaxTopK)
     hipLaunchKernelGGL(k_progressive_final, dim3(grid), dim3(64), 0, (hipStream_t)stream, R, Q, M, W, s0, ids, det,
-                       best, best_id, best_det, K, out_id, out_det, out_count);
+                       best, best_id, best_det, K, out_id, out_det, out_count, flags);
   else
     hipLaunchKernelGGL(k_progressive_final_big, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, Q, M, W, s0, ids,
-                       det, best, best_id, best_det, K, out_id, out_det, out_count);
+                       det, best, best_id, best_det, K, out_id, out_det, out_count, flags);
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }

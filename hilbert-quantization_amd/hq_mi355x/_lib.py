@@ -88,6 +88,7 @@ SIGNATURES = {
     "hq_scan_topk": (_i, [_p, _p, _i, _p, _p, _i64, _i, _i, _i, _d, _i, _i64, _p, _sz, _p, _p, _p, _p, _p]),
     "hq_rescore": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _p, _i, _i64, _p, _p]),
     "hq_progressive_final": (_i, [_i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
+    "hq_progressive_final_ex": (_i, [_i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _i, _p]),
     "hq_cosine_scores": (_i, [_p, _i, _p, _i64, _i, _p, _p]),
     "hq_select_topk": (_i, [_p, _i, _i64, _i, _d, _i, _i64, _p, _p, _p, _p, _p]),
     "hq_select_workspace_size": (_sz, [_i, _i64, _i]),

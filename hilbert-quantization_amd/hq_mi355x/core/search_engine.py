@@ -164,6 +164,11 @@ class IndexCorpus:
             return MAX_SPLIT_K
         return MAX_FUSED_K
 
+    def key32(self, qp) -> bool:
+        """Every vector float32 (query batch and corpus): the reference's sorts then compare numpy float32
+        and Python-float scores in float32 (NEP 50), so rankings use float32-rounded keys (K.THR_KEY32)."""
+        return bool(self.prep.all32 and qp.all32)
+
     def _forced(self, qp):
         """Device bool [Q] of queries that must take the dense exact path (float32 outside the model)."""
         t = torch()
@@ -182,10 +187,13 @@ class IndexCorpus:
         outs = []
         chunk = max(1, (1 << 27) // max(1, self.N))  # <= 1 GiB of scores per launch
         typed = (mode == 0 and thr_mode != 0 and float(np.float32(thr)) != float(thr) and sub.f32 and self.prep.f32)
+        key32 = self.key32(sub)
         for i in range(0, sub.N, chunk):
             part = sub.rows(torch().arange(i, min(sub.N, i + chunk), device=sel.device))
             sc = K.level_scores(part, self.prep, 0 if mode == 0 else -1)
-            if typed:
+            if key32:
+                outs.append(self._select_key32(sc, k, float(thr), thr_mode))
+            elif typed:
                 outs.append(self._select_typed(part, sc, k, float(thr), thr_mode))
             else:
                 outs.append(K.select_topk(sc, k, thr, thr_mode, self.id_base))
@@ -215,6 +223,27 @@ class IndexCorpus:
         pick_b = (bb > ba) | ((bb == ba) & (bib < bia))
         return s, i, t.where(pick_b, bb, ba), t.where(pick_b, bib, bia)
 
+    def _select_key32(self, sc, k: int, thr: float, thr_mode: int):
+        """select_topk for all-float32 searches: the threshold test typed per value (a numpy float32 score
+        against float32(thr), a Python-float one - 0, 0.1, 1 - against thr), the order by float32-rounded
+        keys (score desc, id asc), the first arg-max by key; the scores returned are the exact values."""
+        t = torch()
+        sk = sc.to(t.float32).to(t.float64)
+        ninf = t.full_like(sk, -float("inf"))
+        ok = None
+        if thr_mode:
+            py = (sc == 0.0) | (sc == 0.1) | (sc == 1.0)
+            tt = t.where(py, t.full_like(sc, thr), t.full_like(sc, float(np.float32(thr))))
+            ok = (sc >= tt) if thr_mode == 1 else (sc > tt)
+        _, oi, _, _ = K.select_topk(sk if ok is None else t.where(ok, sk, ninf), k, 0.0, 0, 0)
+        valid = oi >= 0
+        if ok is not None:
+            valid = valid & ok.gather(1, oi.clamp(min=0))
+        os_ = t.where(valid, sc.gather(1, oi.clamp(min=0)), t.full_like(oi, 0, dtype=sc.dtype) - float("inf"))
+        oi = t.where(valid, oi + self.id_base, t.full_like(oi, -1))
+        bi = t.argmax(sk, dim=1)  # the first maximal key
+        return os_, oi, sc.gather(1, bi.view(-1, 1)).view(-1), bi + self.id_base
+
     def exact_topk(self, qp, mode: int, k: int, thr: float = 0.0, thr_mode: int = 0, need_best: bool = False):
         """Exact per-query top-k (score desc, id asc) among candidates passing the threshold test;
         with need_best, also the exact first arg-max for queries where nothing passed.
@@ -231,7 +260,8 @@ class IndexCorpus:
             return sc, ids, cnt, b, bi
         lo_mode = 0 if thr_mode == 0 else 1
         asc, aid, _, _ = K.scan_topk(qp, self.prep, mode, kp, thr - self.EPS, lo_mode, self.id_base)
-        sc, ids, cnt, res = K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, thr_mode, self.EPS, self.id_base)
+        tm = thr_mode | (K.THR_KEY32 if self.key32(qp) else 0)
+        sc, ids, cnt, res = K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, tm, self.EPS, self.id_base)
         redo = (res == 0)
         if need_best:
             redo = redo | (cnt == 0)
@@ -360,7 +390,8 @@ class IndexCorpus:
         lo_mode = 0 if thr_mode == 0 else 1
         asc, aid, _, _ = K.scan_topk(qp, self.prep, mode, k + self.SLACK, thr - self.EPS, lo_mode, self.id_base)
         fn = K.refine_rescore_topk if det else K.refine_topk
-        return fn(qp, self.prep, mode, asc, aid, k, thr, thr_mode, self.EPS, self.id_base, redo=nredo,
+        tm = thr_mode | (K.THR_KEY32 if self.key32(qp) else 0)
+        return fn(qp, self.prep, mode, asc, aid, k, thr, tm, self.EPS, self.id_base, redo=nredo,
                   count_empty=True)
 
     def _final(self, qp, s0, ids, best, bid, K_out: int, bdet=None, det=None):
@@ -371,7 +402,8 @@ class IndexCorpus:
         if bdet is None:
             bdet = K.rescore(qp, self.prep, bid.view(Q, 1), self.id_base).view(Q, -1)
         return K.progressive_final(s0.unsqueeze(0), ids.unsqueeze(0), det.unsqueeze(0),
-                                   best.unsqueeze(0), bid.unsqueeze(0), bdet.unsqueeze(0), K_out)
+                                   best.unsqueeze(0), bid.unsqueeze(0), bdet.unsqueeze(0), K_out,
+                                   key32=self.key32(qp))
 
     def frame_search(self, queries, max_results: int, threshold: float = 0.1):
         """core/video_search.py:215-264: level-0 sim > threshold (strict), stable sort, top-k."""

@@ -112,11 +112,12 @@ class ShardedIndexCorpus:
         return t.cat([pack(s0_, ids_, det), pack(best_.view(-1, 1), bid_.view(-1, 1), bdet)], dim=1)
 
     @staticmethod
-    def merge(g, M: int, max_results: int):
-        """Merge gathered records [R, Q, M + 1, 2 + W] exactly as the single-GPU ranking."""
+    def merge(g, M: int, max_results: int, key32: bool = False):
+        """Merge gathered records [R, Q, M + 1, 2 + W] exactly as the single-GPU ranking (key32: every
+        vector float32, IndexCorpus.key32)."""
         gs, gi, gd = unpack(g[:, :, :M])
         bs, bi, bd = unpack(g[:, :, M])
-        oid, odet, cnt = K.progressive_final(gs, gi, gd, bs, bi, bd, int(max_results))
+        oid, odet, cnt = K.progressive_final(gs, gi, gd, bs, bi, bd, int(max_results), key32=key32)
         return oid, odet[..., 0], odet[..., 1:], cnt
 
     def progressive(self, queries, max_results: int, threshold: float = 0.1, max_candidates_per_level: int = 100):
@@ -140,15 +141,15 @@ class ShardedIndexCorpus:
             det = K.rescore(qp, c.prep, ids, c.id_base)
             bdet = K.rescore(qp, c.prep, bid.view(Q, 1), c.id_base)
             rec = t.cat([pack(s0, ids, det), pack(best.view(Q, 1), bid.view(Q, 1), bdet)], dim=1)
-            return ["rec", rec, M, max_results]
-        return ["pending", self._local_submit(qp, M, threshold), M, max_results]
+            return ["rec", rec, M, max_results, c.key32(qp)]
+        return ["pending", self._local_submit(qp, M, threshold), M, max_results, c.key32(qp)]
 
     def progressive_finish(self, p):
         """Gather and merge a submitted batch (once: the handle then holds the results)."""
         if p[0] == "done":
             return p[1]
         rec = p[1] if p[0] == "rec" else self._local_finish(p[1])
-        out = self.merge(all_gather(rec, self.group, self.comm), p[2], p[3])
+        out = self.merge(all_gather(rec, self.group, self.comm), p[2], p[3], p[4])
         p[:] = ["done", out]
         return out
 
@@ -168,7 +169,7 @@ class ShardedIndexCorpus:
         none_i = t.full((R, Q), -1, dtype=t.int64, device=g.device)
         none_d = t.zeros((R, Q, gd.shape[-1]), dtype=t.float64, device=g.device)
         # lists are sorted by overall (score desc, id asc); the final stable sort by overall keeps it
-        oid, odet, cnt = K.progressive_final(gs, gi, gd, none_s, none_i, none_d, k)
+        oid, odet, cnt = K.progressive_final(gs, gi, gd, none_s, none_i, none_d, k, key32=c.key32(qp))
         return oid, odet[..., 0], odet[..., 1:], cnt
 
     def frame_search(self, queries, max_results: int, threshold: float = 0.1):
@@ -185,5 +186,5 @@ class ShardedIndexCorpus:
         none_s = t.full((R, Q), -float("inf"), dtype=t.float64, device=g.device)
         none_i = t.full((R, Q), -1, dtype=t.int64, device=g.device)
         none_d = t.zeros((R, Q, 1), dtype=t.float64, device=g.device)
-        oid, odet, cnt = K.progressive_final(gs, gi, gd, none_s, none_i, none_d, k)
+        oid, odet, cnt = K.progressive_final(gs, gi, gd, none_s, none_i, none_d, k, key32=c.key32(qp))
         return oid, odet[..., 0], cnt

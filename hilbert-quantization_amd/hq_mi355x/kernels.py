@@ -451,9 +451,13 @@ def rescore(q: Prepared, c: Prepared, ids, id_base: int = 0, exc=None):
     return out
 
 
-def progressive_final(s0, ids, det, best, best_id, best_det, K: int, exc=None):
+THR_KEY32 = 8  # thr_mode bit of the re-rank: float32 sort keys (hq_mi355x.h HQ_THR_KEY32)
+
+
+def progressive_final(s0, ids, det, best, best_id, best_det, K: int, exc=None, key32: bool = False):
     """R-way final stage of progressive search.  s0/ids [R, Q, M], det [R, Q, M, W], best/best_id
-    [R, Q], best_det [R, Q, W].  Returns (out_id [Q, K], out_det [Q, K, W], count [Q])."""
+    [R, Q], best_det [R, Q, W].  Returns (out_id [Q, K], out_det [Q, K, W], count [Q]).  key32: every
+    vector is float32, so scores rank by their float32-rounded values (hq_progressive_final_ex flag 1)."""
     t = torch()
     R, Q, M = ids.shape
     W = det.shape[-1]
@@ -461,9 +465,9 @@ def progressive_final(s0, ids, det, best, best_id, best_det, K: int, exc=None):
     oid = t.empty((Q, K), dtype=t.int64, device=dev)
     odet = t.empty((Q, K, W), dtype=t.float64, device=dev)
     cnt = t.empty(Q, dtype=t.int32, device=dev)
-    _chk(_L().hq_progressive_final(R, Q, M, W - 1, ptr(_contig(s0)), ptr(_contig(ids)), ptr(_contig(det)),
-                                   ptr(_contig(best)), ptr(_contig(best_id)), ptr(_contig(best_det)), K, ptr(oid),
-                                   ptr(odet), ptr(cnt), stream()), exc)
+    _chk(_L().hq_progressive_final_ex(R, Q, M, W - 1, ptr(_contig(s0)), ptr(_contig(ids)), ptr(_contig(det)),
+                                      ptr(_contig(best)), ptr(_contig(best_id)), ptr(_contig(best_det)), K, ptr(oid),
+                                      ptr(odet), ptr(cnt), 1 if key32 else 0, stream()), exc)
     return oid, odet, cnt
 
 

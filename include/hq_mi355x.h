@@ -326,6 +326,15 @@ int hq_progressive_final(int R, int Q, int M, int nseg, const double* s0, const 
                          const double* det, const double* best, const int64_t* best_id,
                          const double* best_det, int K, int64_t* out_id, double* out_det,
                          int* out_count, hq_stream_t stream);
+/* hq_progressive_final with flags: 1 = float32 sort keys (every vector float32: the reference's sort
+ * compares a numpy float32 score with a Python-float one in float32 under NumPy 2 / NEP 50, so the merge
+ * and the stable sort rank by the float32-rounded values; core/search_engine.py:291, :387).  The re-rank
+ * takes the same mode as thr_mode | 8 (HQ_THR_KEY32) on hq_refine_topk / hq_refine_rescore_topk.      */
+#define HQ_THR_KEY32 8
+int hq_progressive_final_ex(int R, int Q, int M, int nseg, const double* s0, const int64_t* ids,
+                            const double* det, const double* best, const int64_t* best_id,
+                            const double* best_det, int K, int64_t* out_id, double* out_det,
+                            int* out_count, int flags, hq_stream_t stream);
 
 /* ---- S5 support: top-k of a dense score matrix (k > 64, e.g. max_candidates_per_level = 100) -----
  * scores f64 Q x N -> out_score/out_id Q x k ordered (score desc, id asc) among candidates passing

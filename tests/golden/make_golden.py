@@ -645,6 +645,99 @@ def api_fixtures(hq):
     return out
 
 
+def _craft_search(score_fn, target_fn, seed, want=1):
+    """Inputs for the float32 / Python-float sort-key goldens: a float32 query q and candidates
+    c(t) = mu + a (q - mean q) + t d along which a float32 score crosses target_fn(q); every float32 t
+    around the crossing is tried until the score equals the target exactly.  The oracle only steers the
+    search; the fixture's outputs are the reference's."""
+    rng = np.random.default_rng(seed)
+    found = []
+    for _ in range(400):
+        mu = rng.uniform(0.6, 1.4)
+        q = (rng.standard_normal(64) + mu).astype(np.float32)
+        d1 = rng.standard_normal(64).astype(np.float32)
+        a = rng.uniform(-1.3, -0.7)
+        base = (mu + a * (q - q.mean())).astype(np.float32)
+        target = target_fn(q)
+        if target is None:
+            continue
+        ts = np.linspace(0, 2, 2001).astype(np.float32)
+        sc = score_fn(q, (base[None, :] + ts[:, None] * d1[None, :]).astype(np.float32))
+        for i in np.nonzero((sc[:-1] - target) * (sc[1:] - target) <= 0)[0][:3]:
+            lo, hi = ts[i].view(np.int32), ts[i + 1].view(np.int32)
+            tt = np.arange(lo, hi + 1, dtype=np.int32).view(np.float32)
+            cc = (base[None, :] + tt[:, None] * d1[None, :]).astype(np.float32)
+            hit = np.nonzero(score_fn(q, cc) == target)[0]
+            if len(hit):
+                found.append((q, cc[hit[0]]))
+                break
+        if len(found) >= want:
+            return found
+    raise RuntimeError("no crafted pair found")
+
+
+def sortkey_fixtures(hq):
+    """Python's mixed-type sort keys (core/search_engine.py:291 and :386, NumPy 2 / NEP 50): a numpy
+    float32 score compares with a Python-float score in float32, so float32(0.1) ties the Python 0.1 of
+    the one-constant-side branch (level-0 filter sort) and an all-constant-branch Python-float overall ties
+    the float32 overall equal to its float32 rounding (final sort); ties keep the pool / survivor order."""
+    import contextlib
+    import io
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import hq_oracle as O
+    from hilbert_quantization.core.search_engine import ProgressiveSimilaritySearchEngine
+    from hilbert_quantization.models import ModelMetadata, QuantizedModel
+    out = {}
+
+    def pool_of(rows):
+        return [QuantizedModel(b"x", (8, 8), 1, 0.8, np.asarray(r, dtype=np.float32),
+                               ModelMetadata(f"m{i}", 1, 1, 1.0, "t")) for i, r in enumerate(rows)]
+
+    def run(tag, q, rows, M, K):
+        eng = ProgressiveSimilaritySearchEngine(similarity_threshold=0.1, max_candidates_per_level=M)
+        pool = pool_of(rows)
+        with contextlib.redirect_stdout(io.StringIO()):
+            r = eng.progressive_search(np.asarray(q, dtype=np.float32), pool, K)
+            b = eng.brute_force_search(np.asarray(q, dtype=np.float32), pool, K)
+        out[f"{tag}_q"] = np.asarray(q, dtype=np.float32)
+        out[f"{tag}_C"] = np.stack(rows).astype(np.float32)
+        out[f"{tag}_M"] = np.array(M)
+        out[f"{tag}_pg_ids"] = np.array([int(x.model.model_id[1:]) for x in r], dtype=np.int64)
+        out[f"{tag}_pg_sc"] = np.array([float(x.similarity_score) for x in r])
+        out[f"{tag}_pg_f32"] = np.array([isinstance(x.similarity_score, np.float32) for x in r])
+        out[f"{tag}_bf_ids"] = np.array([int(x.model.model_id[1:]) for x in b], dtype=np.int64)
+        out[f"{tag}_bf_sc"] = np.array([float(x.similarity_score) for x in b])
+        out[f"{tag}_lv0"] = np.array([float(eng.compare_indices_at_level(q, c, 0)) for c in rows])
+        out[f"{tag}_lv0_f32"] = np.array([isinstance(eng.compare_indices_at_level(q, c, 0), np.float32) for c in rows])
+
+    # (1) level-0 filter: a float32 score exactly float32(0.1) against the Python 0.1 of a constant level-0
+    # segment; M keeps exactly one of the two after the candidates scoring above them
+    t01 = float(np.float32(0.1))
+    [(q, cF)] = _craft_search(lambda q, C: O.level_similarity(q, C, 0), lambda q: t01, 13)
+    rng = np.random.default_rng(31)
+    high = [(q + rng.normal(0, 0.05 * (i + 1), 64)).astype(np.float32) for i in range(6)]
+    cP = rng.standard_normal(64).astype(np.float32)
+    cP[:32] = np.float32(2.5)                     # constant level-0 segment: the reference returns 0.1
+    low = [(-q + rng.normal(0, 0.01, 64)).astype(np.float32) for _ in range(5)]
+    run("lv0_PF", q, high + [cP, cF] + low, 7, 7)   # Python 0.1 first in the pool: it survives (tie)
+    run("lv0_FP", q, high + [cF, cP] + low, 7, 7)   # float32 0.1 first: it survives
+
+    # (2) final sort: an all-constant-branch Python-float overall against the float32 overall equal to its
+    # float32 rounding
+    def p_overall(q):
+        cc = np.full(64, np.float32(q[43] + 0.5), dtype=np.float32)
+        P = O.overall_similarity(q, cc[None])[0][0]
+        return float(np.float32(P)) if float(np.float32(P)) != P else None
+
+    [(q2, cF2)] = _craft_search(lambda q, C: O.overall_similarity(q, C)[0], p_overall, 17)
+    cP2 = np.full(64, np.float32(q2[43] + 0.5), dtype=np.float32)
+    rng = np.random.default_rng(37)
+    other = [(q2 + rng.normal(0, 0.3 * (i + 1), 64)).astype(np.float32) for i in range(4)]
+    run("ov_PF", q2, other[:2] + [cP2, cF2] + other[2:], 20, 6)
+    run("ov_FP", q2, other[:2] + [cF2, cP2] + other[2:], 20, 6)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -655,7 +748,8 @@ def main():
     for name, fn in [("mapper", mapper_fixtures), ("index", index_fixtures), ("quant", quant_fixtures),
                      ("search", search_fixtures), ("search_f32", search_f32_fixtures),
                      ("rag_score", rag_score_fixtures), ("stores", store_fixtures),
-                     ("precomputed", precomputed_fixtures), ("api", api_fixtures)]:
+                     ("precomputed", precomputed_fixtures), ("api", api_fixtures),
+                     ("sortkey", sortkey_fixtures)]:
         if only and name not in only:
             continue
         d = fn(hq)
