@@ -3460,7 +3460,6 @@ __global__ __launch_bounds__(256) void k_refine_lds(HQ_REFINE_ARGS) {
 // ------------------------------------------------------------------------------------------------
 constexpr int kMaxTopKBig = 1024;  // list entries (k + slack) of the long-list path
 constexpr int kSortCap = 4096;     // pool keys sorted whole in LDS (32 KiB); larger pools are cut first
-constexpr int kRefTile = 64;       // candidate rows staged per round of the long-list re-rank
 
 __device__ __forceinline__ int pow2_at_least(int n) {
   int p = 2;
@@ -3585,93 +3584,50 @@ static void launch_pool_select(int K, hipStream_t s, int Q, float* pool_s, int* 
                        out_id, th0, thr0, qflag, qstride, fa, flist, fcount);
 }
 
-// k_refine_lds for kp > 64 (same contract, arithmetic and outputs).  Pass 1 stages the listed candidates'
-// rows in tiles of tb (LDS-DMA), scores the levels the ranking needs (level 0 in mode 0 without odet...
-// every level in mode 1), applies the threshold test and keeps (score, id) per list entry in LDS; the
-// entries are bitonic-sorted by (score desc, id asc).  Pass 2 (odet) re-stages the rows of the ranked
-// output entries and writes their [overall, level..] records with the same exact_level code.
+// k_refine_lds for kp > 64 (same contract, arithmetic and outputs), one 256-thread workgroup per query.
+// Pass 1: each thread scores list entries tid, tid + 256, ... straight from global memory (the level the
+// ranking needs: level 0 in mode 0, the overall in mode 1) — a round's 256 row reads are independent, so
+// they are all in flight — and keeps (score, id) in LDS; a bitonic sort ranks them (score desc, id asc).
+// Pass 2 (odet): one thread per output entry computes its [overall, level..] record (exact_pair writes the
+// levels into the record directly).  The LDS-staged form of round 4's first version (tiles of rows, one
+// level task per thread) spent most of its time in the staging round trips: 111 us at M = 100, 923 us at
+// M = 1000 per 1000-query batch.
 template <bool SM>
 __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  __shared__ int64_t srow[kRefTile];
-  __shared__ int t32s[kRefTile * kMaxSeg];
   __shared__ double se[kMaxTopKBig];
   __shared__ int64_t sid[kMaxTopKBig];
   __shared__ int red[4];
+  (void)tb;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int RW = refine_rw(si), QW = refine_qw(si), W = 1 + si.nseg;
-  double* rq = sm;                          // query row: raw, Z, S
-  double* rows = sm + QW;                   // tb x RW candidate rows: raw, S
-  double* lvs = rows + (int64_t)tb * RW;    // tb x W: overall, levels
-  const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)sm;
-  const int nlev1 = mode == 0 ? 1 : si.nseg;
+  const int W = 1 + si.nseg;
   const int n2 = pow2_at_least(kp);
   const bool k32 = (thr_mode & kThrKey32) != 0;
   thr_mode &= kThrKey32 - 1;
-  // stage the rows srow[0 .. nt) (and the query with the first tile), score levels [0, nlev) of each
-  auto stage_score = [&](int nt, int nlev, bool with_query, int64_t qrow) {
-    if (with_query && wave == 0) {
-      dma_seg(Qs.raw + qrow * si.L, lbase, 8 * si.L, lane);
-      dma_seg(Qs.Z + qrow * si.Lp, lbase + 8u * si.L, 8 * si.Lp, lane);
-      dma_seg(Qs.S + qrow * si.nseg * 4, lbase + 8u * (si.L + si.Lp), 32 * si.nseg, lane);
-    }
-    for (int r = wave; r < nt; r += 4) {
-      const int64_t i = srow[r];
-      if (i < 0) continue;
-      const uint32_t d0 = lbase + 8u * (uint32_t)(QW + r * RW);
-      dma_seg(Cs.raw + i * si.L, d0, 8 * si.L, lane);
-      dma_seg(Cs.S + i * si.nseg * 4, d0 + 8u * si.L, 32 * si.nseg, lane);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int t = tid; t < nlev * nt; t += 256) {
-      const int sg = t / nt, p = t - sg * nt;
-      double v = 0.0;
-      int f32 = 0;
-      if (srow[p] >= 0) {
-        const double* rc = rows + (int64_t)p * RW;
-        v = exact_level<SM>(rq + si.src[sg], rq + si.L + si.poff[sg], rq + si.L + si.Lp + 4 * sg, rc + si.src[sg],
-                            nullptr, rc + si.L + 4 * sg, si.len[sg], &f32);
-      }
-      lvs[(int64_t)p * W + 1 + sg] = v;
-      t32s[p * kMaxSeg + sg] = f32;
-    }
-    __syncthreads();
-  };
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
     const int64_t base = (int64_t)q * kp;
     // ---- pass 1: exact ranking score of every list entry ----
-    for (int t0 = 0; t0 < kp; t0 += tb) {
-      const int nt = kp - t0 < tb ? kp - t0 : tb;
-      if (tid < nt) {
-        const int64_t id = cid[base + t0 + tid];
-        const int64_t c = id - id_base;
-        srow[tid] = (id >= 0 && c >= 0 && c < N) ? c : -1;
-      }
-      __syncthreads();
-      stage_score(nt, nlev1, t0 == 0, q);
-      if (tid < nt) {
-        double e = -__builtin_huge_val();
-        int64_t id = -1;
-        if (srow[tid] >= 0) {
-          const double* lv = lvs + (int64_t)tid * W;
-          e = mode == 0 ? lv[1] : overall_from_levels(lv + 1, t32s + tid * kMaxSeg, si.nseg);
-          const bool pass = mode == 0 ? typed_pass(e, t32s[tid * kMaxSeg], thr, thr_mode)
-                                      : (thr_mode == 0 || (thr_mode == 1 ? e >= thr : e > thr));
-          if (pass) id = cid[base + t0 + tid];
-          else e = -__builtin_huge_val();
-        }
-        se[t0 + tid] = e;
-        sid[t0 + tid] = id;
-      }
-      __syncthreads();
-    }
-    for (int x = kp + tid; x < n2; x += 256) {
-      se[x] = -__builtin_huge_val();
-      sid[x] = -1;
-    }
     int nv = 0;
-    for (int x = tid; x < kp; x += 256) nv += sid[x] >= 0 ? 1 : 0;
+    for (int x = tid; x < n2; x += 256) {
+      double e = -__builtin_huge_val();
+      int64_t id = -1;
+      if (x < kp) {
+        const int64_t cid_x = cid[base + x];
+        const int64_t c = cid_x - id_base;
+        if (cid_x >= 0 && c >= 0 && c < N) {
+          int typed = 0;
+          const double v = exact_pair<SM>(Qs, q, Cs, c, si, mode == 0 ? 0 : -1, nullptr, &typed);
+          const bool pass = mode == 0 ? typed_pass(v, typed, thr, thr_mode)
+                                      : (thr_mode == 0 || (thr_mode == 1 ? v >= thr : v > thr));
+          if (pass) {
+            e = v;
+            id = cid_x;
+            ++nv;
+          }
+        }
+      }
+      se[x] = e;
+      sid[x] = id;
+    }
     nv = wsum64i(nv);
     if (lane == 0) red[wave] = nv;
     __syncthreads();
@@ -3696,8 +3652,15 @@ __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
     for (int x = tid; x < k; x += 256) {
       os[(int64_t)q * k + x] = x < cnt ? se[x] : -__builtin_huge_val();
       oid[(int64_t)q * k + x] = x < cnt ? sid[x] : -1;
-      if (odet && x >= cnt)
-        for (int w = 0; w < W; ++w) odet[((int64_t)q * k + x) * W + w] = 0.0;
+      if (odet) {
+        double* rec = odet + ((int64_t)q * k + x) * W;
+        if (x < cnt) {
+          // ---- pass 2: the output entry's [overall, level..] record ----
+          rec[0] = exact_pair<SM>(Qs, q, Cs, sid[x] - id_base, si, -1, rec + 1);
+        } else {
+          for (int w = 0; w < W; ++w) rec[w] = 0.0;
+        }
+      }
     }
     if (tid == 0) {
       const double kth = n >= k ? se[k - 1] : -__builtin_huge_val();
@@ -3714,19 +3677,6 @@ __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
       }
       ores[q] = res;
       if (oredo && (res == 0 || (count_empty && cnt == 0))) atomicAdd(oredo, 1);
-    }
-    // ---- pass 2: [overall, level..] records of the output entries ----
-    for (int r0 = 0; odet && r0 < cnt; r0 += tb) {
-      const int nt = cnt - r0 < tb ? cnt - r0 : tb;
-      __syncthreads();
-      if (tid < nt) srow[tid] = sid[r0 + tid] - id_base;
-      __syncthreads();
-      stage_score(nt, si.nseg, false, q);
-      if (tid < nt) {
-        double* lv = lvs + (int64_t)tid * W;
-        lv[0] = overall_from_levels(lv + 1, t32s + tid * kMaxSeg, si.nseg);
-        for (int w = 0; w < W; ++w) odet[((int64_t)q * k + r0 + tid) * W + w] = lv[w];
-      }
     }
     __syncthreads();
   }
@@ -4122,10 +4072,10 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     // option sample_variant 1: the full-filter sample pass (k_sample_topf)
     if (opt(OPT_SAMPLE_VARIANT, 0) == 1)
       hipLaunchKernelGGL(k_sample_topf, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
-    else if (opt_on(OPT_SCAN_SPLIT3))
-      hipLaunchKernelGGL(k_sample_topg<false>, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
-    else
+    else if (opt(OPT_SAMPLE_HI, 0) == 1)  // hi.hi step loop + split G epilogue: 58 vs 34 us (the epilogue's loads)
       hipLaunchKernelGGL(k_sample_topg<true>, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
+    else
+      hipLaunchKernelGGL(k_sample_topg<false>, dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
     HQ_CHECK_LAUNCH();
     const int mg = Q < 8192 ? Q : 8192;
     launch_kth(mg, s, (const float*)top, 4 * sa.nchunks, Q, sample_kth, (double)kMarginF, th0, b.gtau, b.pool_n, Sq32,
@@ -4286,23 +4236,15 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
   const int grid = Q < 8192 ? Q : 8192;
   if (out_redo) HQ_CHECK_HIP(hipMemsetAsync(out_redo, 0, sizeof(int), s));
   const bool sm = seg_small(si);
-  if (kp > kMaxTopK) {  // long lists: tiles of tb staged candidate rows (<= 96 KiB of dynamic LDS)
-    if (L % 2) return fail(HQ_E_UNSUPPORTED, "long candidate lists need an even index length (L=%d)", L);
-    const size_t per = ((size_t)refine_rw(si) + (size_t)(1 + si.nseg)) * 8;
-    int tb = (int)((96 * 1024 - (size_t)refine_qw(si) * 8) / per);
-    if (tb > kRefTile) tb = kRefTile;
-    if (tb < 4) return fail(HQ_E_UNSUPPORTED, "index rows too long for the long-list re-rank (L=%d)", L);
-    const size_t lb = (size_t)refine_qw(si) * 8 + (size_t)tb * per;
-    const void* fn = sm ? (const void*)k_refine_big_sm : (const void*)k_refine_big;
-    HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb));
+  if (kp > kMaxTopK) {  // long lists: rows read from global memory, one workgroup per query
     if (sm)
-      hipLaunchKernelGGL(k_refine_big_sm, dim3(grid), dim3(256), lb, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
+      hipLaunchKernelGGL(k_refine_big_sm, dim3(grid), dim3(256), 0, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
                          mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
-                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, tb);
+                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, 0);
     else
-      hipLaunchKernelGGL(k_refine_big, dim3(grid), dim3(256), lb, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
+      hipLaunchKernelGGL(k_refine_big, dim3(grid), dim3(256), 0, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
                          mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
-                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, tb);
+                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, 0);
     HQ_CHECK_LAUNCH();
     return HQ_OK;
   }
@@ -5108,8 +5050,9 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
   sa.nchunks = p.s_nchunks;
   sa.chunk_len = p.s_chunk_len;
   sa.top = reinterpret_cast<float*>(ws + p.off_top);
-  if (opt_on(OPT_SCANOV_SPLIT3)) hipLaunchKernelGGL((k_sampleov<LID, false>), dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
-  else hipLaunchKernelGGL((k_sampleov<LID, true>), dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
+  // the split sample by default: the hi.hi form's epilogue (split G of the kept rows) measured 139 vs 106 us
+  if (opt(OPT_SAMPLE_HI, 0) == 1) hipLaunchKernelGGL((k_sampleov<LID, true>), dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
+  else hipLaunchKernelGGL((k_sampleov<LID, false>), dim3(sa.nqb * sa.nchunks), dim3(64), 0, s, sa);
   HQ_CHECK_LAUNCH();
   const int mg = Q < 8192 ? Q : 8192;
   launch_kth(mg, s, (const float*)sa.top, 4 * sa.nchunks, Q, sample_kth, (double)kMarginF, th0,

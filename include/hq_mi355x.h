@@ -57,6 +57,7 @@ const char* hq_last_error(void);
  * "scan_split3" (the level-0 scan's pre-filter on the three-MFMA split contraction instead of hi.hi),
  * "scan_occ" (4 / 5 / 6: the level-0 scan's register target in waves per SIMD), "scanov_split3" (the
  * overall scan's pre-filter on the split contraction), "ov_occ" (2 / 3 / 4: the overall scan's target),
+ * "sample_hi" (1: the sample passes' step loops on hi.hi with a split-G epilogue),
  * "sample_kth" (0 = provable bound), "scan_v1" (the
  * LDS-tiled level-0 scan), "scan_variant", "scan_wpb" (4 = four waves per level-0 scan block), "scan_pf" (prefetch
  * distance 3 or 4), "sample_variant" (1 = the full-filter sample pass).  Options are process-wide: set them before launching, not

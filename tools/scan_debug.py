@@ -10,6 +10,11 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "hilbert-quantization_amd")]
 import torch  # noqa: E402
 from hq_mi355x import kernels as K  # noqa: E402
 from hq_mi355x.core.search_engine import IndexCorpus  # noqa: E402
+from hq_mi355x import _lib  # noqa: E402
+
+for kv in filter(None, os.environ.get("HQ_DBG_OPTS", "").split(",")):  # kernel variants for A/B passes
+    name, value = kv.split("=")
+    _lib.set_option(name, int(value))
 
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(2)
