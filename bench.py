@@ -545,10 +545,10 @@ def bench_search_strong(args, world, rank, dev):
            "self_match_rate": float((ids[:, 0].cpu() == torch.arange(Qn)).float().mean()),
            "ids_checksum": int((ids_h.astype(np.int64) * (np.arange(ids_h.size).reshape(ids_h.shape) % 7919 + 1)).sum()),
            "data": "8M x 1536-d N(0,1) embeddings (torch seed 4, 1M-row blocks) -> fused map + streaming index (L=64)",
-           "roofline": {"bound": "mfma", "achieved": 3 * 2.0 * Qn * (b - a) * 32 / kern / 1e12,
+           "roofline": {"bound": "mfma", "achieved": 2.0 * Qn * (b - a) * 32 / kern / 1e12,
                         "peak": FP16_MATRIX_PEAK_TFS, "unit": "TFLOP/s",
-                        "frac": 3 * 2.0 * Qn * (b - a) * 32 / kern / 1e12 / FP16_MATRIX_PEAK_TFS,
-                        "note": "this rank's split-f16 level-0 contraction flops per step / step time"}}
+                        "frac": 2.0 * Qn * (b - a) * 32 / kern / 1e12 / FP16_MATRIX_PEAK_TFS,
+                        "note": "this rank's level-0 contraction flops (one f16 pass, 2*Q*N*32) per step / step time"}}
     if comm is not None:
         x = torch.zeros((Qn, 21, 3 + engine.local.nseg), dtype=torch.float64, device=dev)
         _, ak = timed(lambda: comm.all_gather(x), 20, 3, world)
@@ -662,19 +662,23 @@ def main():
         swall, skern = timed(run, args.search_steps, 1, world, drain)
         qps = Qn * args.search_steps / swall
         pairs = Qn * Nc  # level-0 pairs scored per rank per step
-        flops = 3 * 2.0 * pairs * 32  # split-f16 contraction: hi.hi + hi.lo + lo.hi per pair, K = 32
+        # the level-0 contraction once per pair (2 * 32 flops): the scan executes one f16 MFMA pass (hi.hi; the
+        # split hi.lo + lo.hi terms only for the pre-filter's survivors, on the VALU), so the peak is the dense
+        # f16 MFMA peak; rounds 1-3 counted the three split passes against it ("frac_split_accounting")
+        flops = 2.0 * pairs * 32
         ids, ov, _, cnt = engine.progressive(queries, 10, 0.1, 20)
         rec["search"] = {
             "metric": "queries/sec@top-10 over 1M corpus", "value": qps, "unit": "queries/sec",
             "corpus_per_gpu": Nc, "corpus_total": Nc * world, "queries": Qn, "steps": args.search_steps,
             "ms_per_step": swall / args.search_steps * 1e3, "index_prepare_s": prep_s,
-            "mode": "progressive (level-0 split-f16 MFMA scan top-28 >= 0.1 - eps, exact re-rank to top-20, "
-                    f"overall re-score, top-10); up to {depth} batches in flight (submit / finish)",
+            "mode": "progressive (level-0 scan: hi.hi f16 MFMA pre-filter, split G of the survivors, top-28 >= 0.1 - "
+                    f"eps; exact re-rank to top-20, overall re-score, top-10); up to {depth} batches in flight",
             "roofline": {"bound": "mfma", "achieved": flops / skern / 1e12, "peak": FP16_MATRIX_PEAK_TFS,
                          "unit": "TFLOP/s", "frac": flops / skern / 1e12 / FP16_MATRIX_PEAK_TFS,
-                         "note": "3 x 2*Q*N*32 f16 MFMA flops of the split level-0 contraction per step / step "
-                                 "time (the whole pipeline: sample pass, scan, pool select, exact re-rank, final); the scan kernel "
-                                 "alone keeps the matrix cores ~57% busy (DESIGN.md §4.2)"},
+                         "frac_split_accounting": 3 * flops / skern / 1e12 / FP16_MATRIX_PEAK_TFS,
+                         "note": "2*Q*N*32 flops of the level-0 contraction per step (the one f16 MFMA pass the scan "
+                                 "executes) / step time of the whole pipeline (sample pass, scan, pool select, exact "
+                                 "re-rank, final); frac_split_accounting = rounds 1-3's count (three split passes)"},
             "self_match_rate": float((ids[:, 0].cpu() == torch.arange(Qn)).float().mean()),
         }
         # the other two cfg3 modes: brute-force overall top-10 (core/search_engine.py:302-338,
@@ -685,10 +689,10 @@ def main():
         # counted as 2*Q*N*Lp against the FP64 matrix peak
         ovinfo = K.packov_info(L)
         Lp = K.seg_padded_len(L)
-        ov_flops, ov_peak, ov_pname = ((3 * 2.0 * pairs * 32 * ovinfo[0], FP16_MATRIX_PEAK_TFS, "dense F16 MFMA")
+        ov_flops, ov_peak, ov_pname = ((2.0 * pairs * 32 * ovinfo[0], FP16_MATRIX_PEAK_TFS, "dense F16 MFMA")
                                        if ovinfo else (2.0 * pairs * Lp, FP64_MATRIX_PEAK_TFS, "FP64 matrix (spec)"))
         modes = {}
-        l0_flops = 3 * 2.0 * pairs * 32
+        l0_flops = 2.0 * pairs * 32
         for mode, fn, flops, peak, pname in (
                 ("overall", lambda: engine.brute_force(queries, 10), ov_flops, ov_peak, ov_pname),
                 ("level0", lambda: engine.frame_search(queries, 10, 0.1), l0_flops, FP16_MATRIX_PEAK_TFS,
@@ -706,7 +710,7 @@ def main():
                 "max_candidates_per_level": {"m100": 100, "m1000": 1000}.get(mode),
                 "roofline": {"bound": "mfma", "achieved": flops / mk / 1e12, "peak": peak, "unit": "TFLOP/s",
                              "frac": flops / mk / 1e12 / peak,
-                             "note": f"algorithmic contraction flops per step ({('3 x 2*Q*N*32*K-blocks split f16' if ovinfo else '2*Q*N*Lp f64') if mode == 'overall' else '3 x 2*Q*N*32 split f16'}) / "
+                             "note": f"contraction flops per step, one f16 pass ({('2*Q*N*32*K-blocks' if ovinfo else '2*Q*N*Lp f64') if mode == 'overall' else '2*Q*N*32'}) / "
                                      f"GPU step time (HIP events); peak = {pname}"}}
         rec["search"]["modes"] = modes
         if comm is not None:

@@ -1779,13 +1779,6 @@ struct QEntry {
   int qi, row;   // query within the wave, first row (absolute, multiple of 4)
   int pad0, pad1;
 };
-// the hi.hi scan's queue entry: no G (the drain recomputes the split G), 8 B per entry
-struct QEntryHI {
-  int qi, row;
-};
-template <bool HI> struct QEntryOf { using type = QEntry; };
-template <> struct QEntryOf<true> { using type = QEntryHI; };
-
 // wave-local ordering of the queue's LDS accesses (one wave's LDS instructions execute in issue order;
 // this keeps the compiler from moving them across each other)
 __device__ __forceinline__ void wave_lds_sync() {
@@ -1842,7 +1835,7 @@ __device__ __forceinline__ flt4 split_g4(const _Float16* __restrict__ Zq16, cons
 template <int WPB, int PF, int NB = 4, bool HI = true, int OCC = 5>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 8 ? 3 : (HI ? OCC : 1)))) void k_scan0g(Scan0Args a) {
   constexpr int QW = 16 * NB, NP = NB / 2;
-  using QE = typename QEntryOf<HI>::type;
+  using QE = QEntry;  // G_hh kept for the drain's gate (QEntryHI: no gate, measured slower)
   __shared__ QE qe_all[WPB][kQCap];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   QE* qe = qe_all[WPB > 1 ? threadIdx.x >> 6 : 0];
@@ -1911,9 +1904,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
     if (lane < n) {
       const int eqi = qe[lane].qi, erow = qe[lane].row;
       const int q = q0 + eqi;
-      flt4 eg;
-      if constexpr (HI) eg = split_g4(a.Zq16, a.Zc16, q, erow);
-      else eg = qe[lane].g;
+      flt4 eg = qe[lane].g;
       const QConst c = qc[q];
       const float* st = a.Sc32 + (int64_t)(erow >> 2) * 16;  // the SoA group of rows row .. row + 3
       HQ_GUARD(st, a.Sc32, pack0_rows(a.N) * 4 - 15);
@@ -1921,8 +1912,22 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
       const flt4 mn = *reinterpret_cast<const flt4*>(st + 4);
       const flt4 ms = *reinterpret_cast<const flt4*>(st + 8);
       const flt4 fl = *reinterpret_cast<const flt4*>(st + 12);
+      bool need = true;
+      if constexpr (HI) {
+        // gate: the filter is monotone in G and G_split <= G_hh + dG, so a block none of whose rows passes at
+        // G_hh + dG needs no split recompute (most queued blocks: the G-only pre-filter is looser)
+        need = false;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < 4; ++r) {
+          const float Gu = eg[r] + dG;
+          const float E = fmaf(Gu, c1f, c.k0);
+          const float d = fmaf(E, c.qQ + ms[r], fmaf(Gu, c.qA * sd[r], c.qB * mn[r]));
+          need |= erow + r < c_end && __float_as_int(fl[r]) == 0 && fmaxf(E, d) >= 0.0f;
+        }
+        if (need) eg = split_g4(a.Zq16, a.Zc16, q, erow);
+      }
+#pragma unroll
+      for (int r = 0; r < 4 && need; ++r) {
         const int row = erow + r;
         const int f = __float_as_int(fl[r]);
         if (row >= c_end || f != 0) continue;  // past the chunk; flagged rows: k_pool_select
@@ -1957,13 +1962,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
       flt4 tg = {0.0f, 0.0f, 0.0f, 0.0f};
       int tq = 0, tr = 0;
       if (mv) {
-        if constexpr (!HI) tg = qe[b0 + lane].g;
+        tg = qe[b0 + lane].g;
         tq = qe[b0 + lane].qi;
         tr = qe[b0 + lane].row;
       }
       wave_lds_sync();
       if (mv) {
-        if constexpr (!HI) qe[b0 - n + lane].g = tg;
+        qe[b0 - n + lane].g = tg;
         qe[b0 - n + lane].qi = tq;
         qe[b0 - n + lane].row = tr;
       }
@@ -1978,13 +1983,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
     const unsigned lo0 = __builtin_amdgcn_mbcnt_lo((unsigned)m0, 0u), lo1 = __builtin_amdgcn_mbcnt_lo((unsigned)m1, 0u);
     if ((m0 >> lane) & 1ull) {
       const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m0 >> 32), lo0);
-      if constexpr (!HI) qe[pos].g = acc[0];
+      qe[pos].g = acc[0];
       qe[pos].qi = 32 * h + j;
       qe[pos].row = (int)(cs + 4 * g);
     }
     if ((m1 >> lane) & 1ull) {
       const int pos = qn + c0 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m1 >> 32), lo1);
-      if constexpr (!HI) qe[pos].g = acc[1];
+      qe[pos].g = acc[1];
       qe[pos].qi = 32 * h + 16 + j;
       qe[pos].row = (int)(cs + 4 * g);
     }
@@ -3189,8 +3194,9 @@ __global__ __launch_bounds__(64) void k_refine(VecSet Qs, int Q, VecSet Cs, int6
                                                int k, double thr, int thr_mode, double eps, int64_t id_base,
                                                double* __restrict__ os, int64_t* __restrict__ oid,
                                                int* __restrict__ ocnt, int* __restrict__ ores, int count_empty,
-                                               int* __restrict__ oredo) {
+                                               int* __restrict__ oredo, int* __restrict__ onext) {
   __shared__ double es[kMaxTopK];
+  if (onext && blockIdx.x == 0 && threadIdx.x == 0) *onext = 0;  // the next batch's redo counter
   __shared__ int64_t ei[kMaxTopK];
   const int lane = threadIdx.x;
   const bool k32 = (thr_mode & kThrKey32) != 0;
@@ -3322,10 +3328,12 @@ __device__ __forceinline__ double overall_from_levels(const double* lv, const in
   VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si, int mode, const double *__restrict__ cs,                  \
       const int64_t *__restrict__ cid, int kp, int k, double thr, int thr_mode, double eps, int64_t id_base,     \
       double *__restrict__ os, int64_t *__restrict__ oid, int *__restrict__ ocnt, int *__restrict__ ores,        \
-      int count_empty, int *__restrict__ oredo, double *__restrict__ odet, int expt
-#define HQ_REFINE_PASS Qs, Q, Cs, N, si, mode, cs, cid, kp, k, thr, thr_mode, eps, id_base, os, oid, ocnt, ores, count_empty, oredo, odet, expt
+      int count_empty, int *__restrict__ oredo, double *__restrict__ odet, int expt,     \
+      int *__restrict__ onext
+#define HQ_REFINE_PASS Qs, Q, Cs, N, si, mode, cs, cid, kp, k, thr, thr_mode, eps, id_base, os, oid, ocnt, ores, count_empty, oredo, odet, expt, onext
 template <bool SM>
 __device__ __forceinline__ void refine_lds_body(HQ_REFINE_ARGS) {
+  if (onext && blockIdx.x == 0 && threadIdx.x == 0) *onext = 0;  // the next batch's redo counter
   extern __shared__ __attribute__((aligned(16))) double sm[];
   __shared__ int64_t srow[kMaxTopK + 1];  // source row per staged row (-1: empty)
   __shared__ int t32s[kMaxTopK * kMaxSeg];
@@ -3594,6 +3602,7 @@ static void launch_pool_select(int K, hipStream_t s, int Q, float* pool_s, int* 
 // M = 1000 per 1000-query batch.
 template <bool SM>
 __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
+  if (onext && blockIdx.x == 0 && threadIdx.x == 0) *onext = 0;  // the next batch's redo counter
   __shared__ double se[kMaxTopKBig];
   __shared__ int64_t sid[kMaxTopKBig];
   __shared__ int red[4];
@@ -4131,11 +4140,16 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
       const dim3 g1(b.nqb * b.nchunks);
       if (scan_nb == 8) hipLaunchKernelGGL((k_scan0g<1, 2, 8>), g1, dim3(64), 0, s, b);
       else if (opt_on(OPT_SCAN_SPLIT3)) hipLaunchKernelGGL((k_scan0g<1, 2, 4, false>), g1, dim3(64), 0, s, b);
-      else if (opt(OPT_SCAN_OCC, 5) == 4) hipLaunchKernelGGL((k_scan0g<1, 2, 4, true, 4>), g1, dim3(64), 0, s, b);
-      else if (opt(OPT_SCAN_OCC, 5) == 6) hipLaunchKernelGGL((k_scan0g<1, 2, 4, true, 6>), g1, dim3(64), 0, s, b);
-      else if (pf == 4) hipLaunchKernelGGL((k_scan0g<1, 4>), g1, dim3(64), 0, s, b);
-      else if (pf == 3) hipLaunchKernelGGL((k_scan0g<1, 3>), g1, dim3(64), 0, s, b);
-      else hipLaunchKernelGGL((k_scan0g<1, 2>), g1, dim3(64), 0, s, b);
+      else if (opt(OPT_SCAN_OCC, 4) == 5) {
+        if (pf == 4) hipLaunchKernelGGL((k_scan0g<1, 4, 4, true, 5>), g1, dim3(64), 0, s, b);
+        else hipLaunchKernelGGL((k_scan0g<1, 2, 4, true, 5>), g1, dim3(64), 0, s, b);
+      } else {  // 4 waves per SIMD (measured best: 4.69M vs 4.37M QPS at 5)
+        if (pf == 8) hipLaunchKernelGGL((k_scan0g<1, 8, 4, true, 4>), g1, dim3(64), 0, s, b);
+        else if (pf == 6) hipLaunchKernelGGL((k_scan0g<1, 6, 4, true, 4>), g1, dim3(64), 0, s, b);
+        else if (pf == 4) hipLaunchKernelGGL((k_scan0g<1, 4, 4, true, 4>), g1, dim3(64), 0, s, b);
+        else if (pf == 3) hipLaunchKernelGGL((k_scan0g<1, 3, 4, true, 4>), g1, dim3(64), 0, s, b);
+        else hipLaunchKernelGGL((k_scan0g<1, 2, 4, true, 4>), g1, dim3(64), 0, s, b);
+      }
     }
     HQ_CHECK_LAUNCH();
     // flagged rows are rare (usually none): scored inside k_pool_select, before it reads the pools
@@ -4182,13 +4196,10 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
 // std[4], mean[4], msq[4], flags[4] (16 floats), for the rows [0, round_up(N, 4) + kPad0).  k_scan0f
 // reads up to 31 rows past a step start.
 
-__global__ void k_pack0(const double* __restrict__ Z, const double* __restrict__ S, int64_t N, int Lp, int P0,
-                        int nseg, _Float16* __restrict__ Z16, float* __restrict__ S32) {
-  const int64_t rows = z16_rows(N);  // >= pack0_rows(N)
-  const int64_t total = rows * 32;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = t / 32;
-    const int c = (int)(t % 32);
+// one (row, value) of the split level-0 copies (row r < z16_rows(N), value c < 32)
+__device__ __forceinline__ void pack0_elem(const double* __restrict__ Z, const double* __restrict__ S, int64_t N,
+                                           int Lp, int P0, int nseg, _Float16* __restrict__ Z16,
+                                           float* __restrict__ S32, int64_t r, int c) {
     {
       const double z = (r < N && c < P0) ? Z[r * Lp + c] : 0.0;
       const _Float16 hi = (_Float16)z;
@@ -4209,6 +4220,36 @@ __global__ void k_pack0(const double* __restrict__ Z, const double* __restrict__
         o[0] = 0.0f; o[4] = 0.0f; o[8] = 1.0f; o[12] = __int_as_float(4);
       }
     }
+}
+
+__global__ void k_pack0(const double* __restrict__ Z, const double* __restrict__ S, int64_t N, int Lp, int P0,
+                        int nseg, _Float16* __restrict__ Z16, float* __restrict__ S32) {
+  const int64_t rows = z16_rows(N);  // >= pack0_rows(N)
+  const int64_t total = rows * 32;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x)
+    pack0_elem(Z, S, N, Lp, P0, nseg, Z16, S32, t / 32, (int)(t % 32));
+}
+
+// Query batches: k_seg_prepare_lds and k_pack0 in one launch (one wave per row: the row's segments, then
+// its split level-0 copy from the Z / S the wave just wrote; blocks past N write the pad rows), the same
+// arithmetic as the two kernels
+__global__ __launch_bounds__(64) void k_seg_prepare_pack0(const double* __restrict__ idx, int64_t N, SegInfo si,
+                                                          int all_f32, const uint8_t* __restrict__ row_f32,
+                                                          double* __restrict__ Z, double* __restrict__ stats,
+                                                          _Float16* __restrict__ Z16, float* __restrict__ S32) {
+  extern __shared__ double xs[];  // L values
+  const int lane = threadIdx.x;
+  const int64_t rows = z16_rows(N);
+  for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    if (row < N) {
+      for (int i = lane; i < si.L; i += 64) xs[i] = idx[row * si.L + i];
+      __syncthreads();
+      for (int sg = lane; sg < si.nseg; sg += 64) seg_prepare_one(xs, row, sg, si, all_f32, row_f32, Z, stats);
+      __threadfence_block();
+      __syncthreads();
+    }
+    if (lane < 32) pack0_elem(Z, stats, N, si.Lp, si.plen[0], si.nseg, Z16, S32, row, lane);
+    __syncthreads();
   }
 }
 
@@ -4229,22 +4270,25 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
                          const double* Zc, const double* Sc, int64_t N, int L, int mode, const double* cand_score,
                          const int64_t* cand_id, int kp, int k, double threshold, int thr_mode, double eps,
                          int64_t id_base, double* out_score, int64_t* out_id, int* out_count, int* out_resolved,
-                         int count_empty, int* out_redo, double* out_det, hq_stream_t stream) {
+                         int count_empty, int* out_redo, double* out_det, hq_stream_t stream,
+                         int* next_redo = nullptr) {
   SegInfo si;
   seg_info(L, si);
   const hipStream_t s = (hipStream_t)stream;
   const int grid = Q < 8192 ? Q : 8192;
-  if (out_redo) HQ_CHECK_HIP(hipMemsetAsync(out_redo, 0, sizeof(int), s));
+  // next_redo (hq_refine_rescore_topk_pp): out_redo arrives zeroed (cleared by the previous batch's kernel),
+  // the kernel clears next_redo for the next batch; otherwise one 4-byte memset here
+  if (out_redo && !next_redo) HQ_CHECK_HIP(hipMemsetAsync(out_redo, 0, sizeof(int), s));
   const bool sm = seg_small(si);
   if (kp > kMaxTopK) {  // long lists: rows read from global memory, one workgroup per query
     if (sm)
       hipLaunchKernelGGL(k_refine_big_sm, dim3(grid), dim3(256), 0, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
                          mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
-                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, 0);
+                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, next_redo, 0);
     else
       hipLaunchKernelGGL(k_refine_big, dim3(grid), dim3(256), 0, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
                          mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
-                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, 0);
+                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, next_redo, 0);
     HQ_CHECK_LAUNCH();
     return HQ_OK;
   }
@@ -4260,22 +4304,22 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
     if (sm)
       hipLaunchKernelGGL(k_refine_lds_sm, dim3(grid), dim3(256), lds, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc},
                          N, si, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
-                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, expt);
+                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, expt, next_redo);
     else
       hipLaunchKernelGGL(k_refine_lds, dim3(grid), dim3(256), lds, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc},
                          N, si, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
-                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, expt);
+                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, expt, next_redo);
     HQ_CHECK_LAUNCH();
     return HQ_OK;
   }
   if (sm)
     hipLaunchKernelGGL(k_refine<true>, dim3(grid), dim3(64), 0, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
                        mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id, out_count,
-                       out_resolved, count_empty ? 1 : 0, out_redo);
+                       out_resolved, count_empty ? 1 : 0, out_redo, next_redo);
   else
     hipLaunchKernelGGL(k_refine<false>, dim3(grid), dim3(64), 0, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
                        mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id, out_count,
-                       out_resolved, count_empty ? 1 : 0, out_redo);
+                       out_resolved, count_empty ? 1 : 0, out_redo, next_redo);
   HQ_CHECK_LAUNCH();
   if (out_det) return hq_rescore(Rq, Zq, Sq, Q, Rc, Zc, Sc, N, L, out_id, k, id_base, out_det, stream);
   return HQ_OK;
@@ -5210,6 +5254,26 @@ int hq_refine_topk(const double* Rq, const double* Zq, const double* Sq, int Q, 
                        id_base, out_score, out_id, out_count, out_resolved, count_empty, out_redo, nullptr, stream);
 }
 
+int hq_refine_rescore_topk_pp(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
+                              const double* Zc, const double* Sc, int64_t N, int L, int mode,
+                              const double* cand_score, const int64_t* cand_id, int kp, int k, double threshold,
+                              int thr_mode, double eps, int64_t id_base, double* out_score, int64_t* out_id,
+                              int* out_count, int* out_resolved, int count_empty, int* out_redo, int* next_redo,
+                              double* out_det, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || L <= 0 || kp <= 0 || kp > kMaxTopKBig || k <= 0 || k > kp)
+    return fail(HQ_E_INVALID, "bad sizes kp=%d k=%d", kp, k);
+  if (Q == 0) {  // no kernel runs: the next batch's counter is still cleared
+    if (next_redo) HQ_CHECK_HIP(hipMemsetAsync(next_redo, 0, sizeof(int), (hipStream_t)stream));
+    return HQ_OK;
+  }
+  if (!Rq || !Zq || !Sq || !cand_score || !cand_id || !out_score || !out_id || !out_count || !out_resolved ||
+      !out_det || !out_redo || !next_redo || out_redo == next_redo || (N > 0 && (!Rc || !Zc || !Sc)))
+    return fail(HQ_E_INVALID, "null buffer");
+  return refine_launch(Rq, Zq, Sq, Q, Rc, Zc, Sc, N, L, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps,
+                       id_base, out_score, out_id, out_count, out_resolved, count_empty, out_redo, out_det, stream,
+                       next_redo);
+}
+
 int hq_refine_rescore_topk(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
                            const double* Zc, const double* Sc, int64_t N, int L, int mode, const double* cand_score,
                            const int64_t* cand_id, int kp, int k, double threshold, int thr_mode, double eps,
@@ -5306,6 +5370,23 @@ int hq_seg_level0_len(int L) {
   SegInfo si;
   seg_info(L, si);
   return si.nseg > 0 ? si.plen[0] : 0;
+}
+
+int hq_seg_prepare_pack0(const double* idx, int64_t N, int L, int src_f32, const uint8_t* row_f32, double* Z,
+                         double* stats, void* Z16, float* S32, hq_stream_t stream) {
+  if (L <= 0 || N < 0) return fail(HQ_E_INVALID, "bad shape N=%lld L=%d", (long long)N, L);
+  if ((N > 0 && (!idx || !Z || !stats)) || !Z16 || !S32) return fail(HQ_E_INVALID, "null buffer");
+  SegInfo si;
+  seg_info(L, si);
+  if (si.nseg == 0) return fail(HQ_E_INVALID, "no level structure for L=%d", L);
+  if (si.plen[0] > 32) return fail(HQ_E_UNSUPPORTED, "level-0 segment of %d values (<= 32)", si.plen[0]);
+  if (si.L > 4096) return fail(HQ_E_UNSUPPORTED, "L=%d (<= 4096)", L);
+  const int64_t rows = z16_rows(N);
+  hipLaunchKernelGGL(k_seg_prepare_pack0, dim3((unsigned)(rows < 65536 ? rows : 65536)), dim3(64), (size_t)8 * si.L,
+                     (hipStream_t)stream, idx, N, si, src_f32 ? 1 : 0, row_f32, Z, stats,
+                     reinterpret_cast<_Float16*>(Z16), S32);
+  HQ_CHECK_LAUNCH();
+  return HQ_OK;
 }
 
 int hq_seg_pack0_split(const double* Z, const double* S, int64_t N, int L, void* Z16, float* S32,

@@ -74,9 +74,12 @@ SIGNATURES = {
                             _i, _p, _p]),
     "hq_refine_rescore_topk": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _p, _p, _i, _i, _d, _i, _d, _i64, _p, _p,
                                     _p, _p, _i, _p, _p, _p]),
+    "hq_refine_rescore_topk_pp": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _p, _p, _i, _i, _d, _i, _d, _i64, _p,
+                                       _p, _p, _p, _i, _p, _p, _p, _p]),
     "hq_scan_workspace_size": (_sz, [_i, _i64, _i]),
     "hq_seg_level0_len": (_i, [_i]),
     "hq_seg_pack0_split": (_i, [_p, _p, _i64, _i, _p, _p, _p]),
+    "hq_seg_prepare_pack0": (_i, [_p, _i64, _i, _i, _p, _p, _p, _p, _p, _p]),
     "hq_scan0_topk_split": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _d, _i, _i64, _p, _sz, _p, _p, _p]),
     "hq_seg_flag_rows": (_i, [_p, _i64, _p, _p]),
     "hq_scan0_topk_split_fl": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _d, _i, _i64, _p, _sz, _p, _p, _p, _p]),

@@ -147,7 +147,7 @@ class IndexCorpus:
         if q.shape[1] != self.L:
             raise ValueError(f"query index length {q.shape[1]} != corpus index length {self.L}")
         # the overall (brute-force) layout is attached by the first overall scan of the batch (scan_topk)
-        return K.pack0(K.seg_prepare(q, src_f32=f32, row_f32=None if f32 else row_f32))
+        return K.seg_prepare_pack0(q, src_f32=f32, row_f32=None if f32 else row_f32)
 
     def _fused_ok(self, mode: int) -> bool:
         """The fused scans hold the contracted columns in registers: <= 256 padded values (hq_scan_topk)."""
@@ -314,8 +314,8 @@ class IndexCorpus:
             s0, ids, cnt, best, bid = self.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)
             oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
             return PendingSearch(done=(oid, odet[..., 0], odet[..., 1:], ocnt))
-        nredo = self._redo_counter(qp.Z.device)
-        s0, ids, cnt, res, det = self._scan_refine(qp, 0, M, float(threshold), 1, nredo, det=True)
+        nredo, nnext = self._redo_counter(qp.Z.device)
+        s0, ids, cnt, res, det = self._scan_refine(qp, 0, M, float(threshold), 1, nredo, det=True, next_redo=nnext)
         # no arg-max on this path: a query where nothing passed (count 0) is recomputed by the dense path
         # in progressive_finish, so the fallback slot is a constant (-inf, id -1, zero re-scores)
         best, bid, bdet = self._no_fallback(Q, qp.Z.device)
@@ -363,13 +363,17 @@ class IndexCorpus:
         return free.pop() if free else torch().empty(1, dtype=dtype, pin_memory=True)
 
     def _redo_counter(self, dev):
-        """Device int32 [1] the exact re-rank sets to the number of queries needing the dense path."""
+        """(counter, next): device int32 [1] views of a per-stream pair used alternately — the exact re-rank
+        counts this batch's queries needing the dense path in `counter` (zero on entry) and clears `next`,
+        the following batch's counter (hq_refine_rescore_topk_pp: no memset launch per batch)."""
         t = torch()
         cache = self.__dict__.setdefault("_redo", {})
         key = (str(dev), K.stream())
         if key not in cache:
-            cache[key] = t.zeros(1, dtype=t.int32, device=dev)
-        return cache[key]
+            cache[key] = [t.zeros(2, dtype=t.int32, device=dev), 0]
+        pair, i = cache[key]
+        cache[key][1] = 1 - i
+        return pair[i:i + 1], pair[1 - i:2 - i]
 
     def _no_fallback(self, Q: int, dev):
         """Constant (-inf, -1, zeros) fallback slot of a batch of Q queries, cached per stream: the fills
@@ -383,16 +387,19 @@ class IndexCorpus:
                           t.zeros((Q, 1 + self.nseg), dtype=t.float64, device=dev))
         return cache[key]
 
-    def _scan_refine(self, qp, mode: int, k: int, thr: float, thr_mode: int, nredo=None, det: bool = False):
+    def _scan_refine(self, qp, mode: int, k: int, thr: float, thr_mode: int, nredo=None, det: bool = False,
+                     next_redo=None):
         """Fused scan (SLACK extra list entries) + exact re-rank; resolved[q] == 0 marks an unproven list.
         nredo: device counter of queries needing the dense path (unresolved or nothing passed).  det: also
         the exact [overall, levels] re-score of the output (hq_refine_rescore_topk, rows staged once)."""
         lo_mode = 0 if thr_mode == 0 else 1
         asc, aid, _, _ = K.scan_topk(qp, self.prep, mode, k + self.SLACK, thr - self.EPS, lo_mode, self.id_base)
-        fn = K.refine_rescore_topk if det else K.refine_topk
         tm = thr_mode | (K.THR_KEY32 if self.key32(qp) else 0)
-        return fn(qp, self.prep, mode, asc, aid, k, thr, tm, self.EPS, self.id_base, redo=nredo,
-                  count_empty=True)
+        if det:
+            return K.refine_rescore_topk(qp, self.prep, mode, asc, aid, k, thr, tm, self.EPS, self.id_base, redo=nredo,
+                                         count_empty=True, next_redo=next_redo)
+        return K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, tm, self.EPS, self.id_base, redo=nredo,
+                             count_empty=True)
 
     def _final(self, qp, s0, ids, best, bid, K_out: int, bdet=None, det=None):
         """Exact overall + per-level re-score of the survivors and of the arg-max, then the final ranking."""

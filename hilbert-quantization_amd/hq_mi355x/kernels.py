@@ -328,6 +328,33 @@ def pack0(p: Prepared, exc=None) -> Prepared:
     return p
 
 
+def seg_prepare_pack0(idx, exc=None, src_f32: bool = False, row_f32=None) -> Prepared:
+    """seg_prepare + pack0 in one launch (hq_seg_prepare_pack0): a query batch's statistics, normalised
+    rows and split level-0 copies (level-0 segments of <= 32 values; else seg_prepare alone)."""
+    t = torch()
+    i2 = _contig((idx if idx.dim() == 2 else idx.view(1, -1)).to(t.float64))
+    N, L = i2.shape
+    if seg_level0_len(L) > 32 or L > 4096:
+        return pack0(seg_prepare(i2, exc, src_f32, row_f32), exc)
+    Lp, ns = seg_padded_len(L), seg_count(L)
+    Z = t.empty((N, Lp), dtype=t.float64, device=i2.device)
+    S = t.empty((N, ns, 4), dtype=t.float64, device=i2.device)
+    rf = None
+    any32 = all32 = bool(src_f32)
+    if row_f32 is not None and not src_f32:
+        flags = np.asarray(row_f32, dtype=bool).reshape(-1)
+        if flags.size != N:
+            raise ValueError("row_f32 needs one flag per row")
+        any32, all32 = bool(flags.any()), bool(flags.all()) and N > 0
+        rf = _contig(t.from_numpy(flags.astype(np.uint8)).to(i2.device))
+    p = Prepared(i2, Z, S, L, any32, all32)
+    p.Z16 = t.empty(((N + 15) // 16 * 16 + PAD0, 64), dtype=t.float16, device=i2.device)
+    p.S32 = t.empty(((N + 3) // 4 * 4 + PAD0, 4), dtype=t.float32, device=i2.device)
+    _chk(_L().hq_seg_prepare_pack0(ptr(i2), N, L, 1 if src_f32 else 0, ptr(rf), ptr(Z), ptr(S), ptr(p.Z16),
+                                   ptr(p.S32), stream()), exc)
+    return p
+
+
 def flag_rows(p: Prepared, exc=None) -> Prepared:
     """List a corpus's flagged level-0 rows once (hq_seg_flag_rows: int32 [1 + N], count first), so the
     level-0 scan of every query batch skips that pass over the statistics."""
@@ -422,7 +449,7 @@ def refine_topk(q: Prepared, c: Prepared, mode: int, cand_score, cand_id, k: int
 
 def refine_rescore_topk(q: Prepared, c: Prepared, mode: int, cand_score, cand_id, k: int, threshold: float = 0.0,
                         thr_mode: int = 0, eps: float = 1e-9, id_base: int = 0, exc=None, redo=None,
-                        count_empty: bool = False):
+                        count_empty: bool = False, next_redo=None):
     """refine_topk + the exact [overall, level_0..] re-score of its output (rescore's values for the output
     ids, zeros in empty slots) -> (scores, ids, count, resolved, det [Q, k, 1 + nseg])."""
     t = torch()
@@ -433,6 +460,13 @@ def refine_rescore_topk(q: Prepared, c: Prepared, mode: int, cand_score, cand_id
     cnt = t.empty(Q, dtype=t.int32, device=dev)
     res = t.empty(Q, dtype=t.int32, device=dev)
     det = t.empty((Q, k, 1 + q.nseg), dtype=t.float64, device=dev)
+    if next_redo is not None:  # ping-pong counters: redo arrives zeroed, the kernel clears next_redo
+        _chk(_L().hq_refine_rescore_topk_pp(ptr(q.R), ptr(q.Z), ptr(q.S), Q, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L,
+                                            mode, ptr(_contig(cand_score)), ptr(_contig(cand_id)), kp, k,
+                                            float(threshold), thr_mode, float(eps), int(id_base), ptr(os_), ptr(oi),
+                                            ptr(cnt), ptr(res), 1 if count_empty else 0, ptr(redo), ptr(next_redo),
+                                            ptr(det), stream()), exc)
+        return os_, oi, cnt, res, det
     _chk(_L().hq_refine_rescore_topk(ptr(q.R), ptr(q.Z), ptr(q.S), Q, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L, mode,
                                      ptr(_contig(cand_score)), ptr(_contig(cand_id)), kp, k, float(threshold),
                                      thr_mode, float(eps), int(id_base), ptr(os_), ptr(oi), ptr(cnt), ptr(res),

@@ -241,6 +241,10 @@ int hq_scan_topk(const double* Zq, const double* Sq, int Q, const double* Zc, co
  * whose capacity is sized from the sample (an overflowing pool marks its query unresolved).  With K' < k a query can end with fewer than k listed candidates although more pass
  * the caller's threshold: its empty slots then carry score +inf (id -1), which hq_refine_topk /
  * hq_refine_rescore_topk report as unresolved (the caller's dense exact path answers the query).    */
+/* hq_seg_prepare_pack0: hq_seg_prepare_rows + hq_seg_pack0_split in one launch (query batches: one wave
+ * per row, the same arithmetic and outputs as the two calls; L <= 4096, level-0 segment <= 32 values).  */
+int hq_seg_prepare_pack0(const double* idx, int64_t N, int L, int src_f32, const uint8_t* row_f32, double* Z,
+                         double* stats, void* Z16, float* S32, hq_stream_t stream);
 int hq_seg_level0_len(int L);
 int hq_seg_pack0_split(const double* Z, const double* S, int64_t N, int L, void* Z16, float* S32,
                        hq_stream_t stream);
@@ -308,6 +312,17 @@ int hq_refine_rescore_topk(const double* Rq, const double* Zq, const double* Sq,
                            double threshold, int thr_mode, double eps, int64_t id_base,
                            double* out_score, int64_t* out_id, int* out_count, int* out_resolved,
                            int count_empty, int* out_redo, double* out_det, hq_stream_t stream);
+/* hq_refine_rescore_topk with a ping-pong pair of redo counters (no memset launch per batch): out_redo
+ * must be zero on entry (fresh, or cleared by the previous call as its next_redo); the kernel clears
+ * next_redo for the next batch.  Alternate the two counters between consecutive batches of a stream and
+ * copy out_redo to the host behind the batch (the next batch's kernels run after that copy).          */
+int hq_refine_rescore_topk_pp(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
+                              const double* Zc, const double* Sc, int64_t N, int L, int mode,
+                              const double* cand_score, const int64_t* cand_id, int kp, int k,
+                              double threshold, int thr_mode, double eps, int64_t id_base,
+                              double* out_score, int64_t* out_id, int* out_count, int* out_resolved,
+                              int count_empty, int* out_redo, int* next_redo, double* out_det,
+                              hq_stream_t stream);
 
 /* ---- S4 on candidate lists: EXACT overall + per-level scores of selected pairs ---------------
  * ids: int64 Q x k GLOBAL ids (row = id - id_base; out of range / < 0 -> zeros);

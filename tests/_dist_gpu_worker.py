@@ -19,8 +19,17 @@ def main(out_path):
     from hq_mi355x.core.search_engine import IndexCorpus
     from hq_mi355x.distributed import ShardedIndexCorpus, shard_range
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    torch.cuda.set_device(0)
-    dist.init_process_group("gloo")
+    comm = None
+    if os.environ.get("HQ_DIST_RCCL"):
+        # one GPU per rank, RCCL: the records all-gather through the C-ABI (hq_allgather_topk)
+        from hq_mi355x.rccl import Communicator
+        local = int(os.environ.get("LOCAL_RANK", rank))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        comm = Communicator.from_process_group()
+    else:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
     rng = np.random.default_rng(123)
     N, L = 20_011, 64
     C = rng.standard_normal((N, L)).cumsum(1) * 0.1
@@ -29,7 +38,7 @@ def main(out_path):
     Q = np.concatenate([C[[17, 40, 9_999, 20_010]], C[100:160] + rng.normal(0, 0.02, (60, L)),
                         rng.standard_normal((3, L))])
     a, b = shard_range(N, rank, world)
-    sh = ShardedIndexCorpus(C[a:b], id_base=a, n_total=N)
+    sh = ShardedIndexCorpus(C[a:b], id_base=a, n_total=N, comm=comm)
     got = {}
     ids, ov, lv, cnt = sh.progressive(Q, 10, 0.1, 20)
     got["progressive"] = [x.cpu().numpy() for x in (ids, ov, lv, cnt)]
@@ -54,6 +63,8 @@ def main(out_path):
         with open(out_path + ".json", "w") as f:
             json.dump({"world": world, "equal": res}, f)
     dist.barrier()
+    if comm is not None:
+        comm.close()
     dist.destroy_process_group()
 
 

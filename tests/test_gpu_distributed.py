@@ -26,10 +26,22 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_sharded_search_two_processes(hq_lib):
+def _device_count():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.parametrize("backend", ["gloo", "rccl"])
+def test_sharded_search_two_processes(hq_lib, backend):
+    """gloo: both ranks on cuda:0 (runs on a one-GPU box); rccl: one GPU per rank with the records
+    all-gather through the C-ABI (hq_allgather_topk) — runs where two GPUs are visible."""
+    if backend == "rccl" and _device_count() < 2:
+        pytest.skip("the RCCL form needs two GPUs (one rank per GPU)")
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res")
         env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        if backend == "rccl":
+            env["HQ_DIST_RCCL"] = "1"
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
                os.path.join(ROOT, "tests", "_dist_gpu_worker.py"), out]

@@ -184,3 +184,24 @@ def test_dense_level_scores_lds_equal_per_pair_kernel(hq_lib, hq_option, f32):
         assert np.array_equal(got, want), lv
         for a in (0, 3, 8):
             np.testing.assert_array_equal(got[a, :500], O.level_similarity(Q[a], C[:500], lv))
+
+
+@pytest.mark.parametrize("kind", ["f64", "f32", "mixed"])
+def test_fused_query_prepare_equals_two_launches(hq_lib, kind):
+    """hq_seg_prepare_pack0 (query batches: statistics, normalised rows and split level-0 copies in one
+    launch) writes exactly what hq_seg_prepare_rows + hq_seg_pack0_split write, pad rows included."""
+    from hq_mi355x import kernels as K
+    from hq_mi355x._dev import to_dev
+    C = _corpus(1003, 64, 33)
+    flags = None
+    if kind == "f32":
+        C = C.astype(np.float32)
+    elif kind == "mixed":
+        flags = np.arange(len(C)) % 3 == 0
+    x = to_dev(C if kind != "mixed" else C.astype(np.float64))
+    f32 = kind == "f32"
+    a = K.seg_prepare_pack0(x, src_f32=f32, row_f32=flags)
+    b = K.pack0(K.seg_prepare(x, src_f32=f32, row_f32=flags))
+    for name in ("Z", "S", "Z16", "S32"):
+        assert np.array_equal(_np(getattr(a, name)).view(np.uint8), _np(getattr(b, name)).view(np.uint8)), name
+    assert (a.f32, a.all32) == (b.f32, b.all32)
