@@ -4129,8 +4129,9 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
       HQ_CHECK_LAUNCH();
     }
     // options scan_wpb: waves per block (1 = one wave per block, each reading its own fragments);
-    // scan_pf: prefetch distance in steps (2, 3, 4)
-    const int pf = (int)opt(OPT_SCAN_PF, 2);
+    // scan_pf: prefetch distance in steps (2, 3, 4, 6, 8; 4 measured best at 4 waves per SIMD: 4.73M vs
+    // 4.64M QPS at 2, 3.02M at 6 where the queue spills)
+    const int pf = (int)opt(OPT_SCAN_PF, 4);
     if (opt(OPT_SCAN_WPB, 1) == 4) {
       const dim3 g4((b.nqb + 3) / 4 * b.nchunks);
       if (pf == 4) hipLaunchKernelGGL((k_scan0g<4, 4>), g4, dim3(256), 0, s, b);
@@ -4143,7 +4144,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
       else if (opt(OPT_SCAN_OCC, 4) == 5) {
         if (pf == 4) hipLaunchKernelGGL((k_scan0g<1, 4, 4, true, 5>), g1, dim3(64), 0, s, b);
         else hipLaunchKernelGGL((k_scan0g<1, 2, 4, true, 5>), g1, dim3(64), 0, s, b);
-      } else {  // 4 waves per SIMD (measured best: 4.69M vs 4.37M QPS at 5)
+      } else {  // 4 waves per SIMD (measured best: 4.64M vs 1.41M QPS at 5 with the drain gate)
         if (pf == 8) hipLaunchKernelGGL((k_scan0g<1, 8, 4, true, 4>), g1, dim3(64), 0, s, b);
         else if (pf == 6) hipLaunchKernelGGL((k_scan0g<1, 6, 4, true, 4>), g1, dim3(64), 0, s, b);
         else if (pf == 4) hipLaunchKernelGGL((k_scan0g<1, 4, 4, true, 4>), g1, dim3(64), 0, s, b);

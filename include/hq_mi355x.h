@@ -60,7 +60,7 @@ const char* hq_last_error(void);
  * "sample_hi" (1: the sample passes' step loops on hi.hi with a split-G epilogue),
  * "sample_kth" (0 = provable bound), "scan_v1" (the
  * LDS-tiled level-0 scan), "scan_variant", "scan_wpb" (4 = four waves per level-0 scan block), "scan_pf" (prefetch
- * distance 3 or 4), "sample_variant" (1 = the full-filter sample pass).  Options are process-wide: set them before launching, not
+ * distance 2, 3, 4 (default), 6 or 8), "sample_variant" (1 = the full-filter sample pass).  Options are process-wide: set them before launching, not
  * while other host threads launch.  hq_reset_option restores the default; hq_get_option returns 1 when
  * the option is set (value in *value), 0 when it is at its default, HQ_E_INVALID for an unknown name.
  * hq_diag_build() = 1 for a `make DIAG=1` library (diagnostics kernels; HQ_<NAME> environment variables
