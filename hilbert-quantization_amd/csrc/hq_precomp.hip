@@ -46,6 +46,7 @@ struct PrePlan {
   int nt;        // non-temporal output stores
   int znz;       // zero-padding skip: squares listed over all levels (LDS list entries)
   int znleaves;  // zero-padding skip: leaf tasks over the listed squares
+  int nleaves_al;  // LDS-tree partials rounded up so that res stays 16-byte aligned
   PreLevel lv[kPreMaxLevels];
 };
 
@@ -93,6 +94,7 @@ static int pre_plan(int n, int max_levels, int min_sq, PrePlan& p) {
   }
   p.nlev = c;
   if (2 * p.maxper > 64) p.tree_lds = 1;  // a square's leaf lanes would span waves
+  p.nleaves_al = (p.nleaves + 3) & ~3;  // f64 partials: a multiple of 16 B already
   return HQ_OK;
 }
 
@@ -222,7 +224,13 @@ __device__ __forceinline__ T sq_sum(const T* b, int ld) {
       load8<T>(b + r * ld, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) r8[j] = r == 0 ? v[j] : r8[j] + v[j];
-      if (r == 3) __builtin_amdgcn_sched_barrier(0);
+      // rows 4-7 are addressed through a pointer that depends on the first four rows' sums, so no pass
+      // can issue all 16 loads at once (64 VGPRs in flight)
+      if (r == 3) {
+        int z = 0;
+        asm volatile("" : "+v"(z) : "v"(r8[0]), "v"(r8[4]));
+        b += z;
+      }
     }
     return T(0) + (((r8[0] + r8[1]) + (r8[2] + r8[3])) + ((r8[4] + r8[5]) + (r8[6] + r8[7])));
   }
@@ -341,6 +349,109 @@ __device__ __forceinline__ void pre_zero_setup(T* img, float* res, uint32_t* zl,
   lds_barrier();
 }
 
+// squares of <= 128 values: one thread each, level by level (uniform geometry per loop); 4x4 and 8x8
+// squares read whole row segments (their x0 is a multiple of s/2) and sum in registers
+template <typename T, bool SK>
+__device__ __forceinline__ void pre_small_levels(const PreLevel* lv, int nlev, const T* img, int ld, float* res,
+                                                 int tid, const uint32_t* zl) {
+  for (int l = 0; l < nlev; ++l) {
+    // this level's geometry from the LDS copy into SGPRs (indexing the kernarg plan by a loop variable
+    // keeps the whole plan live in SGPRs, which spill)
+    PreLevel L;
+    L.g = __builtin_amdgcn_readfirstlane(lv[l].g);
+    L.s = __builtin_amdgcn_readfirstlane(lv[l].s);
+    L.count = __builtin_amdgcn_readfirstlane(lv[l].count);
+    L.off = __builtin_amdgcn_readfirstlane(lv[l].off);
+    L.lsh = __builtin_amdgcn_readfirstlane(lv[l].lsh);
+    L.leaf0 = __builtin_amdgcn_readfirstlane(lv[l].leaf0);
+    if (L.leaf0 >= 0) continue;
+    // one straight-line loop per square size (the size is uniform per level)
+    L.zcnt = __builtin_amdgcn_readfirstlane(lv[l].zcnt);
+    L.zoff = __builtin_amdgcn_readfirstlane(lv[l].zoff);
+    if (L.s == 2) pre_small<T, 2, SK>(L, img, ld, res, tid, zl);
+    else if (L.s == 4) pre_small<T, 4, SK>(L, img, ld, res, tid, zl);
+    else if (L.s == 8) pre_small<T, 8, SK>(L, img, ld, res, tid, zl);
+    else pre_small<T, 1, SK>(L, img, ld, res, tid, zl);
+  }
+}
+
+// Skip runs: 128-value leaves of the larger squares from the task resolved once per workgroup (lt_b: LDS
+// offset of the half leaf's first value; lt_m: average slot bits 0-11, log2 side 12-15, leaf 16-20, live
+// 24).  Two lanes per leaf: lane h = 0 / 1 keeps NumPy's accumulators r0-r3 / r4-r7 (columns 4h..4h+3 of
+// each 8-value step, 16 steps of one row segment), so ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7)) is one
+// shuffle; a square's leaves sit on consecutive lanes of one wave and combine in NumPy's balanced tree.
+template <typename T>
+__device__ __forceinline__ void pre_leaves_sk(const T* img, int ld, float* res, int tid, int lt_b, int lt_m,
+                                              int maxper) {
+  const int h = tid & 1;
+  // laundered per image: hoisted out of the image loop, the 16 load addresses would hold VGPRs
+  asm volatile("" : "+v"(lt_b), "+v"(lt_m));
+  const bool live = (lt_m >> 24) & 1;
+  const int lsh = (lt_m >> 12) & 15, leaf = (lt_m >> 16) & 31;
+  T v = T(0);
+  if (live) {
+    const T* b = img + lt_b;
+    const int msk = (1 << lsh) - 1;
+    T r[4];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int q = (leaf << 7) + 8 * i;
+      T w4[4];
+      load4<T>(b + (q >> lsh) * ld + (q & msk), w4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = i == 0 ? w4[j] : r[j] + w4[j];
+      if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // at most 8 steps of loads in flight
+    }
+    v = (r[0] + r[1]) + (r[2] + r[3]);
+  }
+  const int per = live ? 1 << (2 * lsh - 7) : 0;
+  {
+    const T o = __shfl_down(v, 1, 64);
+    if (h == 0) v = v + o;
+  }
+  for (int w = 1; w < maxper; w <<= 1) {
+    const T o = __shfl_down(v, 2 * w, 64);
+    if (w < per && h == 0 && (leaf & (2 * w - 1)) == 0) v = v + o;
+  }
+  if (live && h == 0 && leaf == 0) res[lt_m & 0xFFF] = pre_mean<T>(T(0) + v, 2 * lsh);
+}
+
+// The T averages from LDS to the output row o by threads t0 = 0 .. nthr-1: float4 stores from the row's
+// first 16-byte boundary; for 8-B aligned rows (even strides) the float4 comes from two 8-byte LDS reads
+// (2-way bank conflicts at the 16-B lane stride: 8 LDS cycles per wave, where two 4-way ds_read2_b32
+// took 32), else from dword reads; scalar head and tail.  nt: non-temporal (written once).
+__device__ __forceinline__ void pre_store(const float* res, int total, float* o, bool nt, int t0, int nthr) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  const int mis = (int)((reinterpret_cast<uintptr_t>(o) >> 2) & 3);
+  const int head = min((4 - mis) & 3, total);
+  const int nv = (total - head) >> 2;
+  if (t0 < head) o[t0] = res[t0];
+  for (int i = t0; i < nv; i += nthr) {
+    const int a = head + 4 * i;
+    f4v v;
+    if (!(mis & 1)) {
+      // volatile: two ds_read_b64, not one merged ds_read2_b64 (its 16-lane groups conflict 2-way too)
+      typedef __attribute__((address_space(3))) const volatile f2v lds_f2v;
+      const f2v lo = *(lds_f2v*)(res + a);
+      const f2v hi = *(lds_f2v*)(res + a + 2);
+      v = f4v{lo.x, lo.y, hi.x, hi.y};
+    } else {
+      v = f4v{res[a], res[a + 1], res[a + 2], res[a + 3]};
+    }
+    if (nt) __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(o + a));
+    else *reinterpret_cast<f4v*>(o + a) = v;
+  }
+  for (int a = head + 4 * nv + t0; a < total; a += nthr) o[a] = res[a];
+}
+
+// phase-skipping diagnostics (wrong averages): `make DIAG=1` builds only
+#ifdef HQ_DIAG
+#define PRE_DIAG(bit) (plan.diag & (bit))
+#else
+#define PRE_DIAG(bit) false
+#endif
+
 // kind 0: images (n x n row-major, image stride `stride` elements); kind 1: 1-D Hilbert-ordered
 // parameter streams of d values (row stride `stride`), zero-padded to n*n and mapped to 2-D
 // (core/pipeline.py:298-319 _get_2d_representation).
@@ -351,12 +462,16 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ PreLevel lv[kPreMaxLevels];  // per-thread level lookups index LDS, not the kernarg block
   T* img = reinterpret_cast<T*>(smem);
-  T* part = img + ld * n;  // row stride ld = n + pad (16-B aligned rows spread the bank pattern)
-  float* res = reinterpret_cast<float*>(part + (plan.tree_lds ? plan.nleaves : 0));  // part: LDS tree only
-  uint32_t* zl = reinterpret_cast<uint32_t*>(res + plan.total);  // SK: listed squares, per level at zoff
+  T* part = img + ((ld * n + 3) & ~3);  // row stride ld = n + pad (16-B aligned rows spread the bank pattern)
+  float* res = reinterpret_cast<float*>(part + (plan.tree_lds ? plan.nleaves_al : 0));  // part: LDS tree only; res 16-B aligned
+  uint32_t* zl = reinterpret_cast<uint32_t*>(res + ((plan.total + 3) & ~3));  // SK: listed squares, per level at zoff
   __shared__ int zcnt[kPreMaxLevels];
   const int tid = threadIdx.x;
   const int lsh_n = plan.lsh_n;
+  // skip runs are 1-D streams with the group LUT (host): the other load paths are compiled out, so
+  // their loads cannot hold back the wait counters of this one
+  const bool lut_on = SK || use_lut;
+  const int knd = SK ? 1 : kind;
   if (tid < plan.nlev) lv[tid] = plan.lv[tid];
   // The barriers below order LDS only: s_waitcnt lgkmcnt(0) + s_barrier, so the prefetch of the next
   // image (plain global loads into registers) stays in flight through this image's reductions
@@ -369,7 +484,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
   const int G = (n * n) >> 2;
   uint32_t lut[kPreG];
   T pf[kPreG][4];
-  if (use_lut) {
+  if (lut_on) {
     const uint32_t* glut = n == 16 ? kPreLut16.v : (n == 32 ? kPreLut32.v : kPreLut64.v);
 #pragma unroll
     for (int i = 0; i < kPreG; ++i) lut[i] = tid + kPreThreads * i < G ? glut[tid + kPreThreads * i] : 0u;
@@ -420,13 +535,13 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
       }
     }
   }
-  if (PF && use_lut && (int64_t)blockIdx.x < N) fetch(blockIdx.x);
+  if (PF && lut_on && (int64_t)blockIdx.x < N) fetch(blockIdx.x);
   for (int64_t e = blockIdx.x; e < N; e += gridDim.x) {
     const T* src = in + e * stride;
-    if (plan.diag & 4) {
-    } else if (kind == 0) {
+    if (PRE_DIAG(4)) {
+    } else if (knd == 0) {
       for (int i = tid; i < n * n; i += kPreThreads) img[(i >> lsh_n) * ld + (i & (n - 1))] = src[i];
-    } else if (use_lut) {
+    } else if (lut_on) {
       if (!PF) fetch(e);
 #pragma unroll
       for (int i = 0; i < kPreG; ++i) {
@@ -454,28 +569,10 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
       }
     }
     lds_barrier();
-    if (PF && use_lut && e + gridDim.x < N) fetch(e + gridDim.x);
+    if (PF && lut_on && e + gridDim.x < N) fetch(e + gridDim.x);
     // squares of <= 128 values: one thread each, level by level (uniform geometry per loop); 4x4 and
     // 8x8 squares read whole row segments (their x0 is a multiple of s/2) and sum in registers
-    for (int l = 0; l < plan.nlev && !(plan.diag & 1); ++l) {
-      // this level's geometry from the LDS copy into SGPRs (indexing the kernarg plan by a loop
-      // variable keeps the whole plan live in SGPRs, which spill)
-      PreLevel L;
-      L.g = __builtin_amdgcn_readfirstlane(lv[l].g);
-      L.s = __builtin_amdgcn_readfirstlane(lv[l].s);
-      L.count = __builtin_amdgcn_readfirstlane(lv[l].count);
-      L.off = __builtin_amdgcn_readfirstlane(lv[l].off);
-      L.lsh = __builtin_amdgcn_readfirstlane(lv[l].lsh);
-      L.leaf0 = __builtin_amdgcn_readfirstlane(lv[l].leaf0);
-      if (L.leaf0 >= 0) continue;
-      // one straight-line loop per square size (the size is uniform per level)
-      L.zcnt = __builtin_amdgcn_readfirstlane(lv[l].zcnt);
-      L.zoff = __builtin_amdgcn_readfirstlane(lv[l].zoff);
-      if (L.s == 2) pre_small<T, 2, SK>(L, img, ld, res, tid, zl);
-      else if (L.s == 4) pre_small<T, 4, SK>(L, img, ld, res, tid, zl);
-      else if (L.s == 8) pre_small<T, 8, SK>(L, img, ld, res, tid, zl);
-      else pre_small<T, 1, SK>(L, img, ld, res, tid, zl);
-    }
+    if (!PRE_DIAG(1)) pre_small_levels<T, SK>(lv, plan.nlev, img, ld, res, tid, zl);
     // 128-value leaves of the larger squares: 16 steps of 8 consecutive values (one row segment,
     // 8-aligned because x0 is a multiple of s/2 >= 8), eight accumulators as NumPy's pairwise leaf
     // Two lanes per 128-value leaf: lane h = 0 / 1 keeps NumPy's accumulators r0-r3 / r4-r7 (columns
@@ -509,40 +606,9 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
       }
       return (r[0] + r[1]) + (r[2] + r[3]);
     };
-    if (plan.diag & 2) {
+    if (PRE_DIAG(2)) {
     } else if constexpr (SK) {
-      // the same leaf sums and shuffle tree as below, from the task resolved before the image loop
-      const int h = tid & 1;
-      // laundered per image: hoisted out of the image loop, the 16 load addresses would hold VGPRs
-      asm volatile("" : "+v"(lt_b), "+v"(lt_m));
-      const bool live = (lt_m >> 24) & 1;
-      const int lsh = (lt_m >> 12) & 15, leaf = (lt_m >> 16) & 31;
-      T v = T(0);
-      if (live) {
-        const T* b = img + lt_b;
-        const int msk = (1 << lsh) - 1;
-        T r[4];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int q = (leaf << 7) + 8 * i;
-          T w4[4];
-          load4<T>(b + (q >> lsh) * ld + (q & msk), w4);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) r[j] = i == 0 ? w4[j] : r[j] + w4[j];
-          if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // at most 8 steps of loads in flight
-        }
-        v = (r[0] + r[1]) + (r[2] + r[3]);
-      }
-      const int per = live ? 1 << (2 * lsh - 7) : 0;
-      {
-        const T o = __shfl_down(v, 1, 64);
-        if (h == 0) v = v + o;
-      }
-      for (int w = 1; w < plan.maxper; w <<= 1) {
-        const T o = __shfl_down(v, 2 * w, 64);
-        if (w < per && h == 0 && (leaf & (2 * w - 1)) == 0) v = v + o;
-      }
-      if (live && h == 0 && leaf == 0) res[lt_m & 0xFFF] = pre_mean<T>(T(0) + v, 2 * lsh);
+      pre_leaves_sk<T>(img, ld, res, tid, lt_b, lt_m, plan.maxper);
       lds_barrier();
     } else if (!plan.tree_lds) {
       // a square's <= 32 leaves sit on 2 * per consecutive lanes of one wave (leaf0 is aligned to
@@ -587,24 +653,106 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
     }
     lds_barrier();
     }
-    float* o = out + e * out_stride;
-    if (!(plan.diag & 8)) {
-      // float4 stores from the first 16-byte boundary of the row; scalar head and tail
-      const int head = min((int)((4 - ((reinterpret_cast<uintptr_t>(o) >> 2) & 3)) & 3), plan.total);
-      const int nv = (plan.total - head) >> 2;
-      typedef float f4v __attribute__((ext_vector_type(4)));
-      const bool nt = plan.nt;  // non-temporal: the averages are written once (A/B HQ_PRECOMP_NT)
-      if (tid < head) o[tid] = res[tid];
-      for (int i = tid; i < nv; i += kPreThreads) {
-        const int a = head + 4 * i;
-        const f4v v = {res[a], res[a + 1], res[a + 2], res[a + 3]};
-        if (nt) __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(o + a));
-        else *reinterpret_cast<f4v*>(o + a) = v;
-      }
-      for (int a = head + 4 * nv + tid; a < plan.total; a += kPreThreads) o[a] = res[a];
-    }
+    if (!PRE_DIAG(8)) pre_store(res, plan.total, out + e * out_stride, plan.nt, tid, kPreThreads);
     lds_barrier();
   }
+}
+
+// Skip runs of f32 1-D streams, wave-specialised: waves 0-1 load the next image (float4 groups
+// j = lane + 128 i, zero-padded past d) and scatter it into LDS, waves 2-3 store the previous image's
+// averages, both before the image's first barrier; all four waves reduce.  A wave's vector-memory
+// counter then holds one kind of access: on gfx9 the counter is not ordered between loads and stores,
+// so in k_precomp the wait for the prefetched values (vmcnt(0)) also drained the previous image's
+// stores every image.  Two barriers per image instead of three.
+template <int KL>
+__global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))) void k_precomp_ws(
+    const float* __restrict__ in, int64_t N, int64_t stride, int d, int n, PrePlan plan, float* __restrict__ out,
+    int64_t out_stride, int ld) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ PreLevel lv[kPreMaxLevels];
+  __shared__ int zcnt[kPreMaxLevels];
+  float* img = reinterpret_cast<float*>(smem);
+  float* res = img + ((ld * n + 3) & ~3);  // no LDS tree on skip runs
+  uint32_t* zl = reinterpret_cast<uint32_t*>(res + ((plan.total + 3) & ~3));
+  const int tid = threadIdx.x;
+  const bool loader = tid < 128;  // waves 0 and 1
+  const int lt = tid & 127;
+  const int lsh_n = plan.lsh_n;
+  if (tid < plan.nlev) lv[tid] = plan.lv[tid];
+  auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  const int G = (n * n) >> 2;
+  uint32_t lut[KL];
+  float pf[KL][4];
+  {
+    const uint32_t* glut = n == 16 ? kPreLut16.v : (n == 32 ? kPreLut32.v : kPreLut64.v);
+#pragma unroll
+    for (int i = 0; i < KL; ++i) lut[i] = lt + 128 * i < G ? glut[lt + 128 * i] : 0u;
+  }
+  auto fetch = [&](int64_t e) {
+    const float* src = in + e * stride;
+    const bool vec_ok = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+    int dd = d;
+    asm volatile("" : "+s"(dd));
+#pragma unroll
+    for (int i = 0; i < KL; ++i) {
+      const int j = lt + 128 * i;
+      if (vec_ok && 4 * j + 3 < dd) {
+        const float4 q4 = *reinterpret_cast<const float4*>(src + 4 * j);
+        pf[i][0] = q4.x; pf[i][1] = q4.y; pf[i][2] = q4.z; pf[i][3] = q4.w;
+      } else if (4 * j < dd) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) pf[i][m] = 4 * j + m < dd ? src[4 * j + m] : 0.0f;  // zero padding
+      }
+    }
+  };
+  pre_zero_setup<float>(img, res, zl, zcnt, lv, plan.nlev, plan.total, n, d, ld, tid);
+  int lt_b = 0, lt_m = 0;
+  {
+    const int t = tid >> 1;
+    if (t < plan.znleaves) {
+      int l = plan.nlev - 1;
+      while (lv[l].zleaf0 < 0 || t < lv[l].zleaf0) --l;
+      const int lper = 2 * lv[l].lsh - 7;
+      const int slot = (t - lv[l].zleaf0) >> lper, leaf = (t - lv[l].zleaf0) & ((1 << lper) - 1);
+      if (slot < lv[l].zcnt) {
+        const uint32_t ent = zl[lv[l].zoff + slot];
+        lt_b = (int)(ent & 0xFFFFu) + 4 * (tid & 1);
+        lt_m = (lv[l].off + (int)(ent >> 16)) | (lv[l].lsh << 12) | (leaf << 16) | (1 << 24);
+      }
+    }
+  }
+  if ((int64_t)blockIdx.x >= N) return;  // uniform over the workgroup
+  if (loader) fetch(blockIdx.x);
+  int64_t prev = -1;
+  for (int64_t e = blockIdx.x; e < N; e += gridDim.x) {
+    if (loader) {
+#pragma unroll
+      for (int i = 0; i < KL; ++i) {
+        const int j = lt + 128 * i;
+        int dz = d;
+        asm volatile("" : "+s"(dz));
+        if (j >= G || 4 * j >= dz) continue;  // padding stays +0.0 from the setup
+        uint32_t ent = lut[i];
+        asm volatile("" : "+v"(ent));
+        const uint32_t off0 = ent & 0xFFFFu, code = ent >> 16;
+        const uint32_t off = (off0 >> lsh_n) * ld + (off0 & (n - 1));
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const uint32_t b = (code >> (2 * m)) & 3u;
+          img[off + (b & 1u) + (b >> 1) * ld] = pf[i][m];
+        }
+      }
+    } else if (prev >= 0 && !PRE_DIAG(8)) {
+      pre_store(res, plan.total, out + prev * out_stride, plan.nt, lt, 128);
+    }
+    lds_barrier();
+    if (loader && e + gridDim.x < N) fetch(e + gridDim.x);
+    if (!PRE_DIAG(1)) pre_small_levels<float, true>(lv, plan.nlev, img, ld, res, tid, zl);
+    if (!PRE_DIAG(2)) pre_leaves_sk<float>(img, ld, res, tid, lt_b, lt_m, plan.maxper);
+    lds_barrier();
+    prev = e;
+  }
+  if (!loader && !PRE_DIAG(8)) pre_store(res, plan.total, out + prev * out_stride, plan.nt, lt, 128);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -815,7 +963,7 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   // zero-padding skip (pre_zero_plan): 1-D streams with padding, leaves combined in registers;
   // A/B: option precomp_skip = 0 computes every square
   const bool skip = use_lut && !p.tree_lds && opt(OPT_PRECOMP_SKIP, 1) != 0 && pre_zero_plan(n, d, p);
-  const size_t lds = (size_t)esz * ((size_t)ld * n + (p.tree_lds ? p.nleaves : 0)) + 4 * (size_t)p.total +
+  const size_t lds = (size_t)esz * ((size_t)((ld * n + 3) & ~3) + (p.tree_lds ? p.nleaves_al : 0)) + 4 * (size_t)((p.total + 3) & ~3) +
                      (skip ? 4 * (size_t)p.znz : 0);
   if (lds > 160 * 1024) return fail(HQ_E_UNSUPPORTED, "pre-computed index n=%d dtype %d needs %zu B of LDS", n, dtype, lds);
   hipStream_t s = (hipStream_t)stream;
@@ -828,6 +976,17 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   if (dtype == HQ_F32) {
     // groups of 4 values a thread scatters: a skip run touches only groups below d
     const bool kg2 = skip && (d + 3) / 4 <= 2 * kPreThreads;
+    // skip runs: the wave-specialised kernel (loads on waves 0-1, stores on waves 2-3) when the groups
+    // below d fit 128 loader lanes x 4 (A/B: option precomp_ws = 0 keeps k_precomp)
+    const int ngroups = (d + 3) / 4;
+    if (skip && opt(OPT_PRECOMP_WS, 1) != 0 && ngroups <= 128 * 4) {
+      auto wk = ngroups <= 128 * 2 ? k_precomp_ws<2> : (ngroups <= 128 * 3 ? k_precomp_ws<3> : k_precomp_ws<4>);
+      HQ_CHECK_HIP(hipFuncSetAttribute((const void*)wk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(wk, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const float*)in, N, in_stride, d, n,
+                         p, out, out_stride, ld);
+      HQ_CHECK_LAUNCH();
+      return HQ_OK;
+    }
     auto kern = skip ? (kg2 ? (pf ? k_precomp<float, 1, true, 2> : k_precomp<float, 0, true, 2>)
                             : (pf ? k_precomp<float, 1, true, 4> : k_precomp<float, 0, true, 4>))
                      : (pf ? k_precomp<float, 1, false, 4> : k_precomp<float, 0, false, 4>);

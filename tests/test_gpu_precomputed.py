@@ -159,21 +159,28 @@ def test_quantizer_builds_precomputed_index(hq_lib):
     assert qm.metadata.model_name == "pm"
 
 
+@pytest.mark.parametrize("ws", [None, 0])
 @pytest.mark.parametrize("grid", [None, "3"])
 @pytest.mark.parametrize("n,dtype,levels", [(16, np.float32, (6, 2)), (32, np.float32, (6, 2)),
                                              (64, np.float32, (6, 2)), (64, np.float64, (6, 2)),
                                              (32, np.float32, (2, 1)), (64, np.float32, (3, 4))])
-def test_precomputed_stream_zero_padding_skip(hq_lib, hq_option, grid, n, dtype, levels):
+def test_precomputed_stream_zero_padding_skip(hq_lib, hq_option, ws, grid, n, dtype, levels):
     """1-D streams shorter than n*n: squares wholly in the zero padding are skipped (pre_zero_plan) and
     their averages stay +0.0.  d sweeps group edges (d % 4 != 0), block edges and the full image; with
     HQ_PRECOMP_GRID=3 each workgroup loops over several images, so the padding cells and the skipped
-    averages are reused from the once-per-workgroup setup."""
+    averages are reused from the once-per-workgroup setup.  f32 skip runs take the wave-specialised
+    k_precomp_ws (loader / storer waves; 2, 3 or 4 groups per loader lane by d) unless precomp_ws = 0."""
     from hq_mi355x import kernels as K
     if grid is not None:
         hq_option("precomp_grid", int(grid))
+    if ws is not None:
+        hq_option("precomp_ws", ws)
     rng = np.random.default_rng(n * 7 + len(levels))
     ml, ms = levels
-    for d in sorted({1, 3, 4, 5, 63, 64, 65, n * n // 4 + 1, 3 * n * n // 8, n * n - 1, n * n}):
+    ds = {1, 3, 4, 5, 63, 64, 65, n * n // 4 + 1, 3 * n * n // 8, n * n - 1, n * n}
+    if n == 64:
+        ds |= {1023, 1024, 1537, 2047, 2048, 2049, 2050}
+    for d in sorted(ds):
         p = (rng.standard_normal((7, d)) * 10 ** rng.uniform(-2, 2)).astype(dtype)
         p[2] = 0.5
         p[3, ::2] = -0.0
