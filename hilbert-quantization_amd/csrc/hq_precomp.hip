@@ -47,6 +47,7 @@ struct PrePlan {
   int znz;       // zero-padding skip: squares listed over all levels (LDS list entries)
   int znleaves;  // zero-padding skip: leaf tasks over the listed squares
   int nleaves_al;  // LDS-tree partials rounded up so that res stays 16-byte aligned
+  int leaf_rot;    // skip runs: leaf tasks from wave 1 when they fit three waves (pre_leaf_task)
   PreLevel lv[kPreMaxLevels];
 };
 
@@ -95,6 +96,7 @@ static int pre_plan(int n, int max_levels, int min_sq, PrePlan& p) {
   p.nlev = c;
   if (2 * p.maxper > 64) p.tree_lds = 1;  // a square's leaf lanes would span waves
   p.nleaves_al = (p.nleaves + 3) & ~3;  // f64 partials: a multiple of 16 B already
+  p.leaf_rot = 1;
   return HQ_OK;
 }
 
@@ -275,15 +277,16 @@ __device__ __forceinline__ T sq_sum(const T* b, int ld) {
 // all squares of one level with S x S <= 128 values (S = 1, 2, 4, 8): one NumPy pairwise leaf per thread
 template <typename T, int S, bool SK>
 __device__ __forceinline__ void pre_small(const PreLevel& L, const T* img, int ld, float* res, int tid,
-                                          const uint32_t* zl) {
+                                          const uint16_t* zl) {
   const int cnt = SK ? L.zcnt : L.count;
   for (int i = tid; i < cnt; i += kPreThreads) {
     int k;
     const T* b;
     if constexpr (SK) {
-      const uint32_t ent = zl[L.zoff + i];  // (square << 16) | LDS offset of its corner
-      k = (int)(ent >> 16);
-      b = img + (ent & 0xFFFFu);
+      k = zl[L.zoff + i];  // a listed square; its corner from the level geometry
+      int x0, y0;
+      pre_square(L, k, x0, y0);
+      b = img + y0 * ld + x0;
     } else {
       k = i;
       int x0, y0;
@@ -301,7 +304,7 @@ __device__ __forceinline__ void pre_small(const PreLevel& L, const T* img, int l
 
 // once per workgroup before the image loop: see k_precomp's SK path
 template <typename T>
-__device__ __forceinline__ void pre_zero_setup(T* img, float* res, uint32_t* zl, int* zcnt,
+__device__ __forceinline__ void pre_zero_setup(T* img, float* res, uint16_t* zl, int* zcnt,
                                                          const PreLevel* lv, int nlev, int total, int n, int d,
                                                          int ld, int tid) {
   auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
@@ -340,7 +343,7 @@ __device__ __forceinline__ void pre_zero_setup(T* img, float* res, uint32_t* zl,
       base = __shfl(base, 0, 64);
       const int r = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
       if (nz && base + r < L.zcnt)  // counts agree with the host's
-        zl[L.zoff + base + r] = ((uint32_t)k << 16) | (uint32_t)(y0 * ld + x0);
+        zl[L.zoff + base + r] = (uint16_t)k;
     }
   }
   lds_barrier();
@@ -349,11 +352,35 @@ __device__ __forceinline__ void pre_zero_setup(T* img, float* res, uint32_t* zl,
   lds_barrier();
 }
 
+// Skip runs: this thread's half-leaf task, fixed for the workgroup (one round, 2 * znleaves <= 256),
+// resolved once after pre_zero_setup: lt_b = LDS offset of its first value; lt_m = the average's slot
+// (bits 0-11), log2 of the square side (12-15), the leaf within the square (16-20), live (24)
+// When the leaf tasks fit three waves they start at wave 1: the small-square levels fill waves from wave 0
+// (the 8 x 8 squares, fewest, on wave 0 alone), so the waves' LDS work up to the image's barrier evens out.
+__device__ __forceinline__ void pre_leaf_task(const PreLevel* lv, const PrePlan& plan, const uint16_t* zl, int ld,
+                                              int tid, int& lt_b, int& lt_m) {
+  const int rot = 2 * plan.znleaves <= kPreThreads - 64 && plan.leaf_rot ? 64 : 0;
+  const int t = (tid - rot) >> 1;
+  lt_b = 0;
+  lt_m = 0;
+  if (tid < rot || t >= plan.znleaves) return;
+  int l = plan.nlev - 1;
+  while (lv[l].zleaf0 < 0 || t < lv[l].zleaf0) --l;
+  const int lper = 2 * lv[l].lsh - 7;  // log2 of the leaves per square
+  const int slot = (t - lv[l].zleaf0) >> lper, leaf = (t - lv[l].zleaf0) & ((1 << lper) - 1);
+  if (slot >= lv[l].zcnt) return;  // an alignment gap before the next level
+  const int k = zl[lv[l].zoff + slot];
+  int x0, y0;
+  pre_square(lv[l], k, x0, y0);
+  lt_b = y0 * ld + x0 + 4 * (tid & 1);
+  lt_m = (lv[l].off + k) | (lv[l].lsh << 12) | (leaf << 16) | (1 << 24);
+}
+
 // squares of <= 128 values: one thread each, level by level (uniform geometry per loop); 4x4 and 8x8
 // squares read whole row segments (their x0 is a multiple of s/2) and sum in registers
 template <typename T, bool SK>
 __device__ __forceinline__ void pre_small_levels(const PreLevel* lv, int nlev, const T* img, int ld, float* res,
-                                                 int tid, const uint32_t* zl) {
+                                                 int tid, const uint16_t* zl) {
   for (int l = 0; l < nlev; ++l) {
     // this level's geometry from the LDS copy into SGPRs (indexing the kernarg plan by a loop variable
     // keeps the whole plan live in SGPRs, which spill)
@@ -464,7 +491,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
   T* img = reinterpret_cast<T*>(smem);
   T* part = img + ((ld * n + 3) & ~3);  // row stride ld = n + pad (16-B aligned rows spread the bank pattern)
   float* res = reinterpret_cast<float*>(part + (plan.tree_lds ? plan.nleaves_al : 0));  // part: LDS tree only; res 16-B aligned
-  uint32_t* zl = reinterpret_cast<uint32_t*>(res + ((plan.total + 3) & ~3));  // SK: listed squares, per level at zoff
+  uint16_t* zl = reinterpret_cast<uint16_t*>(res + ((plan.total + 3) & ~3));  // SK: listed squares, per level at zoff
   __shared__ int zcnt[kPreMaxLevels];
   const int tid = threadIdx.x;
   const int lsh_n = plan.lsh_n;
@@ -516,24 +543,10 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
       }
     }
   };
-  // SK: this thread's half-leaf task is fixed for the workgroup (one round, 2 * znleaves <= 256):
-  // resolved once here — LDS offset of its first value (lt_b) and, packed in lt_m, the average's slot
-  // (bits 0-11), log2 of the square side (12-15), the leaf within the square (16-20), live (24)
   int lt_b = 0, lt_m = 0;
   if constexpr (SK) {
     pre_zero_setup<T>(img, res, zl, zcnt, lv, plan.nlev, plan.total, n, d, ld, tid);
-    const int t = tid >> 1;
-    if (t < plan.znleaves) {
-      int l = plan.nlev - 1;
-      while (lv[l].zleaf0 < 0 || t < lv[l].zleaf0) --l;
-      const int lper = 2 * lv[l].lsh - 7;  // log2 of the leaves per square
-      const int slot = (t - lv[l].zleaf0) >> lper, leaf = (t - lv[l].zleaf0) & ((1 << lper) - 1);
-      if (slot < lv[l].zcnt) {  // else an alignment gap before the next level
-        const uint32_t ent = zl[lv[l].zoff + slot];
-        lt_b = (int)(ent & 0xFFFFu) + 4 * (tid & 1);
-        lt_m = (lv[l].off + (int)(ent >> 16)) | (lv[l].lsh << 12) | (leaf << 16) | (1 << 24);
-      }
-    }
+    pre_leaf_task(lv, plan, zl, ld, tid, lt_b, lt_m);
   }
   if (PF && lut_on && (int64_t)blockIdx.x < N) fetch(blockIdx.x);
   for (int64_t e = blockIdx.x; e < N; e += gridDim.x) {
@@ -658,13 +671,17 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
   }
 }
 
-// Skip runs of f32 1-D streams, wave-specialised: waves 0-1 load the next image (float4 groups
-// j = lane + 128 i, zero-padded past d) and scatter it into LDS, waves 2-3 store the previous image's
-// averages, both before the image's first barrier; all four waves reduce.  A wave's vector-memory
-// counter then holds one kind of access: on gfx9 the counter is not ordered between loads and stores,
-// so in k_precomp the wait for the prefetched values (vmcnt(0)) also drained the previous image's
-// stores every image.  Two barriers per image instead of three.
-template <int KL>
+// Skip runs of f32 1-D streams, wave-specialised: waves 0-1 load images PD ahead (float4 groups
+// j = lane + 128 i) and scatter them into LDS, waves 2-3 store the previous image's averages, both
+// before the image's first barrier; all four waves reduce.  On gfx9 the vector-memory counter is not
+// ordered between loads and stores: in k_precomp the wait for the prefetched values (vmcnt(0)) also
+// drained the previous image's stores every image.  Here the two roles run separate loops (the same
+// barriers in the same order), so the loader waves' waits count loads only and the storer waves never
+// wait on their stores.  Rows: 16-byte aligned (host), full groups read as float4 (the index clamped,
+// no branch: a fixed number of loads per image, so waiting for image e leaves image e + grid in
+// flight), a partial last group (d % 4) by four clamped dword loads.  Two barriers per image.  The LDS
+// footprint (~30 KiB at n = 64, d = 1536) allows 5 workgroups per CU = 5 waves per SIMD: 96 VGPRs.
+template <int KL, int PD>
 __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))) void k_precomp_ws(
     const float* __restrict__ in, int64_t N, int64_t stride, int d, int n, PrePlan plan, float* __restrict__ out,
     int64_t out_stride, int ld) {
@@ -673,86 +690,98 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
   __shared__ int zcnt[kPreMaxLevels];
   float* img = reinterpret_cast<float*>(smem);
   float* res = img + ((ld * n + 3) & ~3);  // no LDS tree on skip runs
-  uint32_t* zl = reinterpret_cast<uint32_t*>(res + ((plan.total + 3) & ~3));
+  uint16_t* zl = reinterpret_cast<uint16_t*>(res + ((plan.total + 3) & ~3));
   const int tid = threadIdx.x;
-  const bool loader = tid < 128;  // waves 0 and 1
   const int lt = tid & 127;
   const int lsh_n = plan.lsh_n;
   if (tid < plan.nlev) lv[tid] = plan.lv[tid];
   auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  pre_zero_setup<float>(img, res, zl, zcnt, lv, plan.nlev, plan.total, n, d, ld, tid);
+  int lt_b = 0, lt_m = 0;
+  pre_leaf_task(lv, plan, zl, ld, tid, lt_b, lt_m);
+  const int64_t e0 = blockIdx.x, g = gridDim.x;
+  if (e0 >= N) return;  // uniform over the workgroup
+  auto reduce = [&] {
+    if (!PRE_DIAG(1)) pre_small_levels<float, true>(lv, plan.nlev, img, ld, res, tid, zl);
+    if (!PRE_DIAG(2)) pre_leaves_sk<float>(img, ld, res, tid, lt_b, lt_m, plan.maxper);
+  };
+  if (tid >= 128) {  // storer waves: no loads, so their stores are never waited on inside the loop
+    int64_t prev = -1;
+    for (int64_t e = e0; e < N; e += g) {
+      if (prev >= 0 && !PRE_DIAG(8)) pre_store(res, plan.total, out + prev * out_stride, plan.nt, lt, 128);
+      lds_barrier();
+      reduce();
+      lds_barrier();
+      prev = e;
+    }
+    if (!PRE_DIAG(8)) pre_store(res, plan.total, out + prev * out_stride, plan.nt, lt, 128);
+    return;
+  }
+  // loader waves
   const int G = (n * n) >> 2;
+  const int nfull = d >> 2;  // full float4 groups (>= 1: host)
   uint32_t lut[KL];
-  float pf[KL][4];
   {
     const uint32_t* glut = n == 16 ? kPreLut16.v : (n == 32 ? kPreLut32.v : kPreLut64.v);
 #pragma unroll
     for (int i = 0; i < KL; ++i) lut[i] = lt + 128 * i < G ? glut[lt + 128 * i] : 0u;
   }
-  auto fetch = [&](int64_t e) {
+  float pf[PD][KL][4];
+  auto fetch = [&](float (&p)[KL][4], int64_t e) {
     const float* src = in + e * stride;
-    const bool vec_ok = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
-    int dd = d;
-    asm volatile("" : "+s"(dd));
+    int nf = nfull, dd = d;
+    asm volatile("" : "+s"(nf), "+s"(dd));
+#pragma unroll
+    for (int i = 0; i < KL; ++i) {
+      const int j = min(lt + 128 * i, nf - 1);
+      const float4 q4 = *reinterpret_cast<const float4*>(src + 4 * j);
+      p[i][0] = q4.x; p[i][1] = q4.y; p[i][2] = q4.z; p[i][3] = q4.w;
+    }
+    if (dd & 3) {  // the partial group nfull: four clamped loads by every loader lane, kept by its owner
+      float t[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) t[m] = src[min(4 * nf + m, dd - 1)];
+#pragma unroll
+      for (int i = 0; i < KL; ++i)
+        if (lt + 128 * i == nf)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) p[i][m] = 4 * nf + m < dd ? t[m] : 0.0f;
+    }
+  };
+  auto scatter = [&](const float (&p)[KL][4]) {
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
       const int j = lt + 128 * i;
-      if (vec_ok && 4 * j + 3 < dd) {
-        const float4 q4 = *reinterpret_cast<const float4*>(src + 4 * j);
-        pf[i][0] = q4.x; pf[i][1] = q4.y; pf[i][2] = q4.z; pf[i][3] = q4.w;
-      } else if (4 * j < dd) {
+      int dz = d;
+      asm volatile("" : "+s"(dz));
+      if (j >= G || 4 * j >= dz) continue;  // padding stays +0.0 from the setup
+      uint32_t ent = lut[i];
+      asm volatile("" : "+v"(ent));
+      const uint32_t off0 = ent & 0xFFFFu, code = ent >> 16;
+      const uint32_t off = (off0 >> lsh_n) * ld + (off0 & (n - 1));
 #pragma unroll
-        for (int m = 0; m < 4; ++m) pf[i][m] = 4 * j + m < dd ? src[4 * j + m] : 0.0f;  // zero padding
+      for (int m = 0; m < 4; ++m) {
+        const uint32_t b = (code >> (2 * m)) & 3u;
+        img[off + (b & 1u) + (b >> 1) * ld] = p[i][m];
       }
     }
   };
-  pre_zero_setup<float>(img, res, zl, zcnt, lv, plan.nlev, plan.total, n, d, ld, tid);
-  int lt_b = 0, lt_m = 0;
-  {
-    const int t = tid >> 1;
-    if (t < plan.znleaves) {
-      int l = plan.nlev - 1;
-      while (lv[l].zleaf0 < 0 || t < lv[l].zleaf0) --l;
-      const int lper = 2 * lv[l].lsh - 7;
-      const int slot = (t - lv[l].zleaf0) >> lper, leaf = (t - lv[l].zleaf0) & ((1 << lper) - 1);
-      if (slot < lv[l].zcnt) {
-        const uint32_t ent = zl[lv[l].zoff + slot];
-        lt_b = (int)(ent & 0xFFFFu) + 4 * (tid & 1);
-        lt_m = (lv[l].off + (int)(ent >> 16)) | (lv[l].lsh << 12) | (leaf << 16) | (1 << 24);
-      }
+  // every fetch issues its loads (past the last image the index is clamped to N - 1, loaded and never
+  // used): no path without them, so the compiler's wait for set q counts the later sets' loads
+#pragma unroll
+  for (int q = 0; q < PD; ++q) fetch(pf[q], min(e0 + q * g, N - 1));
+  for (int64_t e = e0; e < N; e += PD * g) {
+#pragma unroll
+    for (int q = 0; q < PD; ++q) {
+      const int64_t ee = e + q * g;
+      if (ee >= N) break;  // uniform
+      scatter(pf[q]);
+      lds_barrier();
+      fetch(pf[q], min(ee + PD * g, N - 1));
+      reduce();
+      lds_barrier();
     }
   }
-  if ((int64_t)blockIdx.x >= N) return;  // uniform over the workgroup
-  if (loader) fetch(blockIdx.x);
-  int64_t prev = -1;
-  for (int64_t e = blockIdx.x; e < N; e += gridDim.x) {
-    if (loader) {
-#pragma unroll
-      for (int i = 0; i < KL; ++i) {
-        const int j = lt + 128 * i;
-        int dz = d;
-        asm volatile("" : "+s"(dz));
-        if (j >= G || 4 * j >= dz) continue;  // padding stays +0.0 from the setup
-        uint32_t ent = lut[i];
-        asm volatile("" : "+v"(ent));
-        const uint32_t off0 = ent & 0xFFFFu, code = ent >> 16;
-        const uint32_t off = (off0 >> lsh_n) * ld + (off0 & (n - 1));
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const uint32_t b = (code >> (2 * m)) & 3u;
-          img[off + (b & 1u) + (b >> 1) * ld] = pf[i][m];
-        }
-      }
-    } else if (prev >= 0 && !PRE_DIAG(8)) {
-      pre_store(res, plan.total, out + prev * out_stride, plan.nt, lt, 128);
-    }
-    lds_barrier();
-    if (loader && e + gridDim.x < N) fetch(e + gridDim.x);
-    if (!PRE_DIAG(1)) pre_small_levels<float, true>(lv, plan.nlev, img, ld, res, tid, zl);
-    if (!PRE_DIAG(2)) pre_leaves_sk<float>(img, ld, res, tid, lt_b, lt_m, plan.maxper);
-    lds_barrier();
-    prev = e;
-  }
-  if (!loader && !PRE_DIAG(8)) pre_store(res, plan.total, out + prev * out_stride, plan.nt, lt, 128);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -951,6 +980,7 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
                 n, max_levels, min_square_size);
   if (out_stride < p.total) return fail(HQ_E_INVALID, "out_stride %lld < %d averages", (long long)out_stride, p.total);
   p.nt = opt(OPT_PRECOMP_NT, p.nt) != 0;
+  p.leaf_rot = opt(OPT_PRECOMP_LEAF_ROT, 1) != 0;  // A/B
   if (opt_on(OPT_PRECOMP_TREE_LDS)) p.tree_lds = 1;  // A/B: combine leaves through LDS
 #ifdef HQ_DIAG  // phase-skipping diagnostics (wrong averages): A/B builds only (make DIAG=1)
   p.diag = (int)opt(OPT_PRECOMP_DIAG, p.diag);
@@ -964,7 +994,7 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   // A/B: option precomp_skip = 0 computes every square
   const bool skip = use_lut && !p.tree_lds && opt(OPT_PRECOMP_SKIP, 1) != 0 && pre_zero_plan(n, d, p);
   const size_t lds = (size_t)esz * ((size_t)((ld * n + 3) & ~3) + (p.tree_lds ? p.nleaves_al : 0)) + 4 * (size_t)((p.total + 3) & ~3) +
-                     (skip ? 4 * (size_t)p.znz : 0);
+                     (skip ? 2 * (size_t)p.znz : 0);
   if (lds > 160 * 1024) return fail(HQ_E_UNSUPPORTED, "pre-computed index n=%d dtype %d needs %zu B of LDS", n, dtype, lds);
   hipStream_t s = (hipStream_t)stream;
   // skip runs: a workgroup loops over many images (the list setup is amortised) and prefetches the
@@ -976,11 +1006,17 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   if (dtype == HQ_F32) {
     // groups of 4 values a thread scatters: a skip run touches only groups below d
     const bool kg2 = skip && (d + 3) / 4 <= 2 * kPreThreads;
-    // skip runs: the wave-specialised kernel (loads on waves 0-1, stores on waves 2-3) when the groups
-    // below d fit 128 loader lanes x 4 (A/B: option precomp_ws = 0 keeps k_precomp)
+    // skip runs: the wave-specialised kernel (loads on waves 0-1, stores on waves 2-3) when the row
+    // bases are 16-byte aligned and the groups below d fit 128 loader lanes x 4 (A/B: option
+    // precomp_ws = 0 keeps k_precomp; 2 prefetches two images ahead: 4.36 vs 4.23 ms for one, the
+    // compiler's waits still drain both register sets)
     const int ngroups = (d + 3) / 4;
-    if (skip && opt(OPT_PRECOMP_WS, 1) != 0 && ngroups <= 128 * 4) {
-      auto wk = ngroups <= 128 * 2 ? k_precomp_ws<2> : (ngroups <= 128 * 3 ? k_precomp_ws<3> : k_precomp_ws<4>);
+    const int64_t ws = opt(OPT_PRECOMP_WS, 1);
+    if (skip && ws != 0 && d >= 4 && ngroups <= 128 * 4 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
+        (in_stride & 3) == 0) {
+      const int kl = ngroups <= 128 * 2 ? 2 : (ngroups <= 128 * 3 ? 3 : 4);
+      auto wk = ws == 1 ? (kl == 2 ? k_precomp_ws<2, 1> : (kl == 3 ? k_precomp_ws<3, 1> : k_precomp_ws<4, 1>))
+                        : (kl == 2 ? k_precomp_ws<2, 2> : (kl == 3 ? k_precomp_ws<3, 2> : k_precomp_ws<4, 2>));
       HQ_CHECK_HIP(hipFuncSetAttribute((const void*)wk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       hipLaunchKernelGGL(wk, dim3((unsigned)grid64), dim3(kPreThreads), lds, s, (const float*)in, N, in_stride, d, n,
                          p, out, out_stride, ld);
