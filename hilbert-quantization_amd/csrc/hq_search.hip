@@ -4680,13 +4680,15 @@ __device__ __forceinline__ void ov_bound(const flt4* acc, const float* wia, floa
 // One wave = 32 queries (two blocks b of 16; lane (g, j) owns queries 16b + j) x one chunk, 16 rows per
 // step (lane group g owns rows 4g + r: the MFMA D layout), NG MFMAs (HI: hi.hi only) or NG x 3 (split) per
 // block and step.  HI: the bound takes G_hihi, each segment's slack |G_split - G_hihi| < 1e-3 m + 1e-4 (as
-// k_scan0g) folded into bsum (relu(G + d) <= relu(G) + d), and the drain recomputes the split G of every
-// queued pair (ov_split_g) for the model score; the queue then holds the (row, query) key only.
+// k_scan0g) folded into bsum (relu(G + d) <= relu(G) + d).  The queue holds G_hihi per segment; the drain
+// first evaluates the f32 model at G_hihi + slack — the model is non-decreasing in every G (c1 > 0,
+// qA sd >= 0, monotone f32 operations) so that value bounds the model at the split G — and recomputes
+// the split G (ov_split_g) only for the pairs whose bound reaches the pool threshold.
 template <int LID, int OCC, bool HI = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_scanov(OvArgs a) {
   using T = OvT<LID>;
   constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, NB = kOvQW / 16, GS = 16 * NG + 4 * NC + 8;
-  __shared__ flt4 qg[HI ? 1 : kOvQCap];  // queue: G of each G segment (split form) ...
+  __shared__ flt4 qg[kOvQCap];  // queue: G of each G segment (split form; HI: hi.hi) ...
   __shared__ int qk[kOvQCap];   // ... and (row - c_begin) << 5 | query within the wave
   __shared__ QOvD qs[kOvQW];    // the wave's model constants (the drain reads them per entry)
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
@@ -4767,14 +4769,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
       const QOvD& c = qs[eqi];
       if (row < c_end) {
         float G[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        if constexpr (HI) {
-          ov_split_g<T>(a.Zq, a.Zc, q, row, G);
-        } else {
-          const flt4 eg = qg[lane];
+        const flt4 eg = qg[lane];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) G[i] = eg[i];
+        for (int i = 0; i < 4; ++i) G[i] = eg[i];
+        bool need = true;
+        if constexpr (HI) {  // the gate: the model at G_hihi + slack (an upper bound of the split score)
+          float Gu[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+          for (int i = 0; i < NG; ++i) Gu[i] = G[i] + (1e-3f * (float)o.gplen[i] + 1e-4f);
+          need = ov_model<NG, NC>(o, c, a.Sc32, row, Gu, a.Sq, a.Sc, q) >= c.thl;
+          if (need) ov_split_g<T>(a.Zq, a.Zc, q, row, G);
         }
-        const float s = ov_model<NG, NC>(o, c, a.Sc32, row, G, a.Sq, a.Sc, q);
+        const float s = need ? ov_model<NG, NC>(o, c, a.Sc32, row, G, a.Sq, a.Sc, q) : -1.0f;
         if (s >= c.thl) {
           const int slot = atomicAdd(a.pool_n + q, 1);
           if (slot < a.pool_cap) {
@@ -4790,12 +4796,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
       flt4 tg = {0.0f, 0.0f, 0.0f, 0.0f};
       int tk = 0;
       if (mv) {
-        if constexpr (!HI) tg = qg[b0 + lane];
+        tg = qg[b0 + lane];
         tk = qk[b0 + lane];
       }
       wave_lds_sync();
       if (mv) {
-        if constexpr (!HI) qg[b0 - n + lane] = tg;
+        qg[b0 - n + lane] = tg;
         qk[b0 - n + lane] = tk;
       }
       wave_lds_sync();
@@ -4824,12 +4830,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
       if (m) {
         if ((m >> lane) & 1ull) {
           const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-          if constexpr (!HI) {
-            flt4 gg = {0.0f, 0.0f, 0.0f, 0.0f};
+          flt4 gg = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-            for (int i = 0; i < NG; ++i) gg[i] = acc[i][r];
-            qg[pos] = gg;
-          }
+          for (int i = 0; i < NG; ++i) gg[i] = acc[i][r];
+          qg[pos] = gg;
           qk[pos] = (int)((cs - c_begin + 4 * g + r) << 5) | (16 * b + j);
         }
         qn += __popcll(m);
