@@ -4369,11 +4369,17 @@ template <int LID> struct OvT;
 // never straddles two; padding values are zero in both copies and may be attributed to either side)
 template <> struct OvT<0> {  // L = 64: [32 | 8, 3, 20], one one-value segment
   static constexpr int NKB = 2, NG = 4, NC = 1;
+  // LIN form: the K-block contracted once with per-segment scaled query values (LKB), and whether
+  // K-block 0 holds segment 0 alone (its scaled contraction then seeds the linear sum)
+  static constexpr int LKB = 1;
+  static constexpr bool LC0 = true;
   static constexpr int kb(int i) { return i == 0 ? 0 : 1; }
   static constexpr int seg(int b, int k) { return b == 0 ? 0 : (k < 8 ? 1 : (k < 12 ? 2 : 3)); }
 };
 template <> struct OvT<1> {  // L = 32: [16, 4, 11], one one-value segment
   static constexpr int NKB = 1, NG = 3, NC = 1;
+  static constexpr int LKB = 0;
+  static constexpr bool LC0 = false;
   static constexpr int kb(int) { return 0; }
   static constexpr int seg(int, int k) { return k < 16 ? 0 : (k < 20 ? 1 : 2); }
 };
@@ -4680,15 +4686,24 @@ __device__ __forceinline__ void ov_bound(const flt4* acc, const float* wia, floa
 // One wave = 32 queries (two blocks b of 16; lane (g, j) owns queries 16b + j) x one chunk, 16 rows per
 // step (lane group g owns rows 4g + r: the MFMA D layout), NG MFMAs (HI: hi.hi only) or NG x 3 (split) per
 // block and step.  HI: the bound takes G_hihi, each segment's slack |G_split - G_hihi| < 1e-3 m + 1e-4 (as
-// k_scan0g) folded into bsum (relu(G + d) <= relu(G) + d).  The queue holds G_hihi per segment; the drain
-// first evaluates the f32 model at G_hihi + slack — the model is non-decreasing in every G (c1 > 0,
-// qA sd >= 0, monotone f32 operations) so that value bounds the model at the split G — and recomputes
-// the split G (ov_split_g) only for the pairs whose bound reaches the pool threshold.
-template <int LID, int OCC, bool HI = true>
+// k_scan0g) folded into bsum (relu(G + d) <= relu(G) + d), and the drain recomputes the split G of every
+// queued pair (ov_split_g) for the model score; the queue then holds the (row, query) key only.
+//
+// LIN (default with HI): the weighted relu sum in two parts, w relu(G) = s (G + |G|) with s = w ia / 2
+// per segment and query.  The query's masked copies are pre-scaled by s in f16 (acc_i = s_i G_i), one
+// more contraction of the shared K-block with per-segment scaled values (seeded with K-block 0's
+// acc_0 when that block holds segment 0 alone) gives the linear part sum_i s_i G_i, and the bound is
+// acc_lin + ro + sum_i |acc_i|: one VALU add (abs source modifier) per segment and pair instead of a
+// med3 and an fma; the pair passes when it reaches the query's threshold less bsum and, per matching
+// one-value segment, less its weight (A/B, cfg3 overall QPS: 0.88M vs 0.83M for the med3 + fma bound;
+// a drain gate on the model at G_hihi + slack before the split measured slower, 0.69M, as did keeping
+// G_hihi in the queue: the kernel is not bound by the drain's split recompute).  The f16 scaling errs by <= 2^-11 s_i sum|q c| <= 2^-11 s_i m_i
+// in each part (Cauchy-Schwarz on unit-variance vectors), folded into bsum with the hi.hi slack.
+template <int LID, int OCC, bool HI = true, bool LIN = HI>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_scanov(OvArgs a) {
   using T = OvT<LID>;
   constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, NB = kOvQW / 16, GS = 16 * NG + 4 * NC + 8;
-  __shared__ flt4 qg[kOvQCap];  // queue: G of each G segment (split form; HI: hi.hi) ...
+  __shared__ flt4 qg[HI ? 1 : kOvQCap];  // queue: G of each G segment (split form) ...
   __shared__ int qk[kOvQCap];   // ... and (row - c_begin) << 5 | query within the wave
   __shared__ QOvD qs[kOvQW];    // the wave's model constants (the drain reads them per entry)
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
@@ -4715,8 +4730,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
   }
   wave_lds_sync();
 
-  half8 qh[NB][NG], ql[HI ? 1 : NB][NG];
-  float wia[NB][NG], bsum[NB], wt[NB], qv[NB][NC > 0 ? NC : 1], tolq[NB][NC > 0 ? NC : 1];
+  static_assert(!LIN || HI, "the LIN bound is a hi.hi form");
+  half8 qh[NB][NG], ql[HI ? 1 : NB][NG], qlin[LIN ? NB : 1];
+  float wia[LIN ? 1 : NB][NG], bsum[NB], wt[NB], qv[NB][NC > 0 ? NC : 1], tolq[NB][NC > 0 ? NC : 1];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int q = q0 + 16 * b + j;
@@ -4725,16 +4741,47 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
     half8 lo_unused[NG];
     ov_query_frags<T>(a, qq, g, qh[b], HI ? lo_unused : ql[HI ? 0 : b]);
     const QOv& c = a.qc[qq];
+    float wi[NG];
 #pragma unroll
-    for (int i = 0; i < NG; ++i) wia[b][i] = c.wia[i];
+    for (int i = 0; i < NG; ++i) wi[i] = c.wia[i];
+    if constexpr (!LIN) {
+#pragma unroll
+      for (int i = 0; i < NG; ++i) wia[b][i] = wi[i];
+    }
     bsum[b] = c.bsum;
     if constexpr (HI) {
 #pragma unroll
-      for (int i = 0; i < NG; ++i) bsum[b] = fmaf(wia[b][i], 1e-3f * (float)o.gplen[i] + 1e-4f, bsum[b]);
+      for (int i = 0; i < NG; ++i) bsum[b] = fmaf(wi[i], 1e-3f * (float)o.gplen[i] + 1e-4f, bsum[b]);
     }
 #pragma unroll
     for (int ci = 0; ci < NC; ++ci) { qv[b][ci] = c.cv[ci]; tolq[b][ci] = c.tolq[ci]; }
     wt[b] = (v && __float_as_int(c.flag) == 0) ? c.wthr : __builtin_huge_valf();  // flagged query: dense path
+    if constexpr (LIN) {
+      // scaled copies: masked per segment (s_i q), and the shared K-block with each value scaled by its
+      // segment's s; slack 2 x 2^-11 s_i m_i (both parts) + accumulation
+      float sl = 0.0f;
+#pragma unroll
+      for (int i = 0; i < NG; ++i) {
+        const float si = 0.5f * wi[i];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qh[b][i][e] = (_Float16)(si * (float)qh[b][i][e]);
+        sl = fmaf(si, (float)o.gplen[i] * 1.0e-3f + 1e-5f, sl);
+      }
+      const _Float16* zr = a.Zq + ov_frag(qq, T::LKB, T::NKB, g);
+      const half8 hv = *reinterpret_cast<const half8*>(zr);
+      half8 lv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int i = T::seg(T::LKB, 8 * g + e);
+        float si = 0.0f;
+#pragma unroll
+        for (int ii = 0; ii < NG; ++ii) si = ii == i ? 0.5f * wi[ii] : si;
+        lv[e] = (_Float16)(si * (float)hv[e]);
+      }
+      qlin[b] = lv;
+      bsum[b] += sl;
+      wt[b] = wt[b] - bsum[b];  // the pair passes when acc_lin + sum |acc_i| (+ one-value terms) reach this
+    }
   }
 
   const _Float16* zb = a.Zc + (c_begin >> 4) * NKB * kZ16Tile + lane * 8;
@@ -4769,18 +4816,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
       const QOvD& c = qs[eqi];
       if (row < c_end) {
         float G[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        const flt4 eg = qg[lane];
+        if constexpr (HI) {
+          ov_split_g<T>(a.Zq, a.Zc, q, row, G);
+        } else {
+          const flt4 eg = qg[lane];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) G[i] = eg[i];
-        bool need = true;
-        if constexpr (HI) {  // the gate: the model at G_hihi + slack (an upper bound of the split score)
-          float Gu[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-          for (int i = 0; i < NG; ++i) Gu[i] = G[i] + (1e-3f * (float)o.gplen[i] + 1e-4f);
-          need = ov_model<NG, NC>(o, c, a.Sc32, row, Gu, a.Sq, a.Sc, q) >= c.thl;
-          if (need) ov_split_g<T>(a.Zq, a.Zc, q, row, G);
+          for (int i = 0; i < 4; ++i) G[i] = eg[i];
         }
-        const float s = need ? ov_model<NG, NC>(o, c, a.Sc32, row, G, a.Sq, a.Sc, q) : -1.0f;
+        const float s = ov_model<NG, NC>(o, c, a.Sc32, row, G, a.Sq, a.Sc, q);
         if (s >= c.thl) {
           const int slot = atomicAdd(a.pool_n + q, 1);
           if (slot < a.pool_cap) {
@@ -4796,12 +4839,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
       flt4 tg = {0.0f, 0.0f, 0.0f, 0.0f};
       int tk = 0;
       if (mv) {
-        tg = qg[b0 + lane];
+        if constexpr (!HI) tg = qg[b0 + lane];
         tk = qk[b0 + lane];
       }
       wave_lds_sync();
       if (mv) {
-        qg[b0 - n + lane] = tg;
+        if constexpr (!HI) qg[b0 - n + lane] = tg;
         qk[b0 - n + lane] = tk;
       }
       wave_lds_sync();
@@ -4822,18 +4865,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
       for (int i = 0; i < NG; ++i)
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.f[T::kb(i)][HI ? 0 : 1], qh[b][i], acc[i], 0, 0, 0);
     }
-    float U[4];
-    ov_bound<T>(acc, wia[b], bsum[b], o, qv[b], tolq[b], cur.cv, cur.ro, U);
+    float U[4], W[4];
+    if constexpr (LIN) {
+      const flt4 al = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.f[T::LKB][0], qlin[b], T::LC0 ? acc[0] : flt4{0, 0, 0, 0},
+                                                              0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float u = al[r] + cur.ro[r];  // rows with zero-variance G segments: their smaller bound
+#pragma unroll
+        for (int i = 0; i < NG; ++i) u += fabsf(acc[i][r]);
+        float t = wt[b];
+#pragma unroll
+        for (int ci = 0; ci < NC; ++ci) {
+          const float d = fabsf(qv[b][ci] - cur.cv[ci][r]);
+          t = d <= fmaf(2.5e-7f, fabsf(cur.cv[ci][r]), tolq[b][ci]) ? t - o.cw[ci] : t;
+        }
+        U[r] = u;
+        W[r] = t;
+      }
+    } else {
+      ov_bound<T>(acc, wia[b], bsum[b], o, qv[b], tolq[b], cur.cv, cur.ro, U);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) W[r] = wt[b];
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const unsigned long long m = __builtin_amdgcn_ballot_w64(U[r] >= wt[b]);
+      const unsigned long long m = __builtin_amdgcn_ballot_w64(U[r] >= W[r]);
       if (m) {
         if ((m >> lane) & 1ull) {
           const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-          flt4 gg = {0.0f, 0.0f, 0.0f, 0.0f};
+          if constexpr (!HI) {
+            flt4 gg = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-          for (int i = 0; i < NG; ++i) gg[i] = acc[i][r];
-          qg[pos] = gg;
+            for (int i = 0; i < NG; ++i) gg[i] = acc[i][r];
+            qg[pos] = gg;
+          }
           qk[pos] = (int)((cs - c_begin + 4 * g + r) << 5) | (16 * b + j);
         }
         qn += __popcll(m);
@@ -5121,6 +5187,8 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
   if (opt_on(OPT_SCANOV_SPLIT3)) {
     if (oocc == 3) hipLaunchKernelGGL((k_scanov<LID, 3, false>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
     else hipLaunchKernelGGL((k_scanov<LID, 2, false>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  } else if (opt_on(OPT_SCANOV_V1)) {  // the med3 + fma bound
+    hipLaunchKernelGGL((k_scanov<LID, 4, true, false>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else if (oocc == 2) {
     hipLaunchKernelGGL((k_scanov<LID, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else if (oocc == 3) {
