@@ -4699,7 +4699,7 @@ __device__ __forceinline__ void ov_bound(const flt4* acc, const float* wia, floa
 // a drain gate on the model at G_hihi + slack before the split measured slower, 0.69M, as did keeping
 // G_hihi in the queue: the kernel is not bound by the drain's split recompute).  The f16 scaling errs by <= 2^-11 s_i sum|q c| <= 2^-11 s_i m_i
 // in each part (Cauchy-Schwarz on unit-variance vectors), folded into bsum with the hi.hi slack.
-template <int LID, int OCC, bool HI = true, bool LIN = HI>
+template <int LID, int OCC, bool HI = true, bool LIN = HI, int PF = 1>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_scanov(OvArgs a) {
   using T = OvT<LID>;
   constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, NB = kOvQW / 16, GS = 16 * NG + 4 * NC + 8;
@@ -4915,18 +4915,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
     for (int b = 0; b < NB; ++b) block(b, cur, c_begin + s * kCS);
   };
 
-  CStep cA, cB;
-  load_step(cA, 0);
-  int64_t s = 0;
-  for (; s + 1 < nsteps; s += 2) {
-    load_step(cB, s + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    step(cA, s);
-    load_step(cA, s + 2);
-    __builtin_amdgcn_sched_barrier(0);
-    step(cB, s + 1);
+  if constexpr (PF == 1) {  // two buffers, ping-pong
+    CStep cA, cB;
+    load_step(cA, 0);
+    int64_t s = 0;
+    for (; s + 1 < nsteps; s += 2) {
+      load_step(cB, s + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      step(cA, s);
+      load_step(cA, s + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      step(cB, s + 1);
+    }
+    if (s < nsteps) step(cA, s);
+    wave_lds_sync();
+    while (qn > 0) drain(qn < 64 ? qn : 64);
+    return;
   }
-  if (s < nsteps) step(cA, s);
+  // PF + 1 step buffers in rotation: step s + PF is requested while step s is scored (load_step clamps
+  // the index to the chunk's last step)
+  CStep buf[PF + 1];
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load_step(buf[u], u);
+  auto body = [&](const int64_t st, const CStep& cur, CStep& nn) {
+    load_step(nn, st + PF);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch PF steps ahead
+    step(cur, st);
+  };
+  int64_t s = 0;
+  for (; s + PF < nsteps; s += PF + 1) {
+#pragma unroll
+    for (int u = 0; u <= PF; ++u) body(s + u, buf[u], buf[(u + PF) % (PF + 1)]);
+  }
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (s + u < nsteps) step(buf[u], s + u);
   wave_lds_sync();
   while (qn > 0) drain(qn < 64 ? qn : 64);
 }
@@ -5189,6 +5212,12 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
     else hipLaunchKernelGGL((k_scanov<LID, 2, false>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else if (opt_on(OPT_SCANOV_V1)) {  // the med3 + fma bound
     hipLaunchKernelGGL((k_scanov<LID, 4, true, false>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  } else if (opt(OPT_OV_PF, 1) == 2) {  // prefetch distance (steps)
+    if (oocc == 3) hipLaunchKernelGGL((k_scanov<LID, 3, true, true, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((k_scanov<LID, 4, true, true, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  } else if (opt(OPT_OV_PF, 1) == 3) {
+    if (oocc == 3) hipLaunchKernelGGL((k_scanov<LID, 3, true, true, 3>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((k_scanov<LID, 4, true, true, 3>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else if (oocc == 2) {
     hipLaunchKernelGGL((k_scanov<LID, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else if (oocc == 3) {

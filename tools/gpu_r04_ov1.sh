@@ -16,4 +16,4 @@ import json,sys; d=json.loads(open('$O/ov1_$tag.json').read().strip().splitlines
 print('%-10s search %.3fM  ov %.3fM  l0 %.3fM  m100 %.3fM  m1000 %.3fM' % ('$tag', s['value']/1e6, m['overall']['value']/1e6, m['level0']['value']/1e6, m['m100']['value']/1e6, m['m1000']['value']/1e6))" || echo "$tag rc=$rc"
   return $rc
 }
-run new && run occ3 ov_occ=3 && run v1 scanov_v1=1 && run old HQ_LIB_VARIANT=$GRAFT_REPO_ROOT/.baseline_pc/libhq_mi355x.so && run new2
+run new && run pf2occ3 ov_pf=2 ov_occ=3 && run pf3occ3 ov_pf=3 ov_occ=3 && run pf2 ov_pf=2 && run new2
