@@ -326,8 +326,8 @@ __device__ double exact_pair_rows(const double* ra, const double* za, const doub
   if (level >= 0) {
     if (level >= si.nseg) return 0.0;
     const int s = level;
-    const double v = exact_level<SM>(ra + si.src[s], za + si.poff[s], sa + 4 * s, rb + si.src[s], zb + si.poff[s],
-                                     sb + 4 * s, si.len[s], &t32);
+    const double v = exact_level<SM>(ra + si.src[s], za ? za + si.poff[s] : nullptr, sa + 4 * s, rb + si.src[s],
+                                     zb ? zb + si.poff[s] : nullptr, sb + 4 * s, si.len[s], &t32);
     if (typed) *typed = t32;
     return v;
   }
@@ -337,8 +337,8 @@ __device__ double exact_pair_rows(const double* ra, const double* za, const doub
   double tws = 0.0, tw = 0.0;
   bool acc32 = false;
   for (int s = 0; s < si.nseg; ++s) {
-    const double v = exact_level<SM>(ra + si.src[s], za + si.poff[s], sa + 4 * s, rb + si.src[s], zb + si.poff[s],
-                                 sb + 4 * s, si.len[s], &t32);
+    const double v = exact_level<SM>(ra + si.src[s], za ? za + si.poff[s] : nullptr, sa + 4 * s, rb + si.src[s],
+                                     zb ? zb + si.poff[s] : nullptr, sb + 4 * s, si.len[s], &t32);
     if (lv) lv[s] = v;
     const double w = 1.0 / (double)(s + 1);
     const double term = t32 ? (double)((float)v * (float)w) : v * w;
@@ -361,11 +361,14 @@ __device__ double exact_pair_rows(const double* ra, const double* za, const doub
   return ov > 0.0 ? ov : 0.0;
 }
 
-template <bool SM = false>
+// ZB = false: B's normalised values are recomputed from its raw values and statistics ((x - mean) / std
+// in f64, the exact operation that wrote Z: bit-identical), so B's Z rows are not read — the re-rank and
+// re-score kernels read only the candidates' raw rows and statistics (half the bytes of a row pair)
+template <bool SM = false, bool ZB = true>
 __device__ double exact_pair(const VecSet& A, int64_t ia, const VecSet& B, int64_t ib, const SegInfo& si, int level,
                              double* lv, int* typed = nullptr) {
   return exact_pair_rows<SM>(A.raw + ia * si.L, A.Z + ia * si.Lp, A.S + ia * si.nseg * 4, B.raw + ib * si.L,
-                         B.Z + ib * si.Lp, B.S + ib * si.nseg * 4, si, level, lv, typed);
+                             ZB ? B.Z + ib * si.Lp : nullptr, B.S + ib * si.nseg * 4, si, level, lv, typed);
 }
 
 // The reference's threshold test of a level score (search_engine.py:284-292 `>=`, video_search.py:244 `>`)
@@ -441,7 +444,7 @@ __global__ __launch_bounds__(kLsTile) void k_level_scores_lds(VecSet Qs, int Q, 
 // exact overall + per-level for selected (query, candidate) pairs; ids are global, id_base subtracted.
 // G lanes per pair (G >= nseg): lane s computes level s, the pair's first lane adds them up in level
 // order with the reference's typing (exact_pair's sum), so the 5-7 level scores run in parallel.
-template <int G, bool SM = false>
+template <int G, bool SM = false, bool ZC = true>
 __global__ __launch_bounds__(256) void k_rescore(VecSet Qs, int Q, VecSet Cs, int64_t N, SegInfo si,
                                                  const int64_t* __restrict__ ids, int k, int64_t id_base,
                                                  double* __restrict__ out) {
@@ -461,8 +464,8 @@ __global__ __launch_bounds__(256) void k_rescore(VecSet Qs, int Q, VecSet Cs, in
     if (ok && sub < si.nseg) {
       const int s = sub;
       v = exact_level<SM>(Qs.raw + q * si.L + si.src[s], Qs.Z + q * si.Lp + si.poff[s], Qs.S + (q * si.nseg + s) * 4,
-                      Cs.raw + c * si.L + si.src[s], Cs.Z + c * si.Lp + si.poff[s], Cs.S + (c * si.nseg + s) * 4,
-                      si.len[s], &t32);
+                      Cs.raw + c * si.L + si.src[s], ZC ? Cs.Z + c * si.Lp + si.poff[s] : nullptr,
+                      Cs.S + (c * si.nseg + s) * 4, si.len[s], &t32);
     }
     if (sub < si.nseg) o[1 + sub] = v;
     // search_engine.py:191-230 typed running sum (see exact_pair), gathered from the group's lanes
@@ -3600,7 +3603,9 @@ static void launch_pool_select(int K, hipStream_t s, int Q, float* pool_s, int* 
 // levels into the record directly).  The LDS-staged form of round 4's first version (tiles of rows, one
 // level task per thread) spent most of its time in the staging round trips: 111 us at M = 100, 923 us at
 // M = 1000 per 1000-query batch.
-template <bool SM>
+// ZB: the candidates' normalised values from Z (true) or recomputed from their raw rows (false: half the
+// bytes, an f64 division per value; A/B per 1000-query batch: M = 1000 896 -> 746 us, M = 100 116 -> 129)
+template <bool SM, bool ZB = true>
 __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
   if (onext && blockIdx.x == 0 && threadIdx.x == 0) *onext = 0;  // the next batch's redo counter
   __shared__ double se[kMaxTopKBig];
@@ -3624,7 +3629,7 @@ __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
         const int64_t c = cid_x - id_base;
         if (cid_x >= 0 && c >= 0 && c < N) {
           int typed = 0;
-          const double v = exact_pair<SM>(Qs, q, Cs, c, si, mode == 0 ? 0 : -1, nullptr, &typed);
+          const double v = exact_pair<SM, ZB>(Qs, q, Cs, c, si, mode == 0 ? 0 : -1, nullptr, &typed);
           const bool pass = mode == 0 ? typed_pass(v, typed, thr, thr_mode)
                                       : (thr_mode == 0 || (thr_mode == 1 ? v >= thr : v > thr));
           if (pass) {
@@ -3665,7 +3670,7 @@ __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
         double* rec = odet + ((int64_t)q * k + x) * W;
         if (x < cnt) {
           // ---- pass 2: the output entry's [overall, level..] record ----
-          rec[0] = exact_pair<SM>(Qs, q, Cs, sid[x] - id_base, si, -1, rec + 1);
+          rec[0] = exact_pair<SM, ZB>(Qs, q, Cs, sid[x] - id_base, si, -1, rec + 1);
         } else {
           for (int w = 0; w < W; ++w) rec[w] = 0.0;
         }
@@ -3693,6 +3698,12 @@ __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
 
 __global__ __launch_bounds__(256) void k_refine_big_sm(HQ_REFINE_ARGS, int tb) { refine_big_body<true>(HQ_REFINE_PASS, tb); }
 __global__ __launch_bounds__(256) void k_refine_big(HQ_REFINE_ARGS, int tb) { refine_big_body<false>(HQ_REFINE_PASS, tb); }
+__global__ __launch_bounds__(256) void k_refine_big_sm_raw(HQ_REFINE_ARGS, int tb) {
+  refine_big_body<true, false>(HQ_REFINE_PASS, tb);
+}
+__global__ __launch_bounds__(256) void k_refine_big_raw(HQ_REFINE_ARGS, int tb) {
+  refine_big_body<false, false>(HQ_REFINE_PASS, tb);
+}
 
 // k_progressive_final for M > 64: wave 0 selects the survivors (final_survivors), the workgroup sorts them
 // by (overall desc, survivor position asc) — the reference's stable sort — in LDS
@@ -4282,14 +4293,12 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
   if (out_redo && !next_redo) HQ_CHECK_HIP(hipMemsetAsync(out_redo, 0, sizeof(int), s));
   const bool sm = seg_small(si);
   if (kp > kMaxTopK) {  // long lists: rows read from global memory, one workgroup per query
-    if (sm)
-      hipLaunchKernelGGL(k_refine_big_sm, dim3(grid), dim3(256), 0, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
-                         mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
-                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, next_redo, 0);
-    else
-      hipLaunchKernelGGL(k_refine_big, dim3(grid), dim3(256), 0, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si,
-                         mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id,
-                         out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, next_redo, 0);
+    // lists of >= 512: the candidates' raw rows only (refine_big_body's ZB)
+    const bool raw = kp >= 512;
+    auto kern = sm ? (raw ? k_refine_big_sm_raw : k_refine_big_sm) : (raw ? k_refine_big_raw : k_refine_big);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si, mode,
+                       cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, out_score, out_id, out_count,
+                       out_resolved, count_empty ? 1 : 0, out_redo, out_det, 0, next_redo, 0);
     HQ_CHECK_LAUNCH();
     return HQ_OK;
   }
