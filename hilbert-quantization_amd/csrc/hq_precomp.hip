@@ -54,6 +54,9 @@ struct PrePlan {
   int znleaves;  // zero-padding skip: leaf tasks over the listed squares
   int nleaves_al;  // LDS-tree partials rounded up so that res stays 16-byte aligned
   int leaf_rot;    // skip runs: leaf tasks from wave 1 when they fit three waves (pre_leaf_task)
+  int g2reg;       // k_precomp_ws: the 2 x 2 grid squares (= Hilbert groups) averaged in the loader's
+                   // registers, not listed; g2lvl = their level (-1: none)
+  int g2lvl;
   PreLevel lv[kPreMaxLevels];
 };
 
@@ -103,6 +106,10 @@ static int pre_plan(int n, int max_levels, int min_sq, PrePlan& p) {
   if (2 * p.maxper > 64) p.tree_lds = 1;  // a square's leaf lanes would span waves
   p.nleaves_al = (p.nleaves + 3) & ~3;  // f64 partials: a multiple of 16 B already
   p.leaf_rot = 1;
+  p.g2reg = 0;
+  p.g2lvl = -1;
+  for (int i = 0; i < p.nlev; ++i)
+    if (p.lv[i].s == 2 && p.lv[i].leaf0 < 0) p.g2lvl = i;
   return HQ_OK;
 }
 
@@ -148,6 +155,7 @@ static int pre_zero_plan(int n, int d, PrePlan& p, std::vector<std::vector<int>>
         if (h >= 2) start &= ~(h * h - 1);
         nz |= start < d;
       }
+      if (p.g2reg && l == p.g2lvl && k < L.g * L.g) nz = false;  // averaged in the loader's registers
       L.zcnt += nz;
       if (nz && lists) (*lists)[l].push_back(k);
     }
@@ -239,11 +247,11 @@ static void pre_bank_order(std::vector<int>& ks, const PreLevel& L, int ld) {
 static const uint16_t* pre_zero_lists(int n, int d, int ld, int esz, int max_levels, int min_sq, int order,
                                       const PrePlan& plan, int& err) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, int, int, int, int, int, int>, uint16_t*> cache;
+  static std::map<std::tuple<int, int, int, int, int, int, int, int, int>, uint16_t*> cache;
   int dev = 0;
   err = HQ_OK;
   if (hipGetDevice(&dev) != hipSuccess) { err = HQ_E_HIP; return nullptr; }
-  const auto key = std::make_tuple(dev, n, d, ld, esz, max_levels, min_sq, order);
+  const auto key = std::make_tuple(dev, n, d, ld, esz, max_levels, min_sq, order, plan.g2reg);
   std::lock_guard<std::mutex> g(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
@@ -819,23 +827,42 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
           for (int m = 0; m < 4; ++m) p[i][m] = 4 * nf + m < dd ? t[m] : 0.0f;
     }
   };
+  // plan.g2reg: a 2 x 2 grid square is a Hilbert group, so the loader averages it from the values it
+  // scatters (NumPy's n < 8 sequential sum in C order, as pre_small<2>) and writes it after the barrier
+  float g2v[KL];
+  int g2k[KL];
   auto scatter = [&](const float (&p)[KL][4]) {
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
       const int j = lt + 128 * i;
       int dz = d;
       asm volatile("" : "+s"(dz));
+      g2k[i] = -1;
       if (j >= G || 4 * j >= dz) continue;  // padding stays +0.0 from the setup
       uint32_t ent = lut[i];
       asm volatile("" : "+v"(ent));
       const uint32_t off0 = ent & 0xFFFFu, code = ent >> 16;
       const uint32_t off = (off0 >> lsh_n) * ld + (off0 & (n - 1));
+      float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // values by position: (0,0) (0,1) (1,0) (1,1)
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const uint32_t b = (code >> (2 * m)) & 3u;
         img[off + (b & 1u) + (b >> 1) * ld] = p[i][m];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) c[t] = b == (uint32_t)t ? p[i][m] : c[t];
+      }
+      if (plan.g2reg) {
+        g2v[i] = pre_mean<float>(0.0f + ((((-0.0f + c[0]) + c[1]) + c[2]) + c[3]), 2);
+        g2k[i] = (int)(((off0 >> lsh_n) >> 1) * (uint32_t)(n >> 1) + ((off0 & (n - 1)) >> 1));
       }
     }
+  };
+  auto g2_write = [&] {
+    if (!plan.g2reg) return;
+    const int o2 = lv[plan.g2lvl].off;
+#pragma unroll
+    for (int i = 0; i < KL; ++i)
+      if (g2k[i] >= 0) res[o2 + g2k[i]] = g2v[i];
   };
   // every fetch issues its loads (past the last image the index is clamped to N - 1, loaded and never
   // used): no path without them, so the compiler's wait for set q counts the later sets' loads
@@ -849,6 +876,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
       scatter(pf[q]);
       lds_barrier();
       fetch(pf[q], min(ee + PD * g, N - 1));
+      g2_write();
       reduce();
       lds_barrier();
     }
@@ -1064,6 +1092,19 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   // zero-padding skip (pre_zero_plan): 1-D streams with padding, leaves combined in registers;
   // A/B: option precomp_skip = 0 computes every square
   const bool skip = use_lut && !p.tree_lds && opt(OPT_PRECOMP_SKIP, 1) != 0 && pre_zero_plan(n, d, p);
+  // skip runs of f32 streams take the wave-specialised kernel when the row bases are 16-byte aligned and
+  // the groups below d fit 128 loader lanes x 4 (A/B: option precomp_ws = 0 keeps k_precomp; 2
+  // prefetches two images ahead: 4.36 vs 4.23 ms for one, the compiler's waits still drain both sets)
+  const int ngroups = (d + 3) / 4;
+  const int64_t ws = opt(OPT_PRECOMP_WS, 1);
+  const bool use_ws = dtype == HQ_F32 && skip && ws != 0 && d >= 4 && ngroups <= 128 * 4 &&
+                      (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (in_stride & 3) == 0;
+  // option precomp_g2reg = 1: the 2 x 2 grid squares from the loader's registers (A/B: 4.12-4.15 vs
+  // 3.96-4.01 ms without: the loaders' scatter phase is the longer side of the first phase)
+  if (use_ws && p.g2lvl >= 0 && opt(OPT_PRECOMP_G2REG, 0) != 0) {
+    p.g2reg = 1;  // its 2 x 2 grid squares come from the loader's registers: re-list without them
+    pre_zero_plan(n, d, p);
+  }
   // skip runs: the square lists, built on the host once per configuration (A/B: option
   // precomp_order = 0 keeps them in square order instead of the LDS bank order)
   const uint16_t* glist = nullptr;
@@ -1085,14 +1126,7 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   if (dtype == HQ_F32) {
     // groups of 4 values a thread scatters: a skip run touches only groups below d
     const bool kg2 = skip && (d + 3) / 4 <= 2 * kPreThreads;
-    // skip runs: the wave-specialised kernel (loads on waves 0-1, stores on waves 2-3) when the row
-    // bases are 16-byte aligned and the groups below d fit 128 loader lanes x 4 (A/B: option
-    // precomp_ws = 0 keeps k_precomp; 2 prefetches two images ahead: 4.36 vs 4.23 ms for one, the
-    // compiler's waits still drain both register sets)
-    const int ngroups = (d + 3) / 4;
-    const int64_t ws = opt(OPT_PRECOMP_WS, 1);
-    if (skip && ws != 0 && d >= 4 && ngroups <= 128 * 4 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
-        (in_stride & 3) == 0) {
+    if (use_ws) {
       const int kl = ngroups <= 128 * 2 ? 2 : (ngroups <= 128 * 3 ? 3 : 4);
       auto wk = ws == 1 ? (kl == 2 ? k_precomp_ws<2, 1> : (kl == 3 ? k_precomp_ws<3, 1> : k_precomp_ws<4, 1>))
                         : (kl == 2 ? k_precomp_ws<2, 2> : (kl == 3 ? k_precomp_ws<3, 2> : k_precomp_ws<4, 2>));
