@@ -806,7 +806,8 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
     for (int i = 0; i < KL; ++i) lut[i] = lt + 128 * i < G ? glut[lt + 128 * i] : 0u;
   }
   float pf[PD][KL][4];
-  auto fetch = [&](float (&p)[KL][4], int64_t e) {
+  float tl[PD][4];  // the partial group nfull (d % 4 != 0): uniform scalar loads, substituted at the scatter
+  auto fetch = [&](float (&p)[KL][4], float (&t)[4], int64_t e) {
     const float* src = in + e * stride;
     int nf = nfull, dd = d;
     asm volatile("" : "+s"(nf), "+s"(dd));
@@ -816,22 +817,16 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
       const float4 q4 = *reinterpret_cast<const float4*>(src + 4 * j);
       p[i][0] = q4.x; p[i][1] = q4.y; p[i][2] = q4.z; p[i][3] = q4.w;
     }
-    if (dd & 3) {  // the partial group nfull: four clamped loads by every loader lane, kept by its owner
-      float t[4];
+    // the pf registers are written by these loads only (a VALU write here would make the compiler's wait
+    // for one register set drain the other set's loads too)
 #pragma unroll
-      for (int m = 0; m < 4; ++m) t[m] = src[min(4 * nf + m, dd - 1)];
-#pragma unroll
-      for (int i = 0; i < KL; ++i)
-        if (lt + 128 * i == nf)
-#pragma unroll
-          for (int m = 0; m < 4; ++m) p[i][m] = 4 * nf + m < dd ? t[m] : 0.0f;
-    }
+    for (int m = 0; m < 4; ++m) t[m] = (dd & 3) ? src[min(4 * nf + m, dd - 1)] : 0.0f;
   };
   // plan.g2reg: a 2 x 2 grid square is a Hilbert group, so the loader averages it from the values it
   // scatters (NumPy's n < 8 sequential sum in C order, as pre_small<2>) and writes it after the barrier
   float g2v[KL];
   int g2k[KL];
-  auto scatter = [&](const float (&p)[KL][4]) {
+  auto scatter = [&](const float (&p)[KL][4], const float (&tq)[4]) {
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
       const int j = lt + 128 * i;
@@ -843,13 +838,15 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
       asm volatile("" : "+v"(ent));
       const uint32_t off0 = ent & 0xFFFFu, code = ent >> 16;
       const uint32_t off = (off0 >> lsh_n) * ld + (off0 & (n - 1));
+      const bool part = j == (dz >> 2);  // the partial group: its values from the scalar loads, zero-padded
       float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // values by position: (0,0) (0,1) (1,0) (1,1)
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const uint32_t b = (code >> (2 * m)) & 3u;
-        img[off + (b & 1u) + (b >> 1) * ld] = p[i][m];
+        const float v = part ? (4 * j + m < dz ? tq[m] : 0.0f) : p[i][m];
+        img[off + (b & 1u) + (b >> 1) * ld] = v;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) c[t] = b == (uint32_t)t ? p[i][m] : c[t];
+        for (int t = 0; t < 4; ++t) c[t] = b == (uint32_t)t ? v : c[t];
       }
       if (plan.g2reg) {
         g2v[i] = pre_mean<float>(0.0f + ((((-0.0f + c[0]) + c[1]) + c[2]) + c[3]), 2);
@@ -867,15 +864,15 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
   // every fetch issues its loads (past the last image the index is clamped to N - 1, loaded and never
   // used): no path without them, so the compiler's wait for set q counts the later sets' loads
 #pragma unroll
-  for (int q = 0; q < PD; ++q) fetch(pf[q], min(e0 + q * g, N - 1));
+  for (int q = 0; q < PD; ++q) fetch(pf[q], tl[q], min(e0 + q * g, N - 1));
   for (int64_t e = e0; e < N; e += PD * g) {
 #pragma unroll
     for (int q = 0; q < PD; ++q) {
       const int64_t ee = e + q * g;
       if (ee >= N) break;  // uniform
-      scatter(pf[q]);
+      scatter(pf[q], tl[q]);
       lds_barrier();
-      fetch(pf[q], min(ee + PD * g, N - 1));
+      fetch(pf[q], tl[q], min(ee + PD * g, N - 1));
       g2_write();
       reduce();
       lds_barrier();
