@@ -761,7 +761,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
 // no branch: a fixed number of loads per image, so waiting for image e leaves image e + grid in
 // flight), a partial last group (d % 4) by four clamped dword loads.  Two barriers per image.  The LDS
 // footprint (~30 KiB at n = 64, d = 1536) allows 5 workgroups per CU = 5 waves per SIMD: 96 VGPRs.
-template <int KL, int PD>
+template <int KL, int PD, int LW = 2>
 __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))) void k_precomp_ws(
     const float* __restrict__ in, int64_t N, int64_t stride, int d, int n, PrePlan plan, float* __restrict__ out,
     int64_t out_stride, int ld, const uint16_t* __restrict__ glist) {
@@ -771,7 +771,8 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
   float* res = img + ((ld * n + 3) & ~3);  // no LDS tree on skip runs
   uint16_t* zl = reinterpret_cast<uint16_t*>(res + ((plan.total + 3) & ~3));
   const int tid = threadIdx.x;
-  const int lt = tid & 127;
+  constexpr int NL = 64 * LW;  // loader lanes (waves 0 .. LW - 1); the other waves store
+  const int lt = tid < NL ? tid : tid - NL;
   const int lsh_n = plan.lsh_n;
   if (tid < plan.nlev) lv[tid] = plan.lv[tid];
   auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
@@ -784,16 +785,16 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
     if (!PRE_DIAG(1)) pre_small_levels<float, true>(lv, plan.nlev, img, ld, res, tid, zl);
     if (!PRE_DIAG(2)) pre_leaves_sk<float>(img, ld, res, tid, lt_b, lt_m, plan.maxper);
   };
-  if (tid >= 128) {  // storer waves: no loads, so their stores are never waited on inside the loop
+  if (tid >= NL) {  // storer waves: no loads, so their stores are never waited on inside the loop
     int64_t prev = -1;
     for (int64_t e = e0; e < N; e += g) {
-      if (prev >= 0 && !PRE_DIAG(8)) pre_store(res, plan.total, out + prev * out_stride, plan.nt, lt, 128);
+      if (prev >= 0 && !PRE_DIAG(8)) pre_store(res, plan.total, out + prev * out_stride, plan.nt, lt, kPreThreads - NL);
       lds_barrier();
       reduce();
       lds_barrier();
       prev = e;
     }
-    if (!PRE_DIAG(8)) pre_store(res, plan.total, out + prev * out_stride, plan.nt, lt, 128);
+    if (!PRE_DIAG(8)) pre_store(res, plan.total, out + prev * out_stride, plan.nt, lt, kPreThreads - NL);
     return;
   }
   // loader waves
@@ -803,7 +804,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
   {
     const uint32_t* glut = n == 16 ? kPreLut16.v : (n == 32 ? kPreLut32.v : kPreLut64.v);
 #pragma unroll
-    for (int i = 0; i < KL; ++i) lut[i] = lt + 128 * i < G ? glut[lt + 128 * i] : 0u;
+    for (int i = 0; i < KL; ++i) lut[i] = lt + NL * i < G ? glut[lt + NL * i] : 0u;
   }
   float pf[PD][KL][4];
   float tl[PD][4];  // the partial group nfull (d % 4 != 0): uniform scalar loads, substituted at the scatter
@@ -813,7 +814,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
     asm volatile("" : "+s"(nf), "+s"(dd));
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
-      const int j = min(lt + 128 * i, nf - 1);
+      const int j = min(lt + NL * i, nf - 1);
       const float4 q4 = *reinterpret_cast<const float4*>(src + 4 * j);
       p[i][0] = q4.x; p[i][1] = q4.y; p[i][2] = q4.z; p[i][3] = q4.w;
     }
@@ -829,7 +830,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
   auto scatter = [&](const float (&p)[KL][4], const float (&tq)[4]) {
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
-      const int j = lt + 128 * i;
+      const int j = lt + NL * i;
       int dz = d;
       asm volatile("" : "+s"(dz));
       g2k[i] = -1;
@@ -1127,6 +1128,11 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
       const int kl = ngroups <= 128 * 2 ? 2 : (ngroups <= 128 * 3 ? 3 : 4);
       auto wk = ws == 1 ? (kl == 2 ? k_precomp_ws<2, 1> : (kl == 3 ? k_precomp_ws<3, 1> : k_precomp_ws<4, 1>))
                         : (kl == 2 ? k_precomp_ws<2, 2> : (kl == 3 ? k_precomp_ws<3, 2> : k_precomp_ws<4, 2>));
+      // ws = 3: three loader waves and one storer (groups per loader lane ceil(ngroups / 192))
+      if (ws == 3) {
+        const int k3 = ngroups <= 192 * 2 ? 2 : 3;
+        wk = k3 == 2 ? k_precomp_ws<2, 1, 3> : k_precomp_ws<3, 1, 3>;
+      }
       // more workgroups than the 1,280 resident ones desynchronise the phases of a CU's workgroups
       // (A/B, ms at 1M x 1536: grid 1280 / 5120 / 8192 / 20480 / 65536 -> 4.50 / 4.05 / 3.98 / 3.91 /
       // 4.01); the averages are written once but plain stores measured ~1% faster than non-temporal

@@ -159,7 +159,7 @@ def test_quantizer_builds_precomputed_index(hq_lib):
     assert qm.metadata.model_name == "pm"
 
 
-@pytest.mark.parametrize("ws", [None, 0, "order0", "g2reg"])
+@pytest.mark.parametrize("ws", [None, 0, 3, "order0", "g2reg"])
 @pytest.mark.parametrize("grid", [None, "3"])
 @pytest.mark.parametrize("n,dtype,levels", [(16, np.float32, (6, 2)), (32, np.float32, (6, 2)),
                                              (64, np.float32, (6, 2)), (64, np.float64, (6, 2)),

@@ -14,6 +14,6 @@ for rep in 1 2; do
   pc new HQ_NONE=1 || exit 1
   D=HQ_LIB_VARIANT=$GRAFT_REPO_ROOT/hilbert-quantization_amd/hq_mi355x/libhq_mi355x_diag.so
   pc nows $D HQ_PRECOMP_WS=0 || exit 1
-  pc pd2 $D HQ_PRECOMP_WS=2 || exit 1
+  pc lw3 $D HQ_PRECOMP_WS=3 || exit 1
   [ -f .baseline_pc/libhq_mi355x.so ] && { pc old HQ_LIB_VARIANT=$GRAFT_REPO_ROOT/.baseline_pc/libhq_mi355x.so || exit 1; }
 done
