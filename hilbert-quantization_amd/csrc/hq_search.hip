@@ -4715,7 +4715,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
   __shared__ flt4 qg[HI ? 1 : kOvQCap];  // queue: G of each G segment (split form) ...
   __shared__ int qk[kOvQCap];   // ... and (row - c_begin) << 5 | query within the wave
   __shared__ QOvD qs[kOvQW];    // the wave's model constants (the drain reads them per entry)
+  // LIN: pool appends collected in LDS and written after the scan loop, so the loop issues no global
+  // store or atomic: on gfx9 the vector-memory counter is not ordered between loads and stores, and a
+  // possibly pending store made every wait for the prefetched step a vmcnt(0) (the prefetch collapsed).
+  // A wave whose buffer fills marks the queries it would drop as overflowing (dense path).
+  constexpr int kAB = LIN ? 256 : 1;
+  __shared__ float ab_s[kAB];
+  __shared__ int ab_r[kAB];
+  __shared__ unsigned int ab_over;
+  int nab = 0;
   const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  if (lane == 0) ab_over = 0u;  // visible after the wave_lds_sync below
   const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
   const int chunk = xcd + 8 * (slot / a.nqb);
   const int qb = slot % a.nqb;
@@ -4818,6 +4828,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
   int qn = 0;
   // drain the first n <= 64 entries (one per lane): f32 model score, pool append; then shift the rest down
   auto drain = [&](const int n) {
+    bool ok = false;
+    float sv = 0.0f;
+    int rk = 0;
     if (lane < n) {
       const int key = qk[lane], eqi = key & 31;
       const int64_t row = c_begin + (key >> 5);
@@ -4833,7 +4846,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
           for (int i = 0; i < 4; ++i) G[i] = eg[i];
         }
         const float s = ov_model<NG, NC>(o, c, a.Sc32, row, G, a.Sq, a.Sc, q);
-        if (s >= c.thl) {
+        if constexpr (LIN) {
+          ok = s >= c.thl;
+          sv = s;
+          rk = (int)((row - c_begin) << 5) | eqi;
+        } else if (s >= c.thl) {
           const int slot = atomicAdd(a.pool_n + q, 1);
           if (slot < a.pool_cap) {
             a.pool_s[(int64_t)q * a.pool_cap + slot] = s;
@@ -4841,6 +4858,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
           }
         }
       }
+    }
+    if constexpr (LIN) {  // wave-uniform append position
+      const unsigned long long m = __builtin_amdgcn_ballot_w64(ok);
+      const int pos = nab + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+      if (ok) {
+        if (pos < kAB) {
+          ab_s[pos] = sv;
+          ab_r[pos] = rk;
+        } else {
+          atomicOr(&ab_over, 1u << (rk & 31));  // LDS atomic: no global memory traffic in the loop
+        }
+      }
+      nab += __popcll(m);
+      nab = nab < kAB ? nab : kAB;
     }
     wave_lds_sync();
     for (int b0 = n; b0 < qn; b0 += 64) {
@@ -4924,6 +4955,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
     for (int b = 0; b < NB; ++b) block(b, cur, c_begin + s * kCS);
   };
 
+  // LIN: the wave's pool appends, after its scan loop; queries whose appends did not fit the buffer get a
+  // count past the pool capacity (k_pool_select then sends them to the dense exact path)
+  auto flush = [&] {
+    if constexpr (LIN) {
+      wave_lds_sync();
+      for (int e = lane; e < nab; e += 64) {
+        const int rk2 = ab_r[e], eqi = rk2 & 31, q = q0 + eqi;
+        const int slot = atomicAdd(a.pool_n + q, 1);
+        if (slot < a.pool_cap) {
+          a.pool_s[(int64_t)q * a.pool_cap + slot] = ab_s[e];
+          a.pool_i[(int64_t)q * a.pool_cap + slot] = (int)(c_begin + (rk2 >> 5));
+        }
+      }
+      const unsigned int over = ab_over;
+      if (lane < 32 && ((over >> lane) & 1u) && q0 + lane < a.Q) atomicAdd(a.pool_n + q0 + lane, a.pool_cap + 1);
+    }
+  };
   if constexpr (PF == 1) {  // two buffers, ping-pong
     CStep cA, cB;
     load_step(cA, 0);
@@ -4939,6 +4987,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
     if (s < nsteps) step(cA, s);
     wave_lds_sync();
     while (qn > 0) drain(qn < 64 ? qn : 64);
+    flush();
     return;
   }
   // PF + 1 step buffers in rotation: step s + PF is requested while step s is scored (load_step clamps
@@ -4961,6 +5010,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
     if (s + u < nsteps) step(buf[u], s + u);
   wave_lds_sync();
   while (qn > 0) drain(qn < 64 ? qn : 64);
+  flush();
 }
 
 // Sample pass of the overall scan (as k_sample_topg): 16 queries per wave, whole sample tiles; per lane

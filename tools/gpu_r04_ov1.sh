@@ -16,4 +16,4 @@ import json,sys; d=json.loads(open('$O/ov1_$tag.json').read().strip().splitlines
 print('%-10s search %.3fM  ov %.3fM  l0 %.3fM  m100 %.3fM  m1000 %.3fM' % ('$tag', s['value']/1e6, m['overall']['value']/1e6, m['level0']['value']/1e6, m['m100']['value']/1e6, m['m1000']['value']/1e6))" || echo "$tag rc=$rc"
   return $rc
 }
-run new && run pf2occ3 ov_pf=2 ov_occ=3 && run pf3occ3 ov_pf=3 ov_occ=3 && run pf2 ov_pf=2 && run new2
+run new && run w8k ov_waves=8192 && run w16k ov_waves=16384 && run w32k ov_waves=32768 && run new2
