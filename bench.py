@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--no-precomputed", action="store_true")
     ap.add_argument("--no-ingest", action="store_true")
     ap.add_argument("--no-frames", action="store_true")
+    ap.add_argument("--no-frames-f64", action="store_true", help="skip the f64-score sub-record of the frames leg")
     ap.add_argument("--frames", type=int, default=250_000)
     ap.add_argument("--ingest-models", type=int, default=20000)
     ap.add_argument("--stream-values", type=int, default=7_000_000_000)
@@ -333,7 +334,10 @@ def bench_frames(args, world, rank, dev):
     del F
     torch.cuda.synchronize()
 
-    def step():
+    def step():  # float32 scores: the reference's own score dtype (rag/search/engine.py computes in float32)
+        K.cosine_scores_mfma(K.cos_prepare(Qf), corpus, f32=True)
+
+    def step64():
         K.cosine_scores_mfma(K.cos_prepare(Qf), corpus)
 
     steps = max(2, args.search_steps)
@@ -343,10 +347,15 @@ def bench_frames(args, world, rank, dev):
     res = {"metric": "frame-pair cosine scores/sec (1000 queries x 64x64 frames)",
            "value": Qn * Nf * world * steps / wall, "unit": "pairs/sec", "queries": Qn, "frames_per_gpu": Nf,
            "K": Kd, "steps": steps, "ms_per_step": wall / steps * 1e3, "scaling": "weak",
+           "scores": "float32 (hq_cos_scores_mfma_f32)",
            "roofline": {"bound": "mfma", "achieved": flops / kern / 1e12, "peak": peak, "unit": "TFLOP/s",
                         "frac": flops / kern / 1e12 / peak, "traffic": load_traffic("k_cos_t"),
                         "note": "algorithmic 2*Q*N*K f32 dot flops per step; peak = dense f16 MFMA / 3 (split-f16: "
                                 "hi.hi + hi.lo + lo.hi); traffic = HBM bytes per k_cos_t launch (PMC)"}}
+    if not args.no_frames_f64:
+        w64, k64 = timed(step64, steps, 1, world)
+        res["f64_scores"] = {"value": Qn * Nf * world * steps / w64, "unit": "pairs/sec",
+                             "ms_per_step": w64 / steps * 1e3, "frac": flops / k64 / 1e12 / peak}
     del corpus, Qf
     if rank == 0 and world == 1 and not args.no_cpu:
         from oracle import hq_oracle as O

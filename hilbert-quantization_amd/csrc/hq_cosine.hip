@@ -164,6 +164,7 @@ struct CosArgs {
   int qtiles;
   int64_t ntiles;
   double* out;  // [Q, N]
+  float* outf;  // [Q, N] float32 scores (hq_cos_scores_mfma_f32; k_cos_t EP 3): the reference's precision
 };
 
 // Register-staged baseline.  TQ = query rows per workgroup tile; frames per tile kCosT = 128.  LDS per
@@ -656,6 +657,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         const double v = (iq != 0.0 && ic[j] != 0.0) ? (cs + 1.0) / 2.0 : 0.0;
         if constexpr (EP == 2) {  // diagnostics: no stores (wrong output; A/B of the epilogue's cost)
           if (v == -1.0) a.out[0] = v;
+        } else if constexpr (EP == 3) {  // float32 scores: the f64 value rounded once
+          if (q < a.Q && n < a.N) __builtin_nontemporal_store((float)v, a.outf + q * a.N + n);
         } else if (wide) {
           stage[(4 * (lane >> 4) + r) * 16 * FT + 16 * j + (lane & 15)] = v;
         } else if (q < a.Q && n < a.N) {
@@ -759,6 +762,25 @@ int hq_cos_prepare(const float* X, int64_t N, int64_t ld, int K, void* X16, doub
   return HQ_OK;
 }
 
+int hq_cos_scores_mfma_f32(const void* A16, const double* inv_a, int Q, const void* B16, const double* inv_b, int64_t N,
+                           int K, float* out, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || K <= 0) return fail(HQ_E_INVALID, "bad shape");
+  if (Q == 0 || N == 0) return HQ_OK;
+  if (!A16 || !inv_a || !B16 || !inv_b || !out) return fail(HQ_E_INVALID, "null buffer");
+  CosArgs a;
+  a.A = reinterpret_cast<const _Float16*>(A16);
+  a.B = reinterpret_cast<const _Float16*>(B16);
+  a.ia = inv_a;
+  a.ib = inv_b;
+  a.Q = Q;
+  a.N = N;
+  a.Kp = hq_cos_padded_k(K);
+  a.ntiles = hq_cos_padded_rows(N) / kCosT;
+  a.out = nullptr;
+  a.outf = out;
+  return launch_t<3, 1, 1, 3>(a, (hipStream_t)stream);  // the default kernel, float32 score stores
+}
+
 int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* B16, const double* inv_b, int64_t N,
                        int K, double* out, hq_stream_t stream) {
   if (Q < 0 || N < 0 || K <= 0) return fail(HQ_E_INVALID, "bad shape");
@@ -774,6 +796,7 @@ int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* 
   a.Kp = hq_cos_padded_k(K);
   a.ntiles = hq_cos_padded_rows(N) / kCosT;
   a.out = out;
+  a.outf = nullptr;
   // A/B (option cos_kernel): 1 register-staged two-buffer kernel, 2 lockstep (the DMA kernel without the
   // ping-pong stagger), 3 temporal score stores; DESIGN.md §4.5 has the measurements
   const int64_t ek = opt(OPT_COS_KERNEL, 0);

@@ -108,6 +108,7 @@ SIGNATURES = {
     "hq_cos_padded_rows": (_i64, [_i64]),
     "hq_cos_prepare": (_i, [_p, _i64, _i64, _i, _p, _p, _p]),
     "hq_cos_scores_mfma": (_i, [_p, _p, _i, _p, _p, _i64, _i, _p, _p]),
+    "hq_cos_scores_mfma_f32": (_i, [_p, _p, _i, _p, _p, _i64, _i, _p, _p]),
 }
 
 _lock = threading.Lock()

@@ -679,14 +679,15 @@ def cos_prepare(x, exc=None) -> CosRows:
     return CosRows(X16, inv, N, K)
 
 
-def cosine_scores_mfma(q: CosRows, c: CosRows, exc=None):
-    """(cos + 1) / 2 of every prepared query row against every prepared frame row -> f64 [Q, N]."""
+def cosine_scores_mfma(q: CosRows, c: CosRows, exc=None, f32: bool = False):
+    """(cos + 1) / 2 of every prepared query row against every prepared frame row -> f64 [Q, N]
+    (f32=True: float32 [Q, N], the f64 value rounded once — the reference's own score dtype)."""
     t = torch()
     if q.K != c.K:
         raise ValueError(f"query length {q.K} != frame length {c.K}")
-    out = t.empty((q.N, c.N), dtype=t.float64, device=q.X16.device)
-    _chk(_L().hq_cos_scores_mfma(ptr(q.X16), ptr(q.inv), q.N, ptr(c.X16), ptr(c.inv), c.N, q.K, ptr(out),
-                                 stream()), exc)
+    out = t.empty((q.N, c.N), dtype=t.float32 if f32 else t.float64, device=q.X16.device)
+    fn = _L().hq_cos_scores_mfma_f32 if f32 else _L().hq_cos_scores_mfma
+    _chk(fn(ptr(q.X16), ptr(q.inv), q.N, ptr(c.X16), ptr(c.inv), c.N, q.K, ptr(out), stream()), exc)
     return out
 
 

@@ -428,12 +428,16 @@ int hq_precomputed_similarity(const float* q_avgs, const float* q_norm, const fl
  *   inv [padded rows] = 1 / (scale |x|) (0 for a zero row).  Prepare a corpus once, each query batch per
  *   call, under the same cos_kernel option as the scoring call.
  * hq_cos_scores_mfma: out [Q, N] f64 = (cos + 1) / 2 (0 when a norm is 0), split-f16 MFMA contraction
- *   (v_mfma_f32_16x16x32_f16 x 3), within 1e-5 of the reference's float32 BLAS result.          */
+ *   (v_mfma_f32_16x16x32_f16 x 3), within 1e-5 of the reference's float32 BLAS result.
+ * hq_cos_scores_mfma_f32: the same scores rounded once to float32 (the reference's own score dtype; half
+ *   the output bytes).                                                                           */
 int hq_cos_padded_k(int K);
 int64_t hq_cos_padded_rows(int64_t N);
 int hq_cos_prepare(const float* X, int64_t N, int64_t ld, int K, void* X16, double* inv, hq_stream_t stream);
 int hq_cos_scores_mfma(const void* A16, const double* inv_a, int Q, const void* B16, const double* inv_b, int64_t N,
                        int K, double* out, hq_stream_t stream);
+int hq_cos_scores_mfma_f32(const void* A16, const double* inv_a, int Q, const void* B16, const double* inv_b, int64_t N,
+                           int K, float* out, hq_stream_t stream);
 
 /* ---- S7: the rest of the RAG scorer (rag/search/engine.py) --------------------------------------
  * hq_cosine_scores_dt: as hq_cosine_scores for float32 (HQ_F32) or float64 (HQ_F64) rows; float64

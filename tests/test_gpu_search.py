@@ -317,6 +317,22 @@ def test_cosine_mfma_vs_f64(hq_lib, Q, N, K):
     assert np.all(got[-1] == 0.0) and np.all(got[:, -1] == 0.0)
 
 
+@pytest.mark.parametrize("Q,N,K", [(3, 5, 4096), (257, 129, 1000), (130, 700, 1024)])
+def test_cosine_mfma_f32_scores(hq_lib, Q, N, K):
+    """hq_cos_scores_mfma_f32: exactly the f64 scores rounded once to float32 (ragged tiles, zero rows)."""
+    import torch
+    from hq_mi355x import kernels as K_
+    rng = np.random.default_rng(3 * Q + N + K)
+    A = rng.standard_normal((Q, K)).astype(np.float32)
+    B = rng.standard_normal((N, K)).astype(np.float32)
+    A[-1] = 0.0
+    pa, pb = K_.cos_prepare(torch.from_numpy(A).cuda()), K_.cos_prepare(torch.from_numpy(B).cuda())
+    s64 = _np(K_.cosine_scores_mfma(pa, pb))
+    s32 = _np(K_.cosine_scores_mfma(pa, pb, f32=True))
+    assert s32.dtype == np.float32
+    np.testing.assert_array_equal(s32, s64.astype(np.float32))
+
+
 def test_cosine_mfma_vs_reference_golden(hq_lib, golden):
     """The reference's own float32 cosine values (rag/search/engine.py:622-660) within the north star's 1e-5."""
     import torch
