@@ -130,9 +130,12 @@ def load_traffic(name):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
-            return json.load(f).get(name, {}).get("hbm_bytes_per_launch")
+            rec = json.load(f).get(name)
     except (OSError, ValueError):
         return None
+    if not isinstance(rec, dict):
+        return None
+    return rec.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline_quantize(dim, seconds):

@@ -197,3 +197,20 @@ def test_scan0f_reads_stay_inside_padded_copies(lib):
             assert m < z_rows and m < s_rows, (Q, N, m, z_rows)
             worst = max(worst, m - N)
     assert worst == 46  # reads reach row N + 46: inside the 48 padding rows, 1 row to spare
+
+
+def test_bench_traffic_table_well_formed():
+    """Every kernel bench.py cites in its `traffic` field has a numeric per-launch HBM figure in the committed
+    rocprofv3 PMC table (a malformed record once crashed the round-end bench)."""
+    import importlib.util
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "bench.py")).read()
+    names = sorted(set(re.findall(r'load_traffic\("([A-Za-z0-9_]+)"\)', src)))
+    assert names
+    spec = importlib.util.spec_from_file_location("_bench_mod", os.path.join(root, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    for n in names:
+        v = mod.load_traffic(n)
+        assert isinstance(v, float) and v > 0, (n, v)
