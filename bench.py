@@ -617,6 +617,11 @@ def main():
                                  kernel_ms=kern * 1e3),
     }
 
+    # the pre-computed index leg reads the headline's embeddings; run next to it, before the search legs
+    # churn the allocator (measured: its kernel 4.01 ms here, 4.31 ms after the search legs)
+    if not args.no_precomputed:
+        rec["precomputed"] = bench_precomputed(args, X, world)
+
     if not args.no_search:
         from hq_mi355x.core.search_engine import IndexCorpus
         from hq_mi355x.distributed import ShardedIndexCorpus
@@ -736,9 +741,6 @@ def main():
             del engine
             torch.cuda.empty_cache()
             rec["search"]["strong"] = bench_search_strong(args, world, rank, dev)
-
-    if not args.no_precomputed:
-        rec["precomputed"] = bench_precomputed(args, X, world)
 
     if not args.no_frames:
         rec["frames"] = bench_frames(args, world, rank, dev)
