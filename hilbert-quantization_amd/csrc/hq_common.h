@@ -319,6 +319,18 @@ __device__ __forceinline__ T np_sum(const F& f, int n) {
   }
 }
 
+// Two sums over the same elements in one pass: np_sum<Sum2<T>>(f, n) with f(k) = {a_k, b_k} runs the
+// pairwise order above on each component separately (component-wise +, no cross terms), so .a and .b
+// are bit-identical to two np_sum<T> calls while every element is loaded once
+template <typename T>
+struct Sum2 {
+  T a, b;
+  __device__ __forceinline__ Sum2() = default;
+  __device__ __forceinline__ Sum2(T a_, T b_) : a(a_), b(b_) {}
+  __device__ __forceinline__ explicit Sum2(T v) : a(v), b(v) {}
+  __device__ __forceinline__ Sum2 operator+(const Sum2& o) const { return Sum2(a + o.a, b + o.b); }
+};
+
 // element size of an HQ dtype code (0 if unknown)
 inline int dtype_size(int dt) {
   switch (dt) {

@@ -264,7 +264,10 @@ __device__ __forceinline__ double side_z(const Side& s, int k) {
 // compare_indices_at_level (search_engine.py:111-189) for one segment in the reference's operation
 // order and dtype.  *np32 = 1 when the result is a numpy float32 (both sides f32, general branch,
 // not clamped), else it is a Python float: the type decides the overall weighted sum's arithmetic.
-template <bool SM = false>
+// F2: the correlation's products and the squared differences summed in one pass (Sum2: each sum in its
+// own pairwise order, bit-identical; every element read once, 16 more VGPRs — the long-list re-rank, whose
+// per-thread row reads are request-bound, uses it)
+template <bool SM = false, bool F2 = false>
 __device__ double exact_level_sides(const Side& q, const Side& c, int m, int* np32) {
   *np32 = 0;
   const bool both32 = q.f32 && c.f32;
@@ -272,11 +275,22 @@ __device__ double exact_level_sides(const Side& q, const Side& c, int m, int* np
   if (both32) {
     // float32 throughout: np.mean = f32(f64(f32 pairwise sum) / m) = f32 division (exact double
     // rounding); Python float literals are cast to float32 (NEP 50); no FMA contraction
-    auto fp = [&](int k) -> float { return (float)side_z(q, k) * (float)side_z(c, k); };
-    const float corr = np_sum<float, SM>(fp, m) / (float)m;                          // :154
+    float corr, mse;
+    if constexpr (F2) {
+      auto f2 = [&](int k) -> Sum2<float> {
+        const float d = (float)q.x[k] - (float)c.x[k];
+        return Sum2<float>((float)side_z(q, k) * (float)side_z(c, k), d * d);
+      };
+      const Sum2<float> s2 = np_sum<Sum2<float>, SM>(f2, m);
+      corr = s2.a / (float)m;
+      mse = s2.b / (float)m;
+    } else {
+      auto fp = [&](int k) -> float { return (float)side_z(q, k) * (float)side_z(c, k); };
+      corr = np_sum<float, SM>(fp, m) / (float)m;                                   // :154
+      auto fd = [&](int k) -> float { const float d = (float)q.x[k] - (float)c.x[k]; return d * d; };
+      mse = np_sum<float, SM>(fd, m) / (float)m;                                    // :161
+    }
     const float sim = (corr + 1.0f) / 2.0f;                                        // :158
-    auto fd = [&](int k) -> float { const float d = (float)q.x[k] - (float)c.x[k]; return d * d; };
-    const float mse = np_sum<float, SM>(fd, m) / (float)m;                             // :161
     const float maxmse = (float)q.msq + (float)c.msq;                              // :162
     float ds = 1.0f;
     if (maxmse > 0.0f) {
@@ -290,11 +304,22 @@ __device__ double exact_level_sides(const Side& q, const Side& c, int m, int* np
     }
     return comb < 1.0f ? 0.0 : 1.0;                                                // :174 (Python floats)
   }
-  auto fp = [&](int k) -> double { return side_z(q, k) * side_z(c, k); };
-  const double corr = np_sum<double, SM>(fp, m) / (double)m;                         // :154
+  double corr, mse;
+  if constexpr (F2) {
+    auto f2 = [&](int k) -> Sum2<double> {
+      const double d = q.x[k] - c.x[k];
+      return Sum2<double>(side_z(q, k) * side_z(c, k), d * d);
+    };
+    const Sum2<double> s2 = np_sum<Sum2<double>, SM>(f2, m);
+    corr = s2.a / (double)m;
+    mse = s2.b / (double)m;
+  } else {
+    auto fp = [&](int k) -> double { return side_z(q, k) * side_z(c, k); };
+    corr = np_sum<double, SM>(fp, m) / (double)m;                                  // :154
+    auto fd = [&](int k) -> double { double d = q.x[k] - c.x[k]; return d * d; };
+    mse = np_sum<double, SM>(fd, m) / (double)m;                                   // :161
+  }
   const double sim = (corr + 1.0) / 2.0;                                         // :158
-  auto fd = [&](int k) -> double { double d = q.x[k] - c.x[k]; return d * d; };
-  const double mse = np_sum<double, SM>(fd, m) / (double)m;                          // :161
   const double maxmse = q.msq + c.msq;                                           // :162
   double ds = 1.0;
   if (maxmse > 0.0) {
@@ -308,17 +333,17 @@ __device__ double exact_level_sides(const Side& q, const Side& c, int m, int* np
   return comb > 0.0 ? comb : 0.0;
 }
 
-template <bool SM = false>
+template <bool SM = false, bool F2 = false>
 __device__ double exact_level(const double* q, const double* zq, const double* sq, const double* c,
                               const double* zc, const double* sc, int m, int* np32) {
   const bool qf = (aux_bits(sq) & kAuxF32) != 0, cf = (aux_bits(sc) & kAuxF32) != 0;
-  return exact_level_sides<SM>(make_side<SM>(q, zq, sq, m, qf), make_side<SM>(c, zc, sc, m, cf), m, np32);
+  return exact_level_sides<SM, F2>(make_side<SM>(q, zq, sq, m, qf), make_side<SM>(c, zc, sc, m, cf), m, np32);
 }
 
 // exact_pair on explicit row pointers (raw [L], Z [Lp], S [nseg x 4] of each side; global or LDS)
 // typed (level >= 0, nullable): 1 when the level score is a numpy float32 (the reference's threshold test
 // then compares in float32, NEP 50: see typed_pass)
-template <bool SM = false>
+template <bool SM = false, bool F2 = false>
 __device__ double exact_pair_rows(const double* ra, const double* za, const double* sa, const double* rb,
                                   const double* zb, const double* sb, const SegInfo& si, int level, double* lv,
                                   int* typed = nullptr) {
@@ -326,7 +351,7 @@ __device__ double exact_pair_rows(const double* ra, const double* za, const doub
   if (level >= 0) {
     if (level >= si.nseg) return 0.0;
     const int s = level;
-    const double v = exact_level<SM>(ra + si.src[s], za ? za + si.poff[s] : nullptr, sa + 4 * s, rb + si.src[s],
+    const double v = exact_level<SM, F2>(ra + si.src[s], za ? za + si.poff[s] : nullptr, sa + 4 * s, rb + si.src[s],
                                      zb ? zb + si.poff[s] : nullptr, sb + 4 * s, si.len[s], &t32);
     if (typed) *typed = t32;
     return v;
@@ -337,7 +362,7 @@ __device__ double exact_pair_rows(const double* ra, const double* za, const doub
   double tws = 0.0, tw = 0.0;
   bool acc32 = false;
   for (int s = 0; s < si.nseg; ++s) {
-    const double v = exact_level<SM>(ra + si.src[s], za ? za + si.poff[s] : nullptr, sa + 4 * s, rb + si.src[s],
+    const double v = exact_level<SM, F2>(ra + si.src[s], za ? za + si.poff[s] : nullptr, sa + 4 * s, rb + si.src[s],
                                      zb ? zb + si.poff[s] : nullptr, sb + 4 * s, si.len[s], &t32);
     if (lv) lv[s] = v;
     const double w = 1.0 / (double)(s + 1);
@@ -364,10 +389,10 @@ __device__ double exact_pair_rows(const double* ra, const double* za, const doub
 // ZB = false: B's normalised values are recomputed from its raw values and statistics ((x - mean) / std
 // in f64, the exact operation that wrote Z: bit-identical), so B's Z rows are not read — the re-rank and
 // re-score kernels read only the candidates' raw rows and statistics (half the bytes of a row pair)
-template <bool SM = false, bool ZB = true>
+template <bool SM = false, bool ZB = true, bool F2 = false>
 __device__ double exact_pair(const VecSet& A, int64_t ia, const VecSet& B, int64_t ib, const SegInfo& si, int level,
                              double* lv, int* typed = nullptr) {
-  return exact_pair_rows<SM>(A.raw + ia * si.L, A.Z + ia * si.Lp, A.S + ia * si.nseg * 4, B.raw + ib * si.L,
+  return exact_pair_rows<SM, F2>(A.raw + ia * si.L, A.Z + ia * si.Lp, A.S + ia * si.nseg * 4, B.raw + ib * si.L,
                              ZB ? B.Z + ib * si.Lp : nullptr, B.S + ib * si.nseg * 4, si, level, lv, typed);
 }
 
@@ -3604,7 +3629,10 @@ static void launch_pool_select(int K, hipStream_t s, int Q, float* pool_s, int* 
 // level task per thread) spent most of its time in the staging round trips: 111 us at M = 100, 923 us at
 // M = 1000 per 1000-query batch.
 // ZB: the candidates' normalised values from Z (true) or recomputed from their raw rows (false: half the
-// bytes, an f64 division per value; A/B per 1000-query batch: M = 1000 896 -> 746 us, M = 100 116 -> 129)
+// bytes, an f64 division per value; A/B per 1000-query batch: M = 1000 896 -> 746 us, M = 100 116 -> 129).
+// The raw form sums the correlation and the squared differences in one pass over the row (F2: each row
+// value loaded once; k_refine_big_sm_raw 771 -> 608 us at M = 1000, no scratch); the Z form keeps two
+// passes (F2 there: 248 VGPRs + scratch, M = 100 4% slower)
 template <bool SM, bool ZB = true>
 __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
   if (onext && blockIdx.x == 0 && threadIdx.x == 0) *onext = 0;  // the next batch's redo counter
@@ -3629,7 +3657,7 @@ __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
         const int64_t c = cid_x - id_base;
         if (cid_x >= 0 && c >= 0 && c < N) {
           int typed = 0;
-          const double v = exact_pair<SM, ZB>(Qs, q, Cs, c, si, mode == 0 ? 0 : -1, nullptr, &typed);
+          const double v = exact_pair<SM, ZB, !ZB>(Qs, q, Cs, c, si, mode == 0 ? 0 : -1, nullptr, &typed);
           const bool pass = mode == 0 ? typed_pass(v, typed, thr, thr_mode)
                                       : (thr_mode == 0 || (thr_mode == 1 ? v >= thr : v > thr));
           if (pass) {
@@ -3670,7 +3698,7 @@ __device__ __forceinline__ void refine_big_body(HQ_REFINE_ARGS, int tb) {
         double* rec = odet + ((int64_t)q * k + x) * W;
         if (x < cnt) {
           // ---- pass 2: the output entry's [overall, level..] record ----
-          rec[0] = exact_pair<SM, ZB>(Qs, q, Cs, sid[x] - id_base, si, -1, rec + 1);
+          rec[0] = exact_pair<SM, ZB, !ZB>(Qs, q, Cs, sid[x] - id_base, si, -1, rec + 1);
         } else {
           for (int w = 0; w < W; ++w) rec[w] = 0.0;
         }

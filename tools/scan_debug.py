@@ -28,6 +28,9 @@ mode = sys.argv[1] if len(sys.argv) > 1 else "level0"
 for _ in range(3):
     if mode == "overall":
         K.scan_topk(qp, corpus.prep, 1, 18, -2e-5, 0)
+    elif mode == "m1000":
+        corpus.progressive(C[:1000] + 0.01 * torch.randn((1000, 64), generator=gq, device=dev, dtype=torch.float64),
+                           10, 0.1, 1000)
     else:
         K.scan_topk(qp, corpus.prep, 0, 28, 0.1 - 2e-5, 1)
 torch.cuda.synchronize()
