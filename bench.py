@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--no-ingest", action="store_true")
     ap.add_argument("--no-frames", action="store_true")
     ap.add_argument("--no-frames-f64", action="store_true", help="skip the f64-score sub-record of the frames leg")
+    ap.add_argument("--no-hard", action="store_true", help="skip the fresh / clustered query-distribution search modes")
+    ap.add_argument("--no-api", action="store_true", help="skip the drop-in API per-call latency leg")
+    ap.add_argument("--no-modes", action="store_true", help="skip the overall / level0 / m100 / m1000 search modes")
     ap.add_argument("--frames", type=int, default=250_000)
     ap.add_argument("--ingest-models", type=int, default=20000)
     ap.add_argument("--stream-values", type=int, default=7_000_000_000)
@@ -571,6 +574,167 @@ def bench_search_strong(args, world, rank, dev):
     return res
 
 
+def progressive_rate(engine, Q, M, steps, world, k=10, threshold=0.1):
+    """Pipelined progressive search of one query batch per step (two batches in flight, as the cfg3 leg),
+    with the engine's dense-path counters (IndexCorpus.stats) over the timed and warm-up batches."""
+    pend = []
+
+    def run():
+        pend.append(engine.progressive_submit(Q, k, threshold, M))
+        if len(pend) >= 2:
+            engine.progressive_finish(pend.pop(0))
+
+    def drain():
+        while pend:
+            engine.progressive_finish(pend.pop(0))
+
+    engine.reset_stats()
+    wall, kern = timed(run, steps, 1, world, drain)
+    st = dict(engine.stats)
+    nb = max(1, st["batches"])
+    Qn = int(Q.shape[0])
+    return {"value": Qn * steps / wall, "unit": "queries/sec", "steps": steps, "ms_per_step": wall / steps * 1e3,
+            "max_candidates_per_level": M, "batches": st["batches"], "redo_batches": st["redo_batches"],
+            "redo_queries": st["redo_queries"], "redo_queries_per_batch": st["redo_queries"] / nb,
+            "dense_ms_per_batch": st["dense_s"] / nb * 1e3}
+
+
+def dense_one_query_ms(engine, Q, M, reps=3):
+    """Wall time of the dense exact path (every pair's level-0 score + exact top-M select + arg-max) for ONE
+    query: the cost of one redo."""
+    t = torch
+    qp = engine.prepare_queries(Q[:1])
+    sel = t.zeros(1, dtype=t.int64, device=Q.device)
+    engine._dense(qp, sel, 0, M, 0.1, 1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        engine._dense(qp, sel, 0, M, 0.1, 1)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+def bench_search_hard(args, engine, dev, n, L, world):
+    """Query distributions without a planted near-duplicate: the cfg3 corpus answered
+    for FRESH queries (index vectors of 1000 new seed-5 N(0,1) embeddings: the top-10 sit in the bulk of the
+    score distribution), and a CLUSTERED corpus (1M rows in 64-row runs of near-duplicates: 15,625 seed-6
+    base vectors + N(0, 0.01), queries = 1000 runs' bases + N(0, 0.01)), where one sampled tile can hold
+    16 of a query's 64 best rows.  Per mode and list length: QPS, the queries that took the dense exact
+    path (short or unproven lists) and its time, and the one-query redo cost."""
+    from hq_mi355x import kernels as K
+    from hq_mi355x.core.search_engine import IndexCorpus
+    Qn, d = args.queries, args.dim
+    steps = max(2, args.search_steps // 2)
+    out = {}
+    gf = torch.Generator(device=dev).manual_seed(5)
+    Xf = torch.randn((Qn, d), generator=gf, device=dev, dtype=torch.float32)
+    _, Qf, _ = K.map_index_quantize(Xf, n, L)
+    del Xf
+    fresh = {}
+    for M in (20, 100, 1000):
+        fresh[f"m{M}"] = progressive_rate(engine, Qf, M, steps, world)
+    fresh["dense_one_query_ms"] = {f"m{M}": dense_one_query_ms(engine, Qf, M) for M in (20, 100, 1000)}
+    fresh["queries"] = "fused-kernel index vectors (L=64) of 1000 fresh N(0,1) 1536-d embeddings (torch seed 5)"
+    out["fresh"] = fresh
+    Nc = args.corpus
+    run = 64
+    nb = (Nc + run - 1) // run
+    gc = torch.Generator(device=dev).manual_seed(6)
+    Xb = torch.randn((nb, d), generator=gc, device=dev, dtype=torch.float32)
+    _, B, _ = K.map_index_quantize(Xb, n, L)
+    del Xb
+    C = B.repeat_interleave(run, 0)[:Nc]
+    C.add_(0.01 * torch.randn(C.shape, generator=gc, device=dev, dtype=torch.float64))
+    pick = torch.randperm(nb, generator=torch.Generator().manual_seed(7))[:Qn].to(dev)
+    Qc = B[pick] + 0.01 * torch.randn((Qn, L), generator=gc, device=dev, dtype=torch.float64)
+    del B
+    ce = IndexCorpus(C)
+    torch.cuda.synchronize()
+    clus = {}
+    for M in (20, 100, 1000):
+        clus[f"m{M}"] = progressive_rate(ce, Qc, M, steps, world)
+    ids, _, _, _ = ce.progressive(Qc, 10, 0.1, 20)
+    clus["top1_in_own_run"] = float(((ids[:, 0] // run) == pick).float().mean())
+    clus["corpus"] = (f"{Nc} rows = {nb} seed-6 base index vectors x {run}-row runs + N(0, 0.01); queries = 1000 "
+                      "random runs' bases + N(0, 0.01)")
+    out["clustered"] = clus
+    del ce, C, Qc
+    torch.cuda.empty_cache()
+    return out
+
+
+def bench_api(args):
+    """Per-call latency of the drop-in API (api.py:120-186, 233-297; SURVEY §6 measured the reference's
+    HilbertQuantizer.search of one query over 100 models at 21.2 ms in-container): quantize one 1024-d
+    vector; search one query over 100 and over 10,000 registered models (the query's own quantize, JPEG and
+    pre-computed index included, explicit candidate list); next to the reference-shaped port
+    (oracle/hq_loops.py) doing the same per call on one host core."""
+    import contextlib
+    import io
+    try:
+        import PIL  # noqa: F401
+    except ImportError:
+        return {"skipped": "PIL not importable"}
+    from hq_mi355x.api import HilbertQuantizer
+    rng = np.random.default_rng(13)
+    V = rng.standard_normal((10_100, 1024)).astype(np.float32)
+    hq = HilbertQuantizer()
+    res = {}
+    with contextlib.redirect_stdout(io.StringIO()):
+        hq.quantize(V[0], "warm")
+        reps = 50
+        t0 = time.perf_counter()
+        for i in range(reps):
+            hq.quantize(V[i], f"q{i}")
+        res["quantize_ms"] = (time.perf_counter() - t0) / reps * 1e3
+        models = hq.quantize_many(list(V[100:]), model_ids=[f"m{i}" for i in range(len(V) - 100)])
+        queries = V[100:130] + 0.05 * rng.standard_normal((30, 1024)).astype(np.float32)
+        for pool, name in ((models[:100], "search_100_ms"), (models, "search_10k_ms")):
+            hq.search(queries[0], pool, 10)
+            t0 = time.perf_counter()
+            found = 0
+            for q in queries:
+                found += len(hq.search(q, pool, 10))
+            res[name] = (time.perf_counter() - t0) / len(queries) * 1e3
+            res[name.replace("_ms", "_results_per_call")] = found / len(queries)
+    res["reference_search_100_ms_in_container"] = 21.2
+    res["note"] = ("wall ms per call on the host thread (synchronous API: the query is quantized on the GPU, its "
+                   "JPEG encoded on the host, the pool's resident corpus re-used while the candidate list holds the "
+                   "same index arrays); SURVEY.md §6's 21.2 ms is the reference on the build container's CPU")
+    if not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline_api(models, V, hq.compression_quality, args.cpu_seconds / 4)
+    return res
+
+
+def cpu_baseline_api(models, V, quality, seconds):
+    """The reference's per-call work on one host core, reference-shaped (oracle/hq_loops.py): the query's
+    quantize (per-element map + streaming tree + u8 normalise, PIL JPEG, per-square pre-computed index) and
+    the candidate loop over 100 models' indices; the 10,000-model figure extrapolates the loop linearly."""
+    from hq_mi355x.core.compressor import encode_jpeg
+    from oracle import hq_loops as HL
+    C = np.stack([m.hierarchical_indices for m in models[:100]])
+    n, L = 32, C.shape[1]
+    done, tq, ts, t0 = 0, 0.0, 0.0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        p = V[done % 30]
+        a = time.perf_counter()
+        encode_jpeg(HL.quantize_one(p, n, L), quality)
+        HL.precomputed_one(p, n)
+        b = time.perf_counter()
+        from oracle import hq_oracle as O
+        qidx = O.streaming_index(O.map_from_2d(O.map_to_2d(O.pad_parameters(p, n), n)), L)
+        c = time.perf_counter()
+        HL.progressive_search(qidx, C, 10, 0.1, 20)
+        ts += time.perf_counter() - c
+        tq += b - a
+        done += 1
+    return {"search_100_ms": (tq + ts) / done * 1e3, "search_10k_ms": (tq + 100 * ts) / done * 1e3,
+            "quantize_ms": tq / done * 1e3, "unit": "ms per call", "cores": 1, "kind": "port",
+            "sample": f"{done} calls: reference-shaped quantize (map, streaming tree, u8, PIL JPEG, per-square "
+                      f"pre-computed index) + candidate loop over 100 models (oracle/hq_loops.py), single thread; "
+                      f"10k = quantize + 100 x the 100-model loop"}
+
+
 def main():
     args = parse()
     # multi-core CPU baseline first: worker processes are forked before anything initialises the GPU
@@ -710,7 +874,7 @@ def main():
                                        if ovinfo else (2.0 * pairs * Lp, FP64_MATRIX_PEAK_TFS, "FP64 matrix (spec)"))
         modes = {}
         l0_flops = 2.0 * pairs * 32
-        for mode, fn, flops, peak, pname in (
+        for mode, fn, flops, peak, pname in () if args.no_modes else (
                 ("overall", lambda: engine.brute_force(queries, 10), ov_flops, ov_peak, ov_pname),
                 ("level0", lambda: engine.frame_search(queries, 10, 0.1), l0_flops, FP16_MATRIX_PEAK_TFS,
                  "dense F16 MFMA"),
@@ -730,6 +894,8 @@ def main():
                              "note": f"contraction flops per step, one f16 pass ({('2*Q*N*32*K-blocks' if ovinfo else '2*Q*N*Lp f64') if mode == 'overall' else '2*Q*N*32'}) / "
                                      f"GPU step time (HIP events); peak = {pname}"}}
         rec["search"]["modes"] = modes
+        if not args.no_hard and isinstance(engine, IndexCorpus):
+            rec["search"]["modes"].update(bench_search_hard(args, engine, dev, n, L, world))
         if comm is not None:
             # the one collective of the sharded search alone: the records block of one batch per rank
             x = torch.zeros((Qn, 21, 3 + engine.local.nseg), dtype=torch.float64, device=dev)
@@ -747,6 +913,9 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_ingest:
         rec["ingest"] = bench_ingest(args)
+
+    if rank == 0 and world == 1 and not args.no_api:
+        rec["api"] = bench_api(args)
 
     if not args.no_stream:
         del X, frames, idx, mm, out

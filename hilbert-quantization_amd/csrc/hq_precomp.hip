@@ -244,34 +244,54 @@ static void pre_bank_order(std::vector<int>& ks, const PreLevel& L, int ld) {
 
 // The lists of one configuration in device memory, built once (host) and cached for the process:
 // per level at zoff, the listed squares (small levels in bank order for f32, leaf levels ascending).
+// The first call per configuration allocates the buffer (hipMalloc: may synchronise the device, so a
+// graph capture must not contain that first call) and uploads the list on the caller's stream; an event
+// behind the upload is kept, and every call makes its stream wait on it (a no-op once it completed), so a
+// launch on another stream never reads the list before it arrived.  The host copy stays with the cache
+// entry (the asynchronous copy may read it after the call returns).
+struct PreZeroList {
+  uint16_t* dptr = nullptr;
+  hipEvent_t ready = nullptr;
+  std::vector<uint16_t> host;
+};
+
 static const uint16_t* pre_zero_lists(int n, int d, int ld, int esz, int max_levels, int min_sq, int order,
-                                      const PrePlan& plan, int& err) {
+                                      const PrePlan& plan, hipStream_t s, int& err) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, int, int, int, int, int, int, int>, uint16_t*> cache;
+  static std::map<std::tuple<int, int, int, int, int, int, int, int, int>, PreZeroList*> cache;
   int dev = 0;
   err = HQ_OK;
   if (hipGetDevice(&dev) != hipSuccess) { err = HQ_E_HIP; return nullptr; }
   const auto key = std::make_tuple(dev, n, d, ld, esz, max_levels, min_sq, order, plan.g2reg);
   std::lock_guard<std::mutex> g(mu);
   auto it = cache.find(key);
-  if (it != cache.end()) return it->second;
+  if (it != cache.end()) {
+    if (hipStreamWaitEvent(s, it->second->ready, 0) != hipSuccess) { err = HQ_E_HIP; return nullptr; }
+    return it->second->dptr;
+  }
   PrePlan p = plan;
   std::vector<std::vector<int>> lists;
   pre_zero_plan(n, d, p, &lists);
-  std::vector<uint16_t> flat;
+  PreZeroList* e = new PreZeroList();
   for (int l = 0; l < p.nlev; ++l) {
     if (order && esz == 4 && p.lv[l].leaf0 < 0) pre_bank_order(lists[l], p.lv[l], ld);
-    for (int k : lists[l]) flat.push_back((uint16_t)k);
+    for (int k : lists[l]) e->host.push_back((uint16_t)k);
   }
-  if ((int)flat.size() != p.znz) { err = HQ_E_UNSUPPORTED; return nullptr; }
-  uint16_t* dptr = nullptr;
-  if (hipMalloc(&dptr, flat.size() * sizeof(uint16_t) + 16) != hipSuccess ||
-      hipMemcpy(dptr, flat.data(), flat.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) {
+  if ((int)e->host.size() != p.znz) { delete e; err = HQ_E_UNSUPPORTED; return nullptr; }
+  const size_t bytes = e->host.size() * sizeof(uint16_t);
+  if (hipMalloc(&e->dptr, bytes + 16) != hipSuccess) { delete e; err = HQ_E_HIP; return nullptr; }
+  if (hipMemcpyAsync(e->dptr, e->host.data(), bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventRecord(e->ready, s) != hipSuccess) {
+    (void)hipStreamSynchronize(s);  // the copy may be in flight: let it finish before freeing its buffers
+    if (e->ready) (void)hipEventDestroy(e->ready);
+    (void)hipFree(e->dptr);
+    delete e;
     err = HQ_E_HIP;
     return nullptr;
   }
-  cache[key] = dptr;
-  return dptr;
+  cache[key] = e;
+  return e->dptr;
 }
 
 // top-left corner of square k of a level (grid squares row-major, then offset squares).  g is a power
@@ -1108,7 +1128,8 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
   const uint16_t* glist = nullptr;
   if (skip) {
     int err = HQ_OK;
-    glist = pre_zero_lists(n, d, ld, esz, max_levels, min_square_size, (int)opt(OPT_PRECOMP_ORDER, 1), p, err);
+    glist = pre_zero_lists(n, d, ld, esz, max_levels, min_square_size, (int)opt(OPT_PRECOMP_ORDER, 1), p,
+                           (hipStream_t)stream, err);
     if (!glist) return fail(err, "pre-computed index: zero-padding lists (n=%d d=%d)", n, d);
   }
   const size_t lds = (size_t)esz * ((size_t)((ld * n + 3) & ~3) + (p.tree_lds ? p.nleaves_al : 0)) + 4 * (size_t)((p.total + 3) & ~3) +

@@ -22,6 +22,7 @@
 namespace hq {
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
 
 // Bounds guard of the DIAG build (make DIAG=1): HQ_GUARD(p, base, lim) checks that the element offset
 // p - base lies in [0, lim); a violation is counted (hq_diag_violations, with the source line of the
@@ -3497,7 +3498,7 @@ __global__ __launch_bounds__(256) void k_refine_lds(HQ_REFINE_ARGS) {
 constexpr int kMaxTopKBig = 1024;  // list entries (k + slack) of the long-list path
 constexpr int kSortCap = 4096;     // pool keys sorted whole in LDS (32 KiB); larger pools are cut first
 
-__device__ __forceinline__ int pow2_at_least(int n) {
+__host__ __device__ __forceinline__ int pow2_at_least(int n) {
   int p = 2;
   while (p < n) p <<= 1;
   return p;
@@ -3731,6 +3732,349 @@ __global__ __launch_bounds__(256) void k_refine_big_sm_raw(HQ_REFINE_ARGS, int t
 }
 __global__ __launch_bounds__(256) void k_refine_big_raw(HQ_REFINE_ARGS, int tb) {
   refine_big_body<false, false>(HQ_REFINE_PASS, tb);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Lane-cooperative long-list re-rank (kp > 64, every level segment <= 128 values, L <= 128 even): the
+// default for the reference's M = 100 / 1000 lists.  k_refine_big gives each list entry one thread that
+// walks its candidate row 8 bytes at a time (a wave load instruction touches 64 rows: ~115 L2 requests
+// per pair, 79% of the wave cycles waiting on memory).  Here a group of 8 lanes scores one entry:
+//  * the group stages the candidate's raw row and statistics into its own LDS buffer with 16-byte loads
+//    (one wave load instruction = 8 rows x 128 contiguous bytes), one entry ahead in registers;
+//  * every NumPy pairwise sum of the exact score (n <= 128: eight strided accumulators r_j += a[i + j],
+//    ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), a sequential tail) runs with lane j owning r_j; the combination
+//    is three xor-shuffle adds (IEEE addition is commutative: both partners hold the same bits), the tail
+//    and the sums of < 8 values are evaluated identically by all 8 lanes — bit-identical to np_sum;
+//  * one pass computes every level of the entry (the [overall, level..] record), so each row is gathered
+//    once (k_refine_big: level 0 for the ranking, then the whole row again for the record).  Records of
+//    entries x < k go to odet[q][x] unsorted, the slack entries' to LDS; after the (score desc, id asc)
+//    bitonic sort every thread reads its outputs' records into registers (L1-bypassing loads), a
+//    barrier, then writes them in sorted order.
+// ------------------------------------------------------------------------------------------------
+constexpr int kCoopGroups = 32;              // 8-lane groups per 256-thread workgroup
+constexpr int kCoopMaxW = 7;                 // record width 1 + nseg
+constexpr int kCoopOut = kMaxTopKBig / 256;  // output entries per thread
+
+template <typename T>
+__device__ __forceinline__ T coop_xor(T v, int m) { return __shfl_xor(v, m, 64); }
+template <typename T>
+__device__ __forceinline__ Sum2<T> coop_xor(Sum2<T> v, int m) {
+  return Sum2<T>(__shfl_xor(v.a, m, 64), __shfl_xor(v.b, m, 64));
+}
+
+// np_sum<T, true>(f, n) (n <= 128) over the 8 lanes of a group; j = lane within the group.  Every lane
+// returns the same bits.
+template <typename T, class F>
+__device__ __forceinline__ T coop_sum(const F& f, int n, int j) {
+  T res;
+  if (n < 8) {
+    res = T(-0.0);
+#pragma unroll 1
+    for (int i = 0; i < n; ++i) res = res + f(i);
+  } else {
+    T r = f(j);
+    const int lim = n - (n % 8);
+#pragma unroll 1
+    for (int i = 8 + j; i < lim; i += 8) r = r + f(i);
+    r = r + coop_xor(r, 1);  // r_j + r_(j^1): (r0 + r1) on lanes 0 and 1
+    r = r + coop_xor(r, 2);  // (r0 + r1) + (r2 + r3)
+    r = r + coop_xor(r, 4);  // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
+    res = r;
+#pragma unroll 1
+    for (int i = lim; i < n; ++i) res = res + f(i);
+  }
+  return T(0) + res;
+}
+
+// make_side<true> with the float32 statistics summed by the group
+__device__ __forceinline__ Side coop_side(const double* x, const double* z, const double* st, int m, bool f32, int j) {
+  Side r;
+  r.x = x;
+  r.z = z;
+  r.f32 = f32;
+  if (f32) {
+    auto gx = [=](int k) -> float { return (float)x[k]; };
+    const float mean = coop_sum<float>(gx, m, j) / (float)m;
+    auto gd = [=](int k) -> float { const float d = (float)x[k] - mean; return d * d; };
+    const float sd = sqrtf(coop_sum<float>(gd, m, j) / (float)m);
+    auto gs = [=](int k) -> float { const float v = (float)x[k]; return v * v; };
+    r.mean = mean;
+    r.sd = sd;
+    r.msq = coop_sum<float>(gs, m, j) / (float)m;
+  } else {
+    r.mean = st[0];
+    r.sd = st[1];
+    r.msq = st[2];
+  }
+  return r;
+}
+
+// exact_level_sides<true, true> (one-pass Sum2 form) with the sums over the group
+__device__ __forceinline__ double coop_level_sides(const Side& q, const Side& c, int m, int j, int* np32) {
+  *np32 = 0;
+  const bool both32 = q.f32 && c.f32;
+  if (q.sd == 0.0 || c.sd == 0.0) return const0(q.sd == 0.0, c.sd == 0.0, q.mean, c.mean, both32);  // :141-148
+  if (both32) {
+    auto f2 = [&](int k) -> Sum2<float> {
+      const float d = (float)q.x[k] - (float)c.x[k];
+      return Sum2<float>((float)side_z(q, k) * (float)side_z(c, k), d * d);
+    };
+    const Sum2<float> s2 = coop_sum<Sum2<float>>(f2, m, j);
+    const float corr = s2.a / (float)m;                                            // :154
+    const float mse = s2.b / (float)m;                                             // :161
+    const float sim = (corr + 1.0f) / 2.0f;                                        // :158
+    const float maxmse = (float)q.msq + (float)c.msq;                              // :162
+    float ds = 1.0f;
+    if (maxmse > 0.0f) {
+      ds = 1.0f - mse / maxmse;
+      ds = ds > 0.0f ? ds : 0.0f;
+    }
+    const float comb = 0.7f * sim + 0.3f * ds;                                     // :171
+    if (comb < 1.0f && comb > 0.0f) {
+      *np32 = 1;
+      return comb;
+    }
+    return comb < 1.0f ? 0.0 : 1.0;                                                // :174
+  }
+  auto f2 = [&](int k) -> Sum2<double> {
+    const double d = q.x[k] - c.x[k];
+    return Sum2<double>(side_z(q, k) * side_z(c, k), d * d);
+  };
+  const Sum2<double> s2 = coop_sum<Sum2<double>>(f2, m, j);
+  const double corr = s2.a / (double)m;                                            // :154
+  const double mse = s2.b / (double)m;                                             // :161
+  const double sim = (corr + 1.0) / 2.0;                                           // :158
+  const double maxmse = q.msq + c.msq;                                             // :162
+  double ds = 1.0;
+  if (maxmse > 0.0) {
+    ds = 1.0 - (mse / maxmse);
+    ds = ds > 0.0 ? ds : 0.0;
+  }
+  const double a = 0.7 * sim;
+  const double b = 0.3 * ds;
+  double comb = a + b;                                                             // :171
+  comb = comb < 1.0 ? comb : 1.0;
+  return comb > 0.0 ? comb : 0.0;
+}
+
+// Compact level table of the cooperative kernels (a full SegInfo by value costs SGPRs they need)
+struct CoopSeg {
+  int nseg, L, Lp;
+  int src[kCoopMaxW - 1], len[kCoopMaxW - 1], poff[kCoopMaxW - 1];
+};
+
+// k_rank_pairs + k_rank_sort arguments; workspace per list entry: score (f64), id (i64) and, with records,
+// the [overall, level..] record (W doubles)
+struct RankArgs {
+  const double* Rq; const double* Zq; const double* Sq; int Q;
+  const double* Rc; const double* Sc; int64_t N;
+  CoopSeg cs;
+  int mode, kp, k, thr_mode, det;
+  double thr;
+  int64_t id_base;
+  const int64_t* cid;
+  double* ws_sc; int64_t* ws_id; double* ws_rec;
+};
+
+__host__ __device__ inline int coop_qw(const CoopSeg& c) { return (c.L + c.Lp + 4 * c.nseg + 1) & ~1; }
+__host__ __device__ inline int coop_rw(const CoopSeg& c) { return (c.L + 4 * c.nseg + 1) & ~1; }
+
+// Scoring pass: block (x-block, query) = 32 list entries of one query, one 8-lane group per entry.  The
+// block stages the query row (raw, Z, S) and each group its candidate's raw row and statistics (16-byte
+// loads: one wave load instruction covers 8 rows x 128 contiguous bytes) into LDS, then the group scores
+// every level of the entry (nlev: level 0 only for a mode-0 ranking without records) and writes the
+// ranking score, id and record to the workspace.  One pair per group, no loop: the occupancy hides the
+// row latency.  Bit-identical to exact_pair (coop_level_sides = exact_level_sides<true, true>).
+template <int PPL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_rank_pairs(RankArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double cm[];
+  const int tid = threadIdx.x, g = tid >> 3, j = tid & 7;
+  const int q = blockIdx.y, x = blockIdx.x * kCoopGroups + g;
+  const int L = a.cs.L, Lp = a.cs.Lp, nseg = a.cs.nseg;
+  const int QW = coop_qw(a.cs), RW = coop_rw(a.cs);
+  double* rq = cm;
+  double* rg = cm + QW + g * RW;
+  for (int e = tid; e < L; e += 256) rq[e] = a.Rq[(int64_t)q * L + e];
+  for (int e = tid; e < Lp; e += 256) rq[L + e] = a.Zq[(int64_t)q * Lp + e];
+  for (int e = tid; e < 4 * nseg; e += 256) rq[L + Lp + e] = a.Sq[(int64_t)q * nseg * 4 + e];
+  int64_t c = -1;
+  if (x < a.kp) {
+    const int64_t id = a.cid[(int64_t)q * a.kp + x];
+    const int64_t cc = id - a.id_base;
+    if (id >= 0 && cc >= 0 && cc < a.N) c = cc;
+  }
+  if (c >= 0) {
+    const int np_raw = L / 2, np_all = np_raw + 2 * nseg;
+    const f64x2* rr = reinterpret_cast<const f64x2*>(a.Rc + c * L);
+    const f64x2* rs = reinterpret_cast<const f64x2*>(a.Sc + c * nseg * 4);
+    f64x2 v[PPL];
+#pragma unroll
+    for (int p = 0; p < PPL; ++p) {
+      const int pc = j + 8 * p;
+      if (pc < np_all) v[p] = pc < np_raw ? rr[pc] : rs[pc - np_raw];
+    }
+#pragma unroll
+    for (int p = 0; p < PPL; ++p) {
+      const int pc = j + 8 * p;
+      if (pc < np_all) reinterpret_cast<f64x2*>(rg)[pc] = v[p];
+    }
+  }
+  __syncthreads();
+  if (x >= a.kp) return;
+  const int W = 1 + nseg;
+  const int64_t e0 = (int64_t)q * a.kp + x;
+  double e = -__builtin_huge_val();
+  int64_t id = -1;
+  if (c >= 0) {
+    const int nlev = (a.mode == 0 && !a.det) ? 1 : nseg;
+    double tws = 0.0, tw = 0.0, v0 = 0.0;
+    bool acc32 = false;
+    int t0 = 0;
+#pragma unroll 1
+    for (int s = 0; s < nlev; ++s) {
+      const int m = a.cs.len[s];
+      const double* qst = rq + L + Lp + 4 * s;
+      const double* cst = rg + L + 4 * s;
+      int t32;
+      const double v = coop_level_sides(
+          coop_side(rq + a.cs.src[s], rq + L + a.cs.poff[s], qst, m, (aux_bits(qst) & kAuxF32) != 0, j),
+          coop_side(rg + a.cs.src[s], nullptr, cst, m, (aux_bits(cst) & kAuxF32) != 0, j), m, j, &t32);
+      if (s == 0) {
+        v0 = v;
+        t0 = t32;
+      }
+      if (a.det && j == 0) a.ws_rec[e0 * W + 1 + s] = v;
+      // search_engine.py:191-230 typed running sum (exact_pair_rows)
+      const double w = 1.0 / (double)(s + 1);
+      const double term = t32 ? (double)((float)v * (float)w) : v * w;
+      if (!acc32 && !t32) {
+        tws = tws + term;
+      } else {
+        tws = (double)((float)tws + (float)term);
+        acc32 = true;
+      }
+      tw = tw + w;
+    }
+    double ov = 0.0;
+    if (nlev == nseg) {
+      if (acc32) {
+        const float o = (float)tws / (float)tw;
+        ov = o < 1.0f ? (double)o : 1.0;
+      } else {
+        ov = tw > 0.0 ? tws / tw : 0.0;
+        ov = ov < 1.0 ? ov : 1.0;
+      }
+      ov = ov > 0.0 ? ov : 0.0;
+    }
+    if (a.det && j == 0) a.ws_rec[e0 * W] = ov;
+    const double v = a.mode == 0 ? v0 : ov;
+    const bool pass = a.mode == 0 ? typed_pass(v, t0, a.thr, a.thr_mode)
+                                  : (a.thr_mode == 0 || (a.thr_mode == 1 ? v >= a.thr : v > a.thr));
+    if (pass) {
+      e = v;
+      id = c + a.id_base;
+    }
+  }
+  if (j == 0) {
+    a.ws_sc[e0] = e;
+    a.ws_id[e0] = id;
+  }
+}
+
+// Ranking pass (one 256-thread workgroup per query): the list's exact scores from the workspace, the
+// (score desc, id asc) bitonic sort in LDS, the outputs (records gathered by list position), the count
+// and the completeness proof as refine_big_body.
+__global__ __launch_bounds__(256) void k_rank_sort(RankArgs a, const double* __restrict__ cs, double eps,
+                                                   double* __restrict__ os, int64_t* __restrict__ oid,
+                                                   int* __restrict__ ocnt, int* __restrict__ ores, int count_empty,
+                                                   int* __restrict__ oredo, double* __restrict__ odet,
+                                                   int* __restrict__ onext) {
+  if (onext && blockIdx.x == 0 && threadIdx.x == 0) *onext = 0;  // the next batch's redo counter
+  __shared__ double se[kMaxTopKBig];
+  __shared__ int64_t sid[kMaxTopKBig];
+  __shared__ int pos[kMaxTopKBig];
+  __shared__ int red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kp = a.kp, k = a.k, W = 1 + a.cs.nseg;
+  const int n2 = pow2_at_least(kp);
+  const bool k32 = (a.thr_mode & kThrKey32) != 0;
+  const int thr_mode = a.thr_mode & (kThrKey32 - 1);
+  for (int q = blockIdx.x; q < a.Q; q += gridDim.x) {
+    const int64_t base = (int64_t)q * kp;
+    int nv = 0;
+    for (int x = tid; x < n2; x += 256) {
+      const int64_t i = x < kp ? a.ws_id[base + x] : -1;
+      se[x] = x < kp ? a.ws_sc[base + x] : -__builtin_huge_val();
+      sid[x] = i;
+      pos[x] = x;
+      nv += i >= 0 ? 1 : 0;
+    }
+    nv = wsum64i(nv);
+    if (lane == 0) red[wave] = nv;
+    __syncthreads();
+    const int n = red[0] + red[1] + red[2] + red[3];
+    lds_bitonic(n2,
+                [&](int x, int y) {
+                  const int64_t ix = sid[x], iy = sid[y];
+                  if (iy < 0) return ix >= 0;
+                  const double kx = key_of(se[x], k32), ky = key_of(se[y], k32);
+                  return ix >= 0 && (kx > ky || (kx == ky && ix < iy));
+                },
+                [&](int x, int y) {
+                  const double te = se[x];
+                  se[x] = se[y];
+                  se[y] = te;
+                  const int64_t ti = sid[x];
+                  sid[x] = sid[y];
+                  sid[y] = ti;
+                  const int tp = pos[x];
+                  pos[x] = pos[y];
+                  pos[y] = tp;
+                });
+    const int cnt = n < k ? n : k;
+    for (int r = tid; r < k; r += 256) {
+      os[(int64_t)q * k + r] = r < cnt ? se[r] : -__builtin_huge_val();
+      oid[(int64_t)q * k + r] = r < cnt ? sid[r] : -1;
+    }
+    if (odet) {
+      for (int t = tid; t < k * W; t += 256) {
+        const int r = t / W, w = t - r * W;
+        odet[(int64_t)q * k * W + t] = r < cnt ? a.ws_rec[(base + pos[r]) * W + w] : 0.0;
+      }
+    }
+    if (tid == 0) {
+      const double kth = n >= k ? se[k - 1] : -__builtin_huge_val();
+      ocnt[q] = cnt;
+      const bool full = a.cid[base + kp - 1] >= 0;
+      // an empty last slot with score +inf: the scan's list may be incomplete (k_pool_select)
+      const bool trunc = !full && cs[base + kp - 1] == __builtin_huge_val();
+      int res = trunc ? 0 : 1;
+      if (full) {
+        const double bound = cs[base + kp - 1] + eps;
+        if (n >= k) res = k32 ? (float)bound < (float)kth : bound < kth;
+        else if (thr_mode == 0) res = 0;
+        else res = thr_mode == 1 ? (bound < thr_low(a.thr)) : (bound <= thr_low(a.thr));
+      }
+      ores[q] = res;
+      if (oredo && (res == 0 || (count_empty && cnt == 0))) atomicAdd(oredo, 1);
+    }
+    __syncthreads();
+  }
+}
+
+// shapes of the cooperative re-rank: every segment <= 128 values, L even, record width <= kCoopMaxW,
+// <= 10 16-byte row pieces per lane; 0 = not supported
+static int coop_ppl(const SegInfo& si) {
+  if (!seg_small(si) || si.L % 2 != 0 || 1 + si.nseg > kCoopMaxW) return 0;
+  const int ppl = (si.L / 2 + 2 * si.nseg + 7) / 8;
+  return ppl <= 6 ? 6 : (ppl <= 10 ? 10 : 0);
+}
+
+static size_t refine_ws_bytes(int Q, int kp, int L) {
+  if (Q <= 0 || kp <= 0 || L <= 0) return 0;
+  SegInfo si;
+  seg_info(L, si);
+  return (size_t)Q * kp * (16 + 8 * (size_t)(1 + si.nseg)) + 256;
 }
 
 // k_progressive_final for M > 64: wave 0 selects the survivors (final_survivors), the workgroup sorts them
@@ -4096,7 +4440,9 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
                                         (size_t)Q * 8);
   // k_scan0g (default; option scan_variant 1 = the list-based k_scan0f): per-query constants after the
   // sample tops, 256-B aligned
-  const bool queue_scan = f32 && opt(OPT_SCAN_VARIANT, 0) != 1;
+  // (the list kernel keeps one list entry per lane and nchunks x k pool slots: k <= 64 only, so longer
+  // lists always take the queue scan whatever the option says)
+  const bool queue_scan = f32 && (opt(OPT_SCAN_VARIANT, 0) != 1 || k > kMaxTopK);
   const size_t qc_off = ((size_t)(reinterpret_cast<uint8_t*>(top) - ws) + sample_top_bytes(Q, N) + 255) & ~(size_t)255;
   QConst* qc = queue_scan ? reinterpret_cast<QConst*>(ws + qc_off) : nullptr;
   b.qconst = qc;
@@ -4311,7 +4657,7 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
                          const int64_t* cand_id, int kp, int k, double threshold, int thr_mode, double eps,
                          int64_t id_base, double* out_score, int64_t* out_id, int* out_count, int* out_resolved,
                          int count_empty, int* out_redo, double* out_det, hq_stream_t stream,
-                         int* next_redo = nullptr) {
+                         int* next_redo = nullptr, void* workspace = nullptr, size_t workspace_bytes = 0) {
   SegInfo si;
   seg_info(L, si);
   const hipStream_t s = (hipStream_t)stream;
@@ -4321,6 +4667,36 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
   if (out_redo && !next_redo) HQ_CHECK_HIP(hipMemsetAsync(out_redo, 0, sizeof(int), s));
   const bool sm = seg_small(si);
   if (kp > kMaxTopK) {  // long lists: rows read from global memory, one workgroup per query
+    // with a workspace (hq_refine_topk_ws): the lane-cooperative pair scoring (k_rank_pairs: 8 lanes per
+    // entry, rows staged per group, every level in one pass) + the per-query ranking (k_rank_sort) where
+    // its shapes hold; option refine_coop = 0 keeps the one-thread-per-entry kernels below (A/B, parity)
+    const int ppl = coop_ppl(si);
+    if (workspace && ppl && opt(OPT_REFINE_COOP, 1) != 0 && Q <= 65535) {
+      if (workspace_bytes < refine_ws_bytes(Q, kp, L)) return fail(HQ_E_INVALID, "workspace too small");
+      RankArgs ra;
+      ra.Rq = Rq; ra.Zq = Zq; ra.Sq = Sq; ra.Q = Q; ra.Rc = Rc; ra.Sc = Sc; ra.N = N;
+      ra.cs.nseg = si.nseg; ra.cs.L = si.L; ra.cs.Lp = si.Lp;
+      for (int i = 0; i < kCoopMaxW - 1; ++i) {
+        ra.cs.src[i] = i < si.nseg ? si.src[i] : 0;
+        ra.cs.len[i] = i < si.nseg ? si.len[i] : 0;
+        ra.cs.poff[i] = i < si.nseg ? si.poff[i] : 0;
+      }
+      ra.mode = mode; ra.kp = kp; ra.k = k; ra.thr_mode = thr_mode; ra.det = out_det ? 1 : 0; ra.thr = threshold;
+      ra.id_base = id_base; ra.cid = cand_id;
+      uint8_t* w = reinterpret_cast<uint8_t*>(workspace);
+      ra.ws_sc = reinterpret_cast<double*>(w);
+      ra.ws_id = reinterpret_cast<int64_t*>(w + (size_t)Q * kp * 8);
+      ra.ws_rec = reinterpret_cast<double*>(w + (size_t)Q * kp * 16);
+      const size_t lds = 8 * ((size_t)coop_qw(ra.cs) + (size_t)kCoopGroups * coop_rw(ra.cs));
+      const dim3 g1((kp + kCoopGroups - 1) / kCoopGroups, Q);
+      if (ppl == 6) hipLaunchKernelGGL(k_rank_pairs<6>, g1, dim3(256), lds, s, ra);
+      else hipLaunchKernelGGL(k_rank_pairs<10>, g1, dim3(256), lds, s, ra);
+      HQ_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_rank_sort, dim3(grid), dim3(256), 0, s, ra, cand_score, eps, out_score, out_id, out_count,
+                         out_resolved, count_empty ? 1 : 0, out_redo, out_det, next_redo);
+      HQ_CHECK_LAUNCH();
+      return HQ_OK;
+    }
     // lists of >= 512: the candidates' raw rows only (refine_big_body's ZB)
     const bool raw = kp >= 512;
     auto kern = sm ? (raw ? k_refine_big_sm_raw : k_refine_big_sm) : (raw ? k_refine_big_raw : k_refine_big);
@@ -5409,6 +5785,10 @@ int hq_level_scores(const double* Rq, const double* Zq, const double* Sq, int Q,
   if (level >= 0 && level < si.nseg && si.len[level] <= 128 && !opt_on(OPT_LEVEL_SCORES_V1) &&
       (N + kLsTile - 1) / kLsTile < (int64_t(1) << 31) && (Q + kLsQ - 1) / kLsQ < 65536) {
     const size_t lds = (size_t)kLsTile * (si.len[level] | 1) * 8;
+    // segments of 65..128 values stage up to 132 KB: above the 64 KB default, so opt in (one block per CU)
+    if (lds > 65536)
+      HQ_CHECK_HIP(hipFuncSetAttribute((const void*)k_level_scores_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds));
     hipLaunchKernelGGL(k_level_scores_lds, dim3((unsigned)((N + kLsTile - 1) / kLsTile), (Q + kLsQ - 1) / kLsQ),
                        dim3(kLsTile), lds, (hipStream_t)stream, VecSet{Rq, Zq, Sq}, Q, VecSet{Rc, Zc, Sc}, N, si, level,
                        scores);
@@ -5476,6 +5856,28 @@ int hq_refine_rescore_topk(const double* Rq, const double* Zq, const double* Sq,
     return fail(HQ_E_INVALID, "null buffer");
   return refine_launch(Rq, Zq, Sq, Q, Rc, Zc, Sc, N, L, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps,
                        id_base, out_score, out_id, out_count, out_resolved, count_empty, out_redo, out_det, stream);
+}
+
+size_t hq_refine_workspace_size(int Q, int kp, int L) { return refine_ws_bytes(Q, kp, L); }
+
+int hq_refine_topk_ws(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc, const double* Zc,
+                      const double* Sc, int64_t N, int L, int mode, const double* cand_score, const int64_t* cand_id,
+                      int kp, int k, double threshold, int thr_mode, double eps, int64_t id_base, double* out_score,
+                      int64_t* out_id, int* out_count, int* out_resolved, int count_empty, int* out_redo,
+                      int* next_redo, double* out_det, void* workspace, size_t workspace_bytes, hq_stream_t stream) {
+  if (Q < 0 || N < 0 || L <= 0 || kp <= 0 || kp > kMaxTopKBig || k <= 0 || k > kp)
+    return fail(HQ_E_INVALID, "bad sizes kp=%d k=%d", kp, k);
+  if (Q == 0) {  // no kernel runs: the next batch's counter is still cleared
+    if (next_redo) HQ_CHECK_HIP(hipMemsetAsync(next_redo, 0, sizeof(int), (hipStream_t)stream));
+    return HQ_OK;
+  }
+  if (!Rq || !Zq || !Sq || !cand_score || !cand_id || !out_score || !out_id || !out_count || !out_resolved ||
+      (next_redo && (!out_redo || out_redo == next_redo)) || (N > 0 && (!Rc || !Zc || !Sc)))
+    return fail(HQ_E_INVALID, "null buffer");
+  if (workspace && workspace_bytes < hq_refine_workspace_size(Q, kp, L)) return fail(HQ_E_INVALID, "workspace too small");
+  return refine_launch(Rq, Zq, Sq, Q, Rc, Zc, Sc, N, L, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps,
+                       id_base, out_score, out_id, out_count, out_resolved, count_empty, out_redo, out_det, stream,
+                       next_redo, workspace, workspace_bytes);
 }
 
 size_t hq_scan_workspace_size(int Q, int64_t N, int k) {

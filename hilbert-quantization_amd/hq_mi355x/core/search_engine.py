@@ -270,6 +270,24 @@ class IndexCorpus:
             redo = redo | forced
         sel = t.nonzero(redo).view(-1)
         if sel.numel():
+            # unproven lists (near-ties at the list end, short lists) first get the scan path with a longer
+            # list; nothing-passed rows (arg-max), forced rows and what stays unproven take the dense path
+            try_ = res[sel] == 0
+            if need_best:
+                try_ = try_ & (cnt[sel] > 0)
+            if forced is not None:
+                try_ = try_ & ~forced[sel]
+            rsel = sel[try_]
+            if rsel.numel():
+                got = self._retry_scan(qp.rows(rsel), mode, k, thr, thr_mode, det=False)
+                if got is not None:
+                    s2, i2, c2, r2 = got
+                    ok = (r2 == 1) & (c2 > 0) if need_best else (r2 == 1)
+                    sc[rsel[ok]], ids[rsel[ok]], cnt[rsel[ok]] = s2[ok], i2[ok], c2[ok]
+                    keep = t.ones(sel.numel(), dtype=t.bool, device=dev)
+                    keep[t.nonzero(try_).view(-1)[ok]] = False
+                    sel = sel[keep]
+        if sel.numel():
             s2, i2, b2, bi2 = self._dense(qp, sel, mode, k, thr, thr_mode)
             sc[sel] = s2
             ids[sel] = i2
@@ -277,6 +295,63 @@ class IndexCorpus:
             best[sel] = b2
             bid[sel] = bi2
         return sc, ids, cnt, best, bid
+
+    RETRY_FACTOR = 4
+
+    def _retry_scan(self, qp, mode: int, k: int, thr: float, thr_mode: int, det: bool = False):
+        """The scan path again for queries whose list was not proven complete, with a list RETRY_FACTOR
+        times longer (at most the scan's limit): a list ends in near-ties when more than SLACK candidates
+        lie within EPS of the k-th (runs of near-duplicates in the corpus), or short when the sampled
+        starting threshold overshot.  None when no longer list is available.  Returns refine_topk's
+        (scores, ids, count, resolved) (+ det, the [overall, levels] records, with det)."""
+        kp2 = min(self._max_list(mode), self.RETRY_FACTOR * (k + self.SLACK))
+        if kp2 <= k + self.SLACK or not self._fused_ok(mode) or self.dense_only:
+            return None
+        self.stats["retry_queries"] += qp.N
+        lo_mode = 0 if thr_mode == 0 else 1
+        asc, aid, _, _ = K.scan_topk(qp, self.prep, mode, kp2, thr - self.EPS, lo_mode, self.id_base)
+        tm = thr_mode | (K.THR_KEY32 if self.key32(qp) else 0)
+        if det:
+            return K.refine_rescore_topk(qp, self.prep, mode, asc, aid, k, thr, tm, self.EPS, self.id_base,
+                                         count_empty=True)
+        return K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, tm, self.EPS, self.id_base, count_empty=True)
+
+    def _level0_redo(self, qp, sel, M: int, thr: float, res, cnt, forced):
+        """Exact level-0 top-M (>= thr) records of the queries `sel` the first pass left unproven or empty:
+        unproven lists where something passed are re-scanned with a longer list (_retry_scan); the rest —
+        nothing passed (the arg-max fallback), forced rows, lists the retry leaves unproven — take the dense
+        exact path.  Returns (s0 [n, M], ids [n, M], best [n], bid [n], det [n, M, W], bdet [n, W])."""
+        t = torch()
+        n, dev, W = int(sel.numel()), sel.device, 1 + self.nseg
+        s0 = t.full((n, M), -float("inf"), dtype=t.float64, device=dev)
+        ids = t.full((n, M), -1, dtype=t.int64, device=dev)
+        best = t.full((n,), -float("inf"), dtype=t.float64, device=dev)
+        bid = t.full((n,), -1, dtype=t.int64, device=dev)
+        det = t.zeros((n, M, W), dtype=t.float64, device=dev)
+        bdet = t.zeros((n, W), dtype=t.float64, device=dev)
+        need = t.ones(n, dtype=t.bool, device=dev)
+        try_ = (res[sel] == 0) & (cnt[sel] > 0)
+        if forced is not None:
+            try_ = try_ & ~forced[sel]
+        r = t.nonzero(try_).view(-1)
+        if r.numel():
+            got = self._retry_scan(qp.rows(sel[r]), 0, M, thr, 1, det=True)
+            if got is not None:
+                s2, i2, c2, r2, d2 = got
+                ok = (r2 == 1) & (c2 > 0)
+                rr = r[ok]
+                s0[rr], ids[rr], det[rr] = s2[ok], i2[ok], d2[ok]
+                need[rr] = False
+        d = t.nonzero(need).view(-1)
+        if d.numel():
+            self.stats["dense_queries"] += int(d.numel())
+            dsel = sel[d]
+            sub = qp.rows(dsel)
+            s3, i3, b3, bi3 = self._dense(qp, dsel, 0, M, thr, 1)
+            s0[d], ids[d], best[d], bid[d] = s3, i3, b3, bi3
+            det[d] = K.rescore(sub, self.prep, i3, self.id_base)
+            bdet[d] = K.rescore(sub, self.prep, bi3.view(-1, 1), self.id_base).view(-1, W)
+        return s0, ids, best, bid, det, bdet
 
     # ---- searches ----------------------------------------------------------------------------
     def brute_force(self, queries, max_results: int):
@@ -343,18 +418,41 @@ class IndexCorpus:
         p.event.synchronize()
         nredo = int(p.nredo[0])
         self._pinned_free.setdefault(p.nredo.dtype, []).append(p.nredo)  # read: reusable
+        st = self.stats
+        st["batches"] += 1
+        st["queries"] += p.qp.N
         if nredo > 0:
+            import time as _time
+            t0 = _time.perf_counter()
+            st["redo_batches"] += 1
             redo = (p.res == 0) | (p.cnt == 0)
             if p.forced is not None:
                 redo = redo | p.forced
             sel = t.nonzero(redo).view(-1)
             if sel.numel():
-                s2, i2, b2, bi2 = self._dense(p.qp, sel, 0, p.M, p.threshold, 1)
-                sub = p.qp.rows(sel)
-                o2, d2, c2 = self._final(sub, s2, i2, b2, bi2, p.K_out)
-                oid[sel], odet[sel], ocnt[sel] = o2, d2, c2
+                s2, i2, b2, bi2, d2, bd2 = self._level0_redo(p.qp, sel, p.M, p.threshold, p.res, p.cnt, p.forced)
+                o2, dd2, c2 = self._final(p.qp.rows(sel), s2, i2, b2, bi2, p.K_out, bdet=bd2, det=d2)
+                oid[sel], odet[sel], ocnt[sel] = o2, dd2, c2
+                st["redo_queries"] += int(sel.numel())
+            t.cuda.current_stream().synchronize()
+            st["dense_s"] += _time.perf_counter() - t0
         p.done = (oid, odet[..., 0], odet[..., 1:], ocnt)  # finishing again returns the same results
         return p.done
+
+    @property
+    def stats(self) -> dict:
+        """Counters of the submitted progressive batches: batches / queries finished, batches and queries
+        redone after the first pass (short or unproven lists, nothing passing, forced rows), and the
+        host wall time spent there (dense_s; it synchronises the stream); of the redone queries, those
+        re-scanned with a longer list (retry_queries) and those scored densely (dense_queries)."""
+        st = self.__dict__.get("_stats")
+        if st is None:
+            st = self.__dict__["_stats"] = {"batches": 0, "queries": 0, "redo_batches": 0, "redo_queries": 0,
+                                            "retry_queries": 0, "dense_queries": 0, "dense_s": 0.0}
+        return st
+
+    def reset_stats(self):
+        self.__dict__.pop("_stats", None)
 
     def _pinned(self, dtype):
         """A one-element pinned host buffer: recycled once its batch is finished (a fresh pinned

@@ -88,18 +88,19 @@ class ShardedIndexCorpus:
         flag.copy_(redo.any().view(1), non_blocking=True)
         ev = t.cuda.Event()
         ev.record()
-        return qp, M, float(threshold), rec, redo, flag, ev
+        return qp, M, float(threshold), rec, (redo, res, cnt, forced), flag, ev
 
     def _local_finish(self, pending):
         t = torch()
-        qp, M, threshold, rec, redo, flag, ev = pending
+        qp, M, threshold, rec, (redo, res, cnt, forced), flag, ev = pending
         ev.synchronize()
         any_redo = bool(flag[0])
         self.local._pinned_free.setdefault(flag.dtype, []).append(flag)  # read: reusable
         if any_redo:
+            # unproven lists re-scanned with a longer list, the rest on the dense exact path (IndexCorpus)
             sel = t.nonzero(redo).view(-1)
-            s2, i2, b2, bi2 = self.local._dense(qp, sel, 0, M, threshold, 1)
-            rec[sel] = self._records(qp.rows(sel), s2, i2, b2, bi2)
+            s2, i2, b2, bi2, d2, bd2 = self.local._level0_redo(qp, sel, M, threshold, res, cnt, forced)
+            rec[sel] = self._records(qp.rows(sel), s2, i2, b2, bi2, d2, bd2.view(-1, 1, bd2.shape[-1]))
         return rec
 
     def _records(self, q, s0_, ids_, best_, bid_, det=None, bdet=None):

@@ -440,11 +440,30 @@ def refine_topk(q: Prepared, c: Prepared, mode: int, cand_score, cand_id, k: int
     oi = t.empty((Q, k), dtype=t.int64, device=dev)
     cnt = t.empty(Q, dtype=t.int32, device=dev)
     res = t.empty(Q, dtype=t.int32, device=dev)
+    if kp > 64:  # long lists: the lane-cooperative re-rank with its workspace
+        _refine_ws(q, c, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, os_, oi, cnt, res,
+                   count_empty, redo, None, None, exc)
+        return os_, oi, cnt, res
     _chk(_L().hq_refine_topk(ptr(q.R), ptr(q.Z), ptr(q.S), Q, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L, mode,
                              ptr(_contig(cand_score)), ptr(_contig(cand_id)), kp, k, float(threshold), thr_mode,
                              float(eps), int(id_base), ptr(os_), ptr(oi), ptr(cnt), ptr(res), 1 if count_empty else 0,
                              ptr(redo), stream()), exc)
     return os_, oi, cnt, res
+
+
+def _refine_ws(q, c, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, os_, oi, cnt, res,
+               count_empty, redo, next_redo, det, exc):
+    """hq_refine_topk_ws (lists > 64: k_rank_pairs + k_rank_sort) on the stream's reusable workspace (the
+    scan that produced the list has finished with it in stream order)."""
+    Q = int(cand_id.shape[0])
+    dev = cand_id.device
+    wb = int(_lib.load().hq_refine_workspace_size(Q, kp, c.L))
+    ws = _workspace(wb, dev)
+    _chk(_L().hq_refine_topk_ws(ptr(q.R), ptr(q.Z), ptr(q.S), Q, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L, mode,
+                                ptr(_contig(cand_score)), ptr(_contig(cand_id)), kp, k, float(threshold), thr_mode,
+                                float(eps), int(id_base), ptr(os_), ptr(oi), ptr(cnt), ptr(res),
+                                1 if count_empty else 0, ptr(redo), ptr(next_redo), ptr(det), ptr(ws), wb, stream()),
+         exc)
 
 
 def refine_rescore_topk(q: Prepared, c: Prepared, mode: int, cand_score, cand_id, k: int, threshold: float = 0.0,
@@ -460,6 +479,10 @@ def refine_rescore_topk(q: Prepared, c: Prepared, mode: int, cand_score, cand_id
     cnt = t.empty(Q, dtype=t.int32, device=dev)
     res = t.empty(Q, dtype=t.int32, device=dev)
     det = t.empty((Q, k, 1 + q.nseg), dtype=t.float64, device=dev)
+    if kp > 64:  # long lists: the lane-cooperative re-rank with its workspace
+        _refine_ws(q, c, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps, id_base, os_, oi, cnt, res,
+                   count_empty, redo, next_redo, det, exc)
+        return os_, oi, cnt, res, det
     if next_redo is not None:  # ping-pong counters: redo arrives zeroed, the kernel clears next_redo
         _chk(_L().hq_refine_rescore_topk_pp(ptr(q.R), ptr(q.Z), ptr(q.S), Q, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L,
                                             mode, ptr(_contig(cand_score)), ptr(_contig(cand_id)), kp, k,

@@ -323,6 +323,22 @@ int hq_refine_rescore_topk_pp(const double* Rq, const double* Zq, const double* 
                               double* out_score, int64_t* out_id, int* out_count, int* out_resolved,
                               int count_empty, int* out_redo, int* next_redo, double* out_det,
                               hq_stream_t stream);
+/* The three entries above in one, with a device workspace (hq_refine_workspace_size bytes; may be NULL):
+ * out_det and next_redo nullable (NULL out_det = hq_refine_topk's outputs; a non-NULL next_redo = the
+ * ping-pong counters of hq_refine_rescore_topk_pp).  Lists longer than 64 then run the lane-cooperative
+ * re-rank: 8 lanes score one list entry (NumPy's eight pairwise accumulators one per lane, the row staged
+ * with 16-byte loads), every level of the entry in one pass over its row, the exact scores, ids and records
+ * to the workspace, then one workgroup per query ranks them.  Same outputs, bit for bit.
+ * Replaces the re-rank arithmetic of core/search_engine.py:232-300 (level-0 filter) and :340-388
+ * (overall re-score of the survivors) for the reference's default lists (M = 100, :31; 1000, config.py:181). */
+size_t hq_refine_workspace_size(int Q, int kp, int L);
+int hq_refine_topk_ws(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
+                      const double* Zc, const double* Sc, int64_t N, int L, int mode,
+                      const double* cand_score, const int64_t* cand_id, int kp, int k,
+                      double threshold, int thr_mode, double eps, int64_t id_base,
+                      double* out_score, int64_t* out_id, int* out_count, int* out_resolved,
+                      int count_empty, int* out_redo, int* next_redo, double* out_det,
+                      void* workspace, size_t workspace_bytes, hq_stream_t stream);
 
 /* ---- S4 on candidate lists: EXACT overall + per-level scores of selected pairs ---------------
  * ids: int64 Q x k GLOBAL ids (row = id - id_base; out of range / < 0 -> zeros);

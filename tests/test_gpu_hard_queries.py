@@ -1,0 +1,102 @@
+"""The progressive search on query distributions without a planted near-duplicate,
+at the BASELINE cfg3 size: 1000 FRESH queries (index vectors of new N(0,1) embeddings, whose top-10 sit in
+the bulk of the score distribution) over the 1M-row cfg3 corpus, and a 1M-row CLUSTERED corpus (64-row runs
+of near-duplicates, queries drawn from the runs).  Every query's ids, counts, overall and per-level scores
+at the reference's list lengths M = 20 (HilbertQuantizer), 100 (ProgressiveSimilaritySearchEngine's
+default, core/search_engine.py:31) and 1000 (SearchConfig, config.py:181) are compared with the dense
+exact path (every pair's exact level-0 score, exact top-M select, exact re-score and final ranking,
+core/search_engine.py:232-300, 340-388), and sampled queries with the oracle."""
+import numpy as np
+import pytest
+
+from oracle import hq_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+N, QN, RUN = 1_000_000, 1000, 64
+
+
+def _np(x):
+    from hq_mi355x._dev import to_np
+    return to_np(x)
+
+
+def _dense_progressive(corpus, Q, K_out, thr, M):
+    """The dense exact path for every query (the product's fallback, independent of the scans)."""
+    import torch
+    qp = corpus.prepare_queries(Q)
+    s0, ids, best, bid = corpus._dense(qp, torch.arange(qp.N, device=Q.device), 0, M, thr, 1)
+    oid, odet, ocnt = corpus._final(qp, s0, ids, best, bid, K_out)
+    return oid, odet[..., 0], odet[..., 1:], ocnt
+
+
+def _check_all(corpus, Q, M, max_dense):
+    """progressive() == the dense exact path for every query; at most max_dense queries left for the dense
+    path after the longer-list retry (IndexCorpus._retry_scan)."""
+    corpus.reset_stats()
+    got = [_np(x) for x in corpus.progressive(Q, 10, 0.1, M)]
+    st = dict(corpus.stats)
+    print(f"M={M}: {st}")
+    want = [_np(x) for x in _dense_progressive(corpus, Q, 10, 0.1, M)]
+    for x, y, name in zip(got, want, ("ids", "overall", "levels", "count")):
+        np.testing.assert_array_equal(x, y, err_msg=f"M={M} {name}")
+    assert st["dense_queries"] <= max_dense, (M, st)
+    return got
+
+
+def _oracle_many(Qh, Ch, rows, M):
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(8) as ex:
+        return list(ex.map(lambda a: O.progressive_search(Qh[a], Ch, 10, 0.1, M), rows))
+
+
+def _cfg3_corpus():
+    import torch
+    from hq_mi355x import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(2)
+    Xc = torch.randn((N, 1536), generator=g, device="cuda", dtype=torch.float32)
+    _, C, _ = K.map_index_quantize(Xc, 64, 64)
+    return C
+
+
+def test_fresh_queries_full_size(hq_lib):
+    """1000 fresh queries (seed-5 embeddings through the fused kernel) over the cfg3 corpus: every query
+    equal to the dense exact path at M = 20 / 100 / 1000; sampled queries equal to the oracle."""
+    import torch
+    from hq_mi355x import kernels as K
+    from hq_mi355x.core.search_engine import IndexCorpus
+    C = _cfg3_corpus()
+    gf = torch.Generator(device="cuda").manual_seed(5)
+    _, Q, _ = K.map_index_quantize(torch.randn((QN, 1536), generator=gf, device="cuda", dtype=torch.float32), 64, 64)
+    corpus = IndexCorpus(C)
+    res = {M: _check_all(corpus, Q, M, max_dense=2) for M in (20, 100, 1000)}
+    Ch, Qh = _np(C), _np(Q)
+    for M, rows in ((20, [0, 1, 2, 357, 999]), (100, [3, 500])):
+        ids, ov = res[M][0], res[M][1]
+        for a, (rid, rsc, _, _) in zip(rows, _oracle_many(Qh, Ch, rows, M)):
+            assert list(ids[a]) == list(rid), (M, a)
+            np.testing.assert_allclose(ov[a], rsc, atol=1e-10)
+
+
+def test_clustered_corpus_full_size(hq_lib):
+    """A 1M-row corpus of 64-row runs of near-duplicates (15,625 base vectors + N(0, 0.01)); 1000 queries
+    drawn from the runs: every query equal to the dense exact path at M = 20 / 100 / 1000, its own run on
+    top; sampled queries equal to the oracle."""
+    import torch
+    from hq_mi355x import kernels as K
+    from hq_mi355x.core.search_engine import IndexCorpus
+    nb = N // RUN
+    g = torch.Generator(device="cuda").manual_seed(6)
+    _, B, _ = K.map_index_quantize(torch.randn((nb, 1536), generator=g, device="cuda", dtype=torch.float32), 64, 64)
+    C = B.repeat_interleave(RUN, 0)
+    C.add_(0.01 * torch.randn(C.shape, generator=g, device="cuda", dtype=torch.float64))
+    pick = torch.randperm(nb, generator=torch.Generator().manual_seed(7))[:QN].cuda()
+    Q = B[pick] + 0.01 * torch.randn((QN, 64), generator=g, device="cuda", dtype=torch.float64)
+    corpus = IndexCorpus(C)
+    res = {M: _check_all(corpus, Q, M, max_dense=2) for M in (20, 100, 1000)}
+    assert np.array_equal(res[20][0][:, 0] // RUN, _np(pick))
+    Ch, Qh = _np(C), _np(Q)
+    rows = [0, 11, 640, 999]
+    for a, (rid, rsc, _, _) in zip(rows, _oracle_many(Qh, Ch, rows, 20)):
+        assert list(res[20][0][a]) == list(rid), a
+        np.testing.assert_allclose(res[20][1][a], rsc, atol=1e-10)

@@ -205,3 +205,34 @@ def test_fused_query_prepare_equals_two_launches(hq_lib, kind):
     for name in ("Z", "S", "Z16", "S32"):
         assert np.array_equal(_np(getattr(a, name)).view(np.uint8), _np(getattr(b, name)).view(np.uint8)), name
     assert (a.f32, a.all32) == (b.f32, b.all32)
+
+
+@pytest.mark.parametrize("L", [32, 64, 128])
+@pytest.mark.parametrize("kind", ["f64", "f32", "mixed"])
+def test_cooperative_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind):
+    """The lane-cooperative long-list re-rank (k_refine_coop: 8 lanes per entry, NumPy's eight pairwise
+    accumulators one per lane, rows staged per group) is bit-identical to the one-thread-per-entry kernel
+    (option refine_coop = 0): progressive M = 100 / 1000 (level-0 ranking + [overall, level..] records),
+    brute force k > 64 (overall ranking), frame scan (strict level-0); float64, float32 and mixed pools."""
+    from hq_mi355x.core.search_engine import IndexCorpus
+    C = _corpus(3000 if L == 128 else 20000, L, 41 + L)
+    rng = np.random.default_rng(42)
+    Q = np.concatenate([C[[1, 2, 20, 40]] + 0.0, C[100:108] + rng.normal(0, 0.01, (8, L)),
+                        rng.standard_normal((2, L))])
+    if kind == "f32":
+        C, Q = C.astype(np.float32), Q.astype(np.float32)
+    corpus = IndexCorpus(C, row_f32=(np.arange(len(C)) % 3 == 0) if kind == "mixed" else None)
+
+    def run():
+        out = [_np(x) for x in corpus.progressive(Q, 150, 0.1, 100)]
+        out += [_np(x) for x in corpus.progressive(Q, 1000, 0.1, 1000)]
+        out += [_np(x) for x in corpus.brute_force(Q, 120)]
+        out += [_np(x) for x in corpus.frame_search(Q, 300, 0.1)]
+        return out
+
+    got = run()
+    hq_option("refine_coop", 0)
+    want = run()
+    hq_option("refine_coop", None)
+    for a, (x, y) in enumerate(zip(got, want)):
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (kind, L, a)

@@ -33,7 +33,10 @@ def timed(f, reps=5):
     return e0.elapsed_time(e1) / reps * 1000.0
 
 
-for M in (100, 1000):
+from hq_mi355x import _lib  # noqa: E402
+
+for M, coop in ((100, 1), (100, 0), (1000, 1), (1000, 0)):
+    _lib.set_option("refine_coop", coop)
     kp = M + corpus.SLACK
     asc, aid, _, _ = K.scan_topk(qp, corpus.prep, 0, kp, 0.1 - corpus.EPS, 1, 0)
     t_scan = timed(lambda: K.scan_topk(qp, corpus.prep, 0, kp, 0.1 - corpus.EPS, 1, 0))
@@ -41,5 +44,5 @@ for M in (100, 1000):
     t_det = timed(lambda: K.refine_rescore_topk(qp, corpus.prep, 0, asc, aid, M, 0.1, 1, corpus.EPS, 0))
     _, ids, _, _ = K.refine_topk(qp, corpus.prep, 0, asc, aid, M, 0.1, 1, corpus.EPS, 0)
     t_res = timed(lambda: K.rescore(qp, corpus.prep, ids, 0))
-    print(f"M={M}: scan+select {t_scan:.1f} us  refine {t_ref:.1f} us  refine+records {t_det:.1f} us  "
+    print(f"M={M} coop={coop}: scan+select {t_scan:.1f} us  refine {t_ref:.1f} us  refine+records {t_det:.1f} us  "
           f"rescore of the output {t_res:.1f} us", flush=True)
