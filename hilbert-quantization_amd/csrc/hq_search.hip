@@ -3519,6 +3519,115 @@ __device__ __forceinline__ void lds_bitonic(int n, First first, Swap swp) {
     }
 }
 
+// Sort-based multi-stage select for long lists (k > 64).  The k-pass forms above (select_row, reg_topk)
+// make k passes over every part: 0.74 s for one 1M-entry row at k = 1000.  Here stage 1 gives one
+// 512-thread workgroup to each (query, part of <= kSortPart entries): the part's entries with their
+// threshold test are sorted by (score desc, id asc) in LDS (bitonic; non-passing entries last) and its
+// first k kept, plus the part's first arg-max over all its entries; each merge stage sorts the k-lists of
+// kSortPart / k consecutive parts the same way, until one list per query remains.  The same total order
+// and threshold test as select_row, so the result is identical.
+constexpr int kSortPart = 4096;
+
+__global__ __launch_bounds__(512) void k_select_sort(const double* __restrict__ in_s, const int64_t* __restrict__ in_id,
+                                                     int Q, int64_t n_in, int64_t part, int P, int k, double thr,
+                                                     int thr_mode, int final_stage, int64_t id_add,
+                                                     double* __restrict__ o_s, int64_t* __restrict__ o_id,
+                                                     double* __restrict__ o_b, int64_t* __restrict__ o_bid,
+                                                     const double* __restrict__ i_b, const int64_t* __restrict__ i_bid,
+                                                     int Pb) {
+  __shared__ double ks[kSortPart];
+  __shared__ int64_t ki[kSortPart];
+  __shared__ double rb[8];
+  __shared__ int64_t rbi[8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool first_stage = in_id == nullptr;
+  // (score, id) arg-max over the workgroup's threads (ids < 0: none)
+  auto block_best = [&](double bs, int64_t bi, double& os, int64_t& oi) {
+    for (int o = 1; o < 64; o <<= 1) {
+      const double s2 = __shfl_xor(bs, o, 64);
+      const int64_t i2 = __shfl_xor(bi, o, 64);
+      if (i2 >= 0 && (bi < 0 || better(s2, i2, bs, bi))) { bs = s2; bi = i2; }
+    }
+    if (lane == 0) { rb[wave] = bs; rbi[wave] = bi; }
+    __syncthreads();
+    bs = rb[0];
+    bi = rbi[0];
+    for (int w = 1; w < 8; ++w)
+      if (rbi[w] >= 0 && (bi < 0 || better(rb[w], rbi[w], bs, bi))) { bs = rb[w]; bi = rbi[w]; }
+    __syncthreads();
+    os = bs;
+    oi = bi;
+  };
+  for (int64_t t = blockIdx.x; t < (int64_t)Q * P; t += gridDim.x) {
+    const int64_t q = t / P, p = t % P;
+    const int64_t c0 = p * part;
+    const int n = (int)(c0 >= n_in ? 0 : (n_in - c0 < part ? n_in - c0 : part));
+    const int n2 = pow2_at_least(n > 2 ? n : 2);
+    double bs = 0.0;
+    int64_t bi = -1;
+    for (int x = tid; x < n2; x += 512) {
+      double s = -__builtin_huge_val();
+      int64_t id = -1;
+      if (x < n) {
+        s = in_s[q * n_in + c0 + x];
+        if (first_stage) {
+          id = c0 + x;
+          if (bi < 0 || better(s, id, bs, bi)) { bs = s; bi = id; }  // first arg-max: every entry
+          if (!(thr_mode == 0 || (thr_mode == 1 ? s >= thr : s > thr))) id = -1;
+        } else {
+          id = in_id[q * n_in + c0 + x];
+        }
+      }
+      ks[x] = s;
+      ki[x] = id;
+    }
+    double pbs;
+    int64_t pbi;
+    block_best(bs, bi, pbs, pbi);  // (its barrier also publishes ks / ki)
+    lds_bitonic(n2,
+                [&](int a, int b) {
+                  const int64_t ia = ki[a], ib = ki[b];
+                  return ia >= 0 && (ib < 0 || better(ks[a], ia, ks[b], ib));
+                },
+                [&](int a, int b) {
+                  const double ts = ks[a];
+                  ks[a] = ks[b];
+                  ks[b] = ts;
+                  const int64_t ti = ki[a];
+                  ki[a] = ki[b];
+                  ki[b] = ti;
+                });
+    for (int r = tid; r < k; r += 512) {
+      const bool v = r < n && ki[r] >= 0;
+      o_s[t * k + r] = v ? ks[r] : -__builtin_huge_val();
+      o_id[t * k + r] = v ? ki[r] + (final_stage ? id_add : 0) : -1;
+    }
+    if (o_b) {
+      if (first_stage) {
+        if (tid == 0) {
+          o_b[t] = pbi >= 0 ? pbs : -__builtin_huge_val();
+          o_bid[t] = pbi >= 0 ? pbi + (final_stage ? id_add : 0) : -1;
+        }
+      } else if (final_stage) {  // the first arg-max of the query's stage-1 parts
+        double cs = 0.0;
+        int64_t ci = -1;
+        for (int x = tid; x < Pb; x += 512) {
+          const int64_t i = i_bid[q * Pb + x];
+          if (i >= 0 && (ci < 0 || better(i_b[q * Pb + x], i, cs, ci))) { cs = i_b[q * Pb + x]; ci = i; }
+        }
+        double fs;
+        int64_t fi;
+        block_best(cs, ci, fs, fi);
+        if (tid == 0) {
+          o_b[q] = fi >= 0 ? fs : -__builtin_huge_val();
+          o_bid[q] = fi >= 0 ? fi + id_add : -1;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // pool entry -> 64-bit key, ascending = (score desc, row asc): scores are >= 0, so their f32 bit
 // patterns order like the values; rows are unique within a pool, so keys are unique
 __device__ __forceinline__ uint64_t pool_key(float s, int row) {
@@ -3753,7 +3862,6 @@ __global__ __launch_bounds__(256) void k_refine_big_raw(HQ_REFINE_ARGS, int tb) 
 // ------------------------------------------------------------------------------------------------
 constexpr int kCoopGroups = 32;              // 8-lane groups per 256-thread workgroup
 constexpr int kCoopMaxW = 7;                 // record width 1 + nseg
-constexpr int kCoopOut = kMaxTopKBig / 256;  // output entries per thread
 
 template <typename T>
 __device__ __forceinline__ T coop_xor(T v, int m) { return __shfl_xor(v, m, 64); }
@@ -6112,8 +6220,18 @@ static bool select_reg_ok(int Q, int64_t N, int k) {
 }
 static int64_t select_reg_parts(int64_t N) { return (N + kRegSel - 1) / kRegSel; }
 
+// the sort-based select (k > 64): stage-1 parts of the row and their ping-pong stage buffers
+static bool select_sort_ok(int64_t N, int k) {
+  return N > 0 && k > kMaxTopK && k <= kSortPart / 4 && !opt_on(OPT_SELECT_2STAGE);
+}
+static int64_t select_sort_parts(int64_t N) { return (N + kSortPart - 1) / kSortPart; }
+
 size_t hq_select_workspace_size(int Q, int64_t N, int k) {
   if (Q <= 0 || N <= 0 || k <= 0) return 0;
+  if (select_sort_ok(N, k)) {  // two k-list stage buffers + the stage-1 arg-maxes
+    const size_t P1 = (size_t)select_sort_parts(N);
+    return 2 * (size_t)Q * P1 * k * 16 + (size_t)Q * P1 * 16 + 512;
+  }
   int P;
   int64_t plen;
   select_parts(Q, N, P, plen);
@@ -6130,6 +6248,43 @@ int hq_select_topk_ws(const double* scores, int Q, int64_t N, int k, double thre
                       double* out_best, int64_t* out_best_id, hq_stream_t stream) {
   if (Q < 0 || N < 0 || k <= 0) return fail(HQ_E_INVALID, "bad shape");
   if (Q == 0) return HQ_OK;
+  if (workspace && out_score && out_id && scores && select_sort_ok(N, k)) {
+    if (workspace_bytes < hq_select_workspace_size(Q, N, k)) return fail(HQ_E_INVALID, "workspace too small");
+    const hipStream_t s = (hipStream_t)stream;
+    const int64_t P1 = select_sort_parts(N);
+    const size_t cap = (size_t)Q * P1 * k;
+    uint8_t* w = reinterpret_cast<uint8_t*>(workspace);
+    double* bs[2] = {reinterpret_cast<double*>(w), reinterpret_cast<double*>(w + cap * 16)};
+    int64_t* bi[2] = {reinterpret_cast<int64_t*>(w + cap * 8), reinterpret_cast<int64_t*>(w + cap * 24)};
+    double* pb = reinterpret_cast<double*>(w + cap * 32);
+    int64_t* pbi = reinterpret_cast<int64_t*>(w + cap * 32 + (size_t)Q * P1 * 8);
+    // stage 1: parts of the row (the arg-maxes per part, or straight to the outputs when one part)
+    const int64_t part1 = (N + P1 - 1) / P1;
+    bool last = P1 == 1;
+    int64_t g = (int64_t)Q * P1 < 65536 ? (int64_t)Q * P1 : 65536;
+    hipLaunchKernelGGL(k_select_sort, dim3((unsigned)g), dim3(512), 0, s, scores, (const int64_t*)nullptr, Q, N, part1,
+                       (int)P1, k, threshold, thr_mode, last ? 1 : 0, id_base, last ? out_score : bs[0],
+                       last ? out_id : bi[0], last ? out_best : pb, last ? out_best_id : pbi, (const double*)nullptr,
+                       (const int64_t*)nullptr, 0);
+    HQ_CHECK_LAUNCH();
+    int64_t P = P1;
+    int cur = 0;
+    const int64_t F = kSortPart / k;  // k-lists merged per part (>= 4)
+    while (P > 1) {
+      const int64_t P2 = (P + F - 1) / F;
+      last = P2 == 1;
+      g = (int64_t)Q * P2 < 65536 ? (int64_t)Q * P2 : 65536;
+      hipLaunchKernelGGL(k_select_sort, dim3((unsigned)g), dim3(512), 0, s, (const double*)bs[cur],
+                         (const int64_t*)bi[cur], Q, P * k, F * k, (int)P2, k, threshold, thr_mode, last ? 1 : 0,
+                         id_base, last ? out_score : bs[cur ^ 1], last ? out_id : bi[cur ^ 1],
+                         last ? out_best : (double*)nullptr, last ? out_best_id : (int64_t*)nullptr,
+                         (const double*)pb, (const int64_t*)pbi, (int)P1);
+      HQ_CHECK_LAUNCH();
+      P = P2;
+      cur ^= 1;
+    }
+    return HQ_OK;
+  }
   int P;
   int64_t plen;
   select_parts(Q, N, P, plen);

@@ -236,3 +236,34 @@ def test_cooperative_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind)
     hq_option("refine_coop", None)
     for a, (x, y) in enumerate(zip(got, want)):
         assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (kind, L, a)
+
+
+@pytest.mark.parametrize("k", [65, 300, 1000])
+def test_sort_select_equals_reference_order(hq_lib, hq_option, k):
+    """The sort-based dense select for long lists (k_select_sort: LDS bitonic parts + merge stages) returns
+    exactly the (score desc, id asc) top-k among entries passing the threshold test, and the first arg-max,
+    for heavy ties, every threshold mode and ragged parts; identical to the k-pass two-stage select (option
+    select_2stage), which it replaces for k > 64 (the dense exact path's select)."""
+    import torch
+    from hq_mi355x import kernels as K
+    rng = np.random.default_rng(50 + k)
+    N = 70001
+    sc = np.round(rng.random((3, N)), 3)  # ~1000 distinct values: long runs of ties
+    sc[1, :] = 0.1                         # one row of equal scores (a zero-variance query)
+    sc[2, 5000:5100] = 0.9995
+    dsc = torch.from_numpy(sc).cuda()
+    for thr, mode in ((0.0, 0), (0.5, 1), (0.1, 2), (0.999, 1)):
+        got = [_np(x) for x in K.select_topk(dsc, k, thr, mode, 7)]
+        hq_option("select_2stage", 1)
+        want = [_np(x) for x in K.select_topk(dsc, k, thr, mode, 7)]
+        hq_option("select_2stage", None)
+        for a, b in zip(got, want):
+            assert np.array_equal(a, b), (k, thr, mode)
+        for r in range(3):
+            ok = np.ones(N, bool) if mode == 0 else (sc[r] >= thr if mode == 1 else sc[r] > thr)
+            idx = np.nonzero(ok)[0]
+            order = idx[np.lexsort((idx, -sc[r][idx]))][:k]
+            n = len(order)
+            assert list(got[1][r][:n]) == list(order + 7) and np.all(got[1][r][n:] == -1), (k, thr, mode, r)
+            assert np.array_equal(got[0][r][:n], sc[r][order])
+            assert got[3][r] == int(np.argmax(sc[r])) + 7 and got[2][r] == sc[r].max()
