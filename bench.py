@@ -590,8 +590,10 @@ def progressive_rate(engine, Q, M, steps, world, k=10, threshold=0.1):
         while pend:
             engine.progressive_finish(pend.pop(0))
 
-    run()  # warm-up batch (first-call allocations of the retry path's longer lists), then counters from zero
+    engine.reset_stats()
+    run()  # warm-up batch (first-call allocations, the adaptive list length), then counters from zero
     drain()
+    first = dict(engine.stats)
     engine.reset_stats()
     wall, kern = timed(run, steps, 0, world, drain)
     st = dict(engine.stats)
@@ -601,7 +603,10 @@ def progressive_rate(engine, Q, M, steps, world, k=10, threshold=0.1):
             "max_candidates_per_level": M, "batches": st["batches"], "redo_batches": st["redo_batches"],
             "redo_queries": st["redo_queries"], "redo_queries_per_batch": st["redo_queries"] / nb,
             "retry_queries_per_batch": st["retry_queries"] / nb, "dense_queries_per_batch": st["dense_queries"] / nb,
-            "redo_ms_per_batch": st["dense_s"] / nb * 1e3}
+            "redo_ms_per_batch": st["dense_s"] / nb * 1e3,
+            "warmup_batch": {"redo_queries": first["redo_queries"], "retry_queries": first["retry_queries"],
+                             "dense_queries": first["dense_queries"], "redo_ms": first["dense_s"] * 1e3},
+            "first_pass_list": M + engine.slack_for(M)}
 
 
 def dense_one_query_ms(engine, Q, M, reps=3):

@@ -304,8 +304,9 @@ class IndexCorpus:
         lie within EPS of the k-th (runs of near-duplicates in the corpus), or short when the sampled
         starting threshold overshot.  None when no longer list is available.  Returns refine_topk's
         (scores, ids, count, resolved) (+ det, the [overall, levels] records, with det)."""
-        kp2 = min(self._max_list(mode), self.RETRY_FACTOR * (k + self.SLACK))
-        if kp2 <= k + self.SLACK or not self._fused_ok(mode) or self.dense_only:
+        cur = k + (self.slack_for(k) if mode == 0 else self.SLACK)  # the first pass's list length
+        kp2 = min(self._max_list(mode), self.RETRY_FACTOR * cur)
+        if kp2 <= cur or not self._fused_ok(mode) or self.dense_only:
             return None
         self.stats["retry_queries"] += qp.N
         lo_mode = 0 if thr_mode == 0 else 1
@@ -342,6 +343,13 @@ class IndexCorpus:
                 rr = r[ok]
                 s0[rr], ids[rr], det[rr] = s2[ok], i2[ok], d2[ok]
                 need[rr] = False
+            if r.numel() >= max(8, qp.N // 10) and self.slack_for(M) == self.SLACK:
+                # a tenth of the batch or more ended in near-ties (runs of near-duplicates in the corpus): later
+                # batches at this M take the retry's list length on the first pass (one scan instead of a
+                # scan plus a retry per batch; results are exact either way)
+                kp2 = min(self._max_list(0), self.RETRY_FACTOR * (M + self.SLACK))
+                if kp2 > M + self.SLACK:
+                    self.__dict__.setdefault("_slack", {})[int(M)] = kp2 - M
         d = t.nonzero(need).view(-1)
         if d.numel():
             self.stats["dense_queries"] += int(d.numel())
@@ -390,7 +398,8 @@ class IndexCorpus:
             oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
             return PendingSearch(done=(oid, odet[..., 0], odet[..., 1:], ocnt))
         nredo, nnext = self._redo_counter(qp.Z.device)
-        s0, ids, cnt, res, det = self._scan_refine(qp, 0, M, float(threshold), 1, nredo, det=True, next_redo=nnext)
+        s0, ids, cnt, res, det = self._scan_refine(qp, 0, M, float(threshold), 1, nredo, det=True, next_redo=nnext,
+                                                   slack=self.slack_for(M))
         # no arg-max on this path: a query where nothing passed (count 0) is recomputed by the dense path
         # in progressive_finish, so the fallback slot is a constant (-inf, id -1, zero re-scores)
         best, bid, bdet = self._no_fallback(Q, qp.Z.device)
@@ -485,13 +494,19 @@ class IndexCorpus:
                           t.zeros((Q, 1 + self.nseg), dtype=t.float64, device=dev))
         return cache[key]
 
+    def slack_for(self, M: int) -> int:
+        """Extra list entries of the first pass at list length M: SLACK, or the longer list a corpus with
+        runs of near-duplicates showed it needs (_level0_redo: most lists of a batch ended in near-ties)."""
+        return self.__dict__.get("_slack", {}).get(int(M), self.SLACK)
+
     def _scan_refine(self, qp, mode: int, k: int, thr: float, thr_mode: int, nredo=None, det: bool = False,
-                     next_redo=None):
-        """Fused scan (SLACK extra list entries) + exact re-rank; resolved[q] == 0 marks an unproven list.
-        nredo: device counter of queries needing the dense path (unresolved or nothing passed).  det: also
-        the exact [overall, levels] re-score of the output (hq_refine_rescore_topk, rows staged once)."""
+                     next_redo=None, slack=None):
+        """Fused scan (slack, default SLACK, extra list entries) + exact re-rank; resolved[q] == 0 marks an
+        unproven list.  nredo: device counter of queries needing the dense path (unresolved or nothing
+        passed).  det: also the exact [overall, levels] re-score of the output (rows staged once)."""
         lo_mode = 0 if thr_mode == 0 else 1
-        asc, aid, _, _ = K.scan_topk(qp, self.prep, mode, k + self.SLACK, thr - self.EPS, lo_mode, self.id_base)
+        kp = k + (self.SLACK if slack is None else int(slack))
+        asc, aid, _, _ = K.scan_topk(qp, self.prep, mode, kp, thr - self.EPS, lo_mode, self.id_base)
         tm = thr_mode | (K.THR_KEY32 if self.key32(qp) else 0)
         if det:
             return K.refine_rescore_topk(qp, self.prep, mode, asc, aid, k, thr, tm, self.EPS, self.id_base, redo=nredo,

@@ -76,7 +76,7 @@ class ShardedIndexCorpus:
         t = torch()
         c = self.local
         Q = qp.N
-        s0, ids, cnt, res, det0 = c._scan_refine(qp, 0, M, float(threshold), 1, det=True)
+        s0, ids, cnt, res, det0 = c._scan_refine(qp, 0, M, float(threshold), 1, det=True, slack=c.slack_for(M))
         # no arg-max on the scan path (count-0 rows are redone below): constant fallback slot
         best, bid, bdet0 = c._no_fallback(Q, qp.Z.device)
         rec = self._records(qp, s0, ids, best, bid, det0, bdet0.view(Q, 1, -1))
