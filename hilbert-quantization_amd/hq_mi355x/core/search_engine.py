@@ -306,7 +306,9 @@ class IndexCorpus:
         (scores, ids, count, resolved) (+ det, the [overall, levels] records, with det)."""
         cur = k + (self.slack_for(k) if mode == 0 else self.SLACK)  # the first pass's list length
         kp2 = min(self._max_list(mode), self.RETRY_FACTOR * cur)
-        if kp2 <= cur or not self._fused_ok(mode) or self.dense_only:
+        # (the f64 scans — option scan_v1, odd L — keep the dense path: their lists stop at 64 and their
+        # LDS tiles grow with the list)
+        if kp2 <= cur or self._max_list(mode) <= MAX_FUSED_K or not self._fused_ok(mode) or self.dense_only:
             return None
         self.stats["retry_queries"] += qp.N
         lo_mode = 0 if thr_mode == 0 else 1
