@@ -249,6 +249,8 @@ static void pre_bank_order(std::vector<int>& ks, const PreLevel& L, int ld) {
 // behind the upload is kept, and every call makes its stream wait on it (a no-op once it completed), so a
 // launch on another stream never reads the list before it arrived.  The host copy stays with the cache
 // entry (the asynchronous copy may read it after the call returns).
+__host__ __device__ inline int pre_map_off(int znz) { return (znz + 7) & ~7; }
+
 struct PreZeroList {
   uint16_t* dptr = nullptr;
   hipEvent_t ready = nullptr;
@@ -278,6 +280,12 @@ static const uint16_t* pre_zero_lists(int n, int d, int ld, int esz, int max_lev
     for (int k : lists[l]) e->host.push_back((uint16_t)k);
   }
   if ((int)e->host.size() != p.znz) { delete e; err = HQ_E_UNSUPPORTED; return nullptr; }
+  // then, 16-byte aligned at pre_map_off(znz), the inverse map of the compact averages (k_precomp_ws<.., CMP>):
+  // output slot o -> 1 + its list position (the average's LDS slot), 0 for a square of zero padding
+  e->host.resize((size_t)pre_map_off(p.znz) + p.total, 0);
+  for (int l = 0; l < p.nlev; ++l)
+    for (size_t i = 0; i < lists[l].size(); ++i)
+      e->host[pre_map_off(p.znz) + p.lv[l].off + lists[l][i]] = (uint16_t)(p.lv[l].zoff + i + 1);
   const size_t bytes = e->host.size() * sizeof(uint16_t);
   if (hipMalloc(&e->dptr, bytes + 16) != hipSuccess) { delete e; err = HQ_E_HIP; return nullptr; }
   if (hipMemcpyAsync(e->dptr, e->host.data(), bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -413,7 +421,7 @@ __device__ __forceinline__ T sq_sum(const T* b, int ld) {
 }
 
 // all squares of one level with S x S <= 128 values (S = 1, 2, 4, 8): one NumPy pairwise leaf per thread
-template <typename T, int S, bool SK>
+template <typename T, int S, bool SK, bool CMP = false>
 __device__ __forceinline__ void pre_small(const PreLevel& L, const T* img, int ld, float* res, int tid,
                                           const uint16_t* zl) {
   const int cnt = SK ? L.zcnt : L.count;
@@ -436,7 +444,7 @@ __device__ __forceinline__ void pre_small(const PreLevel& L, const T* img, int l
     else if constexpr (S == 4) sum = sq_sum<T, 4>(b, ld);
     else if constexpr (S == 2) sum = T(0) + ((((T(-0.0) + b[0]) + b[1]) + b[ld]) + b[ld + 1]);  // NumPy n < 8 branch
     else sum = T(0) + (T(-0.0) + b[0]);  // one value
-    res[L.off + k] = pre_mean<T>(sum, 2 * L.lsh);
+    res[CMP ? L.zoff + i : L.off + k] = pre_mean<T>(sum, 2 * L.lsh);  // CMP: compact slot = list position
   }
 }
 
@@ -458,7 +466,7 @@ __device__ __forceinline__ void pre_zero_setup(T* img, float* res, uint16_t* zl,
 // When the leaf tasks fit three waves they start at wave 1: the small-square levels fill waves from wave 0
 // (the 8 x 8 squares, fewest, on wave 0 alone), so the waves' LDS work up to the image's barrier evens out.
 __device__ __forceinline__ void pre_leaf_task(const PreLevel* lv, const PrePlan& plan, const uint16_t* zl, int ld,
-                                              int tid, int& lt_b, int& lt_m) {
+                                              int tid, int& lt_b, int& lt_m, bool cmp = false) {
   const int rot = 2 * plan.znleaves <= kPreThreads - 64 && plan.leaf_rot ? 64 : 0;
   const int t = (tid - rot) >> 1;
   lt_b = 0;
@@ -473,12 +481,12 @@ __device__ __forceinline__ void pre_leaf_task(const PreLevel* lv, const PrePlan&
   int x0, y0;
   pre_square(lv[l], k, x0, y0);
   lt_b = y0 * ld + x0 + 4 * (tid & 1);
-  lt_m = (lv[l].off + k) | (lv[l].lsh << 12) | (leaf << 16) | (1 << 24);
+  lt_m = (cmp ? lv[l].zoff + slot : lv[l].off + k) | (lv[l].lsh << 12) | (leaf << 16) | (1 << 24);
 }
 
 // squares of <= 128 values: one thread each, level by level (uniform geometry per loop); 4x4 and 8x8
 // squares read whole row segments (their x0 is a multiple of s/2) and sum in registers
-template <typename T, bool SK>
+template <typename T, bool SK, bool CMP = false>
 __device__ __forceinline__ void pre_small_levels(const PreLevel* lv, int nlev, const T* img, int ld, float* res,
                                                  int tid, const uint16_t* zl) {
   for (int l = 0; l < nlev; ++l) {
@@ -495,10 +503,10 @@ __device__ __forceinline__ void pre_small_levels(const PreLevel* lv, int nlev, c
     // one straight-line loop per square size (the size is uniform per level)
     L.zcnt = __builtin_amdgcn_readfirstlane(lv[l].zcnt);
     L.zoff = __builtin_amdgcn_readfirstlane(lv[l].zoff);
-    if (L.s == 2) pre_small<T, 2, SK>(L, img, ld, res, tid, zl);
-    else if (L.s == 4) pre_small<T, 4, SK>(L, img, ld, res, tid, zl);
-    else if (L.s == 8) pre_small<T, 8, SK>(L, img, ld, res, tid, zl);
-    else pre_small<T, 1, SK>(L, img, ld, res, tid, zl);
+    if (L.s == 2) pre_small<T, 2, SK, CMP>(L, img, ld, res, tid, zl);
+    else if (L.s == 4) pre_small<T, 4, SK, CMP>(L, img, ld, res, tid, zl);
+    else if (L.s == 8) pre_small<T, 8, SK, CMP>(L, img, ld, res, tid, zl);
+    else pre_small<T, 1, SK, CMP>(L, img, ld, res, tid, zl);
   }
 }
 
@@ -570,6 +578,57 @@ __device__ __forceinline__ void pre_store(const float* res, int total, float* o,
     else *reinterpret_cast<f4v*>(o + a) = v;
   }
   for (int a = head + 4 * nv + t0; a < total; a += nthr) o[a] = res[a];
+}
+
+// pre_store for compact averages (k_precomp_ws<.., CMP>): output slot a holds res[map[a] - 1], or +0.0 where
+// map[a] == 0 (a square of zero padding: np.mean of zeros).  The storer waves issue no global loads in the
+// image loop (on gfx9 a load's wait would also wait for the wave's older stores), so the map entries of a
+// lane's slots live in registers: PreMapRegs::load reads them for one row alignment (the float4 groups start
+// at the row's first 16-byte boundary) and is re-run only when a row's alignment differs from the last one.
+constexpr int kPreStoreG = 6;  // float4 groups per storer lane (128 lanes): total <= 3072 averages
+struct PreMapRegs {
+  uint32_t m[kPreStoreG][2];
+  uint32_t ht;  // head slot (lane < head) in the low half, tail slot (lane < tail count) in the high half
+  int mis;
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ map, int total, int mis_, int t0, int nthr) {
+    mis = mis_;
+    const int head = min((4 - mis) & 3, total);
+    const int nv = (total - head) >> 2;
+#pragma unroll
+    for (int j = 0; j < kPreStoreG; ++j) {
+      const int i = t0 + nthr * j;
+      const int a = head + 4 * i;
+      m[j][0] = m[j][1] = 0u;
+      if (i < nv) {
+        m[j][0] = (uint32_t)map[a] | ((uint32_t)map[a + 1] << 16);
+        m[j][1] = (uint32_t)map[a + 2] | ((uint32_t)map[a + 3] << 16);
+      }
+    }
+    const int ta = head + 4 * nv + t0;
+    ht = (t0 < head ? (uint32_t)map[t0] : 0u) | ((ta < total ? (uint32_t)map[ta] : 0u) << 16);
+  }
+};
+
+__device__ __forceinline__ void pre_store_map(const float* res, const PreMapRegs& mr, int total, float* o, bool nt,
+                                              int t0, int nthr) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  auto val = [&](uint32_t m) -> float { return m ? res[m - 1] : 0.0f; };
+  const int head = min((4 - mr.mis) & 3, total);
+  const int nv = (total - head) >> 2;
+  if (t0 < head) o[t0] = val(mr.ht & 0xFFFFu);
+#pragma unroll
+  for (int j = 0; j < kPreStoreG; ++j) {
+    const int i = t0 + nthr * j;
+    if (i < nv) {
+      const int a = head + 4 * i;
+      const f4v v = f4v{val(mr.m[j][0] & 0xFFFFu), val(mr.m[j][0] >> 16), val(mr.m[j][1] & 0xFFFFu),
+                        val(mr.m[j][1] >> 16)};
+      if (nt) __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(o + a));
+      else *reinterpret_cast<f4v*>(o + a) = v;
+    }
+  }
+  const int ta = head + 4 * nv + t0;
+  if (ta < total) o[ta] = val(mr.ht >> 16);
 }
 
 // phase-skipping diagnostics (wrong averages): `make DIAG=1` builds only
@@ -781,40 +840,54 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))
 // no branch: a fixed number of loads per image, so waiting for image e leaves image e + grid in
 // flight), a partial last group (d % 4) by four clamped dword loads.  Two barriers per image.  The LDS
 // footprint (~30 KiB at n = 64, d = 1536) allows 5 workgroups per CU = 5 waves per SIMD: 96 VGPRs.
-template <int KL, int PD, int LW = 2>
-__global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(5))) void k_precomp_ws(
+template <int KL, int PD, int LW = 2, bool CMP = false>
+__global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(CMP ? 6 : 5))) void k_precomp_ws(
     const float* __restrict__ in, int64_t N, int64_t stride, int d, int n, PrePlan plan, float* __restrict__ out,
     int64_t out_stride, int ld, const uint16_t* __restrict__ glist) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ PreLevel lv[kPreMaxLevels];
   float* img = reinterpret_cast<float*>(smem);
   float* res = img + ((ld * n + 3) & ~3);  // no LDS tree on skip runs
-  uint16_t* zl = reinterpret_cast<uint16_t*>(res + ((plan.total + 3) & ~3));
+  const int nres = CMP ? plan.znz : plan.total;  // CMP: the listed squares' averages only, by list position
+  uint16_t* zl = reinterpret_cast<uint16_t*>(res + ((nres + 3) & ~3));
+  const uint16_t* gmap = glist + pre_map_off(plan.znz);
   const int tid = threadIdx.x;
   constexpr int NL = 64 * LW;  // loader lanes (waves 0 .. LW - 1); the other waves store
   const int lt = tid < NL ? tid : tid - NL;
   const int lsh_n = plan.lsh_n;
   if (tid < plan.nlev) lv[tid] = plan.lv[tid];
   auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-  pre_zero_setup<float>(img, res, zl, glist, plan.znz, plan.total, n, ld, tid);
+  pre_zero_setup<float>(img, res, zl, glist, plan.znz, nres, n, ld, tid);
   int lt_b = 0, lt_m = 0;
-  pre_leaf_task(lv, plan, zl, ld, tid, lt_b, lt_m);
+  pre_leaf_task(lv, plan, zl, ld, tid, lt_b, lt_m, CMP);
   const int64_t e0 = blockIdx.x, g = gridDim.x;
   if (e0 >= N) return;  // uniform over the workgroup
   auto reduce = [&] {
-    if (!PRE_DIAG(1)) pre_small_levels<float, true>(lv, plan.nlev, img, ld, res, tid, zl);
+    if (!PRE_DIAG(1)) pre_small_levels<float, true, CMP>(lv, plan.nlev, img, ld, res, tid, zl);
     if (!PRE_DIAG(2)) pre_leaves_sk<float>(img, ld, res, tid, lt_b, lt_m, plan.maxper);
   };
   if (tid >= NL) {  // storer waves: no loads, so their stores are never waited on inside the loop
     int64_t prev = -1;
+    PreMapRegs mr;
+    mr.mis = -1;
+    auto store = [&](int64_t e) {
+      float* o = out + e * out_stride;
+      if constexpr (CMP) {
+        const int mis = (int)((reinterpret_cast<uintptr_t>(o) >> 2) & 3);
+        if (mis != mr.mis) mr.load(gmap, plan.total, mis, lt, kPreThreads - NL);  // rows of another alignment
+        pre_store_map(res, mr, plan.total, o, plan.nt, lt, kPreThreads - NL);
+      } else {
+        pre_store(res, plan.total, o, plan.nt, lt, kPreThreads - NL);
+      }
+    };
     for (int64_t e = e0; e < N; e += g) {
-      if (prev >= 0 && !PRE_DIAG(8)) pre_store(res, plan.total, out + prev * out_stride, plan.nt, lt, kPreThreads - NL);
+      if (prev >= 0 && !PRE_DIAG(8)) store(prev);
       lds_barrier();
       reduce();
       lds_barrier();
       prev = e;
     }
-    if (!PRE_DIAG(8)) pre_store(res, plan.total, out + prev * out_stride, plan.nt, lt, kPreThreads - NL);
+    if (!PRE_DIAG(8)) store(prev);
     return;
   }
   // loader waves
@@ -1132,6 +1205,13 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
                            (hipStream_t)stream, err);
     if (!glist) return fail(err, "pre-computed index: zero-padding lists (n=%d d=%d)", n, d);
   }
+  // option precomp_compact = 1: the wave-specialised skip runs keep only the listed squares' averages in LDS
+  // (30.2 -> 23.5 KB at n = 64, d = 1536: six workgroups per CU instead of five).  A/B on one box (ms per
+  // 1M x 1536): 4.114 / 4.117 vs 4.085 / 4.088 without — more resident images do not help (the mixed
+  // read/write HBM stream bounds the kernel), so it is off by default
+  const bool cmp = skip && !p.g2reg && p.total <= 128 * 4 * kPreStoreG && opt(OPT_PRECOMP_COMPACT, 0) != 0;
+  const size_t lds_ws = (size_t)esz * ((size_t)((ld * n + 3) & ~3)) + 4 * (size_t)(((cmp ? p.znz : p.total) + 3) & ~3) +
+                        (skip ? 2 * (size_t)p.znz : 0);
   const size_t lds = (size_t)esz * ((size_t)((ld * n + 3) & ~3) + (p.tree_lds ? p.nleaves_al : 0)) + 4 * (size_t)((p.total + 3) & ~3) +
                      (skip ? 2 * (size_t)p.znz : 0);
   if (lds > 160 * 1024) return fail(HQ_E_UNSUPPORTED, "pre-computed index n=%d dtype %d needs %zu B of LDS", n, dtype, lds);
@@ -1149,6 +1229,8 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
       const int kl = ngroups <= 128 * 2 ? 2 : (ngroups <= 128 * 3 ? 3 : 4);
       auto wk = ws == 1 ? (kl == 2 ? k_precomp_ws<2, 1> : (kl == 3 ? k_precomp_ws<3, 1> : k_precomp_ws<4, 1>))
                         : (kl == 2 ? k_precomp_ws<2, 2> : (kl == 3 ? k_precomp_ws<3, 2> : k_precomp_ws<4, 2>));
+      if (cmp && ws == 1)
+        wk = kl == 2 ? k_precomp_ws<2, 1, 2, true> : (kl == 3 ? k_precomp_ws<3, 1, 2, true> : k_precomp_ws<4, 1, 2, true>);
       // ws = 3: three loader waves and one storer (groups per loader lane ceil(ngroups / 192))
       if (ws == 3) {
         const int k3 = ngroups <= 192 * 2 ? 2 : 3;
@@ -1160,8 +1242,9 @@ int hq_precomputed_index(int dtype, int kind, const void* in, int64_t N, int64_t
       const int64_t wcap = opt(OPT_PRECOMP_GRID, 20480);
       const int64_t wgrid = N < wcap ? N : (wcap > 0 ? wcap : 1);
       p.nt = opt(OPT_PRECOMP_NT, 0) != 0;
-      HQ_CHECK_HIP(hipFuncSetAttribute((const void*)wk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(wk, dim3((unsigned)wgrid), dim3(kPreThreads), lds, s, (const float*)in, N, in_stride, d, n,
+      const size_t lw = cmp && ws == 1 ? lds_ws : lds;
+      HQ_CHECK_HIP(hipFuncSetAttribute((const void*)wk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lw));
+      hipLaunchKernelGGL(wk, dim3((unsigned)wgrid), dim3(kPreThreads), lw, s, (const float*)in, N, in_stride, d, n,
                          p, out, out_stride, ld, glist);
       HQ_CHECK_LAUNCH();
       return HQ_OK;

@@ -159,7 +159,7 @@ def test_quantizer_builds_precomputed_index(hq_lib):
     assert qm.metadata.model_name == "pm"
 
 
-@pytest.mark.parametrize("ws", [None, 0, 3, "order0", "g2reg"])
+@pytest.mark.parametrize("ws", [None, 0, 3, "order0", "g2reg", "compact"])
 @pytest.mark.parametrize("grid", [None, "3"])
 @pytest.mark.parametrize("n,dtype,levels", [(16, np.float32, (6, 2)), (32, np.float32, (6, 2)),
                                              (64, np.float32, (6, 2)), (64, np.float64, (6, 2)),
@@ -171,7 +171,9 @@ def test_precomputed_stream_zero_padding_skip(hq_lib, hq_option, ws, grid, n, dt
     averages are reused from the once-per-workgroup setup.  f32 skip runs take the wave-specialised
     k_precomp_ws (loader / storer waves; 2, 3 or 4 groups per loader lane by d) unless precomp_ws = 0;
     the host-built square lists are in LDS bank order unless precomp_order = 0; its 2 x 2 grid squares are
-    averaged from the LDS image unless precomp_g2reg = 1 (the loader's registers)."""
+    averaged from the LDS image unless precomp_g2reg = 1 (the loader's registers); only the listed squares'
+    averages are kept in LDS (compact, mapped back to the output row by the storer waves) with
+    precomp_compact = 1."""
     from hq_mi355x import kernels as K
     if grid is not None:
         hq_option("precomp_grid", int(grid))
@@ -179,6 +181,8 @@ def test_precomputed_stream_zero_padding_skip(hq_lib, hq_option, ws, grid, n, dt
         hq_option("precomp_order", 0)
     elif ws == "g2reg":
         hq_option("precomp_g2reg", 1)
+    elif ws == "compact":
+        hq_option("precomp_compact", 1)
     elif ws is not None:
         hq_option("precomp_ws", ws)
     rng = np.random.default_rng(n * 7 + len(levels))
