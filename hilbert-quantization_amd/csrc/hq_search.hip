@@ -5781,7 +5781,10 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
   if (opt_on(OPT_SCANOV_SPLIT3)) {
     if (oocc == 3) hipLaunchKernelGGL((k_scanov<LID, 3, false>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
     else hipLaunchKernelGGL((k_scanov<LID, 2, false>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
-  } else if (opt_on(OPT_SCANOV_V1)) {  // the med3 + fma bound
+  } else if (opt_on(OPT_SCANOV_V1) || k > kMaxTopK) {
+    // the med3 + fma bound with pool appends straight to global memory: long lists (k > 64) pass more pairs
+    // per wave than the LIN form's 256-entry LDS append buffer holds (its overflow sends queries to the
+    // dense path)
     hipLaunchKernelGGL((k_scanov<LID, 4, true, false>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else if (opt(OPT_OV_PF, 1) == 2) {  // prefetch distance (steps)
     if (oocc == 3) hipLaunchKernelGGL((k_scanov<LID, 3, true, true, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);

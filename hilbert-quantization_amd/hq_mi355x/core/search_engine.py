@@ -288,6 +288,7 @@ class IndexCorpus:
                     keep[t.nonzero(try_).view(-1)[ok]] = False
                     sel = sel[keep]
         if sel.numel():
+            self.stats["dense_queries"] += int(sel.numel())
             s2, i2, b2, bi2 = self._dense(qp, sel, mode, k, thr, thr_mode)
             sc[sel] = s2
             ids[sel] = i2

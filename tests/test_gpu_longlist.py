@@ -110,8 +110,11 @@ def test_long_list_brute_force_and_frame_scan(hq_lib):
     rng = np.random.default_rng(27)
     Q = np.concatenate([C[[20, 40]] + 0.0, C[900:903] + rng.normal(0, 0.01, (3, 64))])
     corpus = IndexCorpus(C)
+    corpus.reset_stats()
     bids, bov, blv = [_np(x) for x in corpus.brute_force(Q, 120)]
     fids, fsc = [_np(x) for x in corpus.frame_search(Q, 300, 0.1)]
+    # long lists stay on the scan path (the overall scan's appends go straight to the pools for k > 64)
+    assert corpus.stats["dense_queries"] == 0, corpus.stats
     for a in range(len(Q)):
         rid, rsc, rlv = O.brute_force_search(Q[a], C, 120)
         assert list(bids[a]) == list(rid), a
@@ -163,16 +166,21 @@ def test_pool_sort_equals_short_select_order(hq_lib, hq_option, k):
             assert list(ids[a]) == list(dids[a]), a
 
 
+@pytest.mark.parametrize("L", [64, 256])
 @pytest.mark.parametrize("f32", [False, True])
-def test_dense_level_scores_lds_equal_per_pair_kernel(hq_lib, hq_option, f32):
+def test_dense_level_scores_lds_equal_per_pair_kernel(hq_lib, hq_option, f32, L):
     """The coalesced dense scorer (k_level_scores_lds: candidate segments staged in LDS) is bit-identical
     to the one-thread-per-pair kernel (option level_scores_v1) at every level, ragged N and Q, float64
-    and float32 index vectors (incl. zero-variance rows); and equal to the reference goldens' values via
+    and float32 index vectors (incl. zero-variance rows), L = 64 and 256 (a 128-value level-0 segment: 132 KB
+    of staged rows, above the 64 KB default LDS allocation); and equal to the reference goldens' values via
     the oracle on a sample."""
     from hq_mi355x.core.search_engine import IndexCorpus
-    C = _corpus(3001, 64, 31)
+    C = _corpus(3001, 64, 31) if L == 64 else np.random.default_rng(31).standard_normal((1501, L))
+    if L != 64:
+        C[1] = 0.0
+        C[2] = 0.1
     rng = np.random.default_rng(32)
-    Q = np.concatenate([C[[1, 2, 20]] + 0.0, C[100:106] + rng.normal(0, 0.01, (6, 64))])
+    Q = np.concatenate([C[[1, 2, 20]] + 0.0, C[100:106] + rng.normal(0, 0.01, (6, L))])
     if f32:
         C, Q = C.astype(np.float32), Q.astype(np.float32)
     corpus = IndexCorpus(C)
