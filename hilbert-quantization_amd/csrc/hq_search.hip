@@ -4747,6 +4747,66 @@ __global__ __launch_bounds__(64) void k_seg_prepare_pack0(const double* __restri
   }
 }
 
+// Query batches, lane-cooperative (every level segment <= 128 values, at most 8 segments): one wave per row,
+// each level segment's NumPy statistics summed by an 8-lane group (coop_sum: lane j owns the pairwise
+// accumulator r_j) and its normalised values written by the group's lanes (m / 8 divisions each), then the
+// split level-0 copy as k_seg_prepare_pack0.  The serial form has one lane walk each segment three times and
+// divide every value.  Same operations as seg_prepare_one, so bit-identical.
+__device__ __forceinline__ void seg_prepare_coop(const double* xrow, int64_t row, int s, const SegInfo& si,
+                                                 int all_f32, const uint8_t* __restrict__ row_f32,
+                                                 double* __restrict__ Z, double* __restrict__ stats, int j) {
+  const double* x = xrow + si.src[s];
+  const int m = si.len[s], plen = si.plen[s];
+  const double mean = coop_sum<double>([=](int k) -> double { return x[k]; }, m, j) / (double)m;            // np.mean
+  const double sd = sqrt(coop_sum<double>([=](int k) -> double { const double d = x[k] - mean; return d * d; }, m, j) /
+                         (double)m);                                                                        // np.std
+  const double msq = coop_sum<double>([=](int k) -> double { return x[k] * x[k]; }, m, j) / (double)m;      // mean(q**2)
+  double* z = Z + row * si.Lp + si.poff[s];
+  double* st = stats + (row * si.nseg + s) * 4;
+  if (row_f32 ? row_f32[row] != 0 : all_f32 != 0) {
+    const float mean32 = coop_sum<float>([=](int k) -> float { return (float)x[k]; }, m, j) / (float)m;
+    const float sd32 = sqrtf(coop_sum<float>([=](int k) -> float { const float d = (float)x[k] - mean32; return d * d; },
+                                             m, j) / (float)m);
+    int aux = kAuxF32;
+    if (!(msq >= 0x1p-100 && msq <= 0x1p100)) aux |= kAuxUnsafe;
+    for (int i = j; i < plen; i += 8) z[i] = (sd32 == 0.0f || i >= m) ? 0.0 : (double)(((float)x[i] - mean32) / sd32);
+    if (j == 0) {
+      st[0] = sd32 == 0.0f ? (double)mean32 : mean;
+      st[1] = (double)sd32;
+      st[2] = msq;
+      st[3] = (double)aux;
+    }
+    return;
+  }
+  for (int i = j; i < plen; i += 8) z[i] = (sd == 0.0 || i >= m) ? 0.0 : (x[i] - mean) / sd;
+  if (j == 0) {
+    st[0] = mean;
+    st[1] = sd;
+    st[2] = msq;
+    st[3] = 0.0;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_seg_prepare_pack0_coop(const double* __restrict__ idx, int64_t N, SegInfo si,
+                                                               int all_f32, const uint8_t* __restrict__ row_f32,
+                                                               double* __restrict__ Z, double* __restrict__ stats,
+                                                               _Float16* __restrict__ Z16, float* __restrict__ S32) {
+  extern __shared__ double xs[];  // L values
+  const int lane = threadIdx.x, gi = lane >> 3, j = lane & 7;
+  const int64_t rows = z16_rows(N);
+  for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    if (row < N) {
+      for (int i = lane; i < si.L; i += 64) xs[i] = idx[row * si.L + i];
+      __syncthreads();
+      for (int sg = gi; sg < si.nseg; sg += 8) seg_prepare_coop(xs, row, sg, si, all_f32, row_f32, Z, stats, j);
+      __threadfence_block();
+      __syncthreads();
+    }
+    if (lane < 32) pack0_elem(Z, stats, N, si.Lp, si.plen[0], si.nseg, Z16, S32, row, lane);
+    __syncthreads();
+  }
+}
+
 template <int KSMAX, bool OVERALL>
 static int launch_scan(const ScanArgs& a, hipStream_t s) {
   const size_t lds = scan_lds_bytes(a.rs, a.nseg_used, a.K);
@@ -6084,6 +6144,14 @@ int hq_seg_prepare_pack0(const double* idx, int64_t N, int L, int src_f32, const
   if (si.plen[0] > 32) return fail(HQ_E_UNSUPPORTED, "level-0 segment of %d values (<= 32)", si.plen[0]);
   if (si.L > 4096) return fail(HQ_E_UNSUPPORTED, "L=%d (<= 4096)", L);
   const int64_t rows = z16_rows(N);
+  // default: the lane-cooperative form where its shapes hold (option prep_coop = 0: the serial form)
+  if (seg_small(si) && si.nseg <= 8 && opt(OPT_PREP_COOP, 1) != 0) {
+    hipLaunchKernelGGL(k_seg_prepare_pack0_coop, dim3((unsigned)(rows < 65536 ? rows : 65536)), dim3(64),
+                       (size_t)8 * si.L, (hipStream_t)stream, idx, N, si, src_f32 ? 1 : 0, row_f32, Z, stats,
+                       reinterpret_cast<_Float16*>(Z16), S32);
+    HQ_CHECK_LAUNCH();
+    return HQ_OK;
+  }
   hipLaunchKernelGGL(k_seg_prepare_pack0, dim3((unsigned)(rows < 65536 ? rows : 65536)), dim3(64), (size_t)8 * si.L,
                      (hipStream_t)stream, idx, N, si, src_f32 ? 1 : 0, row_f32, Z, stats,
                      reinterpret_cast<_Float16*>(Z16), S32);

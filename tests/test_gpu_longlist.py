@@ -194,8 +194,9 @@ def test_dense_level_scores_lds_equal_per_pair_kernel(hq_lib, hq_option, f32, L)
             np.testing.assert_array_equal(got[a, :500], O.level_similarity(Q[a], C[:500], lv))
 
 
+@pytest.mark.parametrize("coop", [1, 0])
 @pytest.mark.parametrize("kind", ["f64", "f32", "mixed"])
-def test_fused_query_prepare_equals_two_launches(hq_lib, kind):
+def test_fused_query_prepare_equals_two_launches(hq_lib, hq_option, kind, coop):
     """hq_seg_prepare_pack0 (query batches: statistics, normalised rows and split level-0 copies in one
     launch) writes exactly what hq_seg_prepare_rows + hq_seg_pack0_split write, pad rows included."""
     from hq_mi355x import kernels as K
@@ -208,6 +209,7 @@ def test_fused_query_prepare_equals_two_launches(hq_lib, kind):
         flags = np.arange(len(C)) % 3 == 0
     x = to_dev(C if kind != "mixed" else C.astype(np.float64))
     f32 = kind == "f32"
+    hq_option("prep_coop", coop)  # 1: lane-cooperative statistics (default), 0: one lane per segment
     a = K.seg_prepare_pack0(x, src_f32=f32, row_f32=flags)
     b = K.pack0(K.seg_prepare(x, src_f32=f32, row_f32=flags))
     for name in ("Z", "S", "Z16", "S32"):
