@@ -107,3 +107,23 @@ def test_clustered_corpus_full_size(hq_lib):
     for a, (rid, rsc, _, _) in zip(rows, _oracle_many(Qh, Ch, rows, 20)):
         assert list(res[20][0][a]) == list(rid), a
         np.testing.assert_allclose(res[20][1][a], rsc, atol=1e-10)
+
+
+def test_bench_queries_every_query_full_size(hq_lib):
+    """The bench's own cfg3 workload (queries = corpus rows 0..999 + N(0, 0.01), seed 3) at full size: EVERY
+    query's progressive result at M = 20 / 100 / 1000 equal to the dense exact path (ids, counts, overall and
+    level scores), and every query's brute-force top-10 (search_engine.py:302-338) equal to the dense exact
+    overall scores' top-10 — the full-size checks test_gpu_fullsize.py samples."""
+    import torch
+    from hq_mi355x.core.search_engine import IndexCorpus
+    C = _cfg3_corpus()
+    gq = torch.Generator(device="cuda").manual_seed(3)
+    Q = C[:QN] + 0.01 * torch.randn((QN, 64), generator=gq, device="cuda", dtype=torch.float64)
+    corpus = IndexCorpus(C)
+    res = {M: _check_all(corpus, Q, M, max_dense=2) for M in (20, 100, 1000)}
+    assert np.array_equal(res[20][0][:, 0], np.arange(QN))
+    ids, ov, lv = [_np(x) for x in corpus.brute_force(Q, 10)]
+    qp = corpus.prepare_queries(Q)
+    ds, di, _, _ = [_np(x) for x in corpus._dense(qp, torch.arange(QN, device="cuda"), 1, 10, 0.0, 0)]
+    assert np.array_equal(ids, di)
+    np.testing.assert_array_equal(ov, ds)
