@@ -3634,26 +3634,27 @@ __device__ __forceinline__ uint64_t pool_key(float s, int row) {
   return ((uint64_t)(0x7FFFFFFFu - __float_as_uint(s)) << 32) | (uint32_t)row;
 }
 
-// k_pool_select for K > 64: the query's pool (<= kSortCap entries) is sorted whole; a larger pool is first
-// cut at its K-th key (bisection over the 64-bit keys in memory) and the K survivors are sorted.
+// k_pool_select for K > 64.  A pool of T > K entries is first cut to exactly its K smallest keys by a radix
+// select (8-bit digits from the top, a 256-bin LDS histogram per digit, stopping as soon as the K-th key's
+// bucket is taken whole: 3-4 digits on scores of one exponent), reading a pool of <= kSortCap entries from
+// LDS and a larger one from memory; only the K (<= kMaxTopKBig) survivors are sorted.  Round 4's form
+// sorted the whole pool (2048-4096 keys at M = 1000: 78 bitonic stages of 8 swaps per thread) and cut larger
+// pools by a 64-step bisection in memory.
+// CAP: pool keys held in LDS, KC: list entries (K <= KC); <1024, 128> for M = 100 (10 KB of LDS: every
+// workgroup of a 1000-query batch resident at once), <kSortCap, kMaxTopKBig> (41 KB) above
+template <int CAP, int KC>
 __global__ __launch_bounds__(256) void k_pool_sort(float* pool_s, int* pool_i, int* pool_n, int cap, int Q, int K,
                                                    int64_t id_base, double* __restrict__ out_score,
                                                    int64_t* __restrict__ out_id, const double* __restrict__ th0,
                                                    double thr0, const float* __restrict__ qflag, int qstride,
                                                    Scan0Args fa, const int* __restrict__ flist,
-                                                   const int* __restrict__ fcount) {
-  __shared__ uint64_t key[kSortCap];
-  __shared__ int red[4];
+                                                   const int* __restrict__ fcount, int lds_cap) {
+  __shared__ uint64_t key[CAP];
+  __shared__ uint64_t sel[KC];
+  __shared__ int hist[256];
+  __shared__ int sb[3];  // the K-th key's bucket, the count before it, its count
   __shared__ int nsel;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  auto bsum = [&](int v) -> int {
-    v = wsum64i(v);
-    if (lane == 0) red[wave] = v;
-    __syncthreads();
-    const int r = red[0] + red[1] + red[2] + red[3];
-    __syncthreads();
-    return r;
-  };
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
     if (fcount) {  // the corpus's flagged rows against this query first (k_pool_select)
       const QConst* qc = reinterpret_cast<const QConst*>(fa.qconst);
@@ -3676,35 +3677,63 @@ __global__ __launch_bounds__(256) void k_pool_sort(float* pool_s, int* pool_i, i
     const float* ps = pool_s + (int64_t)q * cap;
     const int* pi = pool_i + (int64_t)q * cap;
     const int k = T < K ? T : K;
-    int n2;
-    if (T <= kSortCap) {
-      n2 = pow2_at_least(T);
-      for (int x = tid; x < n2; x += 256) key[x] = x < T ? pool_key(ps[x], pi[x]) : ~0ull;
+    const bool in_lds = T <= lds_cap && T <= CAP;
+    if (T <= K) {
+      for (int x = tid; x < T; x += 256) sel[x] = pool_key(ps[x], pi[x]);
     } else {
-      uint64_t lo = 0ull, hi = ~0ull;  // smallest key with count(key <= lo) >= K
-      while (lo < hi) {
-        const uint64_t mid = lo + (hi - lo) / 2;
-        int c = 0;
-        for (int x = tid; x < T; x += 256) c += pool_key(ps[x], pi[x]) <= mid ? 1 : 0;
-        if (bsum(c) >= K) hi = mid; else lo = mid + 1;
+      if (in_lds)
+        for (int x = tid; x < T; x += 256) key[x] = pool_key(ps[x], pi[x]);
+      auto get = [&](int x) -> uint64_t { return in_lds ? key[x] : pool_key(ps[x], pi[x]); };
+      uint64_t prefix = 0ull, mask = 0ull;
+      int need = K;  // keys still to take among those matching prefix on mask
+      for (int shift = 56; shift >= 0; shift -= 8) {
+        hist[tid] = 0;
+        __syncthreads();
+        for (int x = tid; x < T; x += 256) {
+          const uint64_t kk = get(x);
+          if ((kk & mask) == prefix) atomicAdd(&hist[(int)(kk >> shift) & 255], 1);
+        }
+        __syncthreads();
+        if (wave == 0) {  // the bucket holding the need-th matching key
+          const int h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
+          int inc = h0 + h1 + h2 + h3;
+          for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += u;
+          }
+          int c = inc - (h0 + h1 + h2 + h3);
+          const int hs[4] = {h0, h1, h2, h3};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (c < need && c + hs[j] >= need) { sb[0] = 4 * lane + j; sb[1] = c; sb[2] = hs[j]; }
+            c += hs[j];
+          }
+        }
+        __syncthreads();
+        prefix |= (uint64_t)sb[0] << shift;
+        mask |= 0xFFull << shift;
+        need -= sb[1];
+        const bool whole = sb[2] == need;
+        __syncthreads();  // sb read by every thread before the next digit rewrites it
+        if (whole) break;
       }
+      // exactly K keys: those whose digits so far are <= the prefix's (keys are unique)
       if (tid == 0) nsel = 0;
       __syncthreads();
       for (int x = tid; x < T; x += 256) {
-        const uint64_t kk = pool_key(ps[x], pi[x]);
-        if (kk <= lo) key[atomicAdd(&nsel, 1)] = kk;  // exactly K entries
+        const uint64_t kk = get(x);
+        if ((kk & mask) <= prefix) sel[atomicAdd(&nsel, 1)] = kk;
       }
-      n2 = pow2_at_least(K);
-      __syncthreads();
-      for (int x = K + tid; x < n2; x += 256) key[x] = ~0ull;
     }
+    const int n2 = pow2_at_least(k);
+    for (int x = k + tid; x < n2; x += 256) sel[x] = ~0ull;
     __syncthreads();
-    lds_bitonic(n2, [&](int a, int b) { return key[a] < key[b]; },
-                [&](int a, int b) { const uint64_t t = key[a]; key[a] = key[b]; key[b] = t; });
+    lds_bitonic(n2, [&](int a, int b) { return sel[a] < sel[b]; },
+                [&](int a, int b) { const uint64_t t = sel[a]; sel[a] = sel[b]; sel[b] = t; });
     const bool trunc = th0 != nullptr && th0[q] > thr0;
     for (int x = tid; x < K; x += 256) {
       if (x < k) {
-        const uint64_t kk = key[x];
+        const uint64_t kk = sel[x];
         out_score[(int64_t)q * K + x] = (double)__uint_as_float(0x7FFFFFFFu - (uint32_t)(kk >> 32));
         out_id[(int64_t)q * K + x] = (int64_t)(uint32_t)kk + id_base;
       } else {
@@ -3725,9 +3754,14 @@ static void launch_pool_select(int K, hipStream_t s, int Q, float* pool_s, int* 
   if (K <= kMaxTopK)
     hipLaunchKernelGGL(k_pool_select, dim3(mg), dim3(64), 0, s, pool_s, pool_i, pool_n, cap, Q, K, id_base, out_score,
                        out_id, th0, thr0, qflag, qstride, fa, flist, fcount);
+  else if (K <= 128)
+    hipLaunchKernelGGL((k_pool_sort<1024, 128>), dim3(mg), dim3(256), 0, s, pool_s, pool_i, pool_n, cap, Q, K, id_base,
+                       out_score, out_id, th0, thr0, qflag, qstride, fa, flist, fcount,
+                       opt(OPT_POOL_SORT_MEM, 0) ? 0 : 1024);  // option pool_sort_mem: test the memory form
   else
-    hipLaunchKernelGGL(k_pool_sort, dim3(mg), dim3(256), 0, s, pool_s, pool_i, pool_n, cap, Q, K, id_base, out_score,
-                       out_id, th0, thr0, qflag, qstride, fa, flist, fcount);
+    hipLaunchKernelGGL((k_pool_sort<kSortCap, kMaxTopKBig>), dim3(mg), dim3(256), 0, s, pool_s, pool_i, pool_n, cap, Q,
+                       K, id_base, out_score, out_id, th0, thr0, qflag, qstride, fa, flist, fcount,
+                       opt(OPT_POOL_SORT_MEM, 0) ? 0 : kSortCap);
 }
 
 // k_refine_lds for kp > 64 (same contract, arithmetic and outputs), one 256-thread workgroup per query.

@@ -145,11 +145,14 @@ def test_long_list_sharded_merge_equals_single(hq_lib):
     np.testing.assert_array_equal(_np(lv), ref[2])
 
 
+@pytest.mark.parametrize("mem", [0, 1])
 @pytest.mark.parametrize("k", [65, 100, 600])
-def test_pool_sort_equals_short_select_order(hq_lib, hq_option, k):
-    """k > 64 through k_pool_sort + k_refine_big: every query whose list is proven complete returns exactly
-    the dense exact select's top-k (hq_level_scores + hq_select_topk: score desc, id asc), and at most one
-    query is left unresolved."""
+def test_pool_sort_equals_short_select_order(hq_lib, hq_option, k, mem):
+    """k > 64 through k_pool_sort + the long-list re-rank: every query whose list is proven complete returns
+    exactly the dense exact select's top-k (hq_level_scores + hq_select_topk: score desc, id asc), and at
+    most one query is left unresolved.  mem = 1 (option pool_sort_mem): the radix select reads the pool from
+    memory, the form of pools above the LDS capacity (4096 keys)."""
+    hq_option("pool_sort_mem", mem)
     from hq_mi355x import kernels as K
     from hq_mi355x.core.search_engine import IndexCorpus
     C = _corpus(25000, 64, 29)
