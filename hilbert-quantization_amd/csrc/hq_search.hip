@@ -1802,7 +1802,16 @@ __device__ __forceinline__ float max4(const flt4 v) {
   return __builtin_elementwise_maximum(__builtin_elementwise_maximum(v.x, v.y), __builtin_elementwise_maximum(v.z, v.w));
 }
 
-constexpr int kQCap = 256;  // LDS queue entries per wave (a half-step adds at most 128)
+constexpr int kQCap = 192;  // LDS queue entries per wave (< 64 before a half-step, which adds at most 128)
+// Pool appends staged per wave in LDS: (score, row, query | rank << 8), rank = the entry's position among the
+// wave's staged entries of its query; a flush reserves each query's slots with ONE global atomic (lane per
+// query) and writes the entries.  Per passing pair, round 4 paid a returning device-scope atomic on the
+// query's count: 85 us of a 366 us scan at list length 1008 (diagnostics build, 2M appends on 1000 counters).
+constexpr int kStCap = 256;
+struct StEntry {
+  float s;
+  int row, qr;
+};
 struct QEntry {
   flt4 g;        // G of rows row .. row + 3 for query qi
   int qi, row;   // query within the wave, first row (absolute, multiple of 4)
@@ -1849,6 +1858,30 @@ __device__ __forceinline__ flt4 split_g4(const _Float16* __restrict__ Zq16, cons
   return G;
 }
 
+// staged pool entries of one wave to the pools (k_scan0g): one count atomic per query with entries, then the
+// writes.  Out of line: inlined at every drain site it pushed the scan past 128 VGPRs (spills in the step
+// loop); as a call its register saves run only when a flush does (rarely: the stage holds kStCap entries).
+__device__ __noinline__ void stage_flush(StEntry* st, int* scnt, int* sbase, int sn, int qw, int q0, int* pool_n,
+                                         float* pool_s, int* pool_i, int cap) {
+  const int lane = threadIdx.x & 63;
+  wave_lds_sync();
+  for (int t = lane; t < qw; t += 64) {
+    const int c = scnt[t];
+    sbase[t] = c > 0 ? atomicAdd(pool_n + q0 + t, c) : 0;
+    scnt[t] = 0;
+  }
+  wave_lds_sync();
+  for (int e = lane; e < sn; e += 64) {
+    const StEntry x = st[e];
+    const int qi = x.qr & 255, slot = sbase[qi] + (x.qr >> 8);
+    if (slot < cap) {
+      pool_s[(int64_t)(q0 + qi) * cap + slot] = x.s;
+      pool_i[(int64_t)(q0 + qi) * cap + slot] = x.row;
+    }
+  }
+  wave_lds_sync();
+}
+
 // WPB waves per workgroup: the WPB waves of a block take WPB consecutive query blocks of ONE chunk and
 // read the same candidate fragments step by step (a barrier per unrolled iteration keeps them within
 // a few steps of each other, so WPB - 1 of the WPB reads of a fragment hit the CU's L1)
@@ -1866,8 +1899,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
   constexpr int QW = 16 * NB, NP = NB / 2;
   using QE = QEntry;  // G_hh kept for the drain's gate (QEntryHI: no gate, measured slower)
   __shared__ QE qe_all[WPB][kQCap];
+  __shared__ StEntry st_all[WPB][kStCap];
+  __shared__ int scnt_all[WPB][QW], sbase_all[WPB][QW];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   QE* qe = qe_all[WPB > 1 ? threadIdx.x >> 6 : 0];
+  StEntry* st = st_all[WPB > 1 ? threadIdx.x >> 6 : 0];
+  int* scnt = scnt_all[WPB > 1 ? threadIdx.x >> 6 : 0];
+  int* sbase = sbase_all[WPB > 1 ? threadIdx.x >> 6 : 0];
+  for (int t = lane; t < QW; t += 64) scnt[t] = 0;
   const int blk = blockIdx.x, xcd = blk & 7, slot = blk >> 3;
   const int nqg = (a.nqb + WPB - 1) / WPB;
   const int chunk = xcd + 8 * (slot / nqg);
@@ -1928,19 +1967,25 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
   };
 
   int qn = 0;  // queue entries (wave-uniform)
+  int sn = 0;  // staged pool entries (wave-uniform)
+  auto flush = [&]() {
+    stage_flush(st, scnt, sbase, sn, QW, q0, a.pool_n, a.pool_s, a.pool_i, a.pool_cap);
+    sn = 0;
+  };
   // drain n <= 64 entries from the front of the queue, then shift the rest down
   auto drain = [&](const int n) {
     if (lane < n) {
+      float sc[4] = {-1.0f, -1.0f, -1.0f, -1.0f};  // pool scores of the entry's rows (< 0: not appended)
       const int eqi = qe[lane].qi, erow = qe[lane].row;
       const int q = q0 + eqi;
       flt4 eg = qe[lane].g;
       const QConst c = qc[q];
-      const float* st = a.Sc32 + (int64_t)(erow >> 2) * 16;  // the SoA group of rows row .. row + 3
-      HQ_GUARD(st, a.Sc32, pack0_rows(a.N) * 4 - 15);
-      const flt4 sd = *reinterpret_cast<const flt4*>(st);
-      const flt4 mn = *reinterpret_cast<const flt4*>(st + 4);
-      const flt4 ms = *reinterpret_cast<const flt4*>(st + 8);
-      const flt4 fl = *reinterpret_cast<const flt4*>(st + 12);
+      const float* stt = a.Sc32 + (int64_t)(erow >> 2) * 16;  // the SoA group of rows row .. row + 3
+      HQ_GUARD(stt, a.Sc32, pack0_rows(a.N) * 4 - 15);
+      const flt4 sd = *reinterpret_cast<const flt4*>(stt);
+      const flt4 mn = *reinterpret_cast<const flt4*>(stt + 4);
+      const flt4 ms = *reinterpret_cast<const flt4*>(stt + 8);
+      const flt4 fl = *reinterpret_cast<const flt4*>(stt + 12);
       bool need = true;
       if constexpr (HI) {
         // gate: the filter is monotone in G and G_split <= G_hh + dG, so a block none of whose rows passes at
@@ -1956,32 +2001,48 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
         if (need) eg = split_g4(a.Zq16, a.Zc16, q, erow);
       }
 #pragma unroll
-      for (int r = 0; r < 4 && need; ++r) {
+      for (int r = 0; r < 4; ++r) {
         const int row = erow + r;
         const int f = __float_as_int(fl[r]);
-        if (row >= c_end || f != 0) continue;  // past the chunk; flagged rows: k_pool_select
+        if (!need || row >= c_end || f != 0) continue;  // past the chunk; flagged rows: k_pool_select
         const float G = eg[r];
-        float s = -__builtin_huge_valf();
-        {
-          // division-free filter (k_scan0f filter_half), then the list score (k_scan0f insert_half)
-          const float E = fmaf(G, c1f, c.k0);
-          const float num = fmaf(G, c.qA * sd[r], c.qB * mn[r]);
-          const float d = fmaf(E, c.qQ + ms[r], num);
-          if (fmaxf(E, d) >= 0.0f) {
-            float t = num * __builtin_amdgcn_rcpf(c.qQ + ms[r]);
-            t = t > 0.0f ? t : 0.0f;
-            s = fmaf(G, c1f, 0.35f) + t;
-            s = s < 1.0f ? s : 1.0f;
-            s = s > 0.0f ? s : 0.0f;
-          }
+        // division-free filter (k_scan0f filter_half), then the list score (k_scan0f insert_half)
+        const float E = fmaf(G, c1f, c.k0);
+        const float num = fmaf(G, c.qA * sd[r], c.qB * mn[r]);
+        const float d = fmaf(E, c.qQ + ms[r], num);
+        if (fmaxf(E, d) >= 0.0f) {
+          float t = num * __builtin_amdgcn_rcpf(c.qQ + ms[r]);
+          t = t > 0.0f ? t : 0.0f;
+          float v = fmaf(G, c1f, 0.35f) + t;
+          v = v < 1.0f ? v : 1.0f;
+          v = v > 0.0f ? v : 0.0f;
+          if (v >= c.thl) sc[r] = v;
         }
-        if (s >= c.thl) {
-          const int slot = atomicAdd(a.pool_n + q, 1);
-          if (slot < a.pool_cap) {
-            a.pool_s[(int64_t)q * a.pool_cap + slot] = s;
-            a.pool_i[(int64_t)q * a.pool_cap + slot] = row;
-          }
+      }
+      qe[lane].g = flt4{sc[0], sc[1], sc[2], sc[3]};  // the entry's pool scores replace its G (consumed)
+    }
+    wave_lds_sync();
+    // stage the passing rows: ballot + mbcnt positions, LDS ranks per query (one flush check per drain)
+    const flt4 ps = lane < n ? qe[lane].g : flt4{-1.0f, -1.0f, -1.0f, -1.0f};
+    unsigned long long pm[4];
+    int call = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pm[r] = __builtin_amdgcn_ballot_w64(ps[r] >= 0.0f);
+      call += __popcll(pm[r]);
+    }
+    if (call > 0) {
+      if (sn + call > kStCap) flush();
+      const int eqi = lane < n ? qe[lane].qi : 0, erow = lane < n ? qe[lane].row : 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (ps[r] >= 0.0f) {
+          const int rank = atomicAdd(&scnt[eqi], 1);
+          const unsigned long long m = pm[r];
+          const int e = sn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+          st[e] = StEntry{ps[r], erow + r, eqi | (rank << 8)};
         }
+        sn += __popcll(pm[r]);
       }
     }
     wave_lds_sync();
@@ -2076,6 +2137,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 
   for (int u = 0; u < PF; ++u)
     if (s + u < nsteps) body(s + u, buf[u], buf[(u + 1) % (PF + 1)], buf[(u + PF) % (PF + 1)]);
   while (qn > 0) drain(qn < 64 ? qn : 64);
+  if (sn > 0) flush();
 }
 
 // rows of the split copies with a zero-variance / f32-unsafe flag (S32 flag word bits 1, 2): compacted
@@ -4178,10 +4240,19 @@ __global__ __launch_bounds__(256) void k_rank_sort(RankArgs a, const double* __r
       os[(int64_t)q * k + r] = r < cnt ? se[r] : -__builtin_huge_val();
       oid[(int64_t)q * k + r] = r < cnt ? sid[r] : -1;
     }
-    if (odet) {
-      for (int t = tid; t < k * W; t += 256) {
-        const int r = t / W, w = t - r * W;
-        odet[(int64_t)q * k * W + t] = r < cnt ? a.ws_rec[(base + pos[r]) * W + w] : 0.0;
+    if (odet) {  // records gathered by list position, four loads in flight per thread before the stores
+      const double* __restrict__ rec = a.ws_rec;
+      const int tot = k * W;
+      for (int t0 = tid; t0 < tot; t0 += 4 * 256) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int t = t0 + 256 * u, r = t / W, w = t - r * W;
+          v[u] = t < tot && r < cnt ? rec[(base + pos[r]) * W + w] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (t0 + 256 * u < tot) odet[(int64_t)q * tot + t0 + 256 * u] = v[u];
       }
     }
     if (tid == 0) {
@@ -4219,8 +4290,14 @@ static size_t refine_ws_bytes(int Q, int kp, int L) {
   return (size_t)Q * kp * (16 + 8 * (size_t)(1 + si.nseg)) + 256;
 }
 
-// k_progressive_final for M > 64: wave 0 selects the survivors (final_survivors), the workgroup sorts them
-// by (overall desc, survivor position asc) — the reference's stable sort — in LDS
+// k_progressive_final for M > 64: the survivors (one list: its valid prefix, counted by the whole
+// workgroup; R lists: wave 0 merges them, final_survivors) ordered by (overall desc, survivor position asc)
+// — the reference's stable sort.  Only the first K are needed: K <= kFinalRounds takes them by K rounds of a
+// workgroup arg-max over register-held overall scores (one barrier per round); larger K sorts them whole
+// (bitonic in LDS).  Round 4's form sorted all n (1024 keys at M = 1000, 55 bitonic stages) for K = 10 and
+// read the single list's validity from one wave.
+constexpr int kFinalRounds = 32;
+
 __global__ __launch_bounds__(256) void k_progressive_final_big(int R, int Q, int M, int W,
                                                                const double* __restrict__ s0,
                                                                const int64_t* __restrict__ ids,
@@ -4234,12 +4311,36 @@ __global__ __launch_bounds__(256) void k_progressive_final_big(int R, int Q, int
   __shared__ int sel[kMaxTopKBig];
   __shared__ double ovs[kMaxTopKBig];
   __shared__ int pos[kMaxTopKBig];
+  __shared__ double rv[2][4];
+  __shared__ int ri[2][4];
+  __shared__ int red[4];
   __shared__ int sn;
   __shared__ int64_t sfb;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool k32 = (flags & 1) != 0;
+  auto first = [](double a, int ia, double b, int ib) { return ia >= 0 && (ib < 0 || a > b || (a == b && ia < ib)); };
   for (int q = blockIdx.x; q < Q; q += gridDim.x) {
-    if (tid < 64) {
+    if (R == 1) {  // one list in (score desc, id asc) order, its valid entries first
+      int c = 0;
+      for (int i = tid; i < M; i += 256) {
+        const bool v = ids[(int64_t)q * M + i] >= 0;
+        c += v ? 1 : 0;
+        sel[i] = i;
+      }
+      c = wsum64i(c);
+      if (lane == 0) red[wave] = c;
+      __syncthreads();
+      if (tid == 0) {
+        int n = red[0] + red[1] + red[2] + red[3];
+        int64_t fb = -1;
+        if (n == 0 && best_id[q] >= 0) {  // none passed the threshold: the first arg-max (:295-298)
+          n = 1;
+          fb = best_id[q];
+        }
+        sn = n;
+        sfb = fb;
+      }
+    } else if (tid < 64) {
       int64_t fb;
       const int n = final_survivors(R, Q, M, q, s0, ids, best, best_id, sel, &fb, k32);
       if (tid == 0) {
@@ -4255,31 +4356,81 @@ __global__ __launch_bounds__(256) void k_progressive_final_big(int R, int Q, int
       const int64_t rq = (int64_t)(v >> 16) * Q + q;
       return fb_id >= 0 ? rq : rq * M + (v & 0xFFFF);
     };
-    const int n2 = pow2_at_least(n);
-    for (int i = tid; i < n2; i += 256) {
-      ovs[i] = i < n ? key_of(rowbase[row_of(sel[i]) * W], k32) : -__builtin_huge_val();
-      pos[i] = i;
+    const int outn = n < K ? n : K;
+    if (K <= kFinalRounds) {
+      // K rounds of the workgroup's first (overall desc, position asc) among the entries not yet taken
+      double v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = tid + 256 * e;
+        v[e] = i < n ? key_of(rowbase[row_of(sel[i]) * W], k32) : 0.0;
+      }
+      int taken = 0;
+      for (int r = 0; r < outn; ++r) {
+        double bv = 0.0;
+        int bi = -1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = tid + 256 * e;
+          if (i < n && !((taken >> e) & 1) && first(v[e], i, bv, bi)) {
+            bv = v[e];
+            bi = i;
+          }
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const double v2 = __shfl_xor(bv, o, 64);
+          const int i2 = __shfl_xor(bi, o, 64);
+          if (first(v2, i2, bv, bi)) {
+            bv = v2;
+            bi = i2;
+          }
+        }
+        if (lane == 0) {
+          rv[r & 1][wave] = bv;
+          ri[r & 1][wave] = bi;
+        }
+        __syncthreads();  // (the other buffer is rewritten only after the next round's barrier)
+        bv = rv[r & 1][0];
+        bi = ri[r & 1][0];
+#pragma unroll
+        for (int w = 1; w < 4; ++w)
+          if (first(rv[r & 1][w], ri[r & 1][w], bv, bi)) {
+            bv = rv[r & 1][w];
+            bi = ri[r & 1][w];
+          }
+        if ((bi & 255) == tid) taken |= 1 << (bi >> 8);
+        if (tid == 0) pos[r] = bi;
+      }
+    } else {
+      const int n2 = pow2_at_least(n);
+      for (int i = tid; i < n2; i += 256) {
+        ovs[i] = i < n ? key_of(rowbase[row_of(sel[i]) * W], k32) : -__builtin_huge_val();
+        pos[i] = i;
+      }
+      __syncthreads();
+      lds_bitonic(n2, [&](int a, int b) { return ovs[a] > ovs[b] || (ovs[a] == ovs[b] && pos[a] < pos[b]); },
+                  [&](int a, int b) {
+                    const double to = ovs[a];
+                    ovs[a] = ovs[b];
+                    ovs[b] = to;
+                    const int tp = pos[a];
+                    pos[a] = pos[b];
+                    pos[b] = tp;
+                  });
     }
     __syncthreads();
-    lds_bitonic(n2, [&](int a, int b) { return ovs[a] > ovs[b] || (ovs[a] == ovs[b] && pos[a] < pos[b]); },
-                [&](int a, int b) {
-                  const double to = ovs[a];
-                  ovs[a] = ovs[b];
-                  ovs[b] = to;
-                  const int tp = pos[a];
-                  pos[a] = pos[b];
-                  pos[b] = tp;
-                });
-    const int outn = n < K ? n : K;
-    for (int r = tid; r < K; r += 256) {
+    for (int t = tid; t < K * W; t += 256) {  // one record value per thread
+      const int r = t / W, w = t - r * W;
+      double val = 0.0;
       if (r < outn) {
         const int64_t oi = row_of(sel[pos[r]]);
-        out_id[(int64_t)q * K + r] = fb_id >= 0 ? fb_id : ids[oi];
-        for (int w = 0; w < W; ++w) out_det[((int64_t)q * K + r) * W + w] = rowbase[oi * W + w];
-      } else {
+        val = rowbase[oi * W + w];
+        if (w == 0) out_id[(int64_t)q * K + r] = fb_id >= 0 ? fb_id : ids[oi];
+      } else if (w == 0) {
         out_id[(int64_t)q * K + r] = -1;
-        for (int w = 0; w < W; ++w) out_det[((int64_t)q * K + r) * W + w] = 0.0;
       }
+      out_det[(int64_t)q * K * W + t] = val;
     }
     if (tid == 0) out_count[q] = outn;
     __syncthreads();

@@ -46,8 +46,11 @@ def _dense_counter(corpus):
     return calls
 
 
+@pytest.mark.parametrize("kout", ["10", "full"])
 @pytest.mark.parametrize("M", [100, 1000])
-def test_long_list_progressive_matches_oracle(hq_lib, M):
+def test_long_list_progressive_matches_oracle(hq_lib, M, kout):
+    """kout 10: the final ranking's arg-max rounds (K <= 32, tied duplicates ranked by list position);
+    full: its whole-list sort."""
     from hq_mi355x.core.search_engine import IndexCorpus
     C = _corpus(40000, 64, 21)
     rng = np.random.default_rng(22)
@@ -56,7 +59,7 @@ def test_long_list_progressive_matches_oracle(hq_lib, M):
     corpus = IndexCorpus(C)
     assert M + corpus.SLACK <= corpus._max_list(0)  # the scan path, not the dense fallback
     dense = _dense_counter(corpus)
-    K_out = min(M, 200)
+    K_out = 10 if kout == "10" else min(M, 200)
     ids, ov, lv, cnt = [_np(x) for x in corpus.progressive(Q, K_out, 0.1, M)]
     # only the zero-variance query (row 1) may need the dense exact path
     assert sum(dense) <= 1, dense

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The level-0 scan on the bench corpus (cfg3 shape: 1M x 64 level-0 values, 1000 queries), three
 calls, for PMC passes (tools/pmc_kernel.sh).  Argument: level0 (default, the progressive search's scan)
-or overall (the brute-force overall scan), m100 / m1000 (whole progressive searches at M = 100 / 1000)."""
+or overall (the brute-force overall scan), m100 / m1000 (whole progressive searches at M = 100 / 1000), scanNNN (the scan alone, list length NNN)."""
 import os
 import sys
 
@@ -31,6 +31,8 @@ for _ in range(3):
     elif mode in ("m100", "m1000"):
         corpus.progressive(C[:1000] + 0.01 * torch.randn((1000, 64), generator=gq, device=dev, dtype=torch.float64),
                            10, 0.1, int(mode[1:]))
+    elif mode.startswith("scan"):  # scanNNN: the level-0 scan alone at list length NNN
+        K.scan_topk(qp, corpus.prep, 0, int(mode[4:]), 0.1 - 2e-5, 1)
     else:
         K.scan_topk(qp, corpus.prep, 0, 28, 0.1 - 2e-5, 1)
 torch.cuda.synchronize()
