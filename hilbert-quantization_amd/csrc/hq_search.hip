@@ -3959,11 +3959,25 @@ __global__ __launch_bounds__(256) void k_refine_big_raw(HQ_REFINE_ARGS, int tb) 
 constexpr int kCoopGroups = 32;              // 8-lane groups per 256-thread workgroup
 constexpr int kCoopMaxW = 7;                 // record width 1 + nseg
 
-template <typename T>
-__device__ __forceinline__ T coop_xor(T v, int m) { return __shfl_xor(v, m, 64); }
-template <typename T>
-__device__ __forceinline__ Sum2<T> coop_xor(Sum2<T> v, int m) {
-  return Sum2<T>(__shfl_xor(v.a, m, 64), __shfl_xor(v.b, m, 64));
+// the group partner's value by DPP (a VALU operand modifier; __shfl_xor goes through the LDS crossbar,
+// ds_bpermute, three dependent round trips per sum): M = 1, 2 quad_perm [1,0,3,2] / [2,3,0,1]; M = 4
+// row_half_mirror (lane i of 8 reads lane 7 - i: after the first two steps lanes 0-3 hold the same bits and
+// so do lanes 4-7, so any cross pairing gives the same sum)
+template <int M>
+__device__ __forceinline__ int coop_dpp(int v) {
+  constexpr int ctrl = M == 1 ? 0xB1 : (M == 2 ? 0x4E : 0x141);
+  return __builtin_amdgcn_update_dpp(v, v, ctrl, 0xF, 0xF, false);
+}
+template <int M>
+__device__ __forceinline__ float coop_xor(float v) { return __int_as_float(coop_dpp<M>(__float_as_int(v))); }
+template <int M>
+__device__ __forceinline__ double coop_xor(double v) {
+  const int lo = coop_dpp<M>(__double2loint(v)), hi = coop_dpp<M>(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+template <int M, typename T>
+__device__ __forceinline__ Sum2<T> coop_xor(Sum2<T> v) {
+  return Sum2<T>(coop_xor<M>(v.a), coop_xor<M>(v.b));
 }
 
 // np_sum<T, true>(f, n) (n <= 128) over the 8 lanes of a group; j = lane within the group.  Every lane
@@ -3980,9 +3994,9 @@ __device__ __forceinline__ T coop_sum(const F& f, int n, int j) {
     const int lim = n - (n % 8);
 #pragma unroll 1
     for (int i = 8 + j; i < lim; i += 8) r = r + f(i);
-    r = r + coop_xor(r, 1);  // r_j + r_(j^1): (r0 + r1) on lanes 0 and 1
-    r = r + coop_xor(r, 2);  // (r0 + r1) + (r2 + r3)
-    r = r + coop_xor(r, 4);  // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
+    r = r + coop_xor<1>(r);  // r_j + r_(j^1): (r0 + r1) on lanes 0 and 1
+    r = r + coop_xor<2>(r);  // (r0 + r1) + (r2 + r3)
+    r = r + coop_xor<4>(r);  // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
     res = r;
 #pragma unroll 1
     for (int i = lim; i < n; ++i) res = res + f(i);
@@ -4357,7 +4371,10 @@ __global__ __launch_bounds__(256) void k_progressive_final_big(int R, int Q, int
       return fb_id >= 0 ? rq : rq * M + (v & 0xFFFF);
     };
     const int outn = n < K ? n : K;
-    if (K <= kFinalRounds) {
+    // rounds (a wave reduction each, ~3 bitonic stages of work) when cheaper than the whole sort
+    int lg = 1;
+    while ((1 << lg) < n) ++lg;
+    if (K <= kFinalRounds && 3 * outn < lg * (lg + 1) / 2) {
       // K rounds of the workgroup's first (overall desc, position asc) among the entries not yet taken
       double v[4];
 #pragma unroll
