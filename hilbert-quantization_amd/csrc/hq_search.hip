@@ -1893,9 +1893,10 @@ __device__ __noinline__ void stage_flush(StEntry* st, int* scnt, int* sbase, int
 // < 2^-10 (1.002) m + 1e-5 m, so a lane block passes when max G_hihi >= G* - (1e-3 m + 1e-4); the drain then
 // recomputes each queued block's split G (split_g4) for the filter and the pool score.  HI = false: the
 // three-MFMA form (option scan_split3).
-// OCC: waves per SIMD the register allocation targets (HI form: 92 VGPRs at 5, no spills)
+// OCC: waves per SIMD the register allocation targets (at most 4 since the pool-append stage: 9.7 KB of LDS
+// per wave)
 template <int WPB, int PF, int NB = 4, bool HI = true, int OCC = 5>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 8 ? 3 : (HI ? OCC : 1)))) void k_scan0g(Scan0Args a) {
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(NB == 8 ? 3 : (HI ? (OCC < 4 ? OCC : 4) : 1)))) void k_scan0g(Scan0Args a) {
   constexpr int QW = 16 * NB, NP = NB / 2;
   using QE = QEntry;  // G_hh kept for the drain's gate (QEntryHI: no gate, measured slower)
   __shared__ QE qe_all[WPB][kQCap];
@@ -3956,6 +3957,8 @@ __global__ __launch_bounds__(256) void k_refine_big_raw(HQ_REFINE_ARGS, int tb) 
 //    bitonic sort every thread reads its outputs' records into registers (L1-bypassing loads), a
 //    barrier, then writes them in sorted order.
 // ------------------------------------------------------------------------------------------------
+// 1 / (level + 1) of the overall score's weights (search_engine.py:191-230), folded at compile time
+__device__ constexpr double kLevelWeight[8] = {1.0 / 1.0, 1.0 / 2.0, 1.0 / 3.0, 1.0 / 4.0, 1.0 / 5.0, 1.0 / 6.0, 1.0 / 7.0, 1.0 / 8.0};
 constexpr int kCoopGroups = 32;              // 8-lane groups per 256-thread workgroup
 constexpr int kCoopMaxW = 7;                 // record width 1 + nseg
 
@@ -4075,6 +4078,81 @@ __device__ __forceinline__ double coop_level_sides(const Side& q, const Side& c,
   return comb > 0.0 ? comb : 0.0;
 }
 
+// coop_level_sides in two phases, so that the scalar tail of a level (divisions, clamps) runs once per
+// group instead of on all 8 lanes: the sums (all lanes, group-cooperative; kind 0 = a zero-variance side,
+// no sums; 1 = float32 sums; 2 = float64 sums), then level_finish on the lane that owns the level.
+struct LevelStat {
+  double qm, qs, qq, cm, cs, cq;  // both sides' mean, std, mean of squares (their own dtype's values)
+  double sa, sb;                  // the correlation products' and squared differences' sums
+  int kind, both32;
+};
+__device__ __forceinline__ LevelStat coop_level_sums(const Side& q, const Side& c, int m, int j) {
+  LevelStat r;
+  r.qm = q.mean; r.qs = q.sd; r.qq = q.msq;
+  r.cm = c.mean; r.cs = c.sd; r.cq = c.msq;
+  r.both32 = q.f32 && c.f32;
+  r.sa = 0.0;
+  r.sb = 0.0;
+  if (q.sd == 0.0 || c.sd == 0.0) {
+    r.kind = 0;
+  } else if (r.both32) {
+    auto f2 = [&](int k) -> Sum2<float> {
+      const float d = (float)q.x[k] - (float)c.x[k];
+      return Sum2<float>((float)side_z(q, k) * (float)side_z(c, k), d * d);
+    };
+    const Sum2<float> s2 = coop_sum<Sum2<float>>(f2, m, j);
+    r.sa = s2.a;
+    r.sb = s2.b;
+    r.kind = 1;
+  } else {
+    auto f2 = [&](int k) -> Sum2<double> {
+      const double d = q.x[k] - c.x[k];
+      return Sum2<double>(side_z(q, k) * side_z(c, k), d * d);
+    };
+    const Sum2<double> s2 = coop_sum<Sum2<double>>(f2, m, j);
+    r.sa = s2.a;
+    r.sb = s2.b;
+    r.kind = 2;
+  }
+  return r;
+}
+// the tail of coop_level_sides from its sums (the same expressions, the same result bits)
+__device__ __forceinline__ double level_finish(const LevelStat& t, int m, int* np32) {
+  *np32 = 0;
+  if (t.kind == 0) return const0(t.qs == 0.0, t.cs == 0.0, t.qm, t.cm, t.both32 != 0);  // :141-148
+  if (t.kind == 1) {
+    const float corr = (float)t.sa / (float)m;                                     // :154
+    const float mse = (float)t.sb / (float)m;                                      // :161
+    const float sim = (corr + 1.0f) / 2.0f;                                        // :158
+    const float maxmse = (float)t.qq + (float)t.cq;                                // :162
+    float ds = 1.0f;
+    if (maxmse > 0.0f) {
+      ds = 1.0f - mse / maxmse;
+      ds = ds > 0.0f ? ds : 0.0f;
+    }
+    const float comb = 0.7f * sim + 0.3f * ds;                                     // :171
+    if (comb < 1.0f && comb > 0.0f) {
+      *np32 = 1;
+      return comb;
+    }
+    return comb < 1.0f ? 0.0 : 1.0;                                                // :174
+  }
+  const double corr = t.sa / (double)m;                                            // :154
+  const double mse = t.sb / (double)m;                                             // :161
+  const double sim = (corr + 1.0) / 2.0;                                           // :158
+  const double maxmse = t.qq + t.cq;                                               // :162
+  double ds = 1.0;
+  if (maxmse > 0.0) {
+    ds = 1.0 - (mse / maxmse);
+    ds = ds > 0.0 ? ds : 0.0;
+  }
+  const double a = 0.7 * sim;
+  const double b = 0.3 * ds;
+  double comb = a + b;                                                             // :171
+  comb = comb < 1.0 ? comb : 1.0;
+  return comb > 0.0 ? comb : 0.0;
+}
+
 // Compact level table of the cooperative kernels (a full SegInfo by value costs SGPRs they need)
 struct CoopSeg {
   int nseg, L, Lp;
@@ -4095,7 +4173,11 @@ struct RankArgs {
 };
 
 __host__ __device__ inline int coop_qw(const CoopSeg& c) { return (c.L + c.Lp + 4 * c.nseg + 1) & ~1; }
-__host__ __device__ inline int coop_rw(const CoopSeg& c) { return (c.L + 4 * c.nseg + 1) & ~1; }
+// (>= 12: after scoring, a group's buffer carries its 8 level values and flags, k_rank_pairs)
+__host__ __device__ inline int coop_rw(const CoopSeg& c) {
+  const int w = (c.L + 4 * c.nseg + 1) & ~1;
+  return w > 12 ? w : 12;
+}
 
 // Scoring pass: block (x-block, query) = 32 list entries of one query, one 8-lane group per entry.  The
 // block stages the query row (raw, Z, S) and each group its candidate's raw row and statistics (16-byte
@@ -4103,18 +4185,15 @@ __host__ __device__ inline int coop_rw(const CoopSeg& c) { return (c.L + 4 * c.n
 // every level of the entry (nlev: level 0 only for a mode-0 ranking without records) and writes the
 // ranking score, id and record to the workspace.  One pair per group, no loop: the occupancy hides the
 // row latency.  Bit-identical to exact_pair (coop_level_sides = exact_level_sides<true, true>).
+// the query row (raw, Z, S: all NT threads of the block) and, for list entry x < kp, group g's candidate row
+// and statistics (16-byte loads) into LDS; returns the candidate's local row (-1: none)
 template <int PPL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_rank_pairs(RankArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double cm[];
-  const int tid = threadIdx.x, g = tid >> 3, j = tid & 7;
-  const int q = blockIdx.y, x = blockIdx.x * kCoopGroups + g;
+__device__ __forceinline__ int64_t rank_stage(const RankArgs& a, double* rq, double* rg, int q, int x, int tid, int nt,
+                                              int j) {
   const int L = a.cs.L, Lp = a.cs.Lp, nseg = a.cs.nseg;
-  const int QW = coop_qw(a.cs), RW = coop_rw(a.cs);
-  double* rq = cm;
-  double* rg = cm + QW + g * RW;
-  for (int e = tid; e < L; e += 256) rq[e] = a.Rq[(int64_t)q * L + e];
-  for (int e = tid; e < Lp; e += 256) rq[L + e] = a.Zq[(int64_t)q * Lp + e];
-  for (int e = tid; e < 4 * nseg; e += 256) rq[L + Lp + e] = a.Sq[(int64_t)q * nseg * 4 + e];
+  for (int e = tid; e < L; e += nt) rq[e] = a.Rq[(int64_t)q * L + e];
+  for (int e = tid; e < Lp; e += nt) rq[L + e] = a.Zq[(int64_t)q * Lp + e];
+  for (int e = tid; e < 4 * nseg; e += nt) rq[L + Lp + e] = a.Sq[(int64_t)q * nseg * 4 + e];
   int64_t c = -1;
   if (x < a.kp) {
     const int64_t id = a.cid[(int64_t)q * a.kp + x];
@@ -4125,11 +4204,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const int np_raw = L / 2, np_all = np_raw + 2 * nseg;
     const f64x2* rr = reinterpret_cast<const f64x2*>(a.Rc + c * L);
     const f64x2* rs = reinterpret_cast<const f64x2*>(a.Sc + c * nseg * 4);
+    // every piece loaded before the first LDS store (unconditional loads of a clamped piece: a conditionally
+    // filled register array was merged into one 24-register tuple and spilled)
     f64x2 v[PPL];
 #pragma unroll
     for (int p = 0; p < PPL; ++p) {
-      const int pc = j + 8 * p;
-      if (pc < np_all) v[p] = pc < np_raw ? rr[pc] : rs[pc - np_raw];
+      const int pc = j + 8 * p < np_all ? j + 8 * p : np_all - 1;
+      v[p] = *(pc < np_raw ? rr + pc : rs + (pc - np_raw));
     }
 #pragma unroll
     for (int p = 0; p < PPL; ++p) {
@@ -4137,66 +4218,125 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       if (pc < np_all) reinterpret_cast<f64x2*>(rg)[pc] = v[p];
     }
   }
+  return c;
+}
+
+// one list entry scored by its 8-lane group (staged rows: rank_stage): the ranking score e and id (-inf / -1
+// when it fails the threshold or has no row) and, with a.det, its [overall, level..] record in rec[0 .. W)
+// (lane j writes level j).  Every level's sums are group-cooperative; lane j keeps level j's and finishes it
+// alone (the scalar tail of a level runs once per group, not on all 8 lanes); the levels' values reach every
+// lane of the group through its row buffer (the rows are consumed by then).  Bit-identical to exact_pair.
+__device__ __forceinline__ void rank_score(const RankArgs& a, const double* rq, double* rg, int64_t c, int j,
+                                           double* rec, double& e, int64_t& id) {
+  const int L = a.cs.L, Lp = a.cs.Lp, nseg = a.cs.nseg;
+  e = -__builtin_huge_val();
+  id = -1;
+  if (c < 0) return;
+  const int nlev = (a.mode == 0 && !a.det) ? 1 : nseg;
+  LevelStat mine;
+  mine.kind = 0; mine.both32 = 0;
+  mine.qm = mine.qs = mine.qq = mine.cm = mine.cs = mine.cq = mine.sa = mine.sb = 0.0;
+#pragma unroll 1
+  for (int s = 0; s < nlev; ++s) {
+    const int m = a.cs.len[s];
+    const double* qst = rq + L + Lp + 4 * s;
+    const double* cst = rg + L + 4 * s;
+    const LevelStat t = coop_level_sums(
+        coop_side(rq + a.cs.src[s], rq + L + a.cs.poff[s], qst, m, (aux_bits(qst) & kAuxF32) != 0, j),
+        coop_side(rg + a.cs.src[s], nullptr, cst, m, (aux_bits(cst) & kAuxF32) != 0, j), m, j);
+    if (j == s) mine = t;
+  }
+  int t32 = 0;
+  const double vj = j < nlev ? level_finish(mine, a.cs.len[j < nlev ? j : 0], &t32) : 0.0;
+  if (a.det && j < nlev) rec[1 + j] = vj;
+  wave_lds_sync();
+  if (j < nlev) {
+    rg[j] = vj;
+    reinterpret_cast<int*>(rg + 8)[j] = t32;
+  }
+  wave_lds_sync();
+  const double v0 = rg[0];
+  const int t0 = reinterpret_cast<const int*>(rg + 8)[0];
+  double tws = 0.0, tw = 0.0;
+  bool acc32 = false;
+#pragma unroll 1
+  for (int s = 0; s < nlev; ++s) {
+    // search_engine.py:191-230 typed running sum (exact_pair_rows)
+    const double v = rg[s];
+    const int ts = reinterpret_cast<const int*>(rg + 8)[s];
+    const double w = kLevelWeight[s];
+    const double term = ts ? (double)((float)v * (float)w) : v * w;
+    if (!acc32 && !ts) {
+      tws = tws + term;
+    } else {
+      tws = (double)((float)tws + (float)term);
+      acc32 = true;
+    }
+    tw = tw + w;
+  }
+  double ov = 0.0;
+  if (nlev == nseg) {
+    if (acc32) {
+      const float o = (float)tws / (float)tw;
+      ov = o < 1.0f ? (double)o : 1.0;
+    } else {
+      ov = tw > 0.0 ? tws / tw : 0.0;
+      ov = ov < 1.0 ? ov : 1.0;
+    }
+    ov = ov > 0.0 ? ov : 0.0;
+  }
+  if (a.det && j == 0) rec[0] = ov;
+  const double v = a.mode == 0 ? v0 : ov;
+  const int tm = a.thr_mode & (kThrKey32 - 1);  // the test itself (kThrKey32: the sort keys only)
+  const bool pass = a.mode == 0 ? typed_pass(v, t0, a.thr, tm) : (tm == 0 || (tm == 1 ? v >= a.thr : v > a.thr));
+  if (pass) {
+    e = v;
+    id = c + a.id_base;
+  }
+}
+
+// Scoring pass: block (x-block, query) = 32 list entries of one query, one 8-lane group per entry, scores
+// and records to the workspace.  One pair per group, no loop: the occupancy hides the row latency.
+template <int PPL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_rank_pairs(RankArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double cm[];
+  const int tid = threadIdx.x, g = tid >> 3, j = tid & 7;
+  const int q = blockIdx.y, x = blockIdx.x * kCoopGroups + g;
+  double* rq = cm;
+  double* rg = cm + coop_qw(a.cs) + g * coop_rw(a.cs);
+  const int64_t c = rank_stage<PPL>(a, rq, rg, q, x, tid, 256, j);
   __syncthreads();
   if (x >= a.kp) return;
-  const int W = 1 + nseg;
   const int64_t e0 = (int64_t)q * a.kp + x;
-  double e = -__builtin_huge_val();
-  int64_t id = -1;
-  if (c >= 0) {
-    const int nlev = (a.mode == 0 && !a.det) ? 1 : nseg;
-    double tws = 0.0, tw = 0.0, v0 = 0.0;
-    bool acc32 = false;
-    int t0 = 0;
-#pragma unroll 1
-    for (int s = 0; s < nlev; ++s) {
-      const int m = a.cs.len[s];
-      const double* qst = rq + L + Lp + 4 * s;
-      const double* cst = rg + L + 4 * s;
-      int t32;
-      const double v = coop_level_sides(
-          coop_side(rq + a.cs.src[s], rq + L + a.cs.poff[s], qst, m, (aux_bits(qst) & kAuxF32) != 0, j),
-          coop_side(rg + a.cs.src[s], nullptr, cst, m, (aux_bits(cst) & kAuxF32) != 0, j), m, j, &t32);
-      if (s == 0) {
-        v0 = v;
-        t0 = t32;
-      }
-      if (a.det && j == 0) a.ws_rec[e0 * W + 1 + s] = v;
-      // search_engine.py:191-230 typed running sum (exact_pair_rows)
-      const double w = 1.0 / (double)(s + 1);
-      const double term = t32 ? (double)((float)v * (float)w) : v * w;
-      if (!acc32 && !t32) {
-        tws = tws + term;
-      } else {
-        tws = (double)((float)tws + (float)term);
-        acc32 = true;
-      }
-      tw = tw + w;
-    }
-    double ov = 0.0;
-    if (nlev == nseg) {
-      if (acc32) {
-        const float o = (float)tws / (float)tw;
-        ov = o < 1.0f ? (double)o : 1.0;
-      } else {
-        ov = tw > 0.0 ? tws / tw : 0.0;
-        ov = ov < 1.0 ? ov : 1.0;
-      }
-      ov = ov > 0.0 ? ov : 0.0;
-    }
-    if (a.det && j == 0) a.ws_rec[e0 * W] = ov;
-    const double v = a.mode == 0 ? v0 : ov;
-    const bool pass = a.mode == 0 ? typed_pass(v, t0, a.thr, a.thr_mode)
-                                  : (a.thr_mode == 0 || (a.thr_mode == 1 ? v >= a.thr : v > a.thr));
-    if (pass) {
-      e = v;
-      id = c + a.id_base;
-    }
-  }
+  double e;
+  int64_t id;
+  rank_score(a, rq, rg, c, j, a.ws_rec + e0 * (1 + a.cs.nseg), e, id);
   if (j == 0) {
     a.ws_sc[e0] = e;
     a.ws_id[e0] = id;
   }
+}
+
+// the count and the completeness proof of query q's re-ranked list (refine_big_body): n valid entries, kth
+// the k-th exact score (-inf when n < k); the last list slot's approximate score + eps must stay below it
+__device__ __forceinline__ void rank_resolve(const RankArgs& a, const double* __restrict__ cs, double eps, int q,
+                                             int n, bool k32, int thr_mode, double kth, int cnt, int* ocnt,
+                                             int* ores, int count_empty, int* oredo) {
+  const int64_t base = (int64_t)q * a.kp;
+  const int kp = a.kp, k = a.k;
+  ocnt[q] = cnt;
+  const bool full = a.cid[base + kp - 1] >= 0;
+  // an empty last slot with score +inf: the scan's list may be incomplete (k_pool_select)
+  const bool trunc = !full && cs[base + kp - 1] == __builtin_huge_val();
+  int res = trunc ? 0 : 1;
+  if (full) {
+    const double bound = cs[base + kp - 1] + eps;
+    if (n >= k) res = k32 ? (float)bound < (float)kth : bound < kth;
+    else if (thr_mode == 0) res = 0;
+    else res = thr_mode == 1 ? (bound < thr_low(a.thr)) : (bound <= thr_low(a.thr));
+  }
+  ores[q] = res;
+  if (oredo && (res == 0 || (count_empty && cnt == 0))) atomicAdd(oredo, 1);
 }
 
 // Ranking pass (one 256-thread workgroup per query): the list's exact scores from the workspace, the
@@ -4269,22 +4409,86 @@ __global__ __launch_bounds__(256) void k_rank_sort(RankArgs a, const double* __r
           if (t0 + 256 * u < tot) odet[(int64_t)q * tot + t0 + 256 * u] = v[u];
       }
     }
-    if (tid == 0) {
-      const double kth = n >= k ? se[k - 1] : -__builtin_huge_val();
-      ocnt[q] = cnt;
-      const bool full = a.cid[base + kp - 1] >= 0;
-      // an empty last slot with score +inf: the scan's list may be incomplete (k_pool_select)
-      const bool trunc = !full && cs[base + kp - 1] == __builtin_huge_val();
-      int res = trunc ? 0 : 1;
-      if (full) {
-        const double bound = cs[base + kp - 1] + eps;
-        if (n >= k) res = k32 ? (float)bound < (float)kth : bound < kth;
-        else if (thr_mode == 0) res = 0;
-        else res = thr_mode == 1 ? (bound < thr_low(a.thr)) : (bound <= thr_low(a.thr));
+    if (tid == 0)
+      rank_resolve(a, cs, eps, q, n, k32, thr_mode, n >= k ? se[k - 1] : -__builtin_huge_val(), cnt, ocnt, ores,
+                   count_empty, oredo);
+    __syncthreads();
+  }
+}
+
+// Short lists (kp <= 64, the M = 20 headline's 28 entries): k_rank_pairs and k_rank_sort in one kernel, one
+// workgroup of NG 8-lane groups per query (NG >= kp): the entries' scores, ids and records stay in LDS, the
+// (score desc, id asc) order is a rank count (each entry compares itself with the others), the outputs and
+// the proof as k_rank_sort.  Replaces k_refine_lds (one thread per entry walking its row: 20.6 us per
+// 1000-query batch).
+template <int PPL, int NG>
+__global__ __launch_bounds__(8 * NG) __attribute__((amdgpu_waves_per_eu(4))) void k_rank_small(RankArgs a, const double* __restrict__ cs, double eps,
+                                                        double* __restrict__ os, int64_t* __restrict__ oid,
+                                                        int* __restrict__ ocnt, int* __restrict__ ores,
+                                                        int count_empty, int* __restrict__ oredo,
+                                                        double* __restrict__ odet, int* __restrict__ onext) {
+  if (onext && blockIdx.x == 0 && threadIdx.x == 0) *onext = 0;  // the next batch's redo counter
+  extern __shared__ __attribute__((aligned(16))) double cm[];
+  constexpr int NT = 8 * NG;
+  const int tid = threadIdx.x, g = tid >> 3, j = tid & 7;
+  const int kp = a.kp, k = a.k, W = 1 + a.cs.nseg;
+  const bool k32 = (a.thr_mode & kThrKey32) != 0;
+  const int thr_mode = a.thr_mode & (kThrKey32 - 1);
+  const int QW = coop_qw(a.cs), RW = coop_rw(a.cs);
+  double* rq = cm;
+  double* rg = cm + QW + g * RW;
+  double* se = cm + QW + NG * RW;  // [NG] scores, [NG] ids, [NG x W] records, [NG] positions by rank
+  int64_t* sid = reinterpret_cast<int64_t*>(se + NG);
+  double* srec = se + 2 * NG;
+  int* pos = reinterpret_cast<int*>(srec + NG * W);
+  __shared__ int red[NG / 8];
+  for (int q = blockIdx.x; q < a.Q; q += gridDim.x) {
+    const int64_t c = rank_stage<PPL>(a, rq, rg, q, g, tid, NT, j);
+    __syncthreads();
+    if (g < kp) {
+      double e;
+      int64_t id;
+      rank_score(a, rq, rg, c, j, srec + g * W, e, id);
+      if (j == 0) {
+        se[g] = e;
+        sid[g] = id;
       }
-      ores[q] = res;
-      if (oredo && (res == 0 || (count_empty && cnt == 0))) atomicAdd(oredo, 1);
     }
+    __syncthreads();
+    // rank of entry t: the entries before it in (valid first, key desc, id asc, position asc) order
+    int nv = 0;
+    if (tid < kp) {
+      const int64_t it = sid[tid];
+      const double kt = key_of(se[tid], k32);
+      int r = 0;
+      for (int u = 0; u < kp; ++u) {
+        const int64_t iu = sid[u];
+        const double ku = key_of(se[u], k32);
+        const bool before = it < 0 ? (iu >= 0 || u < tid) : (iu >= 0 && (ku > kt || (ku == kt && iu < it)));
+        r += before ? 1 : 0;
+      }
+      pos[r] = tid;
+      nv = it >= 0 ? 1 : 0;
+    }
+    nv = wsum64i(nv);
+    if ((tid & 63) == 0) red[tid >> 6] = nv;
+    __syncthreads();
+    int n = 0;
+#pragma unroll
+    for (int w = 0; w < NG / 8; ++w) n += red[w];
+    const int cnt = n < k ? n : k;
+    for (int r = tid; r < k; r += NT) {
+      os[(int64_t)q * k + r] = r < cnt ? se[pos[r]] : -__builtin_huge_val();
+      oid[(int64_t)q * k + r] = r < cnt ? sid[pos[r]] : -1;
+    }
+    if (odet)
+      for (int t = tid; t < k * W; t += NT) {
+        const int r = t / W, w = t - r * W;
+        odet[(int64_t)q * k * W + t] = r < cnt ? srec[pos[r] * W + w] : 0.0;
+      }
+    if (tid == 0)
+      rank_resolve(a, cs, eps, q, n, k32, thr_mode, n >= k ? se[pos[k - 1]] : -__builtin_huge_val(), cnt, ocnt,
+                   ores, count_empty, oredo);
     __syncthreads();
   }
 }
@@ -5036,6 +5240,46 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
   // the kernel clears next_redo for the next batch; otherwise one 4-byte memset here
   if (out_redo && !next_redo) HQ_CHECK_HIP(hipMemsetAsync(out_redo, 0, sizeof(int), s));
   const bool sm = seg_small(si);
+  auto rank_args = [&]() {
+    RankArgs ra;
+    ra.Rq = Rq; ra.Zq = Zq; ra.Sq = Sq; ra.Q = Q; ra.Rc = Rc; ra.Sc = Sc; ra.N = N;
+    ra.cs.nseg = si.nseg; ra.cs.L = si.L; ra.cs.Lp = si.Lp;
+    for (int i = 0; i < kCoopMaxW - 1; ++i) {
+      ra.cs.src[i] = i < si.nseg ? si.src[i] : 0;
+      ra.cs.len[i] = i < si.nseg ? si.len[i] : 0;
+      ra.cs.poff[i] = i < si.nseg ? si.poff[i] : 0;
+    }
+    ra.mode = mode; ra.kp = kp; ra.k = k; ra.thr_mode = thr_mode; ra.det = out_det ? 1 : 0; ra.thr = threshold;
+    ra.id_base = id_base; ra.cid = cand_id;
+    ra.ws_sc = nullptr; ra.ws_id = nullptr; ra.ws_rec = nullptr;
+    return ra;
+  };
+  // short lists: the fused lane-cooperative re-rank (k_rank_small) where its shapes hold; option
+  // refine_small = 0 keeps k_refine_lds below (A/B, parity)
+  if (kp <= kMaxTopK && coop_ppl(si) && opt(OPT_REFINE_SMALL, 1) != 0) {
+    const RankArgs ra = rank_args();
+    const int ng = kp <= 32 ? 32 : 64, W = 1 + si.nseg;
+    const size_t lds = 8 * ((size_t)coop_qw(ra.cs) + (size_t)ng * coop_rw(ra.cs) + (size_t)ng * (2 + W)) + 4 * (size_t)ng;
+    const int ppl = coop_ppl(si);
+    const void* fn = ng == 32 ? (ppl == 6 ? (const void*)k_rank_small<6, 32> : (const void*)k_rank_small<10, 32>)
+                              : (ppl == 6 ? (const void*)k_rank_small<6, 64> : (const void*)k_rank_small<10, 64>);
+    if (lds > 65536) HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int c = count_empty ? 1 : 0;
+    if (ng == 32 && ppl == 6)
+      hipLaunchKernelGGL((k_rank_small<6, 32>), dim3(grid), dim3(256), lds, s, ra, cand_score, eps, out_score, out_id,
+                         out_count, out_resolved, c, out_redo, out_det, next_redo);
+    else if (ng == 32)
+      hipLaunchKernelGGL((k_rank_small<10, 32>), dim3(grid), dim3(256), lds, s, ra, cand_score, eps, out_score, out_id,
+                         out_count, out_resolved, c, out_redo, out_det, next_redo);
+    else if (ppl == 6)
+      hipLaunchKernelGGL((k_rank_small<6, 64>), dim3(grid), dim3(512), lds, s, ra, cand_score, eps, out_score, out_id,
+                         out_count, out_resolved, c, out_redo, out_det, next_redo);
+    else
+      hipLaunchKernelGGL((k_rank_small<10, 64>), dim3(grid), dim3(512), lds, s, ra, cand_score, eps, out_score, out_id,
+                         out_count, out_resolved, c, out_redo, out_det, next_redo);
+    HQ_CHECK_LAUNCH();
+    return HQ_OK;
+  }
   if (kp > kMaxTopK) {  // long lists: rows read from global memory, one workgroup per query
     // with a workspace (hq_refine_topk_ws): the lane-cooperative pair scoring (k_rank_pairs: 8 lanes per
     // entry, rows staged per group, every level in one pass) + the per-query ranking (k_rank_sort) where
@@ -5043,16 +5287,7 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
     const int ppl = coop_ppl(si);
     if (workspace && ppl && opt(OPT_REFINE_COOP, 1) != 0 && Q <= 65535) {
       if (workspace_bytes < refine_ws_bytes(Q, kp, L)) return fail(HQ_E_INVALID, "workspace too small");
-      RankArgs ra;
-      ra.Rq = Rq; ra.Zq = Zq; ra.Sq = Sq; ra.Q = Q; ra.Rc = Rc; ra.Sc = Sc; ra.N = N;
-      ra.cs.nseg = si.nseg; ra.cs.L = si.L; ra.cs.Lp = si.Lp;
-      for (int i = 0; i < kCoopMaxW - 1; ++i) {
-        ra.cs.src[i] = i < si.nseg ? si.src[i] : 0;
-        ra.cs.len[i] = i < si.nseg ? si.len[i] : 0;
-        ra.cs.poff[i] = i < si.nseg ? si.poff[i] : 0;
-      }
-      ra.mode = mode; ra.kp = kp; ra.k = k; ra.thr_mode = thr_mode; ra.det = out_det ? 1 : 0; ra.thr = threshold;
-      ra.id_base = id_base; ra.cid = cand_id;
+      RankArgs ra = rank_args();
       uint8_t* w = reinterpret_cast<uint8_t*>(workspace);
       ra.ws_sc = reinterpret_cast<double*>(w);
       ra.ws_id = reinterpret_cast<int64_t*>(w + (size_t)Q * kp * 8);

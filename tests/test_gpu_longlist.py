@@ -254,6 +254,37 @@ def test_cooperative_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind)
         assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (kind, L, a)
 
 
+@pytest.mark.parametrize("kind", ["f64", "f32", "mixed"])
+@pytest.mark.parametrize("L", [32, 64, 128])
+def test_short_list_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind):
+    """The fused short-list re-rank (k_rank_small: k_rank_pairs' lane groups and the ranking in one
+    workgroup per query, lists of <= 64 entries) is bit-identical to k_refine_lds (option refine_small = 0):
+    progressive M = 20 (28 entries: 32 groups) and M = 50 (58: 64 groups) with records, brute force top-10
+    (overall ranking), frame scan (strict level-0); float64, float32 and mixed pools, ties included."""
+    from hq_mi355x.core.search_engine import IndexCorpus
+    C = _corpus(3000 if L == 128 else 20000, L, 51 + L)
+    rng = np.random.default_rng(52)
+    Q = np.concatenate([C[[1, 2, 20, 40]] + 0.0, C[100:108] + rng.normal(0, 0.01, (8, L)),
+                        rng.standard_normal((2, L))])
+    if kind == "f32":
+        C, Q = C.astype(np.float32), Q.astype(np.float32)
+    corpus = IndexCorpus(C, row_f32=(np.arange(len(C)) % 3 == 0) if kind == "mixed" else None)
+
+    def run():
+        out = [_np(x) for x in corpus.progressive(Q, 10, 0.1, 20)]
+        out += [_np(x) for x in corpus.progressive(Q, 40, 0.1, 50)]
+        out += [_np(x) for x in corpus.brute_force(Q, 10)]
+        out += [_np(x) for x in corpus.frame_search(Q, 30, 0.1)]
+        return out
+
+    got = run()
+    hq_option("refine_small", 0)
+    want = run()
+    hq_option("refine_small", None)
+    for a, (x, y) in enumerate(zip(got, want)):
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (kind, L, a)
+
+
 @pytest.mark.parametrize("k", [65, 300, 1000])
 def test_sort_select_equals_reference_order(hq_lib, hq_option, k):
     """The sort-based dense select for long lists (k_select_sort: LDS bitonic parts + merge stages) returns

@@ -69,3 +69,30 @@ def test_sort_keys_f64_pool_unchanged(hq_lib, golden):
     q = g["ov_PF_q"].astype(np.float64)
     corpus = IndexCorpus(C)
     assert not corpus.key32(corpus.prepare_queries(q[None]))
+
+
+@pytest.mark.parametrize("M", [20, 100])
+@pytest.mark.parametrize("tag", ["lv0_PF", "lv0_FP"])
+def test_sort_keys_scan_path_equals_dense(hq_lib, golden, tag, M):
+    """The crafted float32(0.1) level-0 tie on the scan path: the golden pool padded with 150 rows that fail
+    level 0 (anti-correlated copies of the query) so the scan and the lane-cooperative re-rank run (M = 20:
+    the short-list kernel, M = 100: the long-list kernels); the tie row passes (`>=` in float32) and every
+    output equals the dense exact path's, which test_dense_select_sort_keys_golden pins to the reference."""
+    import torch
+    from hq_mi355x.core.search_engine import IndexCorpus
+    g = golden("sortkey")
+    q, C = g[f"{tag}_q"], g[f"{tag}_C"]
+    rng = np.random.default_rng(61)
+    pad = (-q[None] + rng.normal(0, 0.01, (150, q.size))).astype(np.float32)
+    corpus = IndexCorpus(np.concatenate([C, pad]))
+    Q = np.repeat(q[None], 3, 0)
+    got = [_np(x) for x in corpus.progressive(Q, 10, 0.1, M)]
+    qp = corpus.prepare_queries(Q)
+    assert corpus.key32(qp)
+    s0, ids, best, bid = corpus._dense(qp, torch.arange(3, device=qp.Z.device), 0, M, 0.1, 1)
+    oid, odet, ocnt = corpus._final(qp, s0, ids, best, bid, 10)
+    want = [_np(x) for x in (oid, odet[..., 0], odet[..., 1:], ocnt)]
+    for x, y in zip(got, want):
+        np.testing.assert_array_equal(x, y)
+    # the reference's survivors at M = 7 (the tie row among them) are all among the longer lists' results
+    assert set(g[f"{tag}_pg_ids"].tolist()) <= set(got[0][0][: got[3][0]].tolist())

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The level-0 scan on the bench corpus (cfg3 shape: 1M x 64 level-0 values, 1000 queries), three
 calls, for PMC passes (tools/pmc_kernel.sh).  Argument: level0 (default, the progressive search's scan)
-or overall (the brute-force overall scan), m100 / m1000 (whole progressive searches at M = 100 / 1000), scanNNN (the scan alone, list length NNN)."""
+or overall (the brute-force overall scan), m20 / m100 / m1000 (whole progressive searches at M = 20 / 100 / 1000), scanNNN (the scan alone, list length NNN)."""
 import os
 import sys
 
@@ -28,7 +28,7 @@ mode = sys.argv[1] if len(sys.argv) > 1 else "level0"
 for _ in range(3):
     if mode == "overall":
         K.scan_topk(qp, corpus.prep, 1, 18, -2e-5, 0)
-    elif mode in ("m100", "m1000"):
+    elif mode in ("m20", "m100", "m1000"):
         corpus.progressive(C[:1000] + 0.01 * torch.randn((1000, 64), generator=gq, device=dev, dtype=torch.float64),
                            10, 0.1, int(mode[1:]))
     elif mode.startswith("scan"):  # scanNNN: the level-0 scan alone at list length NNN
