@@ -3705,8 +3705,8 @@ __device__ __forceinline__ uint64_t pool_key(float s, int row) {
 // pools by a 64-step bisection in memory.
 // CAP: pool keys held in LDS, KC: list entries (K <= KC); <1024, 128> for M = 100 (10 KB of LDS: every
 // workgroup of a 1000-query batch resident at once), <kSortCap, kMaxTopKBig> (41 KB) above
-template <int CAP, int KC>
-__global__ __launch_bounds__(256) void k_pool_sort(float* pool_s, int* pool_i, int* pool_n, int cap, int Q, int K,
+template <int CAP, int KC, int NT = 256>
+__global__ __launch_bounds__(NT) void k_pool_sort(float* pool_s, int* pool_i, int* pool_n, int cap, int Q, int K,
                                                    int64_t id_base, double* __restrict__ out_score,
                                                    int64_t* __restrict__ out_id, const double* __restrict__ th0,
                                                    double thr0, const float* __restrict__ qflag, int qstride,
@@ -3724,13 +3724,13 @@ __global__ __launch_bounds__(256) void k_pool_sort(float* pool_s, int* pool_i, i
       const int n = *fcount;
       if (n > 0 && __float_as_int(qc[q].flag) == 0) {
         const QConst c = qc[q];
-        for (int i = tid; i < n; i += 256) flagged_pair(fa, c, q, flist[i]);
+        for (int i = tid; i < n; i += NT) flagged_pair(fa, c, q, flist[i]);
       }
       __syncthreads();
     }
     const int pn = fcount ? __hip_atomic_load(pool_n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : pool_n[q];
     if (qflag && (__float_as_int(qflag[(int64_t)q * qstride]) != 0 || pn > cap)) {
-      for (int x = tid; x < K; x += 256) {
+      for (int x = tid; x < K; x += NT) {
         out_score[(int64_t)q * K + x] = __builtin_huge_val();
         out_id[(int64_t)q * K + x] = -1;
       }
@@ -3742,17 +3742,17 @@ __global__ __launch_bounds__(256) void k_pool_sort(float* pool_s, int* pool_i, i
     const int k = T < K ? T : K;
     const bool in_lds = T <= lds_cap && T <= CAP;
     if (T <= K) {
-      for (int x = tid; x < T; x += 256) sel[x] = pool_key(ps[x], pi[x]);
+      for (int x = tid; x < T; x += NT) sel[x] = pool_key(ps[x], pi[x]);
     } else {
       if (in_lds)
-        for (int x = tid; x < T; x += 256) key[x] = pool_key(ps[x], pi[x]);
+        for (int x = tid; x < T; x += NT) key[x] = pool_key(ps[x], pi[x]);
       auto get = [&](int x) -> uint64_t { return in_lds ? key[x] : pool_key(ps[x], pi[x]); };
       uint64_t prefix = 0ull, mask = 0ull;
       int need = K;  // keys still to take among those matching prefix on mask
       for (int shift = 56; shift >= 0; shift -= 8) {
-        hist[tid] = 0;
+        if (tid < 256) hist[tid] = 0;
         __syncthreads();
-        for (int x = tid; x < T; x += 256) {
+        for (int x = tid; x < T; x += NT) {
           const uint64_t kk = get(x);
           if ((kk & mask) == prefix) atomicAdd(&hist[(int)(kk >> shift) & 255], 1);
         }
@@ -3783,18 +3783,18 @@ __global__ __launch_bounds__(256) void k_pool_sort(float* pool_s, int* pool_i, i
       // exactly K keys: those whose digits so far are <= the prefix's (keys are unique)
       if (tid == 0) nsel = 0;
       __syncthreads();
-      for (int x = tid; x < T; x += 256) {
+      for (int x = tid; x < T; x += NT) {
         const uint64_t kk = get(x);
         if ((kk & mask) <= prefix) sel[atomicAdd(&nsel, 1)] = kk;
       }
     }
     const int n2 = pow2_at_least(k);
-    for (int x = k + tid; x < n2; x += 256) sel[x] = ~0ull;
+    for (int x = k + tid; x < n2; x += NT) sel[x] = ~0ull;
     __syncthreads();
     lds_bitonic(n2, [&](int a, int b) { return sel[a] < sel[b]; },
                 [&](int a, int b) { const uint64_t t = sel[a]; sel[a] = sel[b]; sel[b] = t; });
     const bool trunc = th0 != nullptr && th0[q] > thr0;
-    for (int x = tid; x < K; x += 256) {
+    for (int x = tid; x < K; x += NT) {
       if (x < k) {
         const uint64_t kk = sel[x];
         out_score[(int64_t)q * K + x] = (double)__uint_as_float(0x7FFFFFFFu - (uint32_t)(kk >> 32));
@@ -3822,7 +3822,7 @@ static void launch_pool_select(int K, hipStream_t s, int Q, float* pool_s, int* 
                        out_score, out_id, th0, thr0, qflag, qstride, fa, flist, fcount,
                        opt(OPT_POOL_SORT_MEM, 0) ? 0 : 1024);  // option pool_sort_mem: test the memory form
   else
-    hipLaunchKernelGGL((k_pool_sort<kSortCap, kMaxTopKBig>), dim3(mg), dim3(256), 0, s, pool_s, pool_i, pool_n, cap, Q,
+    hipLaunchKernelGGL((k_pool_sort<kSortCap, kMaxTopKBig, 512>), dim3(mg), dim3(512), 0, s, pool_s, pool_i, pool_n, cap, Q,
                        K, id_base, out_score, out_id, th0, thr0, qflag, qstride, fa, flist, fcount,
                        opt(OPT_POOL_SORT_MEM, 0) ? 0 : kSortCap);
 }
@@ -4342,7 +4342,8 @@ __device__ __forceinline__ void rank_resolve(const RankArgs& a, const double* __
 // Ranking pass (one 256-thread workgroup per query): the list's exact scores from the workspace, the
 // (score desc, id asc) bitonic sort in LDS, the outputs (records gathered by list position), the count
 // and the completeness proof as refine_big_body.
-__global__ __launch_bounds__(256) void k_rank_sort(RankArgs a, const double* __restrict__ cs, double eps,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __restrict__ cs, double eps,
                                                    double* __restrict__ os, int64_t* __restrict__ oid,
                                                    int* __restrict__ ocnt, int* __restrict__ ores, int count_empty,
                                                    int* __restrict__ oredo, double* __restrict__ odet,
@@ -4351,7 +4352,7 @@ __global__ __launch_bounds__(256) void k_rank_sort(RankArgs a, const double* __r
   __shared__ double se[kMaxTopKBig];
   __shared__ int64_t sid[kMaxTopKBig];
   __shared__ int pos[kMaxTopKBig];
-  __shared__ int red[4];
+  __shared__ int red[NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kp = a.kp, k = a.k, W = 1 + a.cs.nseg;
   const int n2 = pow2_at_least(kp);
@@ -4360,7 +4361,7 @@ __global__ __launch_bounds__(256) void k_rank_sort(RankArgs a, const double* __r
   for (int q = blockIdx.x; q < a.Q; q += gridDim.x) {
     const int64_t base = (int64_t)q * kp;
     int nv = 0;
-    for (int x = tid; x < n2; x += 256) {
+    for (int x = tid; x < n2; x += NT) {
       const int64_t i = x < kp ? a.ws_id[base + x] : -1;
       se[x] = x < kp ? a.ws_sc[base + x] : -__builtin_huge_val();
       sid[x] = i;
@@ -4370,7 +4371,9 @@ __global__ __launch_bounds__(256) void k_rank_sort(RankArgs a, const double* __r
     nv = wsum64i(nv);
     if (lane == 0) red[wave] = nv;
     __syncthreads();
-    const int n = red[0] + red[1] + red[2] + red[3];
+    int n = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) n += red[w];
     lds_bitonic(n2,
                 [&](int x, int y) {
                   const int64_t ix = sid[x], iy = sid[y];
@@ -4390,23 +4393,23 @@ __global__ __launch_bounds__(256) void k_rank_sort(RankArgs a, const double* __r
                   pos[y] = tp;
                 });
     const int cnt = n < k ? n : k;
-    for (int r = tid; r < k; r += 256) {
+    for (int r = tid; r < k; r += NT) {
       os[(int64_t)q * k + r] = r < cnt ? se[r] : -__builtin_huge_val();
       oid[(int64_t)q * k + r] = r < cnt ? sid[r] : -1;
     }
     if (odet) {  // records gathered by list position, four loads in flight per thread before the stores
       const double* __restrict__ rec = a.ws_rec;
       const int tot = k * W;
-      for (int t0 = tid; t0 < tot; t0 += 4 * 256) {
+      for (int t0 = tid; t0 < tot; t0 += 4 * NT) {
         double v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int t = t0 + 256 * u, r = t / W, w = t - r * W;
+          const int t = t0 + NT * u, r = t / W, w = t - r * W;
           v[u] = t < tot && r < cnt ? rec[(base + pos[r]) * W + w] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if (t0 + 256 * u < tot) odet[(int64_t)q * tot + t0 + 256 * u] = v[u];
+          if (t0 + NT * u < tot) odet[(int64_t)q * tot + t0 + NT * u] = v[u];
       }
     }
     if (tid == 0)
@@ -5297,8 +5300,12 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
       if (ppl == 6) hipLaunchKernelGGL(k_rank_pairs<6>, g1, dim3(256), lds, s, ra);
       else hipLaunchKernelGGL(k_rank_pairs<10>, g1, dim3(256), lds, s, ra);
       HQ_CHECK_LAUNCH();
-      hipLaunchKernelGGL(k_rank_sort, dim3(grid), dim3(256), 0, s, ra, cand_score, eps, out_score, out_id, out_count,
-                         out_resolved, count_empty ? 1 : 0, out_redo, out_det, next_redo);
+      if (kp > 512)  // 1024-entry sorts: one compare-exchange per thread and stage
+        hipLaunchKernelGGL(k_rank_sort<512>, dim3(grid), dim3(512), 0, s, ra, cand_score, eps, out_score, out_id,
+                           out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, next_redo);
+      else
+        hipLaunchKernelGGL(k_rank_sort<256>, dim3(grid), dim3(256), 0, s, ra, cand_score, eps, out_score, out_id,
+                           out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, next_redo);
       HQ_CHECK_LAUNCH();
       return HQ_OK;
     }
