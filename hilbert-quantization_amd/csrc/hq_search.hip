@@ -3959,6 +3959,7 @@ __global__ __launch_bounds__(256) void k_refine_big_raw(HQ_REFINE_ARGS, int tb) 
 // ------------------------------------------------------------------------------------------------
 // 1 / (level + 1) of the overall score's weights (search_engine.py:191-230), folded at compile time
 __device__ constexpr double kLevelWeight[8] = {1.0 / 1.0, 1.0 / 2.0, 1.0 / 3.0, 1.0 / 4.0, 1.0 / 5.0, 1.0 / 6.0, 1.0 / 7.0, 1.0 / 8.0};
+constexpr int kFinalRounds = 32;  // final rankings of <= 32 outputs may take arg-max rounds instead of a sort
 constexpr int kCoopGroups = 32;              // 8-lane groups per 256-thread workgroup
 constexpr int kCoopMaxW = 7;                 // record width 1 + nseg
 
@@ -4342,16 +4343,29 @@ __device__ __forceinline__ void rank_resolve(const RankArgs& a, const double* __
 // Ranking pass (one 256-thread workgroup per query): the list's exact scores from the workspace, the
 // (score desc, id asc) bitonic sort in LDS, the outputs (records gathered by list position), the count
 // and the completeness proof as refine_big_body.
+// The progressive search's final ranking fused into the re-rank's sort (one list per query, no arg-max
+// fallback: hq_refine_final_ws): the survivors r < count in level-0 order, ranked by (overall desc, r asc)
+// — k_progressive_final_big's order — K outputs with their records; the level-0 records are not written.
+struct FinalOut {
+  int K;
+  int64_t* id;
+  double* det;
+  int* count;
+};
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __restrict__ cs, double eps,
                                                    double* __restrict__ os, int64_t* __restrict__ oid,
                                                    int* __restrict__ ocnt, int* __restrict__ ores, int count_empty,
                                                    int* __restrict__ oredo, double* __restrict__ odet,
-                                                   int* __restrict__ onext) {
+                                                   int* __restrict__ onext, FinalOut fin) {
   if (onext && blockIdx.x == 0 && threadIdx.x == 0) *onext = 0;  // the next batch's redo counter
   __shared__ double se[kMaxTopKBig];
   __shared__ int64_t sid[kMaxTopKBig];
   __shared__ int pos[kMaxTopKBig];
+  __shared__ int fpos[kMaxTopKBig];
+  __shared__ double rv[2][NT / 64];
+  __shared__ int ri[2][NT / 64];
   __shared__ int red[NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kp = a.kp, k = a.k, W = 1 + a.cs.nseg;
@@ -4416,6 +4430,89 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
       rank_resolve(a, cs, eps, q, n, k32, thr_mode, n >= k ? se[k - 1] : -__builtin_huge_val(), cnt, ocnt, ores,
                    count_empty, oredo);
     __syncthreads();
+    if (fin.id) {
+      // survivors' overall keys in level-0 order (se is free: the proof has read se[k - 1])
+      const double* __restrict__ rec = a.ws_rec;
+      const int m2 = pow2_at_least(cnt > 2 ? cnt : 2);
+      for (int r = tid; r < m2; r += NT) {
+        se[r] = r < cnt ? key_of(rec[(base + pos[r]) * W], k32) : -__builtin_huge_val();
+        fpos[r] = r;
+      }
+      __syncthreads();
+      const int outn = cnt < fin.K ? cnt : fin.K;
+      int lg = 1;
+      while ((1 << lg) < cnt) ++lg;
+      auto first = [](double x, int ix, double y, int iy) { return ix >= 0 && (iy < 0 || x > y || (x == y && ix < iy)); };
+      if (fin.K <= kFinalRounds && 3 * outn < lg * (lg + 1) / 2) {
+        // outn rounds of the workgroup's first (overall desc, position asc) among the entries not yet taken
+        constexpr int E = kMaxTopKBig / NT;
+        double v[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = tid + NT * e < cnt ? se[tid + NT * e] : 0.0;
+        int taken = 0;
+        for (int r = 0; r < outn; ++r) {
+          double bv = 0.0;
+          int bi = -1;
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const int i = tid + NT * e;
+            if (i < cnt && !((taken >> e) & 1) && first(v[e], i, bv, bi)) {
+              bv = v[e];
+              bi = i;
+            }
+          }
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const double v2 = __shfl_xor(bv, o, 64);
+            const int i2 = __shfl_xor(bi, o, 64);
+            if (first(v2, i2, bv, bi)) {
+              bv = v2;
+              bi = i2;
+            }
+          }
+          if (lane == 0) {
+            rv[r & 1][wave] = bv;
+            ri[r & 1][wave] = bi;
+          }
+          __syncthreads();  // (the other buffer is rewritten only after the next round's barrier)
+          bv = rv[r & 1][0];
+          bi = ri[r & 1][0];
+#pragma unroll
+          for (int w = 1; w < NT / 64; ++w)
+            if (first(rv[r & 1][w], ri[r & 1][w], bv, bi)) {
+              bv = rv[r & 1][w];
+              bi = ri[r & 1][w];
+            }
+          if (bi >= 0 && bi % NT == tid) taken |= 1 << (bi / NT);
+          if (tid == 0) fpos[r] = bi;
+        }
+      } else {
+        lds_bitonic(m2, [&](int x, int y) { return se[x] > se[y] || (se[x] == se[y] && fpos[x] < fpos[y]); },
+                    [&](int x, int y) {
+                      const double t = se[x];
+                      se[x] = se[y];
+                      se[y] = t;
+                      const int tp = fpos[x];
+                      fpos[x] = fpos[y];
+                      fpos[y] = tp;
+                    });
+      }
+      __syncthreads();
+      for (int t = tid; t < fin.K * W; t += NT) {
+        const int r = t / W, w = t - r * W;
+        double val = 0.0;
+        if (r < outn) {
+          const int lr = fpos[r];
+          val = rec[(base + pos[lr]) * W + w];
+          if (w == 0) fin.id[(int64_t)q * fin.K + r] = sid[lr];
+        } else if (w == 0) {
+          fin.id[(int64_t)q * fin.K + r] = -1;
+        }
+        fin.det[(int64_t)q * fin.K * W + t] = val;
+      }
+      if (tid == 0) fin.count[q] = outn;
+      __syncthreads();
+    }
   }
 }
 
@@ -4517,8 +4614,6 @@ static size_t refine_ws_bytes(int Q, int kp, int L) {
 // workgroup arg-max over register-held overall scores (one barrier per round); larger K sorts them whole
 // (bitonic in LDS).  Round 4's form sorted all n (1024 keys at M = 1000, 55 bitonic stages) for K = 10 and
 // read the single list's validity from one wave.
-constexpr int kFinalRounds = 32;
-
 __global__ __launch_bounds__(256) void k_progressive_final_big(int R, int Q, int M, int W,
                                                                const double* __restrict__ s0,
                                                                const int64_t* __restrict__ ids,
@@ -5234,7 +5329,8 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
                          const int64_t* cand_id, int kp, int k, double threshold, int thr_mode, double eps,
                          int64_t id_base, double* out_score, int64_t* out_id, int* out_count, int* out_resolved,
                          int count_empty, int* out_redo, double* out_det, hq_stream_t stream,
-                         int* next_redo = nullptr, void* workspace = nullptr, size_t workspace_bytes = 0) {
+                         int* next_redo = nullptr, void* workspace = nullptr, size_t workspace_bytes = 0,
+                         const FinalOut* fin = nullptr) {
   SegInfo si;
   seg_info(L, si);
   const hipStream_t s = (hipStream_t)stream;
@@ -5302,10 +5398,12 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
       HQ_CHECK_LAUNCH();
       if (kp > 512)  // 1024-entry sorts: one compare-exchange per thread and stage
         hipLaunchKernelGGL(k_rank_sort<512>, dim3(grid), dim3(512), 0, s, ra, cand_score, eps, out_score, out_id,
-                           out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, next_redo);
+                           out_count, out_resolved, count_empty ? 1 : 0, out_redo, fin ? nullptr : out_det, next_redo,
+                           fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr});
       else
         hipLaunchKernelGGL(k_rank_sort<256>, dim3(grid), dim3(256), 0, s, ra, cand_score, eps, out_score, out_id,
-                           out_count, out_resolved, count_empty ? 1 : 0, out_redo, out_det, next_redo);
+                           out_count, out_resolved, count_empty ? 1 : 0, out_redo, fin ? nullptr : out_det, next_redo,
+                           fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr});
       HQ_CHECK_LAUNCH();
       return HQ_OK;
     }
@@ -6493,6 +6591,37 @@ int hq_refine_topk_ws(const double* Rq, const double* Zq, const double* Sq, int 
   return refine_launch(Rq, Zq, Sq, Q, Rc, Zc, Sc, N, L, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps,
                        id_base, out_score, out_id, out_count, out_resolved, count_empty, out_redo, out_det, stream,
                        next_redo, workspace, workspace_bytes);
+}
+
+int hq_refine_final_ws(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc, const double* Zc,
+                       const double* Sc, int64_t N, int L, const double* cand_score, const int64_t* cand_id, int kp,
+                       int k, double threshold, int thr_mode, double eps, int64_t id_base, double* out_score,
+                       int64_t* out_id, int* out_count, int* out_resolved, int* out_redo, int* next_redo, int K_out,
+                       int64_t* fin_id, double* fin_det, int* fin_count, void* workspace, size_t workspace_bytes,
+                       hq_stream_t stream) {
+  if (Q < 0 || N < 0 || L <= 0 || kp <= 0 || kp > kMaxTopKBig || k <= 0 || k > kp || K_out <= 0)
+    return fail(HQ_E_INVALID, "bad sizes kp=%d k=%d K=%d", kp, k, K_out);
+  SegInfo si;
+  seg_info(L, si);
+  // the fused form exists on the lane-cooperative long-list path only (the caller keeps the two-step form
+  // otherwise: hq_refine_topk_ws + hq_progressive_final_ex)
+  if (kp <= kMaxTopK || !coop_ppl(si) || opt(OPT_REFINE_COOP, 1) == 0 || Q > 65535)
+    return fail(HQ_E_UNSUPPORTED, "fused final ranking: kp=%d L=%d", kp, L);
+  if (Q == 0) {
+    if (next_redo) HQ_CHECK_HIP(hipMemsetAsync(next_redo, 0, sizeof(int), (hipStream_t)stream));
+    return HQ_OK;
+  }
+  if (!Rq || !Zq || !Sq || !cand_score || !cand_id || !out_score || !out_id || !out_count || !out_resolved ||
+      !fin_id || !fin_det || !fin_count || !workspace || (next_redo && (!out_redo || out_redo == next_redo)) ||
+      (N > 0 && (!Rc || !Zc || !Sc)))
+    return fail(HQ_E_INVALID, "null buffer");
+  if (workspace_bytes < hq_refine_workspace_size(Q, kp, L)) return fail(HQ_E_INVALID, "workspace too small");
+  const FinalOut fin{K_out, fin_id, fin_det, fin_count};
+  // records on (the final ranking reads them from the workspace), count_empty on (nothing passed: redo)
+  double* dummy_det = fin_det;
+  return refine_launch(Rq, Zq, Sq, Q, Rc, Zc, Sc, N, L, 0, cand_score, cand_id, kp, k, threshold, thr_mode, eps,
+                       id_base, out_score, out_id, out_count, out_resolved, 1, out_redo, dummy_det, stream, next_redo,
+                       workspace, workspace_bytes, &fin);
 }
 
 size_t hq_scan_workspace_size(int Q, int64_t N, int k) {

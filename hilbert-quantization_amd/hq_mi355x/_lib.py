@@ -79,6 +79,8 @@ SIGNATURES = {
     "hq_refine_workspace_size": (_sz, [_i, _i, _i]),
     "hq_refine_topk_ws": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _i, _p, _p, _i, _i, _d, _i, _d, _i64, _p, _p, _p,
                                _p, _i, _p, _p, _p, _p, _sz, _p]),
+    "hq_refine_final_ws": (_i, [_p, _p, _p, _i, _p, _p, _p, _i64, _i, _p, _p, _i, _i, _d, _i, _d, _i64, _p, _p, _p, _p,
+                                _p, _p, _i, _p, _p, _p, _p, _sz, _p]),
     "hq_scan_workspace_size": (_sz, [_i, _i64, _i]),
     "hq_seg_level0_len": (_i, [_i]),
     "hq_seg_pack0_split": (_i, [_p, _p, _i64, _i, _p, _p, _p]),

@@ -24,6 +24,7 @@ from .._compat import bases as _bases
 
 MAX_FUSED_K = 64     # list length of the f64 scans (hq_scan_topk)
 MAX_SPLIT_K = 1024   # list length of the split-f16 scans (k > 64: LDS-sorted pools, tiled re-rank)
+_FUSED_FINAL = True  # long lists: the final ranking inside the re-rank's sort (hq_refine_final_ws); False: A/B
 
 
 @dataclass
@@ -401,12 +402,7 @@ class IndexCorpus:
             oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
             return PendingSearch(done=(oid, odet[..., 0], odet[..., 1:], ocnt))
         nredo, nnext = self._redo_counter(qp.Z.device)
-        s0, ids, cnt, res, det = self._scan_refine(qp, 0, M, float(threshold), 1, nredo, det=True, next_redo=nnext,
-                                                   slack=self.slack_for(M))
-        # no arg-max on this path: a query where nothing passed (count 0) is recomputed by the dense path
-        # in progressive_finish, so the fallback slot is a constant (-inf, id -1, zero re-scores)
-        best, bid, bdet = self._no_fallback(Q, qp.Z.device)
-        oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out, bdet, det)
+        cnt, res, oid, odet, ocnt = self._scan_refine_final(qp, M, float(threshold), nredo, nnext, K_out)
         # queries forced onto the dense path (float32 outside the scans' model) join the redo count on the
         # device, so finishing still waits for one pinned value only
         forced = self._forced(qp)
@@ -516,6 +512,26 @@ class IndexCorpus:
                                          count_empty=True, next_redo=next_redo)
         return K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, tm, self.EPS, self.id_base, redo=nredo,
                              count_empty=True)
+
+    def _scan_refine_final(self, qp, M: int, thr: float, nredo, next_redo, K_out: int):
+        """The progressive search's first pass: level-0 scan, exact re-rank, overall re-score and final
+        ranking -> (count, resolved, out_id, out_det, out_count).  Long lists run the re-rank's sort and the
+        final ranking as one kernel (hq_refine_final_ws: the level-0 records stay in the workspace).  No
+        arg-max on this path: a query where nothing passed (count 0) is recomputed by the dense path in
+        progressive_finish, so the fallback slot is a constant (-inf, id -1, zero re-scores)."""
+        kp = M + self.slack_for(M)
+        asc, aid, _, _ = K.scan_topk(qp, self.prep, 0, kp, thr - self.EPS, 1, self.id_base)
+        tm = 1 | (K.THR_KEY32 if self.key32(qp) else 0)
+        if kp > 64 and _FUSED_FINAL:
+            r = K.refine_final_ws(qp, self.prep, asc, aid, M, thr, tm, self.EPS, self.id_base, K_out, redo=nredo,
+                                  next_redo=next_redo)
+            if r is not None:
+                return r
+        s0, ids, cnt, res, det = K.refine_rescore_topk(qp, self.prep, 0, asc, aid, M, thr, tm, self.EPS, self.id_base,
+                                                       redo=nredo, count_empty=True, next_redo=next_redo)
+        best, bid, bdet = self._no_fallback(qp.N, qp.Z.device)
+        oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out, bdet, det)
+        return cnt, res, oid, odet, ocnt
 
     def _final(self, qp, s0, ids, best, bid, K_out: int, bdet=None, det=None):
         """Exact overall + per-level re-score of the survivors and of the arg-max, then the final ranking."""

@@ -466,6 +466,34 @@ def _refine_ws(q, c, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps,
          exc)
 
 
+def refine_final_ws(q: Prepared, c: Prepared, cand_score, cand_id, k: int, threshold: float, thr_mode: int,
+                    eps: float, id_base: int, K_out: int, redo=None, next_redo=None, exc=None):
+    """The level-0 re-rank of a progressive search with its final ranking fused in (hq_refine_final_ws):
+    (count, resolved, out_id [Q, K_out], out_det [Q, K_out, 1 + nseg], out_count) as refine_rescore_topk +
+    progressive_final with one list and no arg-max fallback; None where the fused form does not exist (the
+    caller runs the two steps)."""
+    t = torch()
+    Q, kp = cand_id.shape
+    dev = cand_id.device
+    os_ = t.empty((Q, k), dtype=t.float64, device=dev)
+    oi = t.empty((Q, k), dtype=t.int64, device=dev)
+    cnt = t.empty(Q, dtype=t.int32, device=dev)
+    res = t.empty(Q, dtype=t.int32, device=dev)
+    fid = t.empty((Q, K_out), dtype=t.int64, device=dev)
+    fdet = t.empty((Q, K_out, 1 + q.nseg), dtype=t.float64, device=dev)
+    fcnt = t.empty(Q, dtype=t.int32, device=dev)
+    wb = int(_lib.load().hq_refine_workspace_size(Q, kp, c.L))
+    ws = _workspace(wb, dev)
+    rc = _L().hq_refine_final_ws(ptr(q.R), ptr(q.Z), ptr(q.S), Q, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L,
+                                 ptr(_contig(cand_score)), ptr(_contig(cand_id)), kp, k, float(threshold), thr_mode,
+                                 float(eps), int(id_base), ptr(os_), ptr(oi), ptr(cnt), ptr(res), ptr(redo),
+                                 ptr(next_redo), int(K_out), ptr(fid), ptr(fdet), ptr(fcnt), ptr(ws), wb, stream())
+    if rc == _lib.HQ_E_UNSUPPORTED:
+        return None
+    _chk(rc, exc)
+    return cnt, res, fid, fdet, fcnt
+
+
 def refine_rescore_topk(q: Prepared, c: Prepared, mode: int, cand_score, cand_id, k: int, threshold: float = 0.0,
                         thr_mode: int = 0, eps: float = 1e-9, id_base: int = 0, exc=None, redo=None,
                         count_empty: bool = False, next_redo=None):

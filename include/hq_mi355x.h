@@ -339,6 +339,21 @@ int hq_refine_topk_ws(const double* Rq, const double* Zq, const double* Sq, int 
                       double* out_score, int64_t* out_id, int* out_count, int* out_resolved,
                       int count_empty, int* out_redo, int* next_redo, double* out_det,
                       void* workspace, size_t workspace_bytes, hq_stream_t stream);
+/* The level-0 re-rank of one progressive search (mode 0, records on, count_empty on) with its final
+ * ranking fused in: the level-0 outputs and the proof as hq_refine_topk_ws (out_det not produced), and
+ * fin_id [Q, K_out], fin_det [Q, K_out, 1 + nseg], fin_count [Q] = hq_progressive_final_ex's outputs for
+ * R = 1 and no arg-max fallback (best id -1: a query where nothing passed gets count 0 and is counted in
+ * out_redo).  The final order is core/search_engine.py:387's stable sort by the overall score over the
+ * level-0 order (key32: thr_mode | HQ_THR_KEY32 ranks by float32-rounded keys).  Long lists on the
+ * lane-cooperative path only (kp > 64, the cooperative shapes, workspace required); HQ_E_UNSUPPORTED
+ * otherwise, and the caller keeps the two-step form. */
+int hq_refine_final_ws(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
+                       const double* Zc, const double* Sc, int64_t N, int L, const double* cand_score,
+                       const int64_t* cand_id, int kp, int k, double threshold, int thr_mode, double eps,
+                       int64_t id_base, double* out_score, int64_t* out_id, int* out_count,
+                       int* out_resolved, int* out_redo, int* next_redo, int K_out, int64_t* fin_id,
+                       double* fin_det, int* fin_count, void* workspace, size_t workspace_bytes,
+                       hq_stream_t stream);
 
 /* ---- S4 on candidate lists: EXACT overall + per-level scores of selected pairs ---------------
  * ids: int64 Q x k GLOBAL ids (row = id - id_base; out of range / < 0 -> zeros);

@@ -256,6 +256,37 @@ def test_cooperative_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind)
 
 @pytest.mark.parametrize("kind", ["f64", "f32", "mixed"])
 @pytest.mark.parametrize("L", [32, 64, 128])
+def test_fused_final_ranking_equals_two_steps(hq_lib, L, kind):
+    """Long lists: the final ranking fused into the re-rank's sort (hq_refine_final_ws) equals the two-step
+    form (hq_refine_topk_ws records + hq_progressive_final_ex) bit for bit — M = 100 and 1000, K = 10
+    (arg-max rounds), 40 and 150 (sort), ties (duplicate rows), float64 / float32 / mixed pools."""
+    from hq_mi355x.core import search_engine as SE
+    C = _corpus(3000 if L == 128 else 20000, L, 71 + L)
+    rng = np.random.default_rng(72)
+    Q = np.concatenate([C[[1, 2, 20, 40, 30]] + 0.0, C[100:108] + rng.normal(0, 0.01, (8, L)),
+                        rng.standard_normal((2, L))])
+    if kind == "f32":
+        C, Q = C.astype(np.float32), Q.astype(np.float32)
+    corpus = SE.IndexCorpus(C, row_f32=(np.arange(len(C)) % 3 == 0) if kind == "mixed" else None)
+
+    def run():
+        out = []
+        for M, K_out in ((100, 10), (100, 40), (1000, 10), (1000, 150)):
+            out += [_np(x) for x in corpus.progressive(Q, K_out, 0.1, M)]
+        return out
+
+    got = run()
+    SE._FUSED_FINAL = False
+    try:
+        want = run()
+    finally:
+        SE._FUSED_FINAL = True
+    for a, (x, y) in enumerate(zip(got, want)):
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (kind, L, a)
+
+
+@pytest.mark.parametrize("kind", ["f64", "f32", "mixed"])
+@pytest.mark.parametrize("L", [32, 64, 128])
 def test_short_list_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind):
     """The fused short-list re-rank (k_rank_small: k_rank_pairs' lane groups and the ranking in one
     workgroup per query, lists of <= 64 entries) is bit-identical to k_refine_lds (option refine_small = 0):
