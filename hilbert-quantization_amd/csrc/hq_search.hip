@@ -4353,6 +4353,7 @@ struct FinalOut {
   int* count;
 };
 
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __restrict__ cs, double eps,
                                                    double* __restrict__ os, int64_t* __restrict__ oid,
@@ -4526,7 +4527,8 @@ __global__ __launch_bounds__(8 * NG) __attribute__((amdgpu_waves_per_eu(4))) voi
                                                         double* __restrict__ os, int64_t* __restrict__ oid,
                                                         int* __restrict__ ocnt, int* __restrict__ ores,
                                                         int count_empty, int* __restrict__ oredo,
-                                                        double* __restrict__ odet, int* __restrict__ onext) {
+                                                        double* __restrict__ odet, int* __restrict__ onext,
+                                                        FinalOut fin) {
   if (onext && blockIdx.x == 0 && threadIdx.x == 0) *onext = 0;  // the next batch's redo counter
   extern __shared__ __attribute__((aligned(16))) double cm[];
   constexpr int NT = 8 * NG;
@@ -4541,6 +4543,7 @@ __global__ __launch_bounds__(8 * NG) __attribute__((amdgpu_waves_per_eu(4))) voi
   int64_t* sid = reinterpret_cast<int64_t*>(se + NG);
   double* srec = se + 2 * NG;
   int* pos = reinterpret_cast<int*>(srec + NG * W);
+  int* fpos = pos + NG;  // final ranking: survivor position by final rank
   __shared__ int red[NG / 8];
   for (int q = blockIdx.x; q < a.Q; q += gridDim.x) {
     const int64_t c = rank_stage<PPL>(a, rq, rg, q, g, tid, NT, j);
@@ -4589,6 +4592,33 @@ __global__ __launch_bounds__(8 * NG) __attribute__((amdgpu_waves_per_eu(4))) voi
     if (tid == 0)
       rank_resolve(a, cs, eps, q, n, k32, thr_mode, n >= k ? se[pos[k - 1]] : -__builtin_huge_val(), cnt, ocnt,
                    ores, count_empty, oredo);
+    if (fin.id) {
+      // fused final ranking (k_progressive_final's order: overall desc, level-0 position asc) by rank counting
+      const int outn = cnt < fin.K ? cnt : fin.K;
+      if (tid < cnt) {
+        const double ot = key_of(srec[pos[tid] * W], k32);
+        int r = 0;
+        for (int u = 0; u < cnt; ++u) {
+          const double ou = key_of(srec[pos[u] * W], k32);
+          r += (ou > ot || (ou == ot && u < tid)) ? 1 : 0;
+        }
+        if (r < fin.K) fpos[r] = tid;
+      }
+      __syncthreads();
+      for (int t = tid; t < fin.K * W; t += NT) {
+        const int r = t / W, w = t - r * W;
+        double val = 0.0;
+        if (r < outn) {
+          const int e = pos[fpos[r]];
+          val = srec[e * W + w];
+          if (w == 0) fin.id[(int64_t)q * fin.K + r] = sid[e];
+        } else if (w == 0) {
+          fin.id[(int64_t)q * fin.K + r] = -1;
+        }
+        fin.det[(int64_t)q * fin.K * W + t] = val;
+      }
+      if (tid == 0) fin.count[q] = outn;
+    }
     __syncthreads();
   }
 }
@@ -5358,7 +5388,9 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
   if (kp <= kMaxTopK && coop_ppl(si) && opt(OPT_REFINE_SMALL, 1) != 0) {
     const RankArgs ra = rank_args();
     const int ng = kp <= 32 ? 32 : 64, W = 1 + si.nseg;
-    const size_t lds = 8 * ((size_t)coop_qw(ra.cs) + (size_t)ng * coop_rw(ra.cs) + (size_t)ng * (2 + W)) + 4 * (size_t)ng;
+    const size_t lds = 8 * ((size_t)coop_qw(ra.cs) + (size_t)ng * coop_rw(ra.cs) + (size_t)ng * (2 + W)) + 8 * (size_t)ng;
+    const FinalOut fo = fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr};
+    double* odet_s = fin ? nullptr : out_det;
     const int ppl = coop_ppl(si);
     const void* fn = ng == 32 ? (ppl == 6 ? (const void*)k_rank_small<6, 32> : (const void*)k_rank_small<10, 32>)
                               : (ppl == 6 ? (const void*)k_rank_small<6, 64> : (const void*)k_rank_small<10, 64>);
@@ -5366,16 +5398,16 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
     const int c = count_empty ? 1 : 0;
     if (ng == 32 && ppl == 6)
       hipLaunchKernelGGL((k_rank_small<6, 32>), dim3(grid), dim3(256), lds, s, ra, cand_score, eps, out_score, out_id,
-                         out_count, out_resolved, c, out_redo, out_det, next_redo);
+                         out_count, out_resolved, c, out_redo, odet_s, next_redo, fo);
     else if (ng == 32)
       hipLaunchKernelGGL((k_rank_small<10, 32>), dim3(grid), dim3(256), lds, s, ra, cand_score, eps, out_score, out_id,
-                         out_count, out_resolved, c, out_redo, out_det, next_redo);
+                         out_count, out_resolved, c, out_redo, odet_s, next_redo, fo);
     else if (ppl == 6)
       hipLaunchKernelGGL((k_rank_small<6, 64>), dim3(grid), dim3(512), lds, s, ra, cand_score, eps, out_score, out_id,
-                         out_count, out_resolved, c, out_redo, out_det, next_redo);
+                         out_count, out_resolved, c, out_redo, odet_s, next_redo, fo);
     else
       hipLaunchKernelGGL((k_rank_small<10, 64>), dim3(grid), dim3(512), lds, s, ra, cand_score, eps, out_score, out_id,
-                         out_count, out_resolved, c, out_redo, out_det, next_redo);
+                         out_count, out_resolved, c, out_redo, odet_s, next_redo, fo);
     HQ_CHECK_LAUNCH();
     return HQ_OK;
   }
@@ -6603,19 +6635,20 @@ int hq_refine_final_ws(const double* Rq, const double* Zq, const double* Sq, int
     return fail(HQ_E_INVALID, "bad sizes kp=%d k=%d K=%d", kp, k, K_out);
   SegInfo si;
   seg_info(L, si);
-  // the fused form exists on the lane-cooperative long-list path only (the caller keeps the two-step form
-  // otherwise: hq_refine_topk_ws + hq_progressive_final_ex)
-  if (kp <= kMaxTopK || !coop_ppl(si) || opt(OPT_REFINE_COOP, 1) == 0 || Q > 65535)
-    return fail(HQ_E_UNSUPPORTED, "fused final ranking: kp=%d L=%d", kp, L);
+  // the fused form exists on the lane-cooperative paths only (k_rank_small for lists <= 64, k_rank_pairs +
+  // k_rank_sort above; the caller keeps the two-step form otherwise: hq_refine_topk_ws + hq_progressive_final_ex)
+  const bool small = kp <= kMaxTopK && coop_ppl(si) && opt(OPT_REFINE_SMALL, 1) != 0;
+  const bool big = kp > kMaxTopK && coop_ppl(si) && opt(OPT_REFINE_COOP, 1) != 0 && Q <= 65535;
+  if (!small && !big) return fail(HQ_E_UNSUPPORTED, "fused final ranking: kp=%d L=%d", kp, L);
   if (Q == 0) {
     if (next_redo) HQ_CHECK_HIP(hipMemsetAsync(next_redo, 0, sizeof(int), (hipStream_t)stream));
     return HQ_OK;
   }
   if (!Rq || !Zq || !Sq || !cand_score || !cand_id || !out_score || !out_id || !out_count || !out_resolved ||
-      !fin_id || !fin_det || !fin_count || !workspace || (next_redo && (!out_redo || out_redo == next_redo)) ||
+      !fin_id || !fin_det || !fin_count || (big && !workspace) || (next_redo && (!out_redo || out_redo == next_redo)) ||
       (N > 0 && (!Rc || !Zc || !Sc)))
     return fail(HQ_E_INVALID, "null buffer");
-  if (workspace_bytes < hq_refine_workspace_size(Q, kp, L)) return fail(HQ_E_INVALID, "workspace too small");
+  if (big && workspace_bytes < hq_refine_workspace_size(Q, kp, L)) return fail(HQ_E_INVALID, "workspace too small");
   const FinalOut fin{K_out, fin_id, fin_det, fin_count};
   // records on (the final ranking reads them from the workspace), count_empty on (nothing passed: redo)
   double* dummy_det = fin_det;

@@ -402,13 +402,15 @@ class IndexCorpus:
             oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
             return PendingSearch(done=(oid, odet[..., 0], odet[..., 1:], ocnt))
         nredo, nnext = self._redo_counter(qp.Z.device)
-        cnt, res, oid, odet, ocnt = self._scan_refine_final(qp, M, float(threshold), nredo, nnext, K_out)
         # queries forced onto the dense path (float32 outside the scans' model) join the redo count on the
         # device, so finishing still waits for one pinned value only
         forced = self._forced(qp)
+        cnt, res, oid, odet, ocnt = self._scan_refine_final(qp, M, float(threshold), nredo, nnext, K_out)
         if forced is not None:
             nredo.add_(forced.sum(dtype=t.int32).view(1))
-        # the shared device counter is overwritten by the next batch: this batch's value leaves now
+        # the shared device counter is overwritten by the next batch: this batch's value leaves now (a
+        # last-workgroup write of it to the pinned int from the re-rank kernel measured slower: 21 -> 43 us,
+        # every workgroup's release fence)
         host = self._pinned(nredo.dtype)
         host.copy_(nredo, non_blocking=True)
         ev = t.cuda.Event()
@@ -515,14 +517,15 @@ class IndexCorpus:
 
     def _scan_refine_final(self, qp, M: int, thr: float, nredo, next_redo, K_out: int):
         """The progressive search's first pass: level-0 scan, exact re-rank, overall re-score and final
-        ranking -> (count, resolved, out_id, out_det, out_count).  Long lists run the re-rank's sort and the
-        final ranking as one kernel (hq_refine_final_ws: the level-0 records stay in the workspace).  No
-        arg-max on this path: a query where nothing passed (count 0) is recomputed by the dense path in
+        ranking -> (count, resolved, out_id, out_det, out_count).  On the lane-cooperative paths the re-rank's
+        ranking and the final ranking are one kernel (hq_refine_final_ws: the level-0 records stay on the
+        device).  No arg-max
+        on this path: a query where nothing passed (count 0) is recomputed by the dense path in
         progressive_finish, so the fallback slot is a constant (-inf, id -1, zero re-scores)."""
         kp = M + self.slack_for(M)
         asc, aid, _, _ = K.scan_topk(qp, self.prep, 0, kp, thr - self.EPS, 1, self.id_base)
         tm = 1 | (K.THR_KEY32 if self.key32(qp) else 0)
-        if kp > 64 and _FUSED_FINAL:
+        if _FUSED_FINAL:
             r = K.refine_final_ws(qp, self.prep, asc, aid, M, thr, tm, self.EPS, self.id_base, K_out, redo=nredo,
                                   next_redo=next_redo)
             if r is not None:

@@ -487,7 +487,8 @@ def refine_final_ws(q: Prepared, c: Prepared, cand_score, cand_id, k: int, thres
     rc = _L().hq_refine_final_ws(ptr(q.R), ptr(q.Z), ptr(q.S), Q, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L,
                                  ptr(_contig(cand_score)), ptr(_contig(cand_id)), kp, k, float(threshold), thr_mode,
                                  float(eps), int(id_base), ptr(os_), ptr(oi), ptr(cnt), ptr(res), ptr(redo),
-                                 ptr(next_redo), int(K_out), ptr(fid), ptr(fdet), ptr(fcnt), ptr(ws), wb, stream())
+                                 ptr(next_redo), int(K_out), ptr(fid), ptr(fdet), ptr(fcnt), ptr(ws), wb,
+                                 stream())
     if rc == _lib.HQ_E_UNSUPPORTED:
         return None
     _chk(rc, exc)

@@ -344,9 +344,9 @@ int hq_refine_topk_ws(const double* Rq, const double* Zq, const double* Sq, int 
  * fin_id [Q, K_out], fin_det [Q, K_out, 1 + nseg], fin_count [Q] = hq_progressive_final_ex's outputs for
  * R = 1 and no arg-max fallback (best id -1: a query where nothing passed gets count 0 and is counted in
  * out_redo).  The final order is core/search_engine.py:387's stable sort by the overall score over the
- * level-0 order (key32: thr_mode | HQ_THR_KEY32 ranks by float32-rounded keys).  Long lists on the
- * lane-cooperative path only (kp > 64, the cooperative shapes, workspace required); HQ_E_UNSUPPORTED
- * otherwise, and the caller keeps the two-step form. */
+ * level-0 order (key32: thr_mode | HQ_THR_KEY32 ranks by float32-rounded keys).  On the lane-cooperative
+ * paths only (the cooperative shapes; kp > 64 needs the workspace); HQ_E_UNSUPPORTED otherwise, and the
+ * caller keeps the two-step form. */
 int hq_refine_final_ws(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
                        const double* Zc, const double* Sc, int64_t N, int L, const double* cand_score,
                        const int64_t* cand_id, int kp, int k, double threshold, int thr_mode, double eps,
