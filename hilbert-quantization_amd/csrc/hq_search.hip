@@ -1726,7 +1726,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const int n = __builtin_amdgcn_readlane(nl, ql);
     if (n == 0 || q0 + ql >= a.Q) continue;
     const int bq = __builtin_amdgcn_readlane(base, ql);
-    if (lane < n) {
+    if (lane < n && bq + lane < a.pool_cap) {  // (pools hold nchunks x k entries for k <= 64: never past)
       const int64_t o = (int64_t)(q0 + ql) * a.pool_cap + bq + lane;
       a.pool_s[o] = ls[ql * K + lane];
       a.pool_i[o] = li[ql * K + lane];

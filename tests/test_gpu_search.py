@@ -280,7 +280,10 @@ def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, hq_option):
         for thr, tm in ((0.1, 1), (0.6, 1), (0.1, 2)):
             sc, ids, cnt, _, _ = corpus.exact_topk(qp, 0, 20, thr, tm)
             res[(tag, thr, tm)] = (_np(sc), _np(ids), _np(cnt))
-    for key in ((0.1, 1), (0.6, 1), (0.1, 2)):
+        # M = 100 (a list of 108 > 64: every variant, scan_variant = 1 included, takes the queue scan)
+        sc, ids, cnt, _, _ = corpus.exact_topk(qp, 0, 100, 0.1, 1)
+        res[(tag, "m100", 1)] = (_np(sc), _np(ids), _np(cnt))
+    for key in ((0.1, 1), (0.6, 1), (0.1, 2), ("m100", 1)):
         for tag in list(variants)[1:]:
             a, b = res[("v0",) + key], res[(tag,) + key]
             assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]), (tag, key)
