@@ -51,7 +51,7 @@ enum Opt {
   OPT_SCAN_V1, OPT_SCAN_NOSAMPLE, OPT_SCAN_EXPT, OPT_SCAN_VARIANT, OPT_SCAN_WPB, OPT_SCAN_PF, OPT_SCAN_NB, OPT_OV_WAVES, OPT_OV_OCC,
   OPT_REFINE_GLOBAL, OPT_REFINE_EXPT, OPT_SEG_PREPARE_FLAT, OPT_SELECT_2STAGE, OPT_LEVEL_SCORES_V1, OPT_SCAN_SPLIT3, OPT_SCAN_OCC, OPT_SCANOV_SPLIT3, OPT_SAMPLE_HI,
   OPT_PRECOMP_WS, OPT_PRECOMP_LEAF_ROT, OPT_PRECOMP_ORDER, OPT_SCANOV_V1, OPT_OV_PF, OPT_PRECOMP_G2REG,
-  OPT_REFINE_COOP, OPT_PRECOMP_COMPACT, OPT_PREP_COOP, OPT_POOL_SORT_MEM, OPT_REFINE_SMALL,
+  OPT_REFINE_COOP, OPT_PRECOMP_COMPACT, OPT_PREP_COOP, OPT_POOL_SORT_MEM, OPT_REFINE_SMALL, OPT_FINAL_ROUNDS,
   OPT_COUNT
 };
 int64_t opt(Opt id, int64_t dflt);

@@ -4351,6 +4351,7 @@ struct FinalOut {
   int64_t* id;
   double* det;
   int* count;
+  int rounds;  // 1: K <= kFinalRounds outputs by arg-max rounds where cheaper than the sort (option final_rounds)
 };
 
 
@@ -4444,7 +4445,7 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
       int lg = 1;
       while ((1 << lg) < cnt) ++lg;
       auto first = [](double x, int ix, double y, int iy) { return ix >= 0 && (iy < 0 || x > y || (x == y && ix < iy)); };
-      if (fin.K <= kFinalRounds && 3 * outn < lg * (lg + 1) / 2) {
+      if (fin.rounds && fin.K <= kFinalRounds && 3 * outn < lg * (lg + 1) / 2) {
         // outn rounds of the workgroup's first (overall desc, position asc) among the entries not yet taken
         constexpr int E = kMaxTopKBig / NT;
         double v[E];
@@ -4706,7 +4707,7 @@ __global__ __launch_bounds__(256) void k_progressive_final_big(int R, int Q, int
     // rounds (a wave reduction each, ~3 bitonic stages of work) when cheaper than the whole sort
     int lg = 1;
     while ((1 << lg) < n) ++lg;
-    if (K <= kFinalRounds && 3 * outn < lg * (lg + 1) / 2) {
+    if (!(flags & 2) && K <= kFinalRounds && 3 * outn < lg * (lg + 1) / 2) {
       // K rounds of the workgroup's first (overall desc, position asc) among the entries not yet taken
       double v[4];
 #pragma unroll
@@ -5389,7 +5390,7 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
     const RankArgs ra = rank_args();
     const int ng = kp <= 32 ? 32 : 64, W = 1 + si.nseg;
     const size_t lds = 8 * ((size_t)coop_qw(ra.cs) + (size_t)ng * coop_rw(ra.cs) + (size_t)ng * (2 + W)) + 8 * (size_t)ng;
-    const FinalOut fo = fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr};
+    const FinalOut fo = fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr, 0};
     double* odet_s = fin ? nullptr : out_det;
     const int ppl = coop_ppl(si);
     const void* fn = ng == 32 ? (ppl == 6 ? (const void*)k_rank_small<6, 32> : (const void*)k_rank_small<10, 32>)
@@ -5431,11 +5432,11 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
       if (kp > 512)  // 1024-entry sorts: one compare-exchange per thread and stage
         hipLaunchKernelGGL(k_rank_sort<512>, dim3(grid), dim3(512), 0, s, ra, cand_score, eps, out_score, out_id,
                            out_count, out_resolved, count_empty ? 1 : 0, out_redo, fin ? nullptr : out_det, next_redo,
-                           fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr});
+                           fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr, 0});
       else
         hipLaunchKernelGGL(k_rank_sort<256>, dim3(grid), dim3(256), 0, s, ra, cand_score, eps, out_score, out_id,
                            out_count, out_resolved, count_empty ? 1 : 0, out_redo, fin ? nullptr : out_det, next_redo,
-                           fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr});
+                           fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr, 0});
       HQ_CHECK_LAUNCH();
       return HQ_OK;
     }
@@ -6649,7 +6650,7 @@ int hq_refine_final_ws(const double* Rq, const double* Zq, const double* Sq, int
       (N > 0 && (!Rc || !Zc || !Sc)))
     return fail(HQ_E_INVALID, "null buffer");
   if (big && workspace_bytes < hq_refine_workspace_size(Q, kp, L)) return fail(HQ_E_INVALID, "workspace too small");
-  const FinalOut fin{K_out, fin_id, fin_det, fin_count};
+  const FinalOut fin{K_out, fin_id, fin_det, fin_count, opt(OPT_FINAL_ROUNDS, 1) != 0 ? 1 : 0};
   // records on (the final ranking reads them from the workspace), count_empty on (nothing passed: redo)
   double* dummy_det = fin_det;
   return refine_launch(Rq, Zq, Sq, Q, Rc, Zc, Sc, N, L, 0, cand_score, cand_id, kp, k, threshold, thr_mode, eps,
@@ -6877,7 +6878,8 @@ int hq_progressive_final_ex(int R, int Q, int M, int nseg, const double* s0, con
                        best, best_id, best_det, K, out_id, out_det, out_count, flags);
   else
     hipLaunchKernelGGL(k_progressive_final_big, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, Q, M, W, s0, ids,
-                       det, best, best_id, best_det, K, out_id, out_det, out_count, flags);
+                       det, best, best_id, best_det, K, out_id, out_det, out_count,
+                       (flags & 1) | (opt(OPT_FINAL_ROUNDS, 1) != 0 ? 0 : 2));  // option final_rounds = 0: sort only
   HQ_CHECK_LAUNCH();
   return HQ_OK;
 }
