@@ -579,8 +579,9 @@ def bench_search_strong(args, world, rank, dev):
 def progressive_rate(engine, Q, M, steps, world, k=10, threshold=0.1):
     """Pipelined progressive search of one query batch per step (two batches in flight, as the cfg3 leg),
     with the engine's redo counters (IndexCorpus.stats) over the timed batches: queries re-scanned with a
-    longer list after a near-tie / short list, queries left for the dense exact path, and the host wall time
-    of that redo work per batch."""
+    longer list after a near-tie / short list, queries left for the dense exact path, and the stream time of
+    that redo work per batch (between two events around it: IndexCorpus.stats dense_s); the warm-up batch
+    also with its host wall time (submit to finished redo)."""
     pend = []
 
     def run():
@@ -593,9 +594,12 @@ def progressive_rate(engine, Q, M, steps, world, k=10, threshold=0.1):
             engine.progressive_finish(pend.pop(0))
 
     engine.reset_stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     run()  # warm-up batch (first-call allocations, the adaptive list length), then counters from zero
     drain()
-    first = dict(engine.stats)
+    first = dict(engine.stats)  # (waits for the batch's redo)
+    first_wall = time.perf_counter() - t0
     engine.reset_stats()
     wall, kern = timed(run, steps, 0, world, drain)
     st = dict(engine.stats)
@@ -607,7 +611,8 @@ def progressive_rate(engine, Q, M, steps, world, k=10, threshold=0.1):
             "retry_queries_per_batch": st["retry_queries"] / nb, "dense_queries_per_batch": st["dense_queries"] / nb,
             "redo_ms_per_batch": st["dense_s"] / nb * 1e3,
             "warmup_batch": {"redo_queries": first["redo_queries"], "retry_queries": first["retry_queries"],
-                             "dense_queries": first["dense_queries"], "redo_ms": first["dense_s"] * 1e3},
+                             "dense_queries": first["dense_queries"], "redo_ms": first["dense_s"] * 1e3,
+                             "wall_ms": first_wall * 1e3},
             "first_pass_list": M + engine.slack_for(M)}
 
 

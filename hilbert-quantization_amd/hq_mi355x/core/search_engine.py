@@ -12,6 +12,7 @@ stable-sorts those survivors by the overall score.
 """
 from __future__ import annotations
 
+import threading
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -96,17 +97,24 @@ def combine_levels(lv: np.ndarray, both32: bool) -> np.ndarray:
     return np.maximum(0.0, np.minimum(1.0, out))
 
 
+def _lock(obj):
+    """The object's lock (created on first use; dict.setdefault is atomic under the GIL)."""
+    lk = obj.__dict__.get("_lock_")
+    return lk if lk is not None else obj.__dict__.setdefault("_lock_", threading.RLock())
+
+
 class PendingSearch:
     """A progressive search batch queued on the GPU (IndexCorpus.progressive_submit): its device outputs,
     the pinned copy of its redo count and the event behind that copy; `done` holds the results of the
     synchronous paths (small corpora, dense exact path)."""
 
-    __slots__ = ("done", "qp", "out", "res", "cnt", "forced", "nredo", "event", "threshold", "M", "K_out")
+    __slots__ = ("done", "qp", "out", "res", "cnt", "forced", "nredo", "event", "threshold", "M", "K_out", "kp")
 
     def __init__(self, done=None, qp=None, out=None, res=None, cnt=None, forced=None, nredo=None, event=None,
-                 threshold=0.0, M=0, K_out=0):
+                 threshold=0.0, M=0, K_out=0, kp=0):
         self.done, self.qp, self.out, self.res, self.cnt, self.forced = done, qp, out, res, cnt, forced
         self.nredo, self.event, self.threshold, self.M, self.K_out = nredo, event, threshold, M, K_out
+        self.kp = kp  # the first pass's list length (the retry's base)
 
 
 class IndexCorpus:
@@ -117,7 +125,12 @@ class IndexCorpus:
     Every ranking is EXACT: the fused MFMA scan (approximate scores, |err| << EPS) produces a list
     of SLACK extra candidates per query, hq_refine_topk re-scores the list in the reference's
     operation order and proves (or not) that nothing outside the list can enter the exact top-k;
-    unproven queries and the "none passed" fallback are answered by the dense exact path."""
+    unproven queries and the "none passed" fallback are answered by the dense exact path.
+
+    Re-entrant: the reference calls its engines from ThreadPoolExecutor workers (core/video_search.py:806,
+    854; core/streaming_processor.py:294), so one corpus may serve many threads at once.  Every piece of
+    per-call device state (scan / re-rank workspace, redo counters) is keyed by thread as well as stream,
+    and the host-side caches (pinned buffers, statistics, adaptive list lengths) are guarded by a lock."""
 
     # bound on |approximate - exact| score: the level-0 scan contracts in split f16 on the matrix cores
     # (|dscore| <= ~5.5e-6, hq_mi355x.h), the other scans in f64 (< 1e-13)
@@ -136,11 +149,18 @@ class IndexCorpus:
         # float32 rows outside the scans' model (values whose squares under/overflow in float32): the
         # whole corpus then takes the dense exact path (one host sync, at build time, f32 corpora only)
         self.dense_only = bool(self.prep.unsafe_rows().any()) if self.prep.f32 and self.N else False
+        # the prepared layouts are written on the building thread's stream: a search on another stream waits
+        # for them (an event wait queued on the device, no host sync)
+        self._built_on = K.stream()
+        self._ready = torch().cuda.Event()
+        self._ready.record()
 
     def prepare_queries(self, queries, row_f32=None) -> "K.Prepared":
         """queries: [Q, L] (or [L]); a pair (array, per-row float32 flags) for mixed-dtype batches."""
         if isinstance(queries, tuple):
             queries, row_f32 = queries
+        if K.stream() != self._built_on:
+            torch().cuda.current_stream().wait_event(self._ready)
         f32 = _is_f32(queries)
         q = _f64(queries)
         if q.dim() == 1:
@@ -280,7 +300,7 @@ class IndexCorpus:
                 try_ = try_ & ~forced[sel]
             rsel = sel[try_]
             if rsel.numel():
-                got = self._retry_scan(qp.rows(rsel), mode, k, thr, thr_mode, det=False)
+                got = self._retry_scan(qp.rows(rsel), mode, k, thr, thr_mode, kp, det=False)
                 if got is not None:
                     s2, i2, c2, r2 = got
                     ok = (r2 == 1) & (c2 > 0) if need_best else (r2 == 1)
@@ -289,7 +309,7 @@ class IndexCorpus:
                     keep[t.nonzero(try_).view(-1)[ok]] = False
                     sel = sel[keep]
         if sel.numel():
-            self.stats["dense_queries"] += int(sel.numel())
+            self._bump(dense_queries=int(sel.numel()))
             s2, i2, b2, bi2 = self._dense(qp, sel, mode, k, thr, thr_mode)
             sc[sel] = s2
             ids[sel] = i2
@@ -299,20 +319,29 @@ class IndexCorpus:
         return sc, ids, cnt, best, bid
 
     RETRY_FACTOR = 4
+    ADAPT_LISTS = True  # a batch that mostly needed the retry lengthens later first passes at its M (slack_for)
 
-    def _retry_scan(self, qp, mode: int, k: int, thr: float, thr_mode: int, det: bool = False):
-        """The scan path again for queries whose list was not proven complete, with a list RETRY_FACTOR
-        times longer (at most the scan's limit): a list ends in near-ties when more than SLACK candidates
-        lie within EPS of the k-th (runs of near-duplicates in the corpus), or short when the sampled
-        starting threshold overshot.  None when no longer list is available.  Returns refine_topk's
-        (scores, ids, count, resolved) (+ det, the [overall, levels] records, with det)."""
-        cur = k + (self.slack_for(k) if mode == 0 else self.SLACK)  # the first pass's list length
+    def _retry_len(self, mode: int, cur: int):
+        """List length of the longer-list retry after a first pass of `cur` entries, or None when no retry
+        pays: the f64 scans (option scan_v1, odd L) keep the dense path (their lists stop at 64 and their LDS
+        tiles grow with the list), and a retry that would not at least double the list (M = 1000: 1008 ->
+        1024) is a full re-scan for a few entries, so those rows go straight to the dense path."""
         kp2 = min(self._max_list(mode), self.RETRY_FACTOR * cur)
-        # (the f64 scans — option scan_v1, odd L — keep the dense path: their lists stop at 64 and their
-        # LDS tiles grow with the list)
-        if kp2 <= cur or self._max_list(mode) <= MAX_FUSED_K or not self._fused_ok(mode) or self.dense_only:
+        if kp2 < 2 * cur or self._max_list(mode) <= MAX_FUSED_K or not self._fused_ok(mode) or self.dense_only:
             return None
-        self.stats["retry_queries"] += qp.N
+        return kp2
+
+    def _retry_scan(self, qp, mode: int, k: int, thr: float, thr_mode: int, cur: int, det: bool = False):
+        """The scan path again for queries whose list was not proven complete, with a list RETRY_FACTOR
+        times longer than the first pass's `cur` entries (at most the scan's limit): a list ends in near-ties
+        when more than its slack of candidates lie within EPS of the k-th (runs of near-duplicates in the
+        corpus), or short when the sampled starting threshold overshot.  None when no longer list pays
+        (_retry_len).  Returns refine_topk's (scores, ids, count, resolved) (+ det, the [overall, levels]
+        records, with det)."""
+        kp2 = self._retry_len(mode, cur)
+        if kp2 is None:
+            return None
+        self._bump(retry_queries=qp.N)
         lo_mode = 0 if thr_mode == 0 else 1
         asc, aid, _, _ = K.scan_topk(qp, self.prep, mode, kp2, thr - self.EPS, lo_mode, self.id_base)
         tm = thr_mode | (K.THR_KEY32 if self.key32(qp) else 0)
@@ -321,11 +350,12 @@ class IndexCorpus:
                                          count_empty=True)
         return K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, tm, self.EPS, self.id_base, count_empty=True)
 
-    def _level0_redo(self, qp, sel, M: int, thr: float, res, cnt, forced):
+    def _level0_redo(self, qp, sel, M: int, thr: float, res, cnt, forced, kp: int = 0):
         """Exact level-0 top-M (>= thr) records of the queries `sel` the first pass left unproven or empty:
         unproven lists where something passed are re-scanned with a longer list (_retry_scan); the rest —
         nothing passed (the arg-max fallback), forced rows, lists the retry leaves unproven — take the dense
-        exact path.  Returns (s0 [n, M], ids [n, M], best [n], bid [n], det [n, M, W], bdet [n, W])."""
+        exact path.  kp: the first pass's list length (default M + SLACK).
+        Returns (s0 [n, M], ids [n, M], best [n], bid [n], det [n, M, W], bdet [n, W])."""
         t = torch()
         n, dev, W = int(sel.numel()), sel.device, 1 + self.nseg
         s0 = t.full((n, M), -float("inf"), dtype=t.float64, device=dev)
@@ -339,24 +369,26 @@ class IndexCorpus:
         if forced is not None:
             try_ = try_ & ~forced[sel]
         r = t.nonzero(try_).view(-1)
+        cur = int(kp) if kp else M + self.SLACK
         if r.numel():
-            got = self._retry_scan(qp.rows(sel[r]), 0, M, thr, 1, det=True)
+            got = self._retry_scan(qp.rows(sel[r]), 0, M, thr, 1, cur, det=True)
             if got is not None:
                 s2, i2, c2, r2, d2 = got
                 ok = (r2 == 1) & (c2 > 0)
                 rr = r[ok]
                 s0[rr], ids[rr], det[rr] = s2[ok], i2[ok], d2[ok]
                 need[rr] = False
-            if r.numel() >= max(8, qp.N // 10) and self.slack_for(M) == self.SLACK:
-                # a tenth of the batch or more ended in near-ties (runs of near-duplicates in the corpus): later
-                # batches at this M take the retry's list length on the first pass (one scan instead of a
-                # scan plus a retry per batch; results are exact either way)
-                kp2 = min(self._max_list(0), self.RETRY_FACTOR * (M + self.SLACK))
-                if kp2 > M + self.SLACK:
-                    self.__dict__.setdefault("_slack", {})[int(M)] = kp2 - M
+                if (self.ADAPT_LISTS and r.numel() >= max(8, qp.N // 10) and cur == M + self.SLACK
+                        and rr.numel() * 2 >= r.numel()):
+                    # a tenth of the batch or more ended in near-ties (runs of near-duplicates in the corpus) and
+                    # the longer list resolved most of them: later batches at this M take the retry's list
+                    # length on the first pass (one scan instead of a scan plus a retry per batch; results are
+                    # exact either way).  Only when a retry ran: the scans without one keep their length.
+                    with _lock(self):
+                        self.__dict__.setdefault("_slack", {})[int(M)] = self._retry_len(0, cur) - M
         d = t.nonzero(need).view(-1)
         if d.numel():
-            self.stats["dense_queries"] += int(d.numel())
+            self._bump(dense_queries=int(d.numel()))
             dsel = sel[d]
             sub = qp.rows(dsel)
             s3, i3, b3, bi3 = self._dense(qp, dsel, 0, M, thr, 1)
@@ -405,7 +437,8 @@ class IndexCorpus:
         # queries forced onto the dense path (float32 outside the scans' model) join the redo count on the
         # device, so finishing still waits for one pinned value only
         forced = self._forced(qp)
-        cnt, res, oid, odet, ocnt = self._scan_refine_final(qp, M, float(threshold), nredo, nnext, K_out)
+        kp = M + self.slack_for(M)
+        cnt, res, oid, odet, ocnt = self._scan_refine_final(qp, M, float(threshold), nredo, nnext, K_out, kp)
         if forced is not None:
             nredo.add_(forced.sum(dtype=t.int32).view(1))
         # the shared device counter is overwritten by the next batch: this batch's value leaves now (a
@@ -416,7 +449,7 @@ class IndexCorpus:
         ev = t.cuda.Event()
         ev.record()
         return PendingSearch(qp=qp, out=(oid, odet, ocnt), res=res, cnt=cnt, forced=forced,
-                             nredo=host, event=ev, threshold=float(threshold), M=M, K_out=K_out)
+                             nredo=host, event=ev, threshold=float(threshold), M=M, K_out=K_out, kp=kp)
 
     def progressive_finish(self, p: "PendingSearch"):
         """Wait for a submitted batch's redo count (the one host sync) and recompute the queries whose
@@ -427,60 +460,93 @@ class IndexCorpus:
         oid, odet, ocnt = p.out
         p.event.synchronize()
         nredo = int(p.nredo[0])
-        self._pinned_free.setdefault(p.nredo.dtype, []).append(p.nredo)  # read: reusable
-        st = self.stats
-        st["batches"] += 1
-        st["queries"] += p.qp.N
+        self._unpin(p.nredo)  # read: reusable
+        self._bump(batches=1, queries=p.qp.N)
         if nredo > 0:
-            import time as _time
-            t0 = _time.perf_counter()
-            st["redo_batches"] += 1
+            # the redo's time on the stream, between two events read lazily (stats): no host sync here, so the
+            # host goes on queueing batches while the redo runs
+            e0 = t.cuda.Event(enable_timing=True)
+            e0.record()
             redo = (p.res == 0) | (p.cnt == 0)
             if p.forced is not None:
                 redo = redo | p.forced
             sel = t.nonzero(redo).view(-1)
-            if sel.numel():
-                s2, i2, b2, bi2, d2, bd2 = self._level0_redo(p.qp, sel, p.M, p.threshold, p.res, p.cnt, p.forced)
+            n = int(sel.numel())
+            if n:
+                s2, i2, b2, bi2, d2, bd2 = self._level0_redo(p.qp, sel, p.M, p.threshold, p.res, p.cnt, p.forced,
+                                                             kp=p.kp)
                 o2, dd2, c2 = self._final(p.qp.rows(sel), s2, i2, b2, bi2, p.K_out, bdet=bd2, det=d2)
                 oid[sel], odet[sel], ocnt[sel] = o2, dd2, c2
-                st["redo_queries"] += int(sel.numel())
-            t.cuda.current_stream().synchronize()
-            st["dense_s"] += _time.perf_counter() - t0
+            e1 = t.cuda.Event(enable_timing=True)
+            e1.record()
+            self._bump(redo_batches=1, redo_queries=n, _events=(e0, e1))
         p.done = (oid, odet[..., 0], odet[..., 1:], ocnt)  # finishing again returns the same results
         return p.done
+
+    _STAT_KEYS = ("batches", "queries", "redo_batches", "redo_queries", "retry_queries", "dense_queries")
 
     @property
     def stats(self) -> dict:
         """Counters of the submitted progressive batches: batches / queries finished, batches and queries
         redone after the first pass (short or unproven lists, nothing passing, forced rows), and the
-        host wall time spent there (dense_s; it synchronises the stream); of the redone queries, those
-        re-scanned with a longer list (retry_queries) and those scored densely (dense_queries)."""
-        st = self.__dict__.get("_stats")
-        if st is None:
-            st = self.__dict__["_stats"] = {"batches": 0, "queries": 0, "redo_batches": 0, "redo_queries": 0,
-                                            "retry_queries": 0, "dense_queries": 0, "dense_s": 0.0}
-        return st
+        stream time spent there (dense_s: between two events around each redo, read here — this waits for
+        the redos still running); of the redone queries, those re-scanned with a longer list (retry_queries)
+        and those scored densely (dense_queries).  A snapshot: later batches do not change it."""
+        with _lock(self):
+            st = self.__dict__.setdefault("_stats", dict.fromkeys(self._STAT_KEYS, 0))
+            evs = self.__dict__.setdefault("_stat_events", [])
+            done, evs[:] = list(evs), []
+            st["dense_s"] = st.get("dense_s", 0.0)
+        dt = 0.0
+        for e0, e1 in done:
+            e1.synchronize()
+            dt += e0.elapsed_time(e1) / 1e3
+        with _lock(self):
+            st["dense_s"] += dt
+            return dict(st)
+
+    def _bump(self, _events=None, **counts):
+        with _lock(self):
+            st = self.__dict__.setdefault("_stats", dict.fromkeys(self._STAT_KEYS, 0))
+            for key, v in counts.items():
+                st[key] += v
+            if _events is not None:
+                self.__dict__.setdefault("_stat_events", []).append(_events)
 
     def reset_stats(self):
-        self.__dict__.pop("_stats", None)
+        with _lock(self):
+            self.__dict__.pop("_stats", None)
+            self.__dict__.pop("_stat_events", None)
 
     def _pinned(self, dtype):
         """A one-element pinned host buffer: recycled once its batch is finished (a fresh pinned
         allocation per batch can stall the host between launches)."""
-        free = self.__dict__.setdefault("_pinned_free", {}).setdefault(dtype, [])
-        return free.pop() if free else torch().empty(1, dtype=dtype, pin_memory=True)
+        with _lock(self):
+            free = self.__dict__.setdefault("_pinned_free", {}).setdefault(dtype, [])
+            if free:
+                return free.pop()
+        return torch().empty(1, dtype=dtype, pin_memory=True)
+
+    def _unpin(self, buf):
+        """Return a pinned buffer whose value has been read."""
+        with _lock(self):
+            self.__dict__.setdefault("_pinned_free", {}).setdefault(buf.dtype, []).append(buf)
 
     def _redo_counter(self, dev):
-        """(counter, next): device int32 [1] views of a per-stream pair used alternately — the exact re-rank
-        counts this batch's queries needing the dense path in `counter` (zero on entry) and clears `next`,
-        the following batch's counter (hq_refine_rescore_topk_pp: no memset launch per batch)."""
+        """(counter, next): device int32 [1] views of a pair used alternately by ONE thread on one stream —
+        the exact re-rank counts this batch's queries needing the dense path in `counter` (zero on entry) and
+        clears `next`, the following batch's counter (hq_refine_rescore_topk_pp: no memset launch per batch).
+        Keyed by thread too: two threads sharing a stream would otherwise take the two slots of one pair and
+        each clear the other's count before it is copied out."""
         t = torch()
-        cache = self.__dict__.setdefault("_redo", {})
-        key = (str(dev), K.stream())
-        if key not in cache:
-            cache[key] = [t.zeros(2, dtype=t.int32, device=dev), 0]
-        pair, i = cache[key]
-        cache[key][1] = 1 - i
+        key = (str(dev), K.stream(), threading.get_ident())
+        with _lock(self):
+            cache = self.__dict__.setdefault("_redo", {})
+            ent = cache.get(key)
+            if ent is None:
+                ent = cache[key] = [t.zeros(2, dtype=t.int32, device=dev), 0]
+            pair, i = ent
+            ent[1] = 1 - i
         return pair[i:i + 1], pair[1 - i:2 - i]
 
     def _no_fallback(self, Q: int, dev):
@@ -495,10 +561,16 @@ class IndexCorpus:
                           t.zeros((Q, 1 + self.nseg), dtype=t.float64, device=dev))
         return cache[key]
 
+    def reset_list_lengths(self):
+        """Forget the first-pass list lengths the corpus adapted (slack_for): back to SLACK at every M."""
+        with _lock(self):
+            self.__dict__.pop("_slack", None)
+
     def slack_for(self, M: int) -> int:
         """Extra list entries of the first pass at list length M: SLACK, or the longer list a corpus with
         runs of near-duplicates showed it needs (_level0_redo: most lists of a batch ended in near-ties)."""
-        return self.__dict__.get("_slack", {}).get(int(M), self.SLACK)
+        with _lock(self):
+            return self.__dict__.get("_slack", {}).get(int(M), self.SLACK)
 
     def _scan_refine(self, qp, mode: int, k: int, thr: float, thr_mode: int, nredo=None, det: bool = False,
                      next_redo=None, slack=None):
@@ -515,14 +587,14 @@ class IndexCorpus:
         return K.refine_topk(qp, self.prep, mode, asc, aid, k, thr, tm, self.EPS, self.id_base, redo=nredo,
                              count_empty=True)
 
-    def _scan_refine_final(self, qp, M: int, thr: float, nredo, next_redo, K_out: int):
+    def _scan_refine_final(self, qp, M: int, thr: float, nredo, next_redo, K_out: int, kp: int):
         """The progressive search's first pass: level-0 scan, exact re-rank, overall re-score and final
         ranking -> (count, resolved, out_id, out_det, out_count).  On the lane-cooperative paths the re-rank's
         ranking and the final ranking are one kernel (hq_refine_final_ws: the level-0 records stay on the
         device).  No arg-max
         on this path: a query where nothing passed (count 0) is recomputed by the dense path in
-        progressive_finish, so the fallback slot is a constant (-inf, id -1, zero re-scores)."""
-        kp = M + self.slack_for(M)
+        progressive_finish, so the fallback slot is a constant (-inf, id -1, zero re-scores).  kp: the list
+        length (M + slack_for(M), read once by the caller)."""
         asc, aid, _, _ = K.scan_topk(qp, self.prep, 0, kp, thr - self.EPS, 1, self.id_base)
         tm = 1 | (K.THR_KEY32 if self.key32(qp) else 0)
         if _FUSED_FINAL:
@@ -582,12 +654,13 @@ class ProgressiveSimilaritySearchEngine(*_bases("interfaces", "SimilaritySearchE
         referenced, so an identity match is a match; a QuantizedModel's hierarchical_indices are never
         written after creation (the reference's pipeline builds a new array per model)."""
         arrays = [c.hierarchical_indices for c in pool]
-        hit = self._pool_cache
-        if hit is not None and len(hit[0]) == len(arrays) and all(a is b for a, b in zip(hit[0], arrays)):
-            return hit[1]
-        corpus = self._corpus(arrays)
-        self._pool_cache = (arrays, corpus)
-        return corpus
+        with _lock(self):  # threads searching one pool share one resident corpus (built once)
+            hit = self._pool_cache
+            if hit is not None and len(hit[0]) == len(arrays) and all(a is b for a, b in zip(hit[0], arrays)):
+                return hit[1]
+            corpus = self._corpus(arrays)
+            self._pool_cache = (arrays, corpus)
+            return corpus
 
     def _scores_at_level(self, q: np.ndarray, cands: Sequence[np.ndarray], level: int) -> np.ndarray:
         """compare_indices_at_level(q, c, level) for every candidate, on the GPU."""

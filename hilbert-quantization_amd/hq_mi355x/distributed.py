@@ -76,7 +76,8 @@ class ShardedIndexCorpus:
         t = torch()
         c = self.local
         Q = qp.N
-        s0, ids, cnt, res, det0 = c._scan_refine(qp, 0, M, float(threshold), 1, det=True, slack=c.slack_for(M))
+        slack = c.slack_for(M)
+        s0, ids, cnt, res, det0 = c._scan_refine(qp, 0, M, float(threshold), 1, det=True, slack=slack)
         # no arg-max on the scan path (count-0 rows are redone below): constant fallback slot
         best, bid, bdet0 = c._no_fallback(Q, qp.Z.device)
         rec = self._records(qp, s0, ids, best, bid, det0, bdet0.view(Q, 1, -1))
@@ -88,18 +89,18 @@ class ShardedIndexCorpus:
         flag.copy_(redo.any().view(1), non_blocking=True)
         ev = t.cuda.Event()
         ev.record()
-        return qp, M, float(threshold), rec, (redo, res, cnt, forced), flag, ev
+        return qp, M, float(threshold), rec, (redo, res, cnt, forced, M + slack), flag, ev
 
     def _local_finish(self, pending):
         t = torch()
-        qp, M, threshold, rec, (redo, res, cnt, forced), flag, ev = pending
+        qp, M, threshold, rec, (redo, res, cnt, forced, kp), flag, ev = pending
         ev.synchronize()
         any_redo = bool(flag[0])
-        self.local._pinned_free.setdefault(flag.dtype, []).append(flag)  # read: reusable
+        self.local._unpin(flag)  # read: reusable
         if any_redo:
             # unproven lists re-scanned with a longer list, the rest on the dense exact path (IndexCorpus)
             sel = t.nonzero(redo).view(-1)
-            s2, i2, b2, bi2, d2, bd2 = self.local._level0_redo(qp, sel, M, threshold, res, cnt, forced)
+            s2, i2, b2, bi2, d2, bd2 = self.local._level0_redo(qp, sel, M, threshold, res, cnt, forced, kp=kp)
             rec[sel] = self._records(qp.rows(sel), s2, i2, b2, bi2, d2, bd2.view(-1, 1, bd2.shape[-1]))
         return rec
 

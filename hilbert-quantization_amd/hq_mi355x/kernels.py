@@ -8,6 +8,7 @@ SURVEY.md §7); the reference-shaped classes in `hq_mi355x.core` / `hq_mi355x.ra
 from __future__ import annotations
 
 import functools
+import threading
 
 import ctypes
 from typing import Optional, Tuple
@@ -375,18 +376,26 @@ def level_scores(q: Prepared, c: Prepared, level: int, exc=None):
     return out
 
 
-_WS = {}
+_TLS = threading.local()
 
 
 def _workspace(nbytes: int, dev):
-    """Scan workspace reused across calls on the same stream (stream order makes the reuse safe: the
-    previous scan's kernels finish before the next scan's first write).  Saves an allocation between
-    the query preparation and the first scan launch of every batch."""
+    """Scan / re-rank workspace reused across the calls ONE thread makes on one stream (stream order
+    makes that reuse safe: the previous call's kernels finish before the next call's first write).
+    Saves an allocation between the query preparation and the first scan launch of every batch.
+
+    Per thread, not per stream alone: the reference calls its engines from ThreadPoolExecutor workers
+    (core/video_search.py:806,854), and threads sharing a stream interleave their launches (ctypes drops
+    the GIL), so thread B's scan could otherwise overwrite thread A's workspace between A's scan and A's
+    re-rank.  A thread's buffers return to the caching allocator when the thread ends (stream-ordered)."""
     t = torch()
+    cache = getattr(_TLS, "ws", None)
+    if cache is None:
+        cache = _TLS.ws = {}
     key = (str(dev), stream())
-    ws = _WS.get(key)
+    ws = cache.get(key)
     if ws is None or ws.numel() < nbytes:
-        ws = _WS[key] = t.empty(nbytes, dtype=t.uint8, device=dev)
+        ws = cache[key] = t.empty(nbytes, dtype=t.uint8, device=dev)
     return ws[:nbytes]
 
 
@@ -475,6 +484,12 @@ def refine_final_ws(q: Prepared, c: Prepared, cand_score, cand_id, k: int, thres
     t = torch()
     Q, kp = cand_id.shape
     dev = cand_id.device
+    # support probe: with Q = 0 and no counter the call only checks the form exists (nothing launched)
+    rc = _L().hq_refine_final_ws(None, None, None, 0, None, None, None, c.N, c.L, None, None, kp, k, 0.0, 0, 0.0, 0,
+                                 None, None, None, None, None, None, int(K_out), None, None, None, None, 0, stream())
+    if rc == _lib.HQ_E_UNSUPPORTED:
+        return None
+    _chk(rc, exc)
     os_ = t.empty((Q, k), dtype=t.float64, device=dev)
     oi = t.empty((Q, k), dtype=t.int64, device=dev)
     cnt = t.empty(Q, dtype=t.int32, device=dev)
@@ -482,8 +497,10 @@ def refine_final_ws(q: Prepared, c: Prepared, cand_score, cand_id, k: int, thres
     fid = t.empty((Q, K_out), dtype=t.int64, device=dev)
     fdet = t.empty((Q, K_out, 1 + q.nseg), dtype=t.float64, device=dev)
     fcnt = t.empty(Q, dtype=t.int32, device=dev)
-    wb = int(_lib.load().hq_refine_workspace_size(Q, kp, c.L))
-    ws = _workspace(wb, dev)
+    ws, wb = None, 0
+    if kp > 64:  # lists <= 64 take k_rank_small, which needs no workspace
+        wb = int(_lib.load().hq_refine_workspace_size(Q, kp, c.L))
+        ws = _workspace(wb, dev)
     rc = _L().hq_refine_final_ws(ptr(q.R), ptr(q.Z), ptr(q.S), Q, ptr(c.R), ptr(c.Z), ptr(c.S), c.N, c.L,
                                  ptr(_contig(cand_score)), ptr(_contig(cand_id)), kp, k, float(threshold), thr_mode,
                                  float(eps), int(id_base), ptr(os_), ptr(oi), ptr(cnt), ptr(res), ptr(redo),

@@ -78,13 +78,11 @@ def test_fresh_queries_full_size(hq_lib):
             np.testing.assert_allclose(ov[a], rsc, atol=1e-10)
 
 
-def test_clustered_corpus_full_size(hq_lib):
-    """A 1M-row corpus of 64-row runs of near-duplicates (15,625 base vectors + N(0, 0.01)); 1000 queries
-    drawn from the runs: every query equal to the dense exact path at M = 20 / 100 / 1000, its own run on
-    top; sampled queries equal to the oracle."""
+def _clustered():
+    """1M rows in 64-row runs of near-duplicates (15,625 base vectors + N(0, 0.01)) and 1000 queries drawn
+    from the runs -> (corpus [N, 64], queries [QN, 64], the run of each query)."""
     import torch
     from hq_mi355x import kernels as K
-    from hq_mi355x.core.search_engine import IndexCorpus
     nb = N // RUN
     g = torch.Generator(device="cuda").manual_seed(6)
     _, B, _ = K.map_index_quantize(torch.randn((nb, 1536), generator=g, device="cuda", dtype=torch.float32), 64, 64)
@@ -92,6 +90,15 @@ def test_clustered_corpus_full_size(hq_lib):
     C.add_(0.01 * torch.randn(C.shape, generator=g, device="cuda", dtype=torch.float64))
     pick = torch.randperm(nb, generator=torch.Generator().manual_seed(7))[:QN].cuda()
     Q = B[pick] + 0.01 * torch.randn((QN, 64), generator=g, device="cuda", dtype=torch.float64)
+    return C, Q, pick
+
+
+def test_clustered_corpus_full_size(hq_lib):
+    """A 1M-row corpus of 64-row runs of near-duplicates (15,625 base vectors + N(0, 0.01)); 1000 queries
+    drawn from the runs: every query equal to the dense exact path at M = 20 / 100 / 1000, its own run on
+    top; sampled queries equal to the oracle."""
+    from hq_mi355x.core.search_engine import IndexCorpus
+    C, Q, pick = _clustered()
     corpus = IndexCorpus(C)
     res = {M: _check_all(corpus, Q, M, max_dense=2) for M in (20, 100, 1000)}
     assert np.array_equal(res[20][0][:, 0] // RUN, _np(pick))
@@ -127,3 +134,33 @@ def test_bench_queries_every_query_full_size(hq_lib):
     ds, di, _, _ = [_np(x) for x in corpus._dense(qp, torch.arange(QN, device="cuda"), 1, 10, 0.0, 0)]
     assert np.array_equal(ids, di)
     np.testing.assert_array_equal(ov, ds)
+
+
+@pytest.mark.parametrize("R", [2, 8])
+def test_clustered_sharded_retry_equals_single(hq_lib, R):
+    """The sharded redo path (ShardedIndexCorpus._local_finish -> IndexCorpus._level0_redo: the longer-list
+    retry, then the dense path) on the clustered 1M corpus split into R contiguous shards (run boundaries fall
+    inside shards and across them): at M = 20 / 100 / 1000 the merged records equal the unsharded corpus for
+    EVERY query, and the shards did take the retry (core/search_engine.py:232-300, 340-388)."""
+    import torch
+    from hq_mi355x.core.search_engine import IndexCorpus
+    from hq_mi355x.distributed import ShardedIndexCorpus, shard_range
+    C, Q, _ = _clustered()
+    single = IndexCorpus(C)
+    shards = []
+    for r in range(R):
+        a, b = shard_range(N, r, R)
+        shards.append(ShardedIndexCorpus(C[a:b], id_base=a, n_total=N))
+    for M in (20, 100, 1000):
+        want = [_np(x) for x in single.progressive(Q, 10, 0.1, M)]
+        for sh in shards:
+            sh.local.reset_stats()
+        recs = [sh.local_records(sh.local.prepare_queries(Q), M, 0.1) for sh in shards]
+        got = [_np(x) for x in ShardedIndexCorpus.merge(torch.stack(recs, 0), M, 10)]
+        for x, y, name in zip(got, want, ("ids", "overall", "levels", "count")):
+            np.testing.assert_array_equal(x, y, err_msg=f"R={R} M={M} {name}")
+        st = [sh.local.stats for sh in shards]
+        print(f"R={R} M={M}: " + "; ".join(f"retry {s['retry_queries']} dense {s['dense_queries']}" for s in st))
+        if M == 20:  # (longer lists hold a whole 64-row run: no near-tie at the list end)
+            assert sum(s["retry_queries"] for s in st) > 0, (R, M, st)
+        assert sum(s["dense_queries"] for s in st) <= 2 * R + (QN if M == 1000 else 0), (R, M, st)

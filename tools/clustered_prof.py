@@ -46,6 +46,6 @@ print(f"first pass (scan + re-rank): {wall(lambda: corpus._scan_refine(qp, 0, M,
 sub = qp.rows(sel)
 print(f"rows(): {wall(lambda: qp.rows(sel)):.3f} ms", flush=True)
 print(f"retry scan + re-rank ({sel.numel()} queries, list {corpus.RETRY_FACTOR * (M + corpus.SLACK)}): "
-      f"{wall(lambda: corpus._retry_scan(sub, 0, M, 0.1, 1, det=True)):.3f} ms", flush=True)
+      f"{wall(lambda: corpus._retry_scan(sub, 0, M, 0.1, 1, M + corpus.SLACK, det=True)):.3f} ms", flush=True)
 print(f"level0 redo (retry + bookkeeping): "
       f"{wall(lambda: corpus._level0_redo(qp, sel, M, 0.1, res, cnt, None)):.3f} ms", flush=True)
