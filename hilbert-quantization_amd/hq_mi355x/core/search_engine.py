@@ -26,6 +26,11 @@ from .._compat import bases as _bases
 MAX_FUSED_K = 64     # list length of the f64 scans (hq_scan_topk)
 MAX_SPLIT_K = 1024   # list length of the split-f16 scans (k > 64: LDS-sorted pools, tiled re-rank)
 _FUSED_FINAL = True  # long lists: the final ranking inside the re-rank's sort (hq_refine_final_ws); False: A/B
+# How progressive_finish learns a batch's redo count: "side" — an event right after the re-rank on the batch's
+# stream, and the count read after it on a side stream (the search stream carries no copy: the copy and the
+# bubble behind it cost ~13 us per batch); "copy" — a pinned copy queued behind the re-rank (A/B)
+_COUNT_READ = "side"
+_RING = 16  # redo counters per (device, stream, thread): a slot is re-cleared _RING - 1 batches later
 
 
 @dataclass
@@ -108,13 +113,15 @@ class PendingSearch:
     the pinned copy of its redo count and the event behind that copy; `done` holds the results of the
     synchronous paths (small corpora, dense exact path)."""
 
-    __slots__ = ("done", "qp", "out", "res", "cnt", "forced", "nredo", "event", "threshold", "M", "K_out", "kp")
+    __slots__ = ("done", "qp", "out", "res", "cnt", "forced", "nredo", "event", "threshold", "M", "K_out", "kp",
+                 "ring")
 
     def __init__(self, done=None, qp=None, out=None, res=None, cnt=None, forced=None, nredo=None, event=None,
-                 threshold=0.0, M=0, K_out=0, kp=0):
+                 threshold=0.0, M=0, K_out=0, kp=0, ring=None):
         self.done, self.qp, self.out, self.res, self.cnt, self.forced = done, qp, out, res, cnt, forced
         self.nredo, self.event, self.threshold, self.M, self.K_out = nredo, event, threshold, M, K_out
         self.kp = kp  # the first pass's list length (the retry's base)
+        self.ring = ring  # side reads: (ring entry, slot) of the batch's device counter
 
 
 class IndexCorpus:
@@ -319,6 +326,7 @@ class IndexCorpus:
         return sc, ids, cnt, best, bid
 
     RETRY_FACTOR = 4
+    _count_read = _COUNT_READ
     ADAPT_LISTS = True  # a batch that mostly needed the retry lengthens later first passes at its M (slack_for)
 
     def _retry_len(self, mode: int, cur: int):
@@ -433,17 +441,26 @@ class IndexCorpus:
             s0, ids, cnt, best, bid = self.exact_topk(qp, 0, M, float(threshold), 1, need_best=True)
             oid, odet, ocnt = self._final(qp, s0, ids, best, bid, K_out)
             return PendingSearch(done=(oid, odet[..., 0], odet[..., 1:], ocnt))
-        nredo, nnext = self._redo_counter(qp.Z.device)
+        nredo, nnext, ring = self._redo_counter(qp.Z.device, self._count_read == "side")
         # queries forced onto the dense path (float32 outside the scans' model) join the redo count on the
-        # device, so finishing still waits for one pinned value only
+        # device, so finishing still waits for one value only
         forced = self._forced(qp)
         kp = M + self.slack_for(M)
         cnt, res, oid, odet, ocnt = self._scan_refine_final(qp, M, float(threshold), nredo, nnext, K_out, kp)
         if forced is not None:
             nredo.add_(forced.sum(dtype=t.int32).view(1))
-        # the shared device counter is overwritten by the next batch: this batch's value leaves now (a
-        # last-workgroup write of it to the pinned int from the re-rank kernel measured slower: 21 -> 43 us,
-        # every workgroup's release fence)
+        if ring is not None:
+            # the slot stays untouched until _RING - 1 batches later (and is read before that: _redo_counter);
+            # finish reads it after this event
+            ev = t.cuda.Event()
+            ev.record()
+            p = PendingSearch(qp=qp, out=(oid, odet, ocnt), res=res, cnt=cnt, forced=forced, nredo=nredo,
+                              event=ev, threshold=float(threshold), M=M, K_out=K_out, kp=kp, ring=ring)
+            with _lock(self):
+                ring[0][2][ring[1]] = p
+            return p
+        # the counter's value leaves now, behind the re-rank (a last-workgroup write of it to the pinned int from
+        # the re-rank kernel measured slower: 21 -> 43 us, every workgroup's release fence)
         host = self._pinned(nredo.dtype)
         host.copy_(nredo, non_blocking=True)
         ev = t.cuda.Event()
@@ -458,9 +475,12 @@ class IndexCorpus:
             return p.done
         t = torch()
         oid, odet, ocnt = p.out
-        p.event.synchronize()
-        nredo = int(p.nredo[0])
-        self._unpin(p.nredo)  # read: reusable
+        if p.ring is not None:
+            nredo = self._resolve(p)
+        else:
+            p.event.synchronize()
+            nredo = int(p.nredo[0])
+            self._unpin(p.nredo)  # read: reusable
         self._bump(batches=1, queries=p.qp.N)
         if nredo > 0:
             # the redo's time on the stream, between two events read lazily (stats): no host sync here, so the
@@ -532,22 +552,58 @@ class IndexCorpus:
         with _lock(self):
             self.__dict__.setdefault("_pinned_free", {}).setdefault(buf.dtype, []).append(buf)
 
-    def _redo_counter(self, dev):
-        """(counter, next): device int32 [1] views of a pair used alternately by ONE thread on one stream —
-        the exact re-rank counts this batch's queries needing the dense path in `counter` (zero on entry) and
-        clears `next`, the following batch's counter (hq_refine_rescore_topk_pp: no memset launch per batch).
-        Keyed by thread too: two threads sharing a stream would otherwise take the two slots of one pair and
-        each clear the other's count before it is copied out."""
+    def _redo_counter(self, dev, side: bool = False):
+        """(counter, next, ring): device int32 [1] views of a ring of _RING counters used in turn by ONE thread
+        on one stream — the exact re-rank counts this batch's queries needing the dense path in `counter`
+        (zero on entry) and clears `next`, the following batch's counter (hq_refine_rescore_topk_pp: no memset
+        launch per batch), so a slot is cleared again _RING - 1 batches later; ring[2] counts the batches whose
+        slot is still to be read (progressive_finish).  Keyed by thread too: two threads sharing a stream would
+        otherwise take slots of one ring and clear each other's count before it is read."""
         t = torch()
         key = (str(dev), K.stream(), threading.get_ident())
         with _lock(self):
             cache = self.__dict__.setdefault("_redo", {})
             ent = cache.get(key)
             if ent is None:
-                ent = cache[key] = [t.zeros(2, dtype=t.int32, device=dev), 0]
-            pair, i = ent
-            ent[1] = 1 - i
-        return pair[i:i + 1], pair[1 - i:2 - i]
+                ent = cache[key] = [t.zeros(_RING, dtype=t.int32, device=dev), 0, [None] * _RING]
+            buf, i = ent[0], ent[1]
+            ent[1] = (i + 1) % _RING
+            j = (i + 1) % _RING
+            old = ent[2][j]  # a batch still unread whose slot this batch's re-rank clears: read it first
+        if old is not None:
+            self._resolve(old)
+        return buf[i:i + 1], buf[j:j + 1], ((ent, i) if side else None)
+
+    def _resolve(self, p) -> int:
+        """A side-read batch's redo count (once): wait for its event, read its slot, free the slot."""
+        with _lock(self):
+            if isinstance(p.nredo, int):
+                return p.nredo
+        p.event.synchronize()
+        v = self._side_read(p.nredo)
+        with _lock(self):
+            if not isinstance(p.nredo, int):
+                ent, i = p.ring
+                if ent[2][i] is p:
+                    ent[2][i] = None
+                p.nredo = v
+        return v
+
+    def _side_read(self, slot) -> int:
+        """The value of a finished batch's device counter, read on this thread's side stream (the search
+        stream goes on with the next batch's kernels; no copy is queued on it)."""
+        t = torch()
+        key = (slot.device.index, threading.get_ident())
+        with _lock(self):
+            ss = self.__dict__.setdefault("_side", {})
+            st = ss.get(key)
+            if st is None:
+                st = ss[key] = (t.cuda.Stream(device=slot.device), t.empty(1, dtype=slot.dtype, pin_memory=True))
+        side, host = st
+        with t.cuda.stream(side):
+            host.copy_(slot, non_blocking=True)
+        side.synchronize()
+        return int(host[0])
 
     def _no_fallback(self, Q: int, dev):
         """Constant (-inf, -1, zeros) fallback slot of a batch of Q queries, cached per stream: the fills
