@@ -4318,6 +4318,72 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   }
 }
 
+// Scoring pass, E entries per group (option rank_e, default 2 for lists of >= 256 entries): block (x-block,
+// query) = 32 E list entries of one query; group g scores entries x0 + g + 32 e, e = 0 .. E - 1.  The next
+// entry's candidate row and statistics are requested into registers before the current entry is scored, so
+// a group always has one row gather in flight behind its arithmetic (k_rank_pairs leaves that overlap to the
+// other resident waves: 44% of its wave cycles waited, PMC r05), and the query row is staged once per 32 E
+// entries.  The scoring is rank_score's: bit-identical to k_rank_pairs.
+template <int PPL, int E>
+__global__ __launch_bounds__(256) void k_rank_pairs_e(RankArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double cm[];
+  const int tid = threadIdx.x, g = tid >> 3, j = tid & 7;
+  const int q = blockIdx.y, x0 = blockIdx.x * kCoopGroups * E + g;
+  double* rq = cm;
+  double* rg = cm + coop_qw(a.cs) + g * coop_rw(a.cs);
+  const int L = a.cs.L, Lp = a.cs.Lp, nseg = a.cs.nseg;
+  for (int e = tid; e < L; e += 256) rq[e] = a.Rq[(int64_t)q * L + e];
+  for (int e = tid; e < Lp; e += 256) rq[L + e] = a.Zq[(int64_t)q * Lp + e];
+  for (int e = tid; e < 4 * nseg; e += 256) rq[L + Lp + e] = a.Sq[(int64_t)q * nseg * 4 + e];
+  const int np_raw = L / 2, np_all = np_raw + 2 * nseg;
+  // the candidate (local row, -1: none) of list entry x; load: its pieces into registers (each lane's piece
+  // index clamped, every load unconditional: see rank_stage)
+  auto cand = [&](const int x) -> int64_t {
+    if (x >= a.kp) return -1;
+    const int64_t id = a.cid[(int64_t)q * a.kp + x];
+    const int64_t cc = id - a.id_base;
+    return (id >= 0 && cc >= 0 && cc < a.N) ? cc : -1;
+  };
+  auto load = [&](const int64_t cr, f64x2* v) {  // cr: a valid local row
+    const f64x2* rr = reinterpret_cast<const f64x2*>(a.Rc + cr * L);
+    const f64x2* rs = reinterpret_cast<const f64x2*>(a.Sc + cr * nseg * 4);
+#pragma unroll
+    for (int p = 0; p < PPL; ++p) {
+      const int pc = j + 8 * p < np_all ? j + 8 * p : np_all - 1;
+      v[p] = *(pc < np_raw ? rr + pc : rs + (pc - np_raw));
+    }
+  };
+  f64x2 v[PPL];
+  int64_t c = cand(x0);
+  if (c >= 0) load(c, v);
+  __syncthreads();  // the query row
+#pragma unroll 1
+  for (int e = 0; e < E; ++e) {
+    const int x = x0 + kCoopGroups * e;
+    if (x >= a.kp) break;  // group-uniform (the later entries are further out)
+    wave_lds_sync();       // the previous entry's reads of rg are done
+#pragma unroll
+    for (int p = 0; p < PPL; ++p) {
+      const int pc = j + 8 * p;
+      if (pc < np_all) reinterpret_cast<f64x2*>(rg)[pc] = v[p];
+    }
+    wave_lds_sync();
+    const int64_t cur = c;
+    if (e + 1 < E) {  // the next entry's row in flight while this one is scored
+      c = cand(x + kCoopGroups);
+      if (c >= 0) load(c, v);
+    }
+    const int64_t e0 = (int64_t)q * a.kp + x;
+    double sc;
+    int64_t id;
+    rank_score(a, rq, rg, cur, j, a.ws_rec + e0 * (1 + a.cs.nseg), sc, id);
+    if (j == 0) {
+      a.ws_sc[e0] = sc;
+      a.ws_id[e0] = id;
+    }
+  }
+}
+
 // the count and the completeness proof of query q's re-ranked list (refine_big_body): n valid entries, kth
 // the k-th exact score (-inf when n < k); the last list slot's approximate score + eps must stay below it
 __device__ __forceinline__ void rank_resolve(const RankArgs& a, const double* __restrict__ cs, double eps, int q,
@@ -5425,9 +5491,19 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
       ra.ws_id = reinterpret_cast<int64_t*>(w + (size_t)Q * kp * 8);
       ra.ws_rec = reinterpret_cast<double*>(w + (size_t)Q * kp * 16);
       const size_t lds = 8 * ((size_t)coop_qw(ra.cs) + (size_t)kCoopGroups * coop_rw(ra.cs));
-      const dim3 g1((kp + kCoopGroups - 1) / kCoopGroups, Q);
-      if (ppl == 6) hipLaunchKernelGGL(k_rank_pairs<6>, g1, dim3(256), lds, s, ra);
-      else hipLaunchKernelGGL(k_rank_pairs<10>, g1, dim3(256), lds, s, ra);
+      // entries per group (option rank_e): 1 = k_rank_pairs (one pair per group, no loop)
+      const int re = (int)opt(OPT_RANK_E, 1);
+      if (re == 2 || re == 4) {
+        const dim3 ge((kp + kCoopGroups * re - 1) / (kCoopGroups * re), Q);
+        if (ppl == 6 && re == 2) hipLaunchKernelGGL((k_rank_pairs_e<6, 2>), ge, dim3(256), lds, s, ra);
+        else if (ppl == 6) hipLaunchKernelGGL((k_rank_pairs_e<6, 4>), ge, dim3(256), lds, s, ra);
+        else if (re == 2) hipLaunchKernelGGL((k_rank_pairs_e<10, 2>), ge, dim3(256), lds, s, ra);
+        else hipLaunchKernelGGL((k_rank_pairs_e<10, 4>), ge, dim3(256), lds, s, ra);
+      } else {
+        const dim3 g1((kp + kCoopGroups - 1) / kCoopGroups, Q);
+        if (ppl == 6) hipLaunchKernelGGL(k_rank_pairs<6>, g1, dim3(256), lds, s, ra);
+        else hipLaunchKernelGGL(k_rank_pairs<10>, g1, dim3(256), lds, s, ra);
+      }
       HQ_CHECK_LAUNCH();
       if (kp > 512)  // 1024-entry sorts: one compare-exchange per thread and stage
         hipLaunchKernelGGL(k_rank_sort<512>, dim3(grid), dim3(512), 0, s, ra, cand_score, eps, out_score, out_id,

@@ -223,14 +223,17 @@ def test_fused_query_prepare_equals_two_launches(hq_lib, hq_option, kind, coop):
     assert (a.f32, a.all32) == (b.f32, b.all32)
 
 
+@pytest.mark.parametrize("rank_e", [1, 2, 4])
 @pytest.mark.parametrize("L", [32, 64, 128])
 @pytest.mark.parametrize("kind", ["f64", "f32", "mixed"])
-def test_cooperative_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind):
+def test_cooperative_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind, rank_e):
     """The lane-cooperative long-list re-rank (k_refine_coop: 8 lanes per entry, NumPy's eight pairwise
     accumulators one per lane, rows staged per group) is bit-identical to the one-thread-per-entry kernel
     (option refine_coop = 0): progressive M = 100 / 1000 (level-0 ranking + [overall, level..] records),
-    brute force k > 64 (overall ranking), frame scan (strict level-0); float64, float32 and mixed pools."""
+    brute force k > 64 (overall ranking), frame scan (strict level-0); float64, float32 and mixed pools.
+    rank_e: list entries per 8-lane group (k_rank_pairs_e: the next entry's row gathered while one scores)."""
     from hq_mi355x.core.search_engine import IndexCorpus
+    hq_option("rank_e", rank_e)
     C = _corpus(3000 if L == 128 else 20000, L, 41 + L)
     rng = np.random.default_rng(42)
     Q = np.concatenate([C[[1, 2, 20, 40]] + 0.0, C[100:108] + rng.normal(0, 0.01, (8, L)),

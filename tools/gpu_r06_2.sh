@@ -3,12 +3,12 @@
 export TMPDIR=/tmp
 O=$GRAFT_REPO_ROOT/gpurun_out
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_threads.py tests/test_gpu_search.py tests/test_gpu_longlist.py -x -q --timeout 300 --timeout-method thread > $O/r06_2_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_threads.py tests/test_gpu_search.py tests/test_gpu_longlist.py tests/test_gpu_hard_queries.py -x -q --timeout 300 --timeout-method thread > $O/r06_2_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 $O/r06_2_tests.log; [ $rc -eq 0 ] || exit $rc
-B="--no-cpu --no-stream --no-precomputed --no-ingest --no-frames --no-hard --no-api --steps 3 --warmup 1"
+B="--corpus-total 0 --no-cpu --no-stream --no-precomputed --no-ingest --no-frames --no-hard --no-api --steps 3 --warmup 1"
 i=0
 for rep in 1 2; do
-for v in "IndexCorpus._count_read = 'copy'|" "IndexCorpus._count_read = 'side'|" "IndexCorpus._count_read = 'side'|--option sample_stride=32" "IndexCorpus._count_read = 'side'|--option sample_stride=8"; do
+for v in "IndexCorpus._count_read = 'copy'|" "IndexCorpus._count_read = 'side'|" "IndexCorpus._count_read = 'side'|--option sample_stride=32" "IndexCorpus._count_read = 'side'|--option sample_stride=8" "IndexCorpus._count_read = 'side'|--option rank_e=2" "IndexCorpus._count_read = 'side'|--option rank_e=4"; do
   i=$((i+1)); py="${v%%|*}"; opt="${v#*|}"
   timeout -k 10 300 python tools/ab_py.py "$py" $B $opt > $O/r06_2_ab_$i.json 2> $O/r06_2_ab_$i.err || { echo "fail: $v"; tail -3 $O/r06_2_ab_$i.err; exit 1; }
   python3 -c "
