@@ -15,6 +15,7 @@
 //
 // Index vectors are stored "segment padded": each level segment starts at a multiple of 4 f64 and
 // is zero-filled to a multiple of 4 (Lp columns), so every MFMA k-step lies inside one segment.
+#include <type_traits>
 #include "hq_common.h"
 
 #include <math.h>
@@ -4296,10 +4297,179 @@ __device__ __forceinline__ void rank_score(const RankArgs& a, const double* rq, 
   }
 }
 
+// ---- compile-time level structures of the cooperative scorers (LID 1: L = 64, 2: L = 32; 0: runtime) ----
+// With the structure known, every level loop and every pairwise sum unrolls: the per-level trip counts,
+// the n < 8 branches and the LDS offsets of each level become constants (k_rank_pairs' PMC, r05: 504 SALU
+// per wave, mostly the runtime loops over levels and values).  The arithmetic and its order are rank_score's.
+template <int LID> struct CoopT;
+template <> struct CoopT<1> {  // L = 64: levels [0, 32) [32, 40) [40, 43) [43, 44) [44, 64), Lp = 68
+  static constexpr int L = 64, Lp = 68, NSEG = 5;
+  static constexpr int len(int s) { return s == 0 ? 32 : s == 1 ? 8 : s == 2 ? 3 : s == 3 ? 1 : 20; }
+  static constexpr int src(int s) { return s == 0 ? 0 : s == 1 ? 32 : s == 2 ? 40 : s == 3 ? 43 : 44; }
+  static constexpr int poff(int s) { return s == 0 ? 0 : s == 1 ? 32 : s == 2 ? 40 : s == 3 ? 44 : 48; }
+};
+template <> struct CoopT<2> {  // L = 32: levels [0, 16) [16, 20) [20, 21) [21, 32), Lp = 36
+  static constexpr int L = 32, Lp = 36, NSEG = 4;
+  static constexpr int len(int s) { return s == 0 ? 16 : s == 1 ? 4 : s == 2 ? 1 : 11; }
+  static constexpr int src(int s) { return s == 0 ? 0 : s == 1 ? 16 : s == 2 ? 20 : 21; }
+  static constexpr int poff(int s) { return s == 0 ? 0 : s == 1 ? 16 : s == 2 ? 20 : 24; }
+};
+// the LID whose table equals the runtime structure, else 0
+static int coop_lid(const CoopSeg& c) {
+  auto same = [&](auto t) {
+    using T = decltype(t);
+    if (c.L != T::L || c.Lp != T::Lp || c.nseg != T::NSEG) return false;
+    for (int s = 0; s < T::NSEG; ++s)
+      if (c.len[s] != T::len(s) || c.src[s] != T::src(s) || c.poff[s] != T::poff(s)) return false;
+    return true;
+  };
+  if (opt(OPT_RANK_CT, 1) == 0) return 0;  // option rank_ct 0: the runtime-structure scorer (A/B, parity)
+  // (rank_ct 2: also in the short-list kernel k_rank_small)
+  if (same(CoopT<1>{})) return 1;
+  if (same(CoopT<2>{})) return 2;
+  return 0;
+}
+
+// coop_sum with n known at compile time (every loop unrolled; the same additions in the same order)
+template <typename T, int N, class F>
+__device__ __forceinline__ T coop_sum_n(const F& f, int j) {
+  T res;
+  if constexpr (N < 8) {
+    res = T(-0.0);
+#pragma unroll
+    for (int i = 0; i < N; ++i) res = res + f(i);
+  } else {
+    constexpr int LIM = N - (N % 8);
+    T r = f(j);
+#pragma unroll
+    for (int t = 1; t < LIM / 8; ++t) r = r + f(8 * t + j);
+    r = r + coop_xor<1>(r);
+    r = r + coop_xor<2>(r);
+    r = r + coop_xor<4>(r);
+    res = r;
+#pragma unroll
+    for (int i = LIM; i < N; ++i) res = res + f(i);
+  }
+  return T(0) + res;
+}
+
+// coop_level_sums for a level of M values (float64 sides: the candidate's z recomputed as (x - mean) / std;
+// float32 sides keep the runtime form)
+template <int M>
+__device__ __forceinline__ LevelStat coop_level_sums_n(const Side& q, const Side& c, int j) {
+  if (q.f32 || c.f32) return coop_level_sums(q, c, M, j);
+  LevelStat r;
+  r.qm = q.mean; r.qs = q.sd; r.qq = q.msq;
+  r.cm = c.mean; r.cs = c.sd; r.cq = c.msq;
+  r.both32 = 0;
+  r.sa = 0.0;
+  r.sb = 0.0;
+  if (q.sd == 0.0 || c.sd == 0.0) {
+    r.kind = 0;
+  } else {
+    auto f2 = [&](int k) -> Sum2<double> {
+      const double d = q.x[k] - c.x[k];
+      return Sum2<double>(side_z(q, k) * side_z(c, k), d * d);
+    };
+    const Sum2<double> s2 = coop_sum_n<Sum2<double>, M>(f2, j);
+    r.sa = s2.a;
+    r.sb = s2.b;
+    r.kind = 2;
+  }
+  return r;
+}
+
+// rank_score with the level structure of CoopT<LID> (LID > 0) — the same values, bit for bit
+template <int LID>
+__device__ __forceinline__ void rank_score_t(const RankArgs& a, const double* rq, double* rg, int64_t c, int j,
+                                             double* rec, double& e, int64_t& id) {
+  if constexpr (LID == 0) {
+    rank_score(a, rq, rg, c, j, rec, e, id);
+  } else {
+    using T = CoopT<LID>;
+    constexpr int L = T::L, Lp = T::Lp, NS = T::NSEG;
+    e = -__builtin_huge_val();
+    id = -1;
+    if (c < 0) return;
+    const bool all = !(a.mode == 0 && !a.det);  // every level (records / overall ranking), else level 0 only
+    LevelStat mine;
+    mine.kind = 0; mine.both32 = 0;
+    mine.qm = mine.qs = mine.qq = mine.cm = mine.cs = mine.cq = mine.sa = mine.sb = 0.0;
+    auto level = [&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      constexpr int m = T::len(s);
+      const double* qst = rq + L + Lp + 4 * s;
+      const double* cst = rg + L + 4 * s;
+      const LevelStat t = coop_level_sums_n<m>(
+          coop_side(rq + T::src(s), rq + L + T::poff(s), qst, m, (aux_bits(qst) & kAuxF32) != 0, j),
+          coop_side(rg + T::src(s), nullptr, cst, m, (aux_bits(cst) & kAuxF32) != 0, j), j);
+      if (j == s) mine = t;
+    };
+    level(std::integral_constant<int, 0>{});
+    if (all) {
+      level(std::integral_constant<int, 1>{});
+      level(std::integral_constant<int, 2>{});
+      level(std::integral_constant<int, 3>{});
+      if constexpr (NS > 4) level(std::integral_constant<int, 4>{});
+    }
+    const int nlev = all ? NS : 1;
+    int t32 = 0;
+    int mj = T::len(0);
+#pragma unroll
+    for (int s = 1; s < NS; ++s) mj = j == s ? T::len(s) : mj;
+    const double vj = j < nlev ? level_finish(mine, mj, &t32) : 0.0;
+    if (a.det && j < nlev) rec[1 + j] = vj;
+    wave_lds_sync();
+    if (j < nlev) {
+      rg[j] = vj;
+      reinterpret_cast<int*>(rg + 8)[j] = t32;
+    }
+    wave_lds_sync();
+    const double v0 = rg[0];
+    const int t0 = reinterpret_cast<const int*>(rg + 8)[0];
+    double ov = 0.0;
+    if (all) {
+      double tws = 0.0, tw = 0.0;
+      bool acc32 = false;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        // search_engine.py:191-230 typed running sum (exact_pair_rows)
+        const double v = rg[s];
+        const int ts = reinterpret_cast<const int*>(rg + 8)[s];
+        const double w = kLevelWeight[s];
+        const double term = ts ? (double)((float)v * (float)w) : v * w;
+        if (!acc32 && !ts) {
+          tws = tws + term;
+        } else {
+          tws = (double)((float)tws + (float)term);
+          acc32 = true;
+        }
+        tw = tw + w;
+      }
+      if (acc32) {
+        const float o = (float)tws / (float)tw;
+        ov = o < 1.0f ? (double)o : 1.0;
+      } else {
+        ov = tw > 0.0 ? tws / tw : 0.0;
+        ov = ov < 1.0 ? ov : 1.0;
+      }
+      ov = ov > 0.0 ? ov : 0.0;
+    }
+    if (a.det && j == 0) rec[0] = ov;
+    const double v = a.mode == 0 ? v0 : ov;
+    const int tm = a.thr_mode & (kThrKey32 - 1);
+    const bool pass = a.mode == 0 ? typed_pass(v, t0, a.thr, tm) : (tm == 0 || (tm == 1 ? v >= a.thr : v > a.thr));
+    if (pass) {
+      e = v;
+      id = c + a.id_base;
+    }
+  }
+}
+
 // Scoring pass: block (x-block, query) = 32 list entries of one query, one 8-lane group per entry, scores
 // and records to the workspace.  One pair per group, no loop: the occupancy hides the row latency.
-template <int PPL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_rank_pairs(RankArgs a) {
+template <int PPL, int LID = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LID == 2 ? 6 : 5))) void k_rank_pairs(RankArgs a) {
   extern __shared__ __attribute__((aligned(16))) double cm[];
   const int tid = threadIdx.x, g = tid >> 3, j = tid & 7;
   const int q = blockIdx.y, x = blockIdx.x * kCoopGroups + g;
@@ -4311,76 +4481,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   const int64_t e0 = (int64_t)q * a.kp + x;
   double e;
   int64_t id;
-  rank_score(a, rq, rg, c, j, a.ws_rec + e0 * (1 + a.cs.nseg), e, id);
+  rank_score_t<LID>(a, rq, rg, c, j, a.ws_rec + e0 * (1 + a.cs.nseg), e, id);
   if (j == 0) {
     a.ws_sc[e0] = e;
     a.ws_id[e0] = id;
-  }
-}
-
-// Scoring pass, E entries per group (option rank_e, default 2 for lists of >= 256 entries): block (x-block,
-// query) = 32 E list entries of one query; group g scores entries x0 + g + 32 e, e = 0 .. E - 1.  The next
-// entry's candidate row and statistics are requested into registers before the current entry is scored, so
-// a group always has one row gather in flight behind its arithmetic (k_rank_pairs leaves that overlap to the
-// other resident waves: 44% of its wave cycles waited, PMC r05), and the query row is staged once per 32 E
-// entries.  The scoring is rank_score's: bit-identical to k_rank_pairs.
-template <int PPL, int E>
-__global__ __launch_bounds__(256) void k_rank_pairs_e(RankArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double cm[];
-  const int tid = threadIdx.x, g = tid >> 3, j = tid & 7;
-  const int q = blockIdx.y, x0 = blockIdx.x * kCoopGroups * E + g;
-  double* rq = cm;
-  double* rg = cm + coop_qw(a.cs) + g * coop_rw(a.cs);
-  const int L = a.cs.L, Lp = a.cs.Lp, nseg = a.cs.nseg;
-  for (int e = tid; e < L; e += 256) rq[e] = a.Rq[(int64_t)q * L + e];
-  for (int e = tid; e < Lp; e += 256) rq[L + e] = a.Zq[(int64_t)q * Lp + e];
-  for (int e = tid; e < 4 * nseg; e += 256) rq[L + Lp + e] = a.Sq[(int64_t)q * nseg * 4 + e];
-  const int np_raw = L / 2, np_all = np_raw + 2 * nseg;
-  // the candidate (local row, -1: none) of list entry x; load: its pieces into registers (each lane's piece
-  // index clamped, every load unconditional: see rank_stage)
-  auto cand = [&](const int x) -> int64_t {
-    if (x >= a.kp) return -1;
-    const int64_t id = a.cid[(int64_t)q * a.kp + x];
-    const int64_t cc = id - a.id_base;
-    return (id >= 0 && cc >= 0 && cc < a.N) ? cc : -1;
-  };
-  auto load = [&](const int64_t cr, f64x2* v) {  // cr: a valid local row
-    const f64x2* rr = reinterpret_cast<const f64x2*>(a.Rc + cr * L);
-    const f64x2* rs = reinterpret_cast<const f64x2*>(a.Sc + cr * nseg * 4);
-#pragma unroll
-    for (int p = 0; p < PPL; ++p) {
-      const int pc = j + 8 * p < np_all ? j + 8 * p : np_all - 1;
-      v[p] = *(pc < np_raw ? rr + pc : rs + (pc - np_raw));
-    }
-  };
-  f64x2 v[PPL];
-  int64_t c = cand(x0);
-  if (c >= 0) load(c, v);
-  __syncthreads();  // the query row
-#pragma unroll 1
-  for (int e = 0; e < E; ++e) {
-    const int x = x0 + kCoopGroups * e;
-    if (x >= a.kp) break;  // group-uniform (the later entries are further out)
-    wave_lds_sync();       // the previous entry's reads of rg are done
-#pragma unroll
-    for (int p = 0; p < PPL; ++p) {
-      const int pc = j + 8 * p;
-      if (pc < np_all) reinterpret_cast<f64x2*>(rg)[pc] = v[p];
-    }
-    wave_lds_sync();
-    const int64_t cur = c;
-    if (e + 1 < E) {  // the next entry's row in flight while this one is scored
-      c = cand(x + kCoopGroups);
-      if (c >= 0) load(c, v);
-    }
-    const int64_t e0 = (int64_t)q * a.kp + x;
-    double sc;
-    int64_t id;
-    rank_score(a, rq, rg, cur, j, a.ws_rec + e0 * (1 + a.cs.nseg), sc, id);
-    if (j == 0) {
-      a.ws_sc[e0] = sc;
-      a.ws_id[e0] = id;
-    }
   }
 }
 
@@ -4589,7 +4693,7 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
 // (score desc, id asc) order is a rank count (each entry compares itself with the others), the outputs and
 // the proof as k_rank_sort.  Replaces k_refine_lds (one thread per entry walking its row: 20.6 us per
 // 1000-query batch).
-template <int PPL, int NG>
+template <int PPL, int NG, int LID = 0>
 __global__ __launch_bounds__(8 * NG) __attribute__((amdgpu_waves_per_eu(4))) void k_rank_small(RankArgs a, const double* __restrict__ cs, double eps,
                                                         double* __restrict__ os, int64_t* __restrict__ oid,
                                                         int* __restrict__ ocnt, int* __restrict__ ores,
@@ -4618,7 +4722,7 @@ __global__ __launch_bounds__(8 * NG) __attribute__((amdgpu_waves_per_eu(4))) voi
     if (g < kp) {
       double e;
       int64_t id;
-      rank_score(a, rq, rg, c, j, srec + g * W, e, id);
+      rank_score_t<LID>(a, rq, rg, c, j, srec + g * W, e, id);
       if (j == 0) {
         se[g] = e;
         sid[g] = id;
@@ -5463,7 +5567,22 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
                               : (ppl == 6 ? (const void*)k_rank_small<6, 64> : (const void*)k_rank_small<10, 64>);
     if (lds > 65536) HQ_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int c = count_empty ? 1 : 0;
-    if (ng == 32 && ppl == 6)
+    // compile-time level structures (L = 64, 32) here only with option rank_ct 2: at the 128-VGPR cap of this
+    // kernel the unrolled scorer spills (28 VGPRs for L = 64)
+    const int lid = ppl == 6 && opt(OPT_RANK_CT, 1) == 2 ? coop_lid(ra.cs) : 0;
+    if (lid == 1 && ng == 32)
+      hipLaunchKernelGGL((k_rank_small<6, 32, 1>), dim3(grid), dim3(256), lds, s, ra, cand_score, eps, out_score, out_id,
+                         out_count, out_resolved, c, out_redo, odet_s, next_redo, fo);
+    else if (lid == 2 && ng == 32)
+      hipLaunchKernelGGL((k_rank_small<6, 32, 2>), dim3(grid), dim3(256), lds, s, ra, cand_score, eps, out_score, out_id,
+                         out_count, out_resolved, c, out_redo, odet_s, next_redo, fo);
+    else if (lid == 1)
+      hipLaunchKernelGGL((k_rank_small<6, 64, 1>), dim3(grid), dim3(512), lds, s, ra, cand_score, eps, out_score, out_id,
+                         out_count, out_resolved, c, out_redo, odet_s, next_redo, fo);
+    else if (lid == 2)
+      hipLaunchKernelGGL((k_rank_small<6, 64, 2>), dim3(grid), dim3(512), lds, s, ra, cand_score, eps, out_score, out_id,
+                         out_count, out_resolved, c, out_redo, odet_s, next_redo, fo);
+    else if (ng == 32 && ppl == 6)
       hipLaunchKernelGGL((k_rank_small<6, 32>), dim3(grid), dim3(256), lds, s, ra, cand_score, eps, out_score, out_id,
                          out_count, out_resolved, c, out_redo, odet_s, next_redo, fo);
     else if (ng == 32)
@@ -5491,17 +5610,14 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
       ra.ws_id = reinterpret_cast<int64_t*>(w + (size_t)Q * kp * 8);
       ra.ws_rec = reinterpret_cast<double*>(w + (size_t)Q * kp * 16);
       const size_t lds = 8 * ((size_t)coop_qw(ra.cs) + (size_t)kCoopGroups * coop_rw(ra.cs));
-      // entries per group (option rank_e): 1 = k_rank_pairs (one pair per group, no loop)
-      const int re = (int)opt(OPT_RANK_E, 1);
-      if (re == 2 || re == 4) {
-        const dim3 ge((kp + kCoopGroups * re - 1) / (kCoopGroups * re), Q);
-        if (ppl == 6 && re == 2) hipLaunchKernelGGL((k_rank_pairs_e<6, 2>), ge, dim3(256), lds, s, ra);
-        else if (ppl == 6) hipLaunchKernelGGL((k_rank_pairs_e<6, 4>), ge, dim3(256), lds, s, ra);
-        else if (re == 2) hipLaunchKernelGGL((k_rank_pairs_e<10, 2>), ge, dim3(256), lds, s, ra);
-        else hipLaunchKernelGGL((k_rank_pairs_e<10, 4>), ge, dim3(256), lds, s, ra);
-      } else {
+      // (round 6: two or four entries per group with the next row in flight measured 5-10% slower at M = 100 /
+      // 1000 — profiles/r06_ab_count_read.txt, rank_e rows — the kernel was dropped)
+      {
         const dim3 g1((kp + kCoopGroups - 1) / kCoopGroups, Q);
-        if (ppl == 6) hipLaunchKernelGGL(k_rank_pairs<6>, g1, dim3(256), lds, s, ra);
+        const int lid = ppl == 6 ? coop_lid(ra.cs) : 0;  // compile-time level structures (L = 64, 32)
+        if (lid == 1) hipLaunchKernelGGL((k_rank_pairs<6, 1>), g1, dim3(256), lds, s, ra);
+        else if (lid == 2) hipLaunchKernelGGL((k_rank_pairs<6, 2>), g1, dim3(256), lds, s, ra);
+        else if (ppl == 6) hipLaunchKernelGGL(k_rank_pairs<6>, g1, dim3(256), lds, s, ra);
         else hipLaunchKernelGGL(k_rank_pairs<10>, g1, dim3(256), lds, s, ra);
       }
       HQ_CHECK_LAUNCH();

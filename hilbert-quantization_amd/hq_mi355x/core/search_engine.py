@@ -26,10 +26,12 @@ from .._compat import bases as _bases
 MAX_FUSED_K = 64     # list length of the f64 scans (hq_scan_topk)
 MAX_SPLIT_K = 1024   # list length of the split-f16 scans (k > 64: LDS-sorted pools, tiled re-rank)
 _FUSED_FINAL = True  # long lists: the final ranking inside the re-rank's sort (hq_refine_final_ws); False: A/B
-# How progressive_finish learns a batch's redo count: "side" — an event right after the re-rank on the batch's
-# stream, and the count read after it on a side stream (the search stream carries no copy: the copy and the
-# bubble behind it cost ~13 us per batch); "copy" — a pinned copy queued behind the re-rank (A/B)
-_COUNT_READ = "side"
+# How progressive_finish learns a batch's redo count: "copy" — a pinned copy queued behind the re-rank, read
+# after the event behind it; "side" — an event right after the re-rank and the count read after it on a side
+# stream (no copy on the search stream).  A/B, one box (profiles/r06_ab_count_read.txt): "side" measured
+# 2% (M = 20) to 7% (M = 100) slower — the host's extra copy and stream sync per finish outweigh the ~4 us
+# copy kernel it takes off the search stream — so "copy" stays the default.
+_COUNT_READ = "copy"
 _RING = 16  # redo counters per (device, stream, thread): a slot is re-cleared _RING - 1 batches later
 
 

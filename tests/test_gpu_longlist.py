@@ -223,17 +223,18 @@ def test_fused_query_prepare_equals_two_launches(hq_lib, hq_option, kind, coop):
     assert (a.f32, a.all32) == (b.f32, b.all32)
 
 
-@pytest.mark.parametrize("rank_e", [1, 2, 4])
+@pytest.mark.parametrize("rank_ct", [1, 0, 2])
 @pytest.mark.parametrize("L", [32, 64, 128])
 @pytest.mark.parametrize("kind", ["f64", "f32", "mixed"])
-def test_cooperative_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind, rank_e):
+def test_cooperative_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind, rank_ct):
     """The lane-cooperative long-list re-rank (k_refine_coop: 8 lanes per entry, NumPy's eight pairwise
     accumulators one per lane, rows staged per group) is bit-identical to the one-thread-per-entry kernel
     (option refine_coop = 0): progressive M = 100 / 1000 (level-0 ranking + [overall, level..] records),
     brute force k > 64 (overall ranking), frame scan (strict level-0); float64, float32 and mixed pools.
-    rank_e: list entries per 8-lane group (k_rank_pairs_e: the next entry's row gathered while one scores)."""
+    rank_ct 1 (default): the scorers specialised to the compile-time level structures of L = 64 / 32 (L = 128
+    keeps the runtime form); 0: the runtime-structure scorer everywhere; 2: also in the short-list kernel."""
     from hq_mi355x.core.search_engine import IndexCorpus
-    hq_option("rank_e", rank_e)
+    hq_option("rank_ct", rank_ct)
     C = _corpus(3000 if L == 128 else 20000, L, 41 + L)
     rng = np.random.default_rng(42)
     Q = np.concatenate([C[[1, 2, 20, 40]] + 0.0, C[100:108] + rng.normal(0, 0.01, (8, L)),
@@ -288,14 +289,17 @@ def test_fused_final_ranking_equals_two_steps(hq_lib, L, kind):
         assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (kind, L, a)
 
 
+@pytest.mark.parametrize("rank_ct", [1, 2])
 @pytest.mark.parametrize("kind", ["f64", "f32", "mixed"])
 @pytest.mark.parametrize("L", [32, 64, 128])
-def test_short_list_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind):
+def test_short_list_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind, rank_ct):
     """The fused short-list re-rank (k_rank_small: k_rank_pairs' lane groups and the ranking in one
     workgroup per query, lists of <= 64 entries) is bit-identical to k_refine_lds (option refine_small = 0):
     progressive M = 20 (28 entries: 32 groups) and M = 50 (58: 64 groups) with records, brute force top-10
-    (overall ranking), frame scan (strict level-0); float64, float32 and mixed pools, ties included."""
+    (overall ranking), frame scan (strict level-0); float64, float32 and mixed pools, ties included.
+    rank_ct 2: k_rank_small with the compile-time level structures of L = 64 / 32."""
     from hq_mi355x.core.search_engine import IndexCorpus
+    hq_option("rank_ct", rank_ct)
     C = _corpus(3000 if L == 128 else 20000, L, 51 + L)
     rng = np.random.default_rng(52)
     Q = np.concatenate([C[[1, 2, 20, 40]] + 0.0, C[100:108] + rng.normal(0, 0.01, (8, L)),
