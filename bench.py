@@ -576,6 +576,37 @@ def bench_search_strong(args, world, rank, dev):
     return res
 
 
+def summary(rec) -> dict:
+    """Every leg's rate and roofline fraction in a few hundred bytes (the full records precede it)."""
+    def r3(x):
+        return None if x is None else float(f"{x:.4g}")
+
+    def leg(d):
+        if not isinstance(d, dict) or "value" not in d:
+            return None
+        rf = d.get("roofline") or {}
+        return [r3(d["value"]), d.get("unit", "").replace("queries/sec", "qps").replace("embeddings/sec", "emb/s"),
+                r3(rf.get("frac"))]
+
+    out = {"headline": leg(rec)}
+    s = rec.get("search")
+    if isinstance(s, dict):
+        out["search_m20"] = leg(s)
+        for k, v in (s.get("modes") or {}).items():
+            if isinstance(v, dict) and "value" in v:
+                out[k] = leg(v)
+            elif isinstance(v, dict):  # fresh / clustered: QPS per list length
+                out[k] = {m: r3(x["value"]) for m, x in v.items() if isinstance(x, dict) and "value" in x}
+                wb = (v.get("m20") or {}).get("warmup_batch")
+                if wb:
+                    out[k]["m20_first_batch_ms"] = r3(wb.get("wall_ms"))
+        out["strong_cfg4"] = leg(s.get("strong"))
+    for k in ("frames", "precomputed", "stream", "ingest"):
+        if k in rec:
+            out[k] = leg(rec[k])
+    return out
+
+
 def progressive_rate(engine, Q, M, steps, world, k=10, threshold=0.1):
     """Pipelined progressive search of one query batch per step (two batches in flight, as the cfg3 leg),
     with the engine's redo counters (IndexCorpus.stats) over the timed batches: queries re-scanned with a
@@ -968,6 +999,7 @@ def main():
         if "precomputed" in rec:
             rec["precomputed"]["cpu_baseline"] = cpu_baseline_precomputed(d, args.cpu_seconds / 2)
     if rank == 0:
+        rec["summary"] = summary(rec)  # last key: the end of the line a driver's short stdout tail keeps
         print(json.dumps(rec), flush=True)
     if world > 1:
         import torch.distributed as dist
