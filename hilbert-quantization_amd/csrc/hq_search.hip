@@ -6047,7 +6047,7 @@ __device__ __forceinline__ void ov_bound(const flt4* acc, const float* wia, floa
 // a drain gate on the model at G_hihi + slack before the split measured slower, 0.69M, as did keeping
 // G_hihi in the queue: the kernel is not bound by the drain's split recompute).  The f16 scaling errs by <= 2^-11 s_i sum|q c| <= 2^-11 s_i m_i
 // in each part (Cauchy-Schwarz on unit-variance vectors), folded into bsum with the hi.hi slack.
-template <int LID, int OCC, bool HI = true, bool LIN = HI, int PF = 1, bool ANY = true>
+template <int LID, int OCC, bool HI = true, bool LIN = HI, int PF = 1>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_scanov(OvArgs a) {
   using T = OvT<LID>;
   constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, NB = kOvQW / 16, GS = 16 * NG + 4 * NC + 8;
@@ -6266,15 +6266,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
       ov_bound<T>(acc, wia[b], bsum[b], o, qv[b], tolq[b], cur.cv, cur.ro, U);
 #pragma unroll
       for (int r = 0; r < 4; ++r) W[r] = wt[b];
-    }
-    // ANY (default): one ballot over the block's four rows first, so the common case (no row of the block
-    // passes) takes one compare-and-branch, and the four rows' bound chains are independent (per-row
-    // branches serialised them: each row's add chain, compare and branch ran before the next row's)
-    if constexpr (ANY) {
-      bool anyp = false;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) anyp |= U[r] >= W[r];
-      if (__builtin_amdgcn_ballot_w64(anyp) == 0ull) return;  // (qn < 64 holds: nothing was queued)
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -6632,9 +6623,10 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
     hipLaunchKernelGGL((k_scanov<LID, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else if (oocc == 3) {
     hipLaunchKernelGGL((k_scanov<LID, 3>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
-  } else if (opt(OPT_OV_ANY, 1) == 0) {  // option ov_any 0: a compare-and-branch per row (round-5 form, A/B)
-    hipLaunchKernelGGL((k_scanov<LID, 4, true, true, 1, false>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else {
+    // (round 6: one ballot over a block's four rows before the per-row queueing — the rows' bound chains
+    // independent — pushed this kernel past its 128-VGPR budget at 4 waves per SIMD and spilled: 873 ->
+    // 2420 us per 1000 x 1M scan, profiles/r06_ab_rank_ct.txt; not kept)
     hipLaunchKernelGGL((k_scanov<LID, 4>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   }
   HQ_CHECK_LAUNCH();

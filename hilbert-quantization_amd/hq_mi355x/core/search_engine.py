@@ -104,6 +104,10 @@ def combine_levels(lv: np.ndarray, both32: bool) -> np.ndarray:
     return np.maximum(0.0, np.minimum(1.0, out))
 
 
+_REDO_WARM = False  # IndexCorpus._warm_redo ran in this process
+_WARM_LOCK = threading.Lock()
+
+
 def _lock(obj):
     """The object's lock (created on first use; dict.setdefault is atomic under the GIL)."""
     lk = obj.__dict__.get("_lock_")
@@ -163,6 +167,28 @@ class IndexCorpus:
         self._built_on = K.stream()
         self._ready = torch().cuda.Event()
         self._ready.record()
+        self._warm_redo(x)
+
+    def _warm_redo(self, x):
+        """Once per process, with the first corpus built: one 1-query progressive batch whose list is marked
+        unproven, so the redo path (the longer-list retry, its re-rank, the torch selections and scatters
+        around them) runs once at build time.  ROCm loads a kernel's code object on its first launch (several
+        ms per torch kernel), and without this the first batch that needs a redo paid that for a dozen kernels:
+        57 ms against 1.2 ms warm for the clustered corpus's first batch (profiles/r06_cold_batch.txt)."""
+        global _REDO_WARM
+        M = 20  # HilbertQuantizer's max_candidates_per_level
+        with _WARM_LOCK:
+            if _REDO_WARM or self.N <= M or M + self.SLACK > self._max_list(0) or self.dense_only \
+                    or not self._fused_ok(0) or self._retry_len(0, M + self.SLACK) is None:
+                return
+            _REDO_WARM = True
+        p = self.progressive_submit(x[:1], 10, 0.1, M)
+        if p.done is None and p.ring is None:
+            p.event.synchronize()
+            p.res.zero_()           # the batch's one list "unproven": the retry path runs
+            p.nredo[0] = 1
+            self.progressive_finish(p)
+        self.reset_stats()
 
     def prepare_queries(self, queries, row_f32=None) -> "K.Prepared":
         """queries: [Q, L] (or [L]); a pair (array, per-row float32 flags) for mixed-dtype batches."""
