@@ -2704,16 +2704,34 @@ __global__ __launch_bounds__(64) void k_sample_topg(SampleArgs a) {
       cf1[1] = cfn[1];
     }
   }
-  // epilogue: exact f32 model scores of the selected rows, the stream's kTopT best to the pool
+  // epilogue: exact f32 model scores of the selected rows, the stream's kTopT best to the pool.  Every
+  // statistic is requested before any is used (one round trip): the four rows a lane scores per block are rows
+  // 4g .. 4g + 3 of one sampled tile (steps start at tile boundaries), i.e. one SoA group of Sc32 — four
+  // 16-byte loads; the query's four values likewise.  (The per-row form — flag load, test, then the row's
+  // values — chained ~40 dependent loads through the epilogue: 82 waits, profiles/r06_pmc_sample_topg.txt.)
   const float c1f = (float)a.c1;
   const int ns = 4 * a.nchunks;
+  flt4 qs4[4], sd4[4], mn4[4], ms4[4], fl4[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int q = q0 + 16 * b + j;
+    const int qq = q < a.Q ? q : 0;
+    const int64_t gq = (int64_t)(qq >> 2) * 16 + (qq & 3);  // SoA-per-4 statistics
+    qs4[b] = flt4{a.Sq32[gq], a.Sq32[gq + 4], a.Sq32[gq + 8], a.Sq32[gq + 12]};
+    const int64_t row0 = row_of((int64_t)(bcs[b] >= 0 ? bcs[b] : c_begin) + 4 * g);  // a multiple of 4
+    const float* st = a.Sc32 + (row0 >> 2) * 16;
+    HQ_GUARD(st, a.Sc32, pack0_rows(a.N) * 4 - 16);
+    sd4[b] = *reinterpret_cast<const flt4*>(st);
+    mn4[b] = *reinterpret_cast<const flt4*>(st + 4);
+    ms4[b] = *reinterpret_cast<const flt4*>(st + 8);
+    fl4[b] = *reinterpret_cast<const flt4*>(st + 12);
+  }
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     const int q = q0 + 16 * b + j;
     if (q >= a.Q) continue;
-    const int64_t gq = (int64_t)(q >> 2) * 16 + (q & 3);  // SoA-per-4 statistics
-    const float qA = (float)(0.6 * a.inv_m) * a.Sq32[gq], qB = 0.6f * a.Sq32[gq + 4], qQ = a.Sq32[gq + 8];
-    const bool qok = __float_as_int(a.Sq32[gq + 12]) == 0;
+    const float qA = (float)(0.6 * a.inv_m) * qs4[b][0], qB = 0.6f * qs4[b][1], qQ = qs4[b][2];
+    const bool qok = __float_as_int(qs4[b][3]) == 0;
     float top[kTopT];
 #pragma unroll
     for (int t = 0; t < kTopT; ++t) top[t] = -1.0f;
@@ -2724,13 +2742,10 @@ __global__ __launch_bounds__(64) void k_sample_topg(SampleArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int64_t i = (int64_t)bcs[b] + 4 * g + r;
         if (i >= c_end) continue;
-        const int64_t row = row_of(i);
-        const float* st = a.Sc32 + (row >> 2) * 16 + (row & 3);
-        HQ_GUARD(st, a.Sc32, pack0_rows(a.N) * 4 - 13);
-        if (__float_as_int(st[12]) != 0) continue;  // flagged / pad row
+        if (__float_as_int(fl4[b][r]) != 0) continue;  // flagged / pad row
         const float G = Gs[r];
-        const float num = fmaf(G, qA * st[0], qB * st[4]);
-        float t = num * __builtin_amdgcn_rcpf(qQ + st[8]);
+        const float num = fmaf(G, qA * sd4[b][r], qB * mn4[b][r]);
+        float t = num * __builtin_amdgcn_rcpf(qQ + ms4[b][r]);
         t = t > 0.0f ? t : 0.0f;
         float sc = fmaf(G, c1f, 0.35f) + t;
         sc = sc < 1.0f ? sc : 1.0f;
