@@ -2205,20 +2205,25 @@ __global__ __launch_bounds__(64) void k_pool_select(float* pool_s, int* pool_i, 
     // fcount != null (k_scan0g): the corpus's flagged rows against this query first (lanes over the
     // rows), appended to the pool before it is read; pool_n is then read with an
     // L1-bypassing load (the appends are L2 atomics)
+    // the flagged-row count, the pool count and the query's flag word are requested together (one round
+    // trip; the pool count is read again after flagged appends, which are rare)
+    const int nfl = fcount ? *fcount : 0;
+    int pn = fcount ? __hip_atomic_load(pool_n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : pool_n[q];
+    const int qfw = qflag ? __float_as_int(qflag[(int64_t)q * qstride]) : 0;
     if (fcount) {
       const QConst* qc = reinterpret_cast<const QConst*>(fa.qconst);
-      const int n = *fcount;
-      if (n > 0 && __float_as_int(qc[q].flag) == 0) {
+      const bool app = nfl > 0 && __float_as_int(qc[q].flag) == 0;
+      if (app) {
         const QConst c = qc[q];
-        for (int i = lane; i < n; i += 64) flagged_pair(fa, c, q, flist[i]);
+        for (int i = lane; i < nfl; i += 64) flagged_pair(fa, c, q, flist[i]);
       }
       __syncthreads();
+      if (app) pn = __hip_atomic_load(pool_n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const int pn = fcount ? __hip_atomic_load(pool_n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : pool_n[q];
     // k_scan0g / k_scanov (qflag: the query's flag word in its constants, qstride floats apart): a flagged
     // query (not scanned) or an overflowing pool -> every slot +inf / -1, which the exact re-rank reads
     // as unresolved (the caller's dense exact path answers the query)
-    if (qflag && (__float_as_int(qflag[(int64_t)q * qstride]) != 0 || pn > cap)) {
+    if (qflag && (qfw != 0 || pn > cap)) {
       for (int x = lane; x < K; x += 64) {
         out_score[(int64_t)q * K + x] = __builtin_huge_val();
         out_id[(int64_t)q * K + x] = -1;
@@ -4208,14 +4213,27 @@ template <int PPL>
 __device__ __forceinline__ int64_t rank_stage(const RankArgs& a, double* rq, double* rg, int q, int x, int tid, int nt,
                                               int j) {
   const int L = a.cs.L, Lp = a.cs.Lp, nseg = a.cs.nseg;
-  for (int e = tid; e < L; e += nt) rq[e] = a.Rq[(int64_t)q * L + e];
-  for (int e = tid; e < Lp; e += nt) rq[L + e] = a.Zq[(int64_t)q * Lp + e];
-  for (int e = tid; e < 4 * nseg; e += nt) rq[L + Lp + e] = a.Sq[(int64_t)q * nseg * 4 + e];
+  // the query row, normalised row and statistics (QW = L + Lp + 4 nseg values; one value per thread when
+  // QW <= nt, the cooperative shapes' case) and this group's list entry are requested together: one round trip
+  // before the candidate's row (loop-per-array stores waited for each array in turn: 4 round trips)
+  const int QW = L + Lp + 4 * nseg;
+  const int64_t idr = x < a.kp ? a.cid[(int64_t)q * a.kp + x] : -1;
+  if (QW <= nt) {
+    if (tid < QW) {
+      const double* src = tid < L ? a.Rq + (int64_t)q * L + tid
+                        : tid < L + Lp ? a.Zq + (int64_t)q * Lp + (tid - L)
+                                       : a.Sq + (int64_t)q * nseg * 4 + (tid - L - Lp);
+      rq[tid] = *src;
+    }
+  } else {
+    for (int e = tid; e < L; e += nt) rq[e] = a.Rq[(int64_t)q * L + e];
+    for (int e = tid; e < Lp; e += nt) rq[L + e] = a.Zq[(int64_t)q * Lp + e];
+    for (int e = tid; e < 4 * nseg; e += nt) rq[L + Lp + e] = a.Sq[(int64_t)q * nseg * 4 + e];
+  }
   int64_t c = -1;
   if (x < a.kp) {
-    const int64_t id = a.cid[(int64_t)q * a.kp + x];
-    const int64_t cc = id - a.id_base;
-    if (id >= 0 && cc >= 0 && cc < a.N) c = cc;
+    const int64_t cc = idr - a.id_base;
+    if (idr >= 0 && cc >= 0 && cc < a.N) c = cc;
   }
   if (c >= 0) {
     const int np_raw = L / 2, np_all = np_raw + 2 * nseg;
