@@ -4523,18 +4523,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LID == 2 ? 
 
 // the count and the completeness proof of query q's re-ranked list (refine_big_body): n valid entries, kth
 // the k-th exact score (-inf when n < k); the last list slot's approximate score + eps must stay below it
-__device__ __forceinline__ void rank_resolve(const RankArgs& a, const double* __restrict__ cs, double eps, int q,
+// last_id / last_cs: the list's last slot (cid, approximate score), loaded by the caller ahead of time
+__device__ __forceinline__ void rank_resolve(const RankArgs& a, double last_cs, int64_t last_id, double eps, int q,
                                              int n, bool k32, int thr_mode, double kth, int cnt, int* ocnt,
                                              int* ores, int count_empty, int* oredo) {
-  const int64_t base = (int64_t)q * a.kp;
-  const int kp = a.kp, k = a.k;
+  const int k = a.k;
   ocnt[q] = cnt;
-  const bool full = a.cid[base + kp - 1] >= 0;
+  const bool full = last_id >= 0;
   // an empty last slot with score +inf: the scan's list may be incomplete (k_pool_select)
-  const bool trunc = !full && cs[base + kp - 1] == __builtin_huge_val();
+  const bool trunc = !full && last_cs == __builtin_huge_val();
   int res = trunc ? 0 : 1;
   if (full) {
-    const double bound = cs[base + kp - 1] + eps;
+    const double bound = last_cs + eps;
     if (n >= k) res = k32 ? (float)bound < (float)kth : bound < kth;
     else if (thr_mode == 0) res = 0;
     else res = thr_mode == 1 ? (bound < thr_low(a.thr)) : (bound <= thr_low(a.thr));
@@ -4579,6 +4579,9 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
   const int thr_mode = a.thr_mode & (kThrKey32 - 1);
   for (int q = blockIdx.x; q < a.Q; q += gridDim.x) {
     const int64_t base = (int64_t)q * kp;
+    // the proof's inputs (the list's last slot) requested with the workspace reads, not after the sort
+    const double last_cs = tid == 0 ? cs[base + kp - 1] : 0.0;
+    const int64_t last_id = tid == 0 ? a.cid[base + kp - 1] : -1;
     int nv = 0;
     for (int x = tid; x < n2; x += NT) {
       const int64_t i = x < kp ? a.ws_id[base + x] : -1;
@@ -4632,8 +4635,8 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
       }
     }
     if (tid == 0)
-      rank_resolve(a, cs, eps, q, n, k32, thr_mode, n >= k ? se[k - 1] : -__builtin_huge_val(), cnt, ocnt, ores,
-                   count_empty, oredo);
+      rank_resolve(a, last_cs, last_id, eps, q, n, k32, thr_mode, n >= k ? se[k - 1] : -__builtin_huge_val(), cnt,
+                   ocnt, ores, count_empty, oredo);
     __syncthreads();
     if (fin.id) {
       // survivors' overall keys in level-0 order (se is free: the proof has read se[k - 1])
@@ -4749,7 +4752,15 @@ __global__ __launch_bounds__(8 * NG) __attribute__((amdgpu_waves_per_eu(4))) voi
   int* pos = reinterpret_cast<int*>(srec + NG * W);
   int* fpos = pos + NG;  // final ranking: survivor position by final rank
   __shared__ int red[NG / 8];
+  __shared__ double s_last_cs;
+  __shared__ int64_t s_last_id;
   for (int q = blockIdx.x; q < a.Q; q += gridDim.x) {
+    // the proof's inputs (the list's last slot) requested with the staging loads, not after the ranking, and
+    // parked in LDS (registers are this kernel's limit)
+    if (tid == 0) {
+      s_last_cs = cs[(int64_t)q * kp + kp - 1];
+      s_last_id = a.cid[(int64_t)q * kp + kp - 1];
+    }
     const int64_t c = rank_stage<PPL>(a, rq, rg, q, g, tid, NT, j);
     __syncthreads();
     if (g < kp) {
@@ -4794,7 +4805,7 @@ __global__ __launch_bounds__(8 * NG) __attribute__((amdgpu_waves_per_eu(4))) voi
         odet[(int64_t)q * k * W + t] = r < cnt ? srec[pos[r] * W + w] : 0.0;
       }
     if (tid == 0)
-      rank_resolve(a, cs, eps, q, n, k32, thr_mode, n >= k ? se[pos[k - 1]] : -__builtin_huge_val(), cnt, ocnt,
+      rank_resolve(a, s_last_cs, s_last_id, eps, q, n, k32, thr_mode, n >= k ? se[pos[k - 1]] : -__builtin_huge_val(), cnt, ocnt,
                    ores, count_empty, oredo);
     if (fin.id) {
       // fused final ranking (k_progressive_final's order: overall desc, level-0 position asc) by rank counting
@@ -6080,7 +6091,7 @@ __device__ __forceinline__ void ov_bound(const flt4* acc, const float* wia, floa
 // a drain gate on the model at G_hihi + slack before the split measured slower, 0.69M, as did keeping
 // G_hihi in the queue: the kernel is not bound by the drain's split recompute).  The f16 scaling errs by <= 2^-11 s_i sum|q c| <= 2^-11 s_i m_i
 // in each part (Cauchy-Schwarz on unit-variance vectors), folded into bsum with the hi.hi slack.
-template <int LID, int OCC, bool HI = true, bool LIN = HI, int PF = 1>
+template <int LID, int OCC, bool HI = true, bool LIN = HI, int PF = 1, bool ANY = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_scanov(OvArgs a) {
   using T = OvT<LID>;
   constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, NB = kOvQW / 16, GS = 16 * NG + 4 * NC + 8;
@@ -6299,6 +6310,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
       ov_bound<T>(acc, wia[b], bsum[b], o, qv[b], tolq[b], cur.cv, cur.ro, U);
 #pragma unroll
       for (int r = 0; r < 4; ++r) W[r] = wt[b];
+    }
+    // ANY (option ov_any, with ov_occ 3): one ballot over the block's four rows first (the common case — no row
+    // passes — is one compare-and-branch, and the rows' bound chains are independent); at 4 waves per SIMD its
+    // longer live ranges spilled (873 -> 2420 us, profiles/r06_ab_rank_ct.txt), so it exists at 3 only
+    if constexpr (ANY) {
+      bool anyp = false;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) anyp |= U[r] >= W[r];
+      if (__builtin_amdgcn_ballot_w64(anyp) == 0ull) return;  // (qn < 64 holds: nothing was queued)
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -6654,6 +6674,8 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
     else hipLaunchKernelGGL((k_scanov<LID, 4, true, true, 3>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else if (oocc == 2) {
     hipLaunchKernelGGL((k_scanov<LID, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
+  } else if (oocc == 3 && opt(OPT_OV_ANY, 0) == 1) {
+    hipLaunchKernelGGL((k_scanov<LID, 3, true, true, 1, true>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else if (oocc == 3) {
     hipLaunchKernelGGL((k_scanov<LID, 3>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else {

@@ -606,6 +606,10 @@ def test_overall_split_scan_matches_f64_scan(hq_lib, hq_option, N, L):
     hq_option("ov_occ", 3)                         # the 3-waves-per-SIMD build of k_scanov
     occ3 = [_np(x) for x in corpus.exact_topk(qp, 1, k)[:3]]
     assert np.array_equal(got[1], occ3[1]) and np.array_equal(got[0], occ3[0])
+    hq_option("ov_any", 1)                         # ... with one ballot per block of rows: the same scan lists
+    sc0, ids0, _, _ = K_.scan_topk(qp, corpus.prep, 1, k + corpus.SLACK, -corpus.EPS, 0)
+    assert np.array_equal(_np(ids0), _np(ids)) and np.array_equal(_np(sc0).view(np.uint8), _np(sc).view(np.uint8))
+    hq_option("ov_any", None)
     hq_option("ov_occ", None)
     hq_option("scan_v1", 1)
     ref = [_np(x) for x in corpus.exact_topk(qp, 1, k)[:3]]
