@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--option", action="append", default=[],
                     help="name=value: select a kernel variant (hq_set_option; A/B runs only)")
+    ap.add_argument("--py-set", action="append", default=[],
+                    help="module:attribute=int: a host-side variant, e.g. hq_mi355x.kernels:FINAL_LEVEL0_LISTS=1 "
+                         "(A/B runs only)")
     return ap.parse_args()
 
 
@@ -795,6 +798,11 @@ def main():
         for o in args.option:
             name, value = o.split("=", 1)
             _lib.set_option(name, int(value))
+    for o in args.py_set:  # host-side variants: module:attribute=int (A/B runs only)
+        import importlib
+        target, value = o.split("=", 1)
+        mod, attr = target.split(":", 1)
+        setattr(importlib.import_module(mod), attr, type(getattr(importlib.import_module(mod), attr))(int(value)))
     from hq_mi355x.core.pipeline import quantize_batch
 
     dev = torch.device("cuda", torch.cuda.current_device())

@@ -3981,6 +3981,7 @@ __global__ __launch_bounds__(256) void k_refine_big_raw(HQ_REFINE_ARGS, int tb) 
 // 1 / (level + 1) of the overall score's weights (search_engine.py:191-230), folded at compile time
 __device__ constexpr double kLevelWeight[8] = {1.0 / 1.0, 1.0 / 2.0, 1.0 / 3.0, 1.0 / 4.0, 1.0 / 5.0, 1.0 / 6.0, 1.0 / 7.0, 1.0 / 8.0};
 constexpr int kFinalRounds = 32;  // final rankings of <= 32 outputs may take arg-max rounds instead of a sort
+constexpr int kSelRounds = 16;    // fused final ranking without level-0 lists: n - k + 1 rounds instead of the sort
 constexpr int kCoopGroups = 32;              // 8-lane groups per 256-thread workgroup
 constexpr int kCoopMaxW = 7;                 // record width 1 + nseg
 
@@ -4596,6 +4597,102 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
     int n = 0;
 #pragma unroll
     for (int w = 0; w < NT / 64; ++w) n += red[w];
+    // Fused final ranking without the level-0 lists (os == null): the level-0 order is needed only to drop the
+    // n - k lowest valid entries, to name the k-th (the proof) and to break ties of the overall score, so when
+    // n - k + 1 is small (lists of M + slack entries: <= slack + 1) it is found by that many workgroup rounds
+    // of the order's last entry instead of sorting all kp; the final ranking then takes outn rounds of the
+    // first (overall desc, level-0 order asc) survivor — the level-0 order of two entries read from their
+    // (key, id) directly.  The same outputs as the sort path.
+    constexpr int E = kMaxTopKBig / NT;
+    if (!os && fin.id && fin.rounds && fin.K <= kFinalRounds && n - k + 1 <= kSelRounds) {
+      // level-0 order of list entries x, y (workspace positions): valid first, key desc, id asc
+      auto before = [&](int x, int y) -> bool {
+        if (x < 0) return false;
+        if (y < 0) return true;
+        const int64_t ix = sid[x], iy = sid[y];
+        if (iy < 0) return ix >= 0;
+        const double kx = key_of(se[x], k32), ky = key_of(se[y], k32);
+        return ix >= 0 && (kx > ky || (kx == ky && ix < iy));
+      };
+      // workgroup arg-best over the live entries (live: bit e of `live` for entry tid + NT e) under `better`
+      int live = 0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) live |= (tid + NT * e < kp && sid[tid + NT * e] >= 0 ? 1 : 0) << e;
+      int rnd = 0;  // rounds so far (alternating reduction buffers)
+      auto arg_best = [&](auto better) -> int {
+        int bi = -1;
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (((live >> e) & 1) && better(tid + NT * e, bi)) bi = tid + NT * e;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int i2 = __shfl_xor(bi, o, 64);
+          if (better(i2, bi)) bi = i2;
+        }
+        if (lane == 0) ri[rnd & 1][wave] = bi;
+        __syncthreads();  // (the other buffer is rewritten only after the next round's barrier)
+        int b = ri[rnd & 1][0];
+#pragma unroll
+        for (int w = 1; w < NT / 64; ++w)
+          if (better(ri[rnd & 1][w], b)) b = ri[rnd & 1][w];
+        ++rnd;
+        return b;
+      };
+      const int cnt = n < k ? n : k;
+      int kth_x = -1;
+      if (n >= k) {
+        // n - k + 1 rounds of the order's last live entry: the first n - k leave (not survivors), the last is
+        // the k-th of the level-0 order
+        for (int r = 0; r <= n - k; ++r) {
+          const int x = arg_best([&](int u, int v) { return u >= 0 && (v < 0 || before(v, u)); });
+          if (r < n - k) {
+            if (x >= 0 && x % NT == tid) live &= ~(1 << (x / NT));
+          } else {
+            kth_x = x;
+          }
+        }
+      }
+      if (tid == 0)
+        rank_resolve(a, last_cs, last_id, eps, q, n, k32, thr_mode, kth_x >= 0 ? se[kth_x] : -__builtin_huge_val(),
+                     cnt, ocnt, ores, count_empty, oredo);
+      // the survivors' overall keys, in registers; outn rounds of the first (overall desc, level-0 order)
+      const double* __restrict__ rec = a.ws_rec;
+      double ov[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) ov[e] = ((live >> e) & 1) ? key_of(rec[(base + tid + NT * e) * W], k32) : 0.0;
+      __shared__ double ovs[kMaxTopKBig];  // the same keys by position (tie-breaks read them across threads)
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if ((live >> e) & 1) ovs[tid + NT * e] = ov[e];
+      __syncthreads();
+      const int outn = cnt < fin.K ? cnt : fin.K;
+      for (int r = 0; r < outn; ++r) {
+        const int x = arg_best([&](int u, int v) {
+          if (u < 0) return false;
+          if (v < 0) return true;
+          const double ou = ovs[u], ow = ovs[v];
+          return ou > ow || (ou == ow && before(u, v));
+        });
+        if (x >= 0 && x % NT == tid) live &= ~(1 << (x / NT));
+        if (tid == 0) fpos[r] = x;
+      }
+      __syncthreads();
+      for (int t = tid; t < fin.K * W; t += NT) {
+        const int r = t / W, w = t - r * W;
+        double val = 0.0;
+        if (r < outn) {
+          const int x = fpos[r];
+          val = rec[(base + x) * W + w];
+          if (w == 0) fin.id[(int64_t)q * fin.K + r] = sid[x];
+        } else if (w == 0) {
+          fin.id[(int64_t)q * fin.K + r] = -1;
+        }
+        fin.det[(int64_t)q * fin.K * W + t] = val;
+      }
+      if (tid == 0) fin.count[q] = outn;
+      __syncthreads();
+      continue;
+    }
     lds_bitonic(n2,
                 [&](int x, int y) {
                   const int64_t ix = sid[x], iy = sid[y];
@@ -4615,10 +4712,11 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
                   pos[y] = tp;
                 });
     const int cnt = n < k ? n : k;
-    for (int r = tid; r < k; r += NT) {
-      os[(int64_t)q * k + r] = r < cnt ? se[r] : -__builtin_huge_val();
-      oid[(int64_t)q * k + r] = r < cnt ? sid[r] : -1;
-    }
+    if (os)  // (the fused final ranking may go without the level-0 lists: hq_refine_final_ws)
+      for (int r = tid; r < k; r += NT) {
+        os[(int64_t)q * k + r] = r < cnt ? se[r] : -__builtin_huge_val();
+        oid[(int64_t)q * k + r] = r < cnt ? sid[r] : -1;
+      }
     if (odet) {  // records gathered by list position, four loads in flight per thread before the stores
       const double* __restrict__ rec = a.ws_rec;
       const int tot = k * W;
@@ -4795,10 +4893,11 @@ __global__ __launch_bounds__(8 * NG) __attribute__((amdgpu_waves_per_eu(4))) voi
 #pragma unroll
     for (int w = 0; w < NG / 8; ++w) n += red[w];
     const int cnt = n < k ? n : k;
-    for (int r = tid; r < k; r += NT) {
-      os[(int64_t)q * k + r] = r < cnt ? se[pos[r]] : -__builtin_huge_val();
-      oid[(int64_t)q * k + r] = r < cnt ? sid[pos[r]] : -1;
-    }
+    if (os)  // (the fused final ranking may go without the level-0 lists: hq_refine_final_ws)
+      for (int r = tid; r < k; r += NT) {
+        os[(int64_t)q * k + r] = r < cnt ? se[pos[r]] : -__builtin_huge_val();
+        oid[(int64_t)q * k + r] = r < cnt ? sid[pos[r]] : -1;
+      }
     if (odet)
       for (int t = tid; t < k * W; t += NT) {
         const int r = t / W, w = t - r * W;
@@ -6895,7 +6994,8 @@ int hq_refine_final_ws(const double* Rq, const double* Zq, const double* Sq, int
     if (next_redo) HQ_CHECK_HIP(hipMemsetAsync(next_redo, 0, sizeof(int), (hipStream_t)stream));
     return HQ_OK;
   }
-  if (!Rq || !Zq || !Sq || !cand_score || !cand_id || !out_score || !out_id || !out_count || !out_resolved ||
+  // out_score / out_id may both be null: the level-0 lists are then not written
+  if (!Rq || !Zq || !Sq || !cand_score || !cand_id || (!out_score != !out_id) || !out_count || !out_resolved ||
       !fin_id || !fin_det || !fin_count || (big && !workspace) || (next_redo && (!out_redo || out_redo == next_redo)) ||
       (N > 0 && (!Rc || !Zc || !Sc)))
     return fail(HQ_E_INVALID, "null buffer");

@@ -475,6 +475,9 @@ def _refine_ws(q, c, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps,
          exc)
 
 
+FINAL_LEVEL0_LISTS = False  # refine_final_ws: also write the (unreturned) level-0 lists (A/B of the sort they need)
+
+
 def refine_final_ws(q: Prepared, c: Prepared, cand_score, cand_id, k: int, threshold: float, thr_mode: int,
                     eps: float, id_base: int, K_out: int, redo=None, next_redo=None, exc=None):
     """The level-0 re-rank of a progressive search with its final ranking fused in (hq_refine_final_ws):
@@ -490,8 +493,9 @@ def refine_final_ws(q: Prepared, c: Prepared, cand_score, cand_id, k: int, thres
     if rc == _lib.HQ_E_UNSUPPORTED:
         return None
     _chk(rc, exc)
-    os_ = t.empty((Q, k), dtype=t.float64, device=dev)
-    oi = t.empty((Q, k), dtype=t.int64, device=dev)
+    # the level-0 lists are not returned: not written (FINAL_LEVEL0_LISTS = True keeps them, the A/B form)
+    os_ = t.empty((Q, k), dtype=t.float64, device=dev) if FINAL_LEVEL0_LISTS else None
+    oi = t.empty((Q, k), dtype=t.int64, device=dev) if FINAL_LEVEL0_LISTS else None
     cnt = t.empty(Q, dtype=t.int32, device=dev)
     res = t.empty(Q, dtype=t.int32, device=dev)
     fid = t.empty((Q, K_out), dtype=t.int64, device=dev)

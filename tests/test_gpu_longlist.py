@@ -258,13 +258,18 @@ def test_cooperative_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind,
         assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (kind, L, a)
 
 
+@pytest.mark.parametrize("lists", [False, True])
 @pytest.mark.parametrize("kind", ["f64", "f32", "mixed"])
 @pytest.mark.parametrize("L", [32, 64, 128])
-def test_fused_final_ranking_equals_two_steps(hq_lib, L, kind):
+def test_fused_final_ranking_equals_two_steps(hq_lib, L, kind, lists):
     """Long lists: the final ranking fused into the re-rank's sort (hq_refine_final_ws) equals the two-step
     form (hq_refine_topk_ws records + hq_progressive_final_ex) bit for bit — M = 100 and 1000, K = 10
-    (arg-max rounds), 40 and 150 (sort), ties (duplicate rows), float64 / float32 / mixed pools."""
+    (arg-max rounds), 40 and 150 (sort), ties (duplicate rows), float64 / float32 / mixed pools.  lists False
+    (default): the level-0 lists are not written, so K = 10 takes the selection rounds (the n - k lowest
+    entries and the k-th by workgroup rounds, no level-0 sort); True: the sort path."""
+    from hq_mi355x import kernels as K_
     from hq_mi355x.core import search_engine as SE
+    K_.FINAL_LEVEL0_LISTS = lists
     C = _corpus(3000 if L == 128 else 20000, L, 71 + L)
     rng = np.random.default_rng(72)
     Q = np.concatenate([C[[1, 2, 20, 40, 30]] + 0.0, C[100:108] + rng.normal(0, 0.01, (8, L)),
@@ -279,7 +284,10 @@ def test_fused_final_ranking_equals_two_steps(hq_lib, L, kind):
             out += [_np(x) for x in corpus.progressive(Q, K_out, 0.1, M)]
         return out
 
-    got = run()
+    try:
+        got = run()
+    finally:
+        K_.FINAL_LEVEL0_LISTS = False
     SE._FUSED_FINAL = False
     try:
         want = run()
