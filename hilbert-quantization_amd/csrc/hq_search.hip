@@ -1761,12 +1761,10 @@ struct QConst {
   float thl, gs, low, flag;  // list threshold (f32 lower bound), G* pre-filter bound, 0.1 admitted, query flags
 };
 
-// per-query constants of the scan from the query's statistics and starting threshold t0 (f64)
-__device__ __forceinline__ QConst qconst_of(const float* Sq32, int q, double t0, double inv_m, float c1f) {
-  const int64_t gq = (int64_t)(q >> 2) * 16 + (q & 3);  // SoA-per-4 statistics
+// per-query constants of the scan from the query's statistics (std, mean, mean of squares, flag word, as in
+// Sq32) and starting threshold t0 (f64)
+__device__ __forceinline__ QConst qconst_vals(float sd, float mn, float ms, int fl, double t0, double inv_m) {
   QConst c;
-  const float sd = Sq32[gq], mn = Sq32[gq + 4], ms = Sq32[gq + 8];
-  const int fl = __float_as_int(Sq32[gq + 12]);
   c.qA = (float)(0.6 * inv_m) * sd;
   c.qB = 0.6f * mn;
   c.qQ = ms;
@@ -1781,8 +1779,12 @@ __device__ __forceinline__ QConst qconst_of(const float* Sq32, int q, double t0,
     c.gs = gstar0(c.thl, c.qA, c.qB, c.qQ, (float)(0.35 * inv_m));
     c.low = (0.1f >= c.thl - kMarginF) ? 1.0f : 0.0f;
   }
-  (void)c1f;
   return c;
+}
+__device__ __forceinline__ QConst qconst_of(const float* Sq32, int q, double t0, double inv_m, float c1f) {
+  const int64_t gq = (int64_t)(q >> 2) * 16 + (q & 3);  // SoA-per-4 statistics
+  (void)c1f;
+  return qconst_vals(Sq32[gq], Sq32[gq + 4], Sq32[gq + 8], __float_as_int(Sq32[gq + 12]), t0, inv_m);
 }
 
 // one thread per query: QConst from the caller's threshold alone (no sample pass)
@@ -2789,6 +2791,13 @@ __global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top
       pool_n[q] = 0;
     }
     const float* p = top + (int64_t)q * P;
+    // the query's statistics for its constants, requested with the pool (one round trip)
+    float st[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (qc && lane == 0) {
+      const int64_t gq = (int64_t)(q >> 2) * 16 + (q & 3);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) st[e] = Sq32[gq + 4 * e];
+    }
     uint32_t u[R];
 #pragma unroll
     for (int e = 0; e < R; ++e) {
@@ -2813,7 +2822,7 @@ __global__ __launch_bounds__(64) void k_sample_kth(const float* __restrict__ top
     }
     if (lane == 0) {
       th0[q] = t;
-      if (qc) qc[q] = qconst_of(Sq32, q, t > thr0 ? t : thr0, inv_m, 0.0f);
+      if (qc) qc[q] = qconst_vals(st[0], st[1], st[2], __float_as_int(st[3]), t > thr0 ? t : thr0, inv_m);
     }
   }
 }
@@ -3981,7 +3990,6 @@ __global__ __launch_bounds__(256) void k_refine_big_raw(HQ_REFINE_ARGS, int tb) 
 // 1 / (level + 1) of the overall score's weights (search_engine.py:191-230), folded at compile time
 __device__ constexpr double kLevelWeight[8] = {1.0 / 1.0, 1.0 / 2.0, 1.0 / 3.0, 1.0 / 4.0, 1.0 / 5.0, 1.0 / 6.0, 1.0 / 7.0, 1.0 / 8.0};
 constexpr int kFinalRounds = 32;  // final rankings of <= 32 outputs may take arg-max rounds instead of a sort
-constexpr int kSelRounds = 16;    // fused final ranking without level-0 lists: n - k + 1 rounds instead of the sort
 constexpr int kCoopGroups = 32;              // 8-lane groups per 256-thread workgroup
 constexpr int kCoopMaxW = 7;                 // record width 1 + nseg
 
@@ -4597,102 +4605,6 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
     int n = 0;
 #pragma unroll
     for (int w = 0; w < NT / 64; ++w) n += red[w];
-    // Fused final ranking without the level-0 lists (os == null): the level-0 order is needed only to drop the
-    // n - k lowest valid entries, to name the k-th (the proof) and to break ties of the overall score, so when
-    // n - k + 1 is small (lists of M + slack entries: <= slack + 1) it is found by that many workgroup rounds
-    // of the order's last entry instead of sorting all kp; the final ranking then takes outn rounds of the
-    // first (overall desc, level-0 order asc) survivor — the level-0 order of two entries read from their
-    // (key, id) directly.  The same outputs as the sort path.
-    constexpr int E = kMaxTopKBig / NT;
-    if (!os && fin.id && fin.rounds && fin.K <= kFinalRounds && n - k + 1 <= kSelRounds) {
-      // level-0 order of list entries x, y (workspace positions): valid first, key desc, id asc
-      auto before = [&](int x, int y) -> bool {
-        if (x < 0) return false;
-        if (y < 0) return true;
-        const int64_t ix = sid[x], iy = sid[y];
-        if (iy < 0) return ix >= 0;
-        const double kx = key_of(se[x], k32), ky = key_of(se[y], k32);
-        return ix >= 0 && (kx > ky || (kx == ky && ix < iy));
-      };
-      // workgroup arg-best over the live entries (live: bit e of `live` for entry tid + NT e) under `better`
-      int live = 0;
-#pragma unroll
-      for (int e = 0; e < E; ++e) live |= (tid + NT * e < kp && sid[tid + NT * e] >= 0 ? 1 : 0) << e;
-      int rnd = 0;  // rounds so far (alternating reduction buffers)
-      auto arg_best = [&](auto better) -> int {
-        int bi = -1;
-#pragma unroll
-        for (int e = 0; e < E; ++e)
-          if (((live >> e) & 1) && better(tid + NT * e, bi)) bi = tid + NT * e;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int i2 = __shfl_xor(bi, o, 64);
-          if (better(i2, bi)) bi = i2;
-        }
-        if (lane == 0) ri[rnd & 1][wave] = bi;
-        __syncthreads();  // (the other buffer is rewritten only after the next round's barrier)
-        int b = ri[rnd & 1][0];
-#pragma unroll
-        for (int w = 1; w < NT / 64; ++w)
-          if (better(ri[rnd & 1][w], b)) b = ri[rnd & 1][w];
-        ++rnd;
-        return b;
-      };
-      const int cnt = n < k ? n : k;
-      int kth_x = -1;
-      if (n >= k) {
-        // n - k + 1 rounds of the order's last live entry: the first n - k leave (not survivors), the last is
-        // the k-th of the level-0 order
-        for (int r = 0; r <= n - k; ++r) {
-          const int x = arg_best([&](int u, int v) { return u >= 0 && (v < 0 || before(v, u)); });
-          if (r < n - k) {
-            if (x >= 0 && x % NT == tid) live &= ~(1 << (x / NT));
-          } else {
-            kth_x = x;
-          }
-        }
-      }
-      if (tid == 0)
-        rank_resolve(a, last_cs, last_id, eps, q, n, k32, thr_mode, kth_x >= 0 ? se[kth_x] : -__builtin_huge_val(),
-                     cnt, ocnt, ores, count_empty, oredo);
-      // the survivors' overall keys, in registers; outn rounds of the first (overall desc, level-0 order)
-      const double* __restrict__ rec = a.ws_rec;
-      double ov[E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) ov[e] = ((live >> e) & 1) ? key_of(rec[(base + tid + NT * e) * W], k32) : 0.0;
-      __shared__ double ovs[kMaxTopKBig];  // the same keys by position (tie-breaks read them across threads)
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-        if ((live >> e) & 1) ovs[tid + NT * e] = ov[e];
-      __syncthreads();
-      const int outn = cnt < fin.K ? cnt : fin.K;
-      for (int r = 0; r < outn; ++r) {
-        const int x = arg_best([&](int u, int v) {
-          if (u < 0) return false;
-          if (v < 0) return true;
-          const double ou = ovs[u], ow = ovs[v];
-          return ou > ow || (ou == ow && before(u, v));
-        });
-        if (x >= 0 && x % NT == tid) live &= ~(1 << (x / NT));
-        if (tid == 0) fpos[r] = x;
-      }
-      __syncthreads();
-      for (int t = tid; t < fin.K * W; t += NT) {
-        const int r = t / W, w = t - r * W;
-        double val = 0.0;
-        if (r < outn) {
-          const int x = fpos[r];
-          val = rec[(base + x) * W + w];
-          if (w == 0) fin.id[(int64_t)q * fin.K + r] = sid[x];
-        } else if (w == 0) {
-          fin.id[(int64_t)q * fin.K + r] = -1;
-        }
-        fin.det[(int64_t)q * fin.K * W + t] = val;
-      }
-      if (tid == 0) fin.count[q] = outn;
-      __syncthreads();
-      continue;
-    }
     lds_bitonic(n2,
                 [&](int x, int y) {
                   const int64_t ix = sid[x], iy = sid[y];
@@ -5150,10 +5062,11 @@ static void scan_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& chu
 }
 
 // k_scan0: ~16 resident waves per CU-pair of rounds; nchunks multiple of 8 (XCD mapping), <= 512
-static void scan0_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& chunk_len, int qw = kQW) {
+static void scan0_geometry(int Q, int64_t N, int& nqb, int& nchunks, int64_t& chunk_len, int qw = kQW, int occ = 4) {
   nqb = (Q + qw - 1) / qw;
-  // ~4096 waves of 64 queries (4 per SIMD); 128-query waves (k_scan0g<.., 8>, 3 per SIMD): one round of 3072
-  const int64_t waves = qw <= kQW ? 4096LL * (kQW / qw) : 3072;
+  // ~4096 waves of 64 queries (4 per SIMD); 128-query waves (k_scan0g<.., 8>, 3 per SIMD): one round of 3072;
+  // occ 3 (option scan_occ 3: 64-query waves at 3 per SIMD, deeper prefetch): one round of 3072
+  const int64_t waves = qw <= kQW ? (occ == 3 ? 3072LL : 4096LL * (kQW / qw)) : 3072;
   int64_t target = (waves + nqb - 1) / nqb;
   int64_t max_chunks = (N + kCS - 1) / kCS;
   if (target > max_chunks) target = max_chunks;
@@ -5364,7 +5277,9 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
 #endif
   // option scan_nb 8: 128-query waves (k_scan0g<1, PF, 8>) and their geometry
   const int scan_nb = f32 && opt(OPT_SCAN_NB, 4) == 8 && opt(OPT_SCAN_WPB, 1) != 4 ? 8 : 4;
-  scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len, 16 * scan_nb);
+  // option scan_occ 3: 3 waves per SIMD (168 VGPRs: room for a deeper prefetch, scan_pf 6 / 8), 3072 waves
+  const int socc = f32 && scan_nb == 4 && opt(OPT_SCAN_WPB, 1) != 4 && opt(OPT_SCAN_OCC, 4) == 3 ? 3 : 4;
+  scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len, 16 * scan_nb, socc);
   uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
   b.ws_score = reinterpret_cast<double*>(ws);
   b.ws_id = reinterpret_cast<int64_t*>(ws + (size_t)b.nchunks * Q * k * 8);
@@ -5485,6 +5400,10 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
       else if (opt(OPT_SCAN_OCC, 4) == 5) {
         if (pf == 4) hipLaunchKernelGGL((k_scan0g<1, 4, 4, true, 5>), g1, dim3(64), 0, s, b);
         else hipLaunchKernelGGL((k_scan0g<1, 2, 4, true, 5>), g1, dim3(64), 0, s, b);
+      } else if (socc == 3) {
+        if (pf == 8) hipLaunchKernelGGL((k_scan0g<1, 8, 4, true, 3>), g1, dim3(64), 0, s, b);
+        else if (pf == 6) hipLaunchKernelGGL((k_scan0g<1, 6, 4, true, 3>), g1, dim3(64), 0, s, b);
+        else hipLaunchKernelGGL((k_scan0g<1, 4, 4, true, 3>), g1, dim3(64), 0, s, b);
       } else {  // 4 waves per SIMD (measured best: 4.64M vs 1.41M QPS at 5 with the drain gate)
         if (pf == 8) hipLaunchKernelGGL((k_scan0g<1, 8, 4, true, 4>), g1, dim3(64), 0, s, b);
         else if (pf == 6) hipLaunchKernelGGL((k_scan0g<1, 6, 4, true, 4>), g1, dim3(64), 0, s, b);
@@ -6190,7 +6109,7 @@ __device__ __forceinline__ void ov_bound(const flt4* acc, const float* wia, floa
 // a drain gate on the model at G_hihi + slack before the split measured slower, 0.69M, as did keeping
 // G_hihi in the queue: the kernel is not bound by the drain's split recompute).  The f16 scaling errs by <= 2^-11 s_i sum|q c| <= 2^-11 s_i m_i
 // in each part (Cauchy-Schwarz on unit-variance vectors), folded into bsum with the hi.hi slack.
-template <int LID, int OCC, bool HI = true, bool LIN = HI, int PF = 1, bool ANY = false>
+template <int LID, int OCC, bool HI = true, bool LIN = HI, int PF = 1>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_scanov(OvArgs a) {
   using T = OvT<LID>;
   constexpr int NG = T::NG, NC = T::NC, NKB = T::NKB, NB = kOvQW / 16, GS = 16 * NG + 4 * NC + 8;
@@ -6409,15 +6328,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
       ov_bound<T>(acc, wia[b], bsum[b], o, qv[b], tolq[b], cur.cv, cur.ro, U);
 #pragma unroll
       for (int r = 0; r < 4; ++r) W[r] = wt[b];
-    }
-    // ANY (option ov_any, with ov_occ 3): one ballot over the block's four rows first (the common case — no row
-    // passes — is one compare-and-branch, and the rows' bound chains are independent); at 4 waves per SIMD its
-    // longer live ranges spilled (873 -> 2420 us, profiles/r06_ab_rank_ct.txt), so it exists at 3 only
-    if constexpr (ANY) {
-      bool anyp = false;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) anyp |= U[r] >= W[r];
-      if (__builtin_amdgcn_ballot_w64(anyp) == 0ull) return;  // (qn < 64 holds: nothing was queued)
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -6773,14 +6683,12 @@ static int ov_launch(const OvArgs& a0, const OvPlan& p, const SegInfo& si, int k
     else hipLaunchKernelGGL((k_scanov<LID, 4, true, true, 3>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else if (oocc == 2) {
     hipLaunchKernelGGL((k_scanov<LID, 2>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
-  } else if (oocc == 3 && opt(OPT_OV_ANY, 0) == 1) {
-    hipLaunchKernelGGL((k_scanov<LID, 3, true, true, 1, true>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else if (oocc == 3) {
     hipLaunchKernelGGL((k_scanov<LID, 3>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   } else {
     // (round 6: one ballot over a block's four rows before the per-row queueing — the rows' bound chains
-    // independent — pushed this kernel past its 128-VGPR budget at 4 waves per SIMD and spilled: 873 ->
-    // 2420 us per 1000 x 1M scan, profiles/r06_ab_rank_ct.txt; not kept)
+    // independent — spilled at 4 waves per SIMD (873 -> 2420 us per 1000 x 1M scan) and measured 16% slower
+    // at 3 (0.77 vs 0.91M QPS, no spill): profiles/r06_ab_rank_ct.txt, r06_ab_final_select.txt; not kept)
     hipLaunchKernelGGL((k_scanov<LID, 4>), dim3(a.nqb * a.nchunks), dim3(64), 0, s, a);
   }
   HQ_CHECK_LAUNCH();

@@ -475,7 +475,10 @@ def _refine_ws(q, c, mode, cand_score, cand_id, kp, k, threshold, thr_mode, eps,
          exc)
 
 
-FINAL_LEVEL0_LISTS = False  # refine_final_ws: also write the (unreturned) level-0 lists (A/B of the sort they need)
+# refine_final_ws: write the level-0 lists (not returned).  False (the library then skips them, and in round 6 also
+# their sort, by selection rounds) measured slower at M = 100 / 1000 (profiles/r06_ab_final_select.txt); the
+# selection path was removed, the NULL form kept
+FINAL_LEVEL0_LISTS = True
 
 
 def refine_final_ws(q: Prepared, c: Prepared, cand_score, cand_id, k: int, threshold: float, thr_mode: int,
@@ -493,7 +496,7 @@ def refine_final_ws(q: Prepared, c: Prepared, cand_score, cand_id, k: int, thres
     if rc == _lib.HQ_E_UNSUPPORTED:
         return None
     _chk(rc, exc)
-    # the level-0 lists are not returned: not written (FINAL_LEVEL0_LISTS = True keeps them, the A/B form)
+    # the level-0 lists are not returned (FINAL_LEVEL0_LISTS False: not written)
     os_ = t.empty((Q, k), dtype=t.float64, device=dev) if FINAL_LEVEL0_LISTS else None
     oi = t.empty((Q, k), dtype=t.int64, device=dev) if FINAL_LEVEL0_LISTS else None
     cnt = t.empty(Q, dtype=t.int32, device=dev)

@@ -347,10 +347,7 @@ int hq_refine_topk_ws(const double* Rq, const double* Zq, const double* Sq, int 
  * level-0 order (key32: thr_mode | HQ_THR_KEY32 ranks by float32-rounded keys).  On the lane-cooperative
  * paths only (the cooperative shapes; kp > 64 needs the workspace); HQ_E_UNSUPPORTED otherwise, and the
  * caller keeps the two-step form.  out_score and out_id may both be NULL: the level-0 lists are then not
- * written, and a long list (kp > 64) whose valid entries exceed k by at most 15 (the M + slack lists) skips
- * the level-0 sort: the n - k lowest entries and the k-th are found by workgroup rounds, the final ranking's
- * level-0 tie-break compares (score, id) directly — the same final outputs, count, resolved flag and redo
- * count. */
+ * written (the final outputs, count, resolved flag and redo count are the same). */
 int hq_refine_final_ws(const double* Rq, const double* Zq, const double* Sq, int Q, const double* Rc,
                        const double* Zc, const double* Sc, int64_t N, int L, const double* cand_score,
                        const int64_t* cand_id, int kp, int k, double threshold, int thr_mode, double eps,

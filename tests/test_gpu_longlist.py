@@ -264,9 +264,8 @@ def test_cooperative_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind,
 def test_fused_final_ranking_equals_two_steps(hq_lib, L, kind, lists):
     """Long lists: the final ranking fused into the re-rank's sort (hq_refine_final_ws) equals the two-step
     form (hq_refine_topk_ws records + hq_progressive_final_ex) bit for bit — M = 100 and 1000, K = 10
-    (arg-max rounds), 40 and 150 (sort), ties (duplicate rows), float64 / float32 / mixed pools.  lists False
-    (default): the level-0 lists are not written, so K = 10 takes the selection rounds (the n - k lowest
-    entries and the k-th by workgroup rounds, no level-0 sort); True: the sort path."""
+    (arg-max rounds), 40 and 150 (sort), ties (duplicate rows), float64 / float32 / mixed pools; with and without
+    the (unreturned) level-0 lists written (hq_refine_final_ws accepts NULL for them)."""
     from hq_mi355x import kernels as K_
     from hq_mi355x.core import search_engine as SE
     K_.FINAL_LEVEL0_LISTS = lists
@@ -287,7 +286,7 @@ def test_fused_final_ranking_equals_two_steps(hq_lib, L, kind, lists):
     try:
         got = run()
     finally:
-        K_.FINAL_LEVEL0_LISTS = False
+        K_.FINAL_LEVEL0_LISTS = True
     SE._FUSED_FINAL = False
     try:
         want = run()

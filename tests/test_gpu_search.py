@@ -247,7 +247,7 @@ def test_rag_scores(hq_lib, golden):
 
 
 def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, hq_option):
-    """The level-0 scan variants (k_scan0g at 1 or 4 waves per block, 64 or 128 queries per wave and prefetch distance 2-4, the
+    """The level-0 scan variants (k_scan0g at 1 or 4 waves per block, 64 or 128 queries per wave, 4 or 3 waves per SIMD and prefetch distance 2-8, the
     G-selected or full-filter sample pass or none, the list-based k_scan0f) give the same exact top-k as
     the LDS-tiled k_scan (option scan_v1) and as the oracle, on a corpus with a ragged chunk tail, zero-variance level-0 segments on both sides,
     duplicate runs across chunks and a query count that is not a multiple of 64."""
@@ -270,12 +270,15 @@ def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, hq_option):
         "v0-wpb4-pf3": {"scan_wpb": 4, "scan_pf": 3},
         "v0-pf4": {"scan_pf": 4},
         "v0-nb8": {"scan_nb": 8},  # 128-query waves
+        "v0-occ3-pf4": {"scan_occ": 3, "scan_pf": 4},  # 3 waves per SIMD, 3072-wave geometry
+        "v0-occ3-pf8": {"scan_occ": 3, "scan_pf": 8},
         "v0-sample-full": {"sample_variant": 1},
         "v0-list": {"scan_variant": 1},  # k_scan0f
         "v1": {"scan_v1": 1},
     }
     for tag, opts in variants.items():
-        for name in ("scan_nosample", "scan_wpb", "scan_pf", "scan_nb", "sample_variant", "scan_variant", "scan_v1"):
+        for name in ("scan_nosample", "scan_wpb", "scan_pf", "scan_nb", "scan_occ", "sample_variant", "scan_variant",
+                     "scan_v1"):
             hq_option(name, opts.get(name))
         for thr, tm in ((0.1, 1), (0.6, 1), (0.1, 2)):
             sc, ids, cnt, _, _ = corpus.exact_topk(qp, 0, 20, thr, tm)
@@ -606,10 +609,6 @@ def test_overall_split_scan_matches_f64_scan(hq_lib, hq_option, N, L):
     hq_option("ov_occ", 3)                         # the 3-waves-per-SIMD build of k_scanov
     occ3 = [_np(x) for x in corpus.exact_topk(qp, 1, k)[:3]]
     assert np.array_equal(got[1], occ3[1]) and np.array_equal(got[0], occ3[0])
-    hq_option("ov_any", 1)                         # ... with one ballot per block of rows: the same scan lists
-    sc0, ids0, _, _ = K_.scan_topk(qp, corpus.prep, 1, k + corpus.SLACK, -corpus.EPS, 0)
-    assert np.array_equal(_np(ids0), _np(ids)) and np.array_equal(_np(sc0).view(np.uint8), _np(sc).view(np.uint8))
-    hq_option("ov_any", None)
     hq_option("ov_occ", None)
     hq_option("scan_v1", 1)
     ref = [_np(x) for x in corpus.exact_topk(qp, 1, k)[:3]]
