@@ -4567,7 +4567,11 @@ struct FinalOut {
 };
 
 
-template <int NT>
+// REG (NT = n2 / 2, n2 = kp rounded up to a power of two): the level-0 bitonic sort on two register-held entries
+// per thread (entries 2t, 2t + 1): partners within a wave are exchanged by lane shuffles (no barrier), only the
+// stages whose partner lies in another wave (distance >= 128) go through LDS.  The same network and order
+// as lds_bitonic (whose 55 barriered LDS stages for 1,024 entries set this kernel's time).
+template <int NT, bool REG = false>
 __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __restrict__ cs, double eps,
                                                    double* __restrict__ os, int64_t* __restrict__ oid,
                                                    int* __restrict__ ocnt, int* __restrict__ ores, int count_empty,
@@ -4592,20 +4596,102 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
     const double last_cs = tid == 0 ? cs[base + kp - 1] : 0.0;
     const int64_t last_id = tid == 0 ? a.cid[base + kp - 1] : -1;
     int nv = 0;
-    for (int x = tid; x < n2; x += NT) {
-      const int64_t i = x < kp ? a.ws_id[base + x] : -1;
-      se[x] = x < kp ? a.ws_sc[base + x] : -__builtin_huge_val();
-      sid[x] = i;
-      pos[x] = x;
-      nv += i >= 0 ? 1 : 0;
+    if constexpr (REG) {
+      auto first = [&](double sx, int64_t ix, double sy, int64_t iy) -> bool {
+        if (iy < 0) return ix >= 0;
+        const double kx = key_of(sx, k32), ky = key_of(sy, k32);
+        return ix >= 0 && (kx > ky || (kx == ky && ix < iy));
+      };
+      double sv[2];
+      int64_t iv[2];
+      int pv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int x = 2 * tid + u;
+        iv[u] = x < kp ? a.ws_id[base + x] : -1;
+        sv[u] = x < kp ? a.ws_sc[base + x] : -__builtin_huge_val();
+        pv[u] = x;
+        nv += iv[u] >= 0 ? 1 : 0;
+      }
+      nv = wsum64i(nv);
+      if (lane == 0) red[wave] = nv;
+      for (int size = 2; size <= n2; size <<= 1) {
+        for (int st = size >> 1; st > 0; st >>= 1) {
+          if (st == 1) {  // the thread's own pair (2t, 2t + 1)
+            const bool normal = ((2 * tid) & size) == 0;
+            if (first(sv[1], iv[1], sv[0], iv[0]) == normal) {
+              const double ts = sv[0]; sv[0] = sv[1]; sv[1] = ts;
+              const int64_t ti = iv[0]; iv[0] = iv[1]; iv[1] = ti;
+              const int tp = pv[0]; pv[0] = pv[1]; pv[1] = tp;
+            }
+            continue;
+          }
+          const int tx = st >> 1;  // partner thread tid ^ tx, same slot
+          double ps[2];
+          int64_t pi[2];
+          int pp[2];
+          if (tx < 64) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              ps[u] = __shfl_xor(sv[u], tx, 64);
+              pi[u] = __shfl_xor(iv[u], tx, 64);
+              pp[u] = __shfl_xor(pv[u], tx, 64);
+            }
+          } else {  // another wave's entries: through LDS
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              se[2 * tid + u] = sv[u];
+              sid[2 * tid + u] = iv[u];
+              pos[2 * tid + u] = pv[u];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int x = (2 * tid + u) ^ st;
+              ps[u] = se[x];
+              pi[u] = sid[x];
+              pp[u] = pos[x];
+            }
+            __syncthreads();
+          }
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int e = 2 * tid + u, pe = e ^ st;
+            const bool lo = e < pe;
+            const bool normal = ((lo ? e : pe) & size) == 0;
+            // lds_bitonic's rule: the pair swaps iff first(hi, lo) == normal
+            const bool hi_first = lo ? first(ps[u], pi[u], sv[u], iv[u]) : first(sv[u], iv[u], ps[u], pi[u]);
+            if (hi_first == normal) {
+              sv[u] = ps[u];
+              iv[u] = pi[u];
+              pv[u] = pp[u];
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        se[2 * tid + u] = sv[u];
+        sid[2 * tid + u] = iv[u];
+        pos[2 * tid + u] = pv[u];
+      }
+      __syncthreads();
+    } else {
+      for (int x = tid; x < n2; x += NT) {
+        const int64_t i = x < kp ? a.ws_id[base + x] : -1;
+        se[x] = x < kp ? a.ws_sc[base + x] : -__builtin_huge_val();
+        sid[x] = i;
+        pos[x] = x;
+        nv += i >= 0 ? 1 : 0;
+      }
+      nv = wsum64i(nv);
+      if (lane == 0) red[wave] = nv;
+      __syncthreads();
     }
-    nv = wsum64i(nv);
-    if (lane == 0) red[wave] = nv;
-    __syncthreads();
     int n = 0;
 #pragma unroll
     for (int w = 0; w < NT / 64; ++w) n += red[w];
-    lds_bitonic(n2,
+    if (!REG) lds_bitonic(n2,
                 [&](int x, int y) {
                   const int64_t ix = sid[x], iy = sid[y];
                   if (iy < 0) return ix >= 0;
@@ -5683,14 +5769,31 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
         else hipLaunchKernelGGL(k_rank_pairs<10>, g1, dim3(256), lds, s, ra);
       }
       HQ_CHECK_LAUNCH();
-      if (kp > 512)  // 1024-entry sorts: one compare-exchange per thread and stage
-        hipLaunchKernelGGL(k_rank_sort<512>, dim3(grid), dim3(512), 0, s, ra, cand_score, eps, out_score, out_id,
-                           out_count, out_resolved, count_empty ? 1 : 0, out_redo, fin ? nullptr : out_det, next_redo,
-                           fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr, 0});
-      else
-        hipLaunchKernelGGL(k_rank_sort<256>, dim3(grid), dim3(256), 0, s, ra, cand_score, eps, out_score, out_id,
-                           out_count, out_resolved, count_empty ? 1 : 0, out_redo, fin ? nullptr : out_det, next_redo,
-                           fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr, 0});
+      // the level-0 ranking: register bitonic with NT = n2 / 2 threads (option rank_sort_reg 0: the LDS form)
+      const int n2 = kp <= 128 ? 128 : kp <= 256 ? 256 : kp <= 512 ? 512 : 1024;
+      const FinalOut fo = fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr, 0};
+      double* od = fin ? nullptr : out_det;
+      const int ce = count_empty ? 1 : 0;
+      if (opt(OPT_RANK_SORT_REG, 1) == 0) {
+        if (kp > 512)  // 1024-entry sorts: one compare-exchange per thread and stage
+          hipLaunchKernelGGL(k_rank_sort<512>, dim3(grid), dim3(512), 0, s, ra, cand_score, eps, out_score, out_id,
+                             out_count, out_resolved, ce, out_redo, od, next_redo, fo);
+        else
+          hipLaunchKernelGGL(k_rank_sort<256>, dim3(grid), dim3(256), 0, s, ra, cand_score, eps, out_score, out_id,
+                             out_count, out_resolved, ce, out_redo, od, next_redo, fo);
+      } else if (n2 == 128) {
+        hipLaunchKernelGGL((k_rank_sort<64, true>), dim3(grid), dim3(64), 0, s, ra, cand_score, eps, out_score, out_id,
+                           out_count, out_resolved, ce, out_redo, od, next_redo, fo);
+      } else if (n2 == 256) {
+        hipLaunchKernelGGL((k_rank_sort<128, true>), dim3(grid), dim3(128), 0, s, ra, cand_score, eps, out_score,
+                           out_id, out_count, out_resolved, ce, out_redo, od, next_redo, fo);
+      } else if (n2 == 512) {
+        hipLaunchKernelGGL((k_rank_sort<256, true>), dim3(grid), dim3(256), 0, s, ra, cand_score, eps, out_score,
+                           out_id, out_count, out_resolved, ce, out_redo, od, next_redo, fo);
+      } else {
+        hipLaunchKernelGGL((k_rank_sort<512, true>), dim3(grid), dim3(512), 0, s, ra, cand_score, eps, out_score,
+                           out_id, out_count, out_resolved, ce, out_redo, od, next_redo, fo);
+      }
       HQ_CHECK_LAUNCH();
       return HQ_OK;
     }
