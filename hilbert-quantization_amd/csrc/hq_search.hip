@@ -4567,11 +4567,10 @@ struct FinalOut {
 };
 
 
-// REG (NT = n2 / 2, n2 = kp rounded up to a power of two): the level-0 bitonic sort on two register-held entries
-// per thread (entries 2t, 2t + 1): partners within a wave are exchanged by lane shuffles (no barrier), only the
-// stages whose partner lies in another wave (distance >= 128) go through LDS.  The same network and order
-// as lds_bitonic (whose 55 barriered LDS stages for 1,024 entries set this kernel's time).
-template <int NT, bool REG = false>
+// (round 6: a register-resident form — two entries per thread, in-wave partners by lane shuffles, LDS only
+// across waves, NT = n2 / 2 — measured slower, 97.5 -> 121 us at M = 1000 and 20.8 -> 28.2 us at M = 100:
+// profiles/r06_ab_scan_occ.txt; not kept)
+template <int NT>
 __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __restrict__ cs, double eps,
                                                    double* __restrict__ os, int64_t* __restrict__ oid,
                                                    int* __restrict__ ocnt, int* __restrict__ ores, int count_empty,
@@ -4596,102 +4595,20 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
     const double last_cs = tid == 0 ? cs[base + kp - 1] : 0.0;
     const int64_t last_id = tid == 0 ? a.cid[base + kp - 1] : -1;
     int nv = 0;
-    if constexpr (REG) {
-      auto first = [&](double sx, int64_t ix, double sy, int64_t iy) -> bool {
-        if (iy < 0) return ix >= 0;
-        const double kx = key_of(sx, k32), ky = key_of(sy, k32);
-        return ix >= 0 && (kx > ky || (kx == ky && ix < iy));
-      };
-      double sv[2];
-      int64_t iv[2];
-      int pv[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int x = 2 * tid + u;
-        iv[u] = x < kp ? a.ws_id[base + x] : -1;
-        sv[u] = x < kp ? a.ws_sc[base + x] : -__builtin_huge_val();
-        pv[u] = x;
-        nv += iv[u] >= 0 ? 1 : 0;
-      }
-      nv = wsum64i(nv);
-      if (lane == 0) red[wave] = nv;
-      for (int size = 2; size <= n2; size <<= 1) {
-        for (int st = size >> 1; st > 0; st >>= 1) {
-          if (st == 1) {  // the thread's own pair (2t, 2t + 1)
-            const bool normal = ((2 * tid) & size) == 0;
-            if (first(sv[1], iv[1], sv[0], iv[0]) == normal) {
-              const double ts = sv[0]; sv[0] = sv[1]; sv[1] = ts;
-              const int64_t ti = iv[0]; iv[0] = iv[1]; iv[1] = ti;
-              const int tp = pv[0]; pv[0] = pv[1]; pv[1] = tp;
-            }
-            continue;
-          }
-          const int tx = st >> 1;  // partner thread tid ^ tx, same slot
-          double ps[2];
-          int64_t pi[2];
-          int pp[2];
-          if (tx < 64) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              ps[u] = __shfl_xor(sv[u], tx, 64);
-              pi[u] = __shfl_xor(iv[u], tx, 64);
-              pp[u] = __shfl_xor(pv[u], tx, 64);
-            }
-          } else {  // another wave's entries: through LDS
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              se[2 * tid + u] = sv[u];
-              sid[2 * tid + u] = iv[u];
-              pos[2 * tid + u] = pv[u];
-            }
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              const int x = (2 * tid + u) ^ st;
-              ps[u] = se[x];
-              pi[u] = sid[x];
-              pp[u] = pos[x];
-            }
-            __syncthreads();
-          }
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int e = 2 * tid + u, pe = e ^ st;
-            const bool lo = e < pe;
-            const bool normal = ((lo ? e : pe) & size) == 0;
-            // lds_bitonic's rule: the pair swaps iff first(hi, lo) == normal
-            const bool hi_first = lo ? first(ps[u], pi[u], sv[u], iv[u]) : first(sv[u], iv[u], ps[u], pi[u]);
-            if (hi_first == normal) {
-              sv[u] = ps[u];
-              iv[u] = pi[u];
-              pv[u] = pp[u];
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        se[2 * tid + u] = sv[u];
-        sid[2 * tid + u] = iv[u];
-        pos[2 * tid + u] = pv[u];
-      }
-      __syncthreads();
-    } else {
-      for (int x = tid; x < n2; x += NT) {
-        const int64_t i = x < kp ? a.ws_id[base + x] : -1;
-        se[x] = x < kp ? a.ws_sc[base + x] : -__builtin_huge_val();
-        sid[x] = i;
-        pos[x] = x;
-        nv += i >= 0 ? 1 : 0;
-      }
-      nv = wsum64i(nv);
-      if (lane == 0) red[wave] = nv;
-      __syncthreads();
+    for (int x = tid; x < n2; x += NT) {
+      const int64_t i = x < kp ? a.ws_id[base + x] : -1;
+      se[x] = x < kp ? a.ws_sc[base + x] : -__builtin_huge_val();
+      sid[x] = i;
+      pos[x] = x;
+      nv += i >= 0 ? 1 : 0;
     }
+    nv = wsum64i(nv);
+    if (lane == 0) red[wave] = nv;
+    __syncthreads();
     int n = 0;
 #pragma unroll
     for (int w = 0; w < NT / 64; ++w) n += red[w];
-    if (!REG) lds_bitonic(n2,
+    lds_bitonic(n2,
                 [&](int x, int y) {
                   const int64_t ix = sid[x], iy = sid[y];
                   if (iy < 0) return ix >= 0;
@@ -5363,8 +5280,9 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
 #endif
   // option scan_nb 8: 128-query waves (k_scan0g<1, PF, 8>) and their geometry
   const int scan_nb = f32 && opt(OPT_SCAN_NB, 4) == 8 && opt(OPT_SCAN_WPB, 1) != 4 ? 8 : 4;
-  // option scan_occ 3: 3 waves per SIMD (168 VGPRs: room for a deeper prefetch, scan_pf 6 / 8), 3072 waves
-  const int socc = f32 && scan_nb == 4 && opt(OPT_SCAN_WPB, 1) != 4 && opt(OPT_SCAN_OCC, 4) == 3 ? 3 : 4;
+  // 3 waves per SIMD (default since round 6; 168 VGPRs: room for a 6-step prefetch), 3072 waves: the list-1008
+  // scan 197 -> 161 us (profiles/r06_ab_scan_occ.txt).  Option scan_occ 4: the round-5 form (4 per SIMD, 4 steps)
+  const int socc = f32 && scan_nb == 4 && opt(OPT_SCAN_WPB, 1) != 4 && opt(OPT_SCAN_OCC, 3) == 3 ? 3 : 4;
   scan0_geometry(Q, N, b.nqb, b.nchunks, b.chunk_len, 16 * scan_nb, socc);
   uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
   b.ws_score = reinterpret_cast<double*>(ws);
@@ -5473,7 +5391,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
     // options scan_wpb: waves per block (1 = one wave per block, each reading its own fragments);
     // scan_pf: prefetch distance in steps (2, 3, 4, 6, 8; 4 measured best at 4 waves per SIMD: 4.73M vs
     // 4.64M QPS at 2, 3.02M at 6 where the queue spills)
-    const int pf = (int)opt(OPT_SCAN_PF, 4);
+    const int pf = (int)opt(OPT_SCAN_PF, socc == 3 ? 6 : 4);
     if (opt(OPT_SCAN_WPB, 1) == 4) {
       const dim3 g4((b.nqb + 3) / 4 * b.nchunks);
       if (pf == 4) hipLaunchKernelGGL((k_scan0g<4, 4>), g4, dim3(256), 0, s, b);
@@ -5483,7 +5401,7 @@ static int scan0_run(bool f32, int ks, const double* Zq, const double* Sq, const
       const dim3 g1(b.nqb * b.nchunks);
       if (scan_nb == 8) hipLaunchKernelGGL((k_scan0g<1, 2, 8>), g1, dim3(64), 0, s, b);
       else if (opt_on(OPT_SCAN_SPLIT3)) hipLaunchKernelGGL((k_scan0g<1, 2, 4, false>), g1, dim3(64), 0, s, b);
-      else if (opt(OPT_SCAN_OCC, 4) == 5) {
+      else if (opt(OPT_SCAN_OCC, 3) == 5) {
         if (pf == 4) hipLaunchKernelGGL((k_scan0g<1, 4, 4, true, 5>), g1, dim3(64), 0, s, b);
         else hipLaunchKernelGGL((k_scan0g<1, 2, 4, true, 5>), g1, dim3(64), 0, s, b);
       } else if (socc == 3) {
@@ -5769,31 +5687,15 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
         else hipLaunchKernelGGL(k_rank_pairs<10>, g1, dim3(256), lds, s, ra);
       }
       HQ_CHECK_LAUNCH();
-      // the level-0 ranking: register bitonic with NT = n2 / 2 threads (option rank_sort_reg 0: the LDS form)
-      const int n2 = kp <= 128 ? 128 : kp <= 256 ? 256 : kp <= 512 ? 512 : 1024;
       const FinalOut fo = fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr, 0};
       double* od = fin ? nullptr : out_det;
       const int ce = count_empty ? 1 : 0;
-      if (opt(OPT_RANK_SORT_REG, 1) == 0) {
-        if (kp > 512)  // 1024-entry sorts: one compare-exchange per thread and stage
-          hipLaunchKernelGGL(k_rank_sort<512>, dim3(grid), dim3(512), 0, s, ra, cand_score, eps, out_score, out_id,
-                             out_count, out_resolved, ce, out_redo, od, next_redo, fo);
-        else
-          hipLaunchKernelGGL(k_rank_sort<256>, dim3(grid), dim3(256), 0, s, ra, cand_score, eps, out_score, out_id,
-                             out_count, out_resolved, ce, out_redo, od, next_redo, fo);
-      } else if (n2 == 128) {
-        hipLaunchKernelGGL((k_rank_sort<64, true>), dim3(grid), dim3(64), 0, s, ra, cand_score, eps, out_score, out_id,
+      if (kp > 512)  // 1024-entry sorts: one compare-exchange per thread and stage
+        hipLaunchKernelGGL(k_rank_sort<512>, dim3(grid), dim3(512), 0, s, ra, cand_score, eps, out_score, out_id,
                            out_count, out_resolved, ce, out_redo, od, next_redo, fo);
-      } else if (n2 == 256) {
-        hipLaunchKernelGGL((k_rank_sort<128, true>), dim3(grid), dim3(128), 0, s, ra, cand_score, eps, out_score,
-                           out_id, out_count, out_resolved, ce, out_redo, od, next_redo, fo);
-      } else if (n2 == 512) {
-        hipLaunchKernelGGL((k_rank_sort<256, true>), dim3(grid), dim3(256), 0, s, ra, cand_score, eps, out_score,
-                           out_id, out_count, out_resolved, ce, out_redo, od, next_redo, fo);
-      } else {
-        hipLaunchKernelGGL((k_rank_sort<512, true>), dim3(grid), dim3(512), 0, s, ra, cand_score, eps, out_score,
-                           out_id, out_count, out_resolved, ce, out_redo, od, next_redo, fo);
-      }
+      else
+        hipLaunchKernelGGL(k_rank_sort<256>, dim3(grid), dim3(256), 0, s, ra, cand_score, eps, out_score, out_id,
+                           out_count, out_resolved, ce, out_redo, od, next_redo, fo);
       HQ_CHECK_LAUNCH();
       return HQ_OK;
     }
@@ -6829,7 +6731,7 @@ int hq_scan0_geometry(int Q, int64_t N, int* nqb, int* nchunks, int64_t* chunk_l
   if (Q <= 0 || N <= 0) return fail(HQ_E_INVALID, "bad shape Q=%d N=%lld", Q, (long long)N);
   int a = 0, b = 0;
   int64_t c = 0;
-  scan0_geometry(Q, N, a, b, c);
+  scan0_geometry(Q, N, a, b, c, kQW, opt(OPT_SCAN_OCC, 3) == 3 ? 3 : 4);  // the default scan's geometry
   if (nqb) *nqb = a;
   if (nchunks) *nchunks = b;
   if (chunk_len) *chunk_len = c;

@@ -232,11 +232,9 @@ def test_cooperative_rerank_equals_per_thread_kernel(hq_lib, hq_option, L, kind,
     (option refine_coop = 0): progressive M = 100 / 1000 (level-0 ranking + [overall, level..] records),
     brute force k > 64 (overall ranking), frame scan (strict level-0); float64, float32 and mixed pools.
     rank_ct 1 (default): the scorers specialised to the compile-time level structures of L = 64 / 32 (L = 128
-    keeps the runtime form); 0: the runtime-structure scorer everywhere, and the level-0 ranking's LDS bitonic
-    (option rank_sort_reg 0) instead of the register-resident one; 2: also in the short-list kernel."""
+    keeps the runtime form); 0: the runtime-structure scorer everywhere; 2: also in the short-list kernel."""
     from hq_mi355x.core.search_engine import IndexCorpus
     hq_option("rank_ct", rank_ct)
-    hq_option("rank_sort_reg", 0 if rank_ct == 0 else None)
     C = _corpus(3000 if L == 128 else 20000, L, 41 + L)
     rng = np.random.default_rng(42)
     Q = np.concatenate([C[[1, 2, 20, 40]] + 0.0, C[100:108] + rng.normal(0, 0.01, (8, L)),

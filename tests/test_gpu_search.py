@@ -268,10 +268,11 @@ def test_level0_scan_kernels_agree_and_match_oracle(hq_lib, hq_option):
         "v0": {},
         "v0-nosample": {"scan_nosample": 1},
         "v0-wpb4-pf3": {"scan_wpb": 4, "scan_pf": 3},
-        "v0-pf4": {"scan_pf": 4},
+        "v0-pf4": {"scan_pf": 4},  # (the default scan is 3 waves per SIMD with 6 steps of prefetch)
         "v0-nb8": {"scan_nb": 8},  # 128-query waves
-        "v0-occ3-pf4": {"scan_occ": 3, "scan_pf": 4},  # 3 waves per SIMD, 3072-wave geometry
+        "v0-occ4-pf4": {"scan_occ": 4, "scan_pf": 4},  # round 5's 4 waves per SIMD, 4096-wave geometry
         "v0-occ3-pf8": {"scan_occ": 3, "scan_pf": 8},
+        "v0-occ3-pf4": {"scan_occ": 3, "scan_pf": 4},
         "v0-sample-full": {"sample_variant": 1},
         "v0-list": {"scan_variant": 1},  # k_scan0f
         "v1": {"scan_v1": 1},
