@@ -4742,6 +4742,8 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
 // (score desc, id asc) order is a rank count (each entry compares itself with the others), the outputs and
 // the proof as k_rank_sort.  Replaces k_refine_lds (one thread per entry walking its row: 20.6 us per
 // 1000-query batch).
+// (round 6: at 3 waves per SIMD — 142 VGPRs, none of the 8 spilled at the 128-VGPR cap of 4 — 2-5% slower at
+// M = 20: profiles/r06_ab_count_kernel.txt, rank_occ rows; not kept)
 template <int PPL, int NG, int LID = 0>
 __global__ __launch_bounds__(8 * NG) __attribute__((amdgpu_waves_per_eu(4))) void k_rank_small(RankArgs a, const double* __restrict__ cs, double eps,
                                                         double* __restrict__ os, int64_t* __restrict__ oid,

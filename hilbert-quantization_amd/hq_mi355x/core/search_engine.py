@@ -30,7 +30,10 @@ _FUSED_FINAL = True  # long lists: the final ranking inside the re-rank's sort (
 # after the event behind it; "side" — an event right after the re-rank and the count read after it on a side
 # stream (no copy on the search stream).  A/B, one box (profiles/r06_ab_count_read.txt): "side" measured
 # 2% (M = 20) to 7% (M = 100) slower — the host's extra copy and stream sync per finish outweigh the ~4 us
-# copy kernel it takes off the search stream — so "copy" stays the default.
+# copy kernel it takes off the search stream — so "copy" stays the default.  Two forms where the re-rank
+# kernel itself hands the count to pinned host memory measured slower too (profiles/r06_ab_count_kernel.txt):
+# the last workgroup to finish (a ticket atomic per workgroup; M = 20 5.5M -> 5.3M QPS) and a system-scope
+# store of each query's redo flag (5.5M -> 5.2M).
 _COUNT_READ = "copy"
 _RING = 16  # redo counters per (device, stream, thread): a slot is re-cleared _RING - 1 batches later
 

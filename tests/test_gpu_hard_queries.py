@@ -164,3 +164,42 @@ def test_clustered_sharded_retry_equals_single(hq_lib, R):
         if M == 20:  # (longer lists hold a whole 64-row run: no near-tie at the list end)
             assert sum(s["retry_queries"] for s in st) > 0, (R, M, st)
         assert sum(s["dense_queries"] for s in st) <= 2 * R + (QN if M == 1000 else 0), (R, M, st)
+
+
+@pytest.mark.parametrize("mode", ["copy", "side"])
+def test_redo_count_read_modes(hq_lib, mode):
+    """How progressive_finish learns a batch's redo count (IndexCorpus._count_read): "copy" —
+    a pinned copy behind the re-rank, "side" — a ring slot read on a side stream.  On the clustered 1M corpus
+    with no list adaptation (every M = 20 batch has hundreds of redos): the value read equals the count of
+    unresolved / empty queries, four batches in flight at once give the serial results, and every query
+    equals the dense exact path."""
+    import torch
+    from hq_mi355x.core.search_engine import IndexCorpus
+    C, Q, _ = _clustered()
+    corpus = IndexCorpus(C)
+    corpus.ADAPT_LISTS = False
+    corpus._count_read = mode
+    for M in (20, 100, 1000):
+        p = corpus.progressive_submit(Q, 10, 0.1, M)
+        want = _np((p.res == 0) | (p.cnt == 0)).astype(np.int32)
+        want_n = int(want.sum())
+        if mode == "side":
+            got_n = corpus._resolve(p)
+        else:
+            p.event.synchronize()
+            got_n = int(p.nredo[0])
+        assert got_n == want_n, (mode, M, got_n, want_n)
+        if M == 20:
+            assert want_n > 0
+        got = [_np(x) for x in corpus.progressive_finish(p)]
+        want = [_np(x) for x in _dense_progressive(corpus, Q, 10, 0.1, M)]
+        for x, y, name in zip(got, want, ("ids", "overall", "levels", "count")):
+            np.testing.assert_array_equal(x, y, err_msg=f"{mode} M={M} {name}")
+    # batches in flight: four submitted before any is finished (the ring of counters shared on the stream)
+    parts = [Q[i * 250:(i + 1) * 250] for i in range(4)]
+    serial = [[_np(x) for x in corpus.progressive(q, 10, 0.1, 20)] for q in parts]
+    pend = [corpus.progressive_submit(q, 10, 0.1, 20) for q in parts]
+    for pp, s in zip(pend, serial):
+        for x, y in zip([_np(x) for x in corpus.progressive_finish(pp)], s):
+            np.testing.assert_array_equal(x, y)
+    torch.cuda.synchronize()
