@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--queries", type=int, default=1000)
     # 50 batches: the pipeline's fill and drain (one batch's host submit, the last batch's wait) stay ~2% of
     # the timed region (at 20 they were ~5%: 201 us per step against 190 us of kernels per batch)
-    ap.add_argument("--search-steps", type=int, default=50)
+    ap.add_argument("--search-steps", type=int, default=200)
     ap.add_argument("--no-search", action="store_true")
     ap.add_argument("--no-stream", action="store_true")
     ap.add_argument("--no-precomputed", action="store_true")
@@ -72,7 +72,8 @@ def parse():
     ap.add_argument("--option", action="append", default=[],
                     help="name=value: select a kernel variant (hq_set_option; A/B runs only)")
     ap.add_argument("--py-set", action="append", default=[],
-                    help="module:attribute=int: a host-side variant, e.g. hq_mi355x.kernels:FINAL_LEVEL0_LISTS=1 "
+                    help="module:attribute=value (int, or str where the attribute is one; attribute may be Class.attr): "
+                         "a host-side variant, e.g. hq_mi355x.kernels:FINAL_LEVEL0_LISTS=1 "
                          "(A/B runs only)")
     return ap.parse_args()
 
@@ -110,6 +111,14 @@ def max_over_ranks(x, world):
     t = torch.tensor([x], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+# batches of a pipelined progressive search in flight (progressive_submit / progressive_finish): with 2, the
+# host's submit of batch i + 2 started only once batch i was finished and left the GPU idle at times (M = 20:
+# 173 vs 165 us per batch in profiles/r06_ab_count_kernel.txt's host cost rows; 5.70-5.73M vs 5.76-5.77M QPS
+# in the bench leg, r06_ab_search_depth.txt); 3 keeps one batch queued behind the running one.
+# HQ_SEARCH_DEPTH: A/B knob
+SEARCH_DEPTH = int(os.environ.get("HQ_SEARCH_DEPTH", "3"))
 
 
 def timed(fn, steps, warmup, world, drain=None):
@@ -547,7 +556,7 @@ def bench_search_strong(args, world, rank, dev):
 
     def run():
         pend.append(engine.progressive_submit(Q, 10, 0.1, 20))
-        if len(pend) >= 2:
+        if len(pend) >= SEARCH_DEPTH:
             engine.progressive_finish(pend.pop(0))
 
     def drain():
@@ -611,7 +620,7 @@ def summary(rec) -> dict:
 
 
 def progressive_rate(engine, Q, M, steps, world, k=10, threshold=0.1):
-    """Pipelined progressive search of one query batch per step (two batches in flight, as the cfg3 leg),
+    """Pipelined progressive search of one query batch per step (SEARCH_DEPTH batches in flight, as the cfg3 leg),
     with the engine's redo counters (IndexCorpus.stats) over the timed batches: queries re-scanned with a
     longer list after a near-tie / short list, queries left for the dense exact path, and the stream time of
     that redo work per batch (between two events around it: IndexCorpus.stats dense_s); the warm-up batch
@@ -620,7 +629,7 @@ def progressive_rate(engine, Q, M, steps, world, k=10, threshold=0.1):
 
     def run():
         pend.append(engine.progressive_submit(Q, k, threshold, M))
-        if len(pend) >= 2:
+        if len(pend) >= SEARCH_DEPTH:
             engine.progressive_finish(pend.pop(0))
 
     def drain():
@@ -802,7 +811,12 @@ def main():
         import importlib
         target, value = o.split("=", 1)
         mod, attr = target.split(":", 1)
-        setattr(importlib.import_module(mod), attr, type(getattr(importlib.import_module(mod), attr))(int(value)))
+        obj = importlib.import_module(mod)
+        *path, attr = attr.split(".")  # module:Class.attribute too
+        for a in path:
+            obj = getattr(obj, a)
+        old = getattr(obj, attr)
+        setattr(obj, attr, value if isinstance(old, str) else type(old)(int(value)))
     from hq_mi355x.core.pipeline import quantize_batch
 
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -877,7 +891,7 @@ def main():
         # alternates the batches over n HIP streams: 2 / 3 streams measured 1.43M / 0.7-1.05M vs 2.07M QPS
         # on one (two batches' scans contend for the CUs), so one stream is the default
         nstreams = int(os.environ.get("HQ_SEARCH_STREAMS", "1"))
-        depth = int(os.environ.get("HQ_SEARCH_DEPTH", "2"))  # batches in flight (A/B knob; 3 measured equal)
+        depth = SEARCH_DEPTH
         streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
         pend, nsub = [], [0]
 
@@ -941,10 +955,27 @@ def main():
                 ("m1000", lambda: engine.progressive(queries, 10, 0.1, 1000), l0_flops, FP16_MATRIX_PEAK_TFS,
                  "dense F16 MFMA")):
             msteps = max(2, args.search_steps // 2)
-            mw, mk = timed(fn, msteps, 1, world)
+            Mm = {"m100": 100, "m1000": 1000}.get(mode)
+            sync = None
+            if Mm is not None:
+                # pipelined as the M = 20 leg (SEARCH_DEPTH batches in flight); the synchronous call's rate beside
+                sw, _ = timed(fn, msteps, 1, world)
+                sync = {"value": Qn * msteps / sw, "ms_per_step": sw / msteps * 1e3,
+                        "note": "engine.progressive per step (submit + finish, the host waits for each batch)"}
+                pend_m = []
+
+                def fn(M=Mm):
+                    pend_m.append(engine.progressive_submit(queries, 10, 0.1, M))
+                    if len(pend_m) >= SEARCH_DEPTH:
+                        engine.progressive_finish(pend_m.pop(0))
+
+                def drain_m():
+                    while pend_m:
+                        engine.progressive_finish(pend_m.pop(0))
+            mw, mk = timed(fn, msteps, 1, world, drain_m if Mm is not None else None)
             modes[mode] = {
                 "value": Qn * msteps / mw, "unit": "queries/sec", "steps": msteps, "ms_per_step": mw / msteps * 1e3,
-                "max_candidates_per_level": {"m100": 100, "m1000": 1000}.get(mode),
+                "max_candidates_per_level": Mm, "pipelined": Mm is not None, "sync": sync,
                 "roofline": {"bound": "mfma", "achieved": flops / mk / 1e12, "peak": peak, "unit": "TFLOP/s",
                              "frac": flops / mk / 1e12 / peak,
                              "note": f"contraction flops per step, one f16 pass ({('2*Q*N*32*K-blocks' if ovinfo else '2*Q*N*Lp f64') if mode == 'overall' else '2*Q*N*32'}) / "
