@@ -33,7 +33,8 @@ _FUSED_FINAL = True  # long lists: the final ranking inside the re-rank's sort (
 # copy kernel it takes off the search stream — so "copy" stays the default.  Two forms where the re-rank
 # kernel itself hands the count to pinned host memory measured slower too (profiles/r06_ab_count_kernel.txt):
 # the last workgroup to finish (a ticket atomic per workgroup; M = 20 5.5M -> 5.3M QPS) and a system-scope
-# store of each query's redo flag (5.5M -> 5.2M).
+# store of each query's redo flag (5.5M -> 5.2M).  So did the copy queued at submit on a side stream that waits
+# for the re-rank's event (5.82-5.83M -> 5.67-5.69M at three batches in flight).
 _COUNT_READ = "copy"
 _RING = 16  # redo counters per (device, stream, thread): a slot is re-cleared _RING - 1 batches later
 
