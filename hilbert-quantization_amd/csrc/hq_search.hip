@@ -4201,6 +4201,7 @@ struct RankArgs {
   int64_t id_base;
   const int64_t* cid;
   double* ws_sc; int64_t* ws_id; double* ws_rec;
+  int win;  // k_rank_sort: window ranking before the bitonic sort (option rank_win, default 1)
 };
 
 __host__ __device__ inline int coop_qw(const CoopSeg& c) { return (c.L + c.Lp + 4 * c.nseg + 1) & ~1; }
@@ -4584,6 +4585,8 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
   __shared__ double rv[2][NT / 64];
   __shared__ int ri[2][NT / 64];
   __shared__ int red[NT / 64];
+  __shared__ double csl[kMaxTopKBig];  // window ranking: the list's approximate scores (-inf: empty slot)
+  __shared__ unsigned long long vmask[kMaxTopKBig / 64];  // valid entries, 64 list positions per word
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kp = a.kp, k = a.k, W = 1 + a.cs.nseg;
   const int n2 = pow2_at_least(kp);
@@ -4595,12 +4598,19 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
     const double last_cs = tid == 0 ? cs[base + kp - 1] : 0.0;
     const int64_t last_id = tid == 0 ? a.cid[base + kp - 1] : -1;
     int nv = 0;
-    for (int x = tid; x < n2; x += NT) {
+    auto load = [&](int x) {
       const int64_t i = x < kp ? a.ws_id[base + x] : -1;
       se[x] = x < kp ? a.ws_sc[base + x] : -__builtin_huge_val();
       sid[x] = i;
       pos[x] = x;
-      nv += i >= 0 ? 1 : 0;
+      return i >= 0 ? 1 : 0;
+    };
+    for (int x = tid; x < n2; x += NT) {
+      nv += load(x);
+      if (a.win && n2 <= 2 * NT) {
+        csl[x] = x < kp && a.cid[base + x] >= 0 ? cs[base + x] : -__builtin_huge_val();
+        fpos[x] = -1;
+      }
     }
     nv = wsum64i(nv);
     if (lane == 0) red[wave] = nv;
@@ -4608,6 +4618,89 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
     int n = 0;
 #pragma unroll
     for (int w = 0; w < NT / 64; ++w) n += red[w];
+    // Window ranking.  The list arrives in approximate-score order (k_pool_sort: approximate score desc, id
+    // asc) and |exact - approximate| < eps (the completeness proof's own premise), so a valid entry's rank in
+    // the (exact key desc, id asc) order is the count of valid entries whose approximate score lies more than
+    // 2 eps above its own, plus its exact comparisons with the entries inside that window; invalid entries
+    // follow in list order.  The result is checked — every rank taken once and every adjacent pair of valid
+    // entries in order, which holds for the sorted order alone — and the bitonic sort below runs instead when
+    // the check fails or a window passes kRankWin entries (runs of near-equal scores), so the ranking is the
+    // sort's whatever the input.  Replaces the sort's 10 x 11 / 2 barrier stages by a few LDS reads per entry.
+    bool sorted = false;
+    if (a.win && n2 <= 2 * NT) {
+      constexpr int kRankWin = 32;
+      for (int c = wave; c < n2 / 64; c += NT / 64) {
+        const unsigned long long m = __ballot(sid[64 * c + lane] >= 0);
+        if (lane == 0) vmask[c] = m;
+      }
+      __syncthreads();
+      auto before_n = [&](int x) {  // valid entries at list positions < x
+        int p = 0;
+        for (int c = 0; c < (x >> 6); ++c) p += __popcll(vmask[c]);
+        return p + __popcll(vmask[x >> 6] & ((1ull << (x & 63)) - 1ull));
+      };
+      const double wd = 2.0 * eps;
+      bool bad = false;
+      int rk[2] = {-1, -1};
+      double ms[2] = {0.0, 0.0};
+      int64_t mi[2] = {-1, -1};
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int x = tid + NT * e;
+        if (x >= n2) continue;
+        const int64_t ix = sid[x];
+        ms[e] = se[x];
+        mi[e] = ix;
+        if (ix < 0) {
+          rk[e] = n + (x - before_n(x));
+          continue;
+        }
+        const double ci = csl[x], kx = key_of(ms[e], k32);
+        auto ahead = [&](int j) {  // valid entry j ranks before x
+          const int64_t ij = sid[j];
+          if (ij < 0) return 0;
+          const double kj = key_of(se[j], k32);
+          return (kj > kx || (kj == kx && ij < ix)) ? 1 : 0;
+        };
+        int lo = x;
+        while (lo > 0 && csl[lo - 1] <= ci + wd && x - lo < kRankWin) --lo;
+        if (lo > 0 && csl[lo - 1] <= ci + wd) bad = true;
+        int r = before_n(lo);
+        for (int j = lo; j < x; ++j) r += ahead(j);
+        int hi = x + 1;
+        while (hi < n2 && csl[hi] >= ci - wd && hi - x <= kRankWin) r += ahead(hi++);
+        if (hi < n2 && csl[hi] >= ci - wd) bad = true;
+        rk[e] = r;
+      }
+      bad = __syncthreads_or(bad);
+      if (!bad) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int r = rk[e];
+          if (r >= 0 && r < n2) {
+            se[r] = ms[e];
+            sid[r] = mi[e];
+            pos[r] = tid + NT * e;
+            fpos[r] = tid + NT * e;
+          }
+        }
+        __syncthreads();
+        for (int r = tid; r < n2; r += NT) {
+          if (fpos[r] < 0) bad = true;
+          if (r + 1 < n) {
+            const double k0 = key_of(se[r], k32), k1 = key_of(se[r + 1], k32);
+            if (!(k0 > k1 || (k0 == k1 && sid[r] < sid[r + 1]))) bad = true;
+          }
+        }
+        bad = __syncthreads_or(bad);
+        if (bad) {  // the scattered arrays are not the sorted order: back to the list order for the sort
+          for (int x = tid; x < n2; x += NT) load(x);
+          __syncthreads();
+        }
+      }
+      sorted = !bad;
+    }
+    if (!sorted)
     lds_bitonic(n2,
                 [&](int x, int y) {
                   const int64_t ix = sid[x], iy = sid[y];
@@ -5620,6 +5713,7 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
     ra.mode = mode; ra.kp = kp; ra.k = k; ra.thr_mode = thr_mode; ra.det = out_det ? 1 : 0; ra.thr = threshold;
     ra.id_base = id_base; ra.cid = cand_id;
     ra.ws_sc = nullptr; ra.ws_id = nullptr; ra.ws_rec = nullptr;
+    ra.win = (int)opt(OPT_RANK_WIN, 1);
     return ra;
   };
   // short lists: the fused lane-cooperative re-rank (k_rank_small) where its shapes hold; option

@@ -359,3 +359,41 @@ def test_sort_select_equals_reference_order(hq_lib, hq_option, k):
             assert list(got[1][r][:n]) == list(order + 7) and np.all(got[1][r][n:] == -1), (k, thr, mode, r)
             assert np.array_equal(got[0][r][:n], sc[r][order])
             assert got[3][r] == int(np.argmax(sc[r])) + 7 and got[2][r] == sc[r].max()
+
+
+@pytest.mark.parametrize("dups", [0, 40])
+@pytest.mark.parametrize("kind", ["f64", "f32"])
+def test_window_ranking_equals_sort(hq_lib, hq_option, kind, dups):
+    """k_rank_sort's window ranking (option rank_win 1: each entry ranked from the approximate-score order of
+    the list plus exact comparisons inside its 2-eps window, the result checked and the bitonic sort run when
+    the check fails) is bit-identical to the sort alone (rank_win 0) and to the one-thread-per-entry kernels
+    (refine_coop 0): progressive M = 100 / 1000 with K = 10 and 150, brute force k > 64, frame scan.
+    dups 40: runs of 40 identical rows (windows past the 32-entry cap: the sort fallback on every list
+    holding a run) beside distinct rows."""
+    from hq_mi355x.core.search_engine import IndexCorpus
+    C = _corpus(20000, 64, 91)
+    if dups:
+        C[1000:1000 + 50 * dups] = np.repeat(C[1000:1050], dups, axis=0)
+    rng = np.random.default_rng(92)
+    Q = np.concatenate([C[[1, 2, 20, 40, 30, 1000, 1000 + 3 * dups]] + 0.0,
+                        C[100:106] + rng.normal(0, 0.01, (6, 64)), rng.standard_normal((2, 64))])
+    if kind == "f32":
+        C, Q = C.astype(np.float32), Q.astype(np.float32)
+    corpus = IndexCorpus(C)
+
+    def run():
+        out = []
+        for M, K_out in ((100, 10), (100, 150), (1000, 10), (1000, 150)):
+            out += [_np(x) for x in corpus.progressive(Q, K_out, 0.1, M)]
+        out += [_np(x) for x in corpus.brute_force(Q, 120)]
+        out += [_np(x) for x in corpus.frame_search(Q, 300, 0.1)]
+        return out
+
+    got = run()
+    hq_option("rank_win", 0)
+    want = run()
+    hq_option("refine_coop", 0)
+    ref = run()
+    for a, (x, y, z) in enumerate(zip(got, want, ref)):
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (kind, dups, a)
+        assert np.array_equal(x.view(np.uint8), z.view(np.uint8)), (kind, dups, a)
