@@ -4587,6 +4587,7 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
   __shared__ int red[NT / 64];
   __shared__ double csl[kMaxTopKBig];  // window ranking: the list's approximate scores (-inf: empty slot)
   __shared__ unsigned long long vmask[kMaxTopKBig / 64];  // valid entries, 64 list positions per word
+  __shared__ int vpre[kMaxTopKBig / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kp = a.kp, k = a.k, W = 1 + a.cs.nseg;
   const int n2 = pow2_at_least(kp);
@@ -4634,10 +4635,14 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
         if (lane == 0) vmask[c] = m;
       }
       __syncthreads();
-      auto before_n = [&](int x) {  // valid entries at list positions < x
+      if (tid < n2 / 64) {  // valid entries before each 64-position word
         int p = 0;
-        for (int c = 0; c < (x >> 6); ++c) p += __popcll(vmask[c]);
-        return p + __popcll(vmask[x >> 6] & ((1ull << (x & 63)) - 1ull));
+        for (int c = 0; c < tid; ++c) p += __popcll(vmask[c]);
+        vpre[tid] = p;
+      }
+      __syncthreads();
+      auto before_n = [&](int x) {  // valid entries at list positions < x
+        return vpre[x >> 6] + __popcll(vmask[x >> 6] & ((1ull << (x & 63)) - 1ull));
       };
       const double wd = 2.0 * eps;
       bool bad = false;
@@ -4648,6 +4653,7 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
       for (int e = 0; e < 2; ++e) {
         const int x = tid + NT * e;
         if (x >= n2) continue;
+        __builtin_amdgcn_sched_barrier(0);  // one entry's window at a time (fewer live registers)
         const int64_t ix = sid[x];
         ms[e] = se[x];
         mi[e] = ix;
@@ -4663,11 +4669,14 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
           return (kj > kx || (kj == kx && ij < ix)) ? 1 : 0;
         };
         int lo = x;
+#pragma unroll 1
         while (lo > 0 && csl[lo - 1] <= ci + wd && x - lo < kRankWin) --lo;
         if (lo > 0 && csl[lo - 1] <= ci + wd) bad = true;
         int r = before_n(lo);
+#pragma unroll 1
         for (int j = lo; j < x; ++j) r += ahead(j);
         int hi = x + 1;
+#pragma unroll 1
         while (hi < n2 && csl[hi] >= ci - wd && hi - x <= kRankWin) r += ahead(hi++);
         if (hi < n2 && csl[hi] >= ci - wd) bad = true;
         rk[e] = r;
