@@ -4608,7 +4608,7 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
     };
     for (int x = tid; x < n2; x += NT) {
       nv += load(x);
-      if (a.win && n2 <= 2 * NT) {
+      if (a.win && n2 <= (kMaxTopKBig / NT) * NT) {
         csl[x] = x < kp && a.cid[base + x] >= 0 ? cs[base + x] : -__builtin_huge_val();
         fpos[x] = -1;
       }
@@ -4628,7 +4628,8 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
     // the check fails or a window passes kRankWin entries (runs of near-equal scores), so the ranking is the
     // sort's whatever the input.  Replaces the sort's 10 x 11 / 2 barrier stages by a few LDS reads per entry.
     bool sorted = false;
-    if (a.win && n2 <= 2 * NT) {
+    constexpr int WE = kMaxTopKBig / NT;  // list entries per thread
+    if (a.win && n2 <= WE * NT) {
       constexpr int kRankWin = 32;
       for (int c = wave; c < n2 / 64; c += NT / 64) {
         const unsigned long long m = __ballot(sid[64 * c + lane] >= 0);
@@ -4646,11 +4647,17 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
       };
       const double wd = 2.0 * eps;
       bool bad = false;
-      int rk[2] = {-1, -1};
-      double ms[2] = {0.0, 0.0};
-      int64_t mi[2] = {-1, -1};
+      int rk[WE];
+      double ms[WE];
+      int64_t mi[WE];
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
+      for (int e = 0; e < WE; ++e) {
+        rk[e] = -1;
+        ms[e] = 0.0;
+        mi[e] = -1;
+      }
+#pragma unroll
+      for (int e = 0; e < WE; ++e) {
         const int x = tid + NT * e;
         if (x >= n2) continue;
         __builtin_amdgcn_sched_barrier(0);  // one entry's window at a time (fewer live registers)
@@ -4684,7 +4691,7 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
       bad = __syncthreads_or(bad);
       if (!bad) {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
+        for (int e = 0; e < WE; ++e) {
           const int r = rk[e];
           if (r >= 0 && r < n2) {
             se[r] = ms[e];
@@ -5795,7 +5802,9 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
       const FinalOut fo = fin ? *fin : FinalOut{0, nullptr, nullptr, nullptr, 0};
       double* od = fin ? nullptr : out_det;
       const int ce = count_empty ? 1 : 0;
-      if (kp > 512)  // 1024-entry sorts: one compare-exchange per thread and stage
+      // lists > 512: 256 threads, four entries each (4 queries per CU at 118 VGPRs: M = 1000 1.70 -> 1.76M QPS,
+      // profiles/r06_ab_rank_win.txt); option rank_sort_nt 512: one compare-exchange per thread and stage
+      if (kp > 512 && opt(OPT_RANK_SORT_NT, 256) == 512)
         hipLaunchKernelGGL(k_rank_sort<512>, dim3(grid), dim3(512), 0, s, ra, cand_score, eps, out_score, out_id,
                            out_count, out_resolved, ce, out_redo, od, next_redo, fo);
       else

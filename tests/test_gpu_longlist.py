@@ -361,16 +361,19 @@ def test_sort_select_equals_reference_order(hq_lib, hq_option, k):
             assert got[3][r] == int(np.argmax(sc[r])) + 7 and got[2][r] == sc[r].max()
 
 
+@pytest.mark.parametrize("nt", [512, 256])
 @pytest.mark.parametrize("dups", [0, 40])
 @pytest.mark.parametrize("kind", ["f64", "f32"])
-def test_window_ranking_equals_sort(hq_lib, hq_option, kind, dups):
+def test_window_ranking_equals_sort(hq_lib, hq_option, kind, dups, nt):
     """k_rank_sort's window ranking (option rank_win 1: each entry ranked from the approximate-score order of
     the list plus exact comparisons inside its 2-eps window, the result checked and the bitonic sort run when
     the check fails) is bit-identical to the sort alone (rank_win 0) and to the one-thread-per-entry kernels
     (refine_coop 0): progressive M = 100 / 1000 with K = 10 and 150, brute force k > 64, frame scan.
     dups 40: runs of 40 identical rows (windows past the 32-entry cap: the sort fallback on every list
-    holding a run) beside distinct rows."""
+    holding a run) beside distinct rows.  nt: workgroup size of the lists > 512 (option rank_sort_nt: two or four
+    entries per thread)."""
     from hq_mi355x.core.search_engine import IndexCorpus
+    hq_option("rank_sort_nt", nt)
     C = _corpus(20000, 64, 91)
     if dups:
         C[1000:1000 + 50 * dups] = np.repeat(C[1000:1050], dups, axis=0)
