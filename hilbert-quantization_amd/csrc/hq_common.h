@@ -52,7 +52,7 @@ enum Opt {
   OPT_REFINE_GLOBAL, OPT_REFINE_EXPT, OPT_SEG_PREPARE_FLAT, OPT_SELECT_2STAGE, OPT_LEVEL_SCORES_V1, OPT_SCAN_SPLIT3, OPT_SCAN_OCC, OPT_SCANOV_SPLIT3, OPT_SAMPLE_HI,
   OPT_PRECOMP_WS, OPT_PRECOMP_LEAF_ROT, OPT_PRECOMP_ORDER, OPT_SCANOV_V1, OPT_OV_PF, OPT_PRECOMP_G2REG,
   OPT_REFINE_COOP, OPT_PRECOMP_COMPACT, OPT_PREP_COOP, OPT_POOL_SORT_MEM, OPT_REFINE_SMALL, OPT_FINAL_ROUNDS,
-  OPT_RANK_CT, OPT_RANK_WIN, OPT_RANK_SORT_NT,
+  OPT_RANK_CT, OPT_RANK_WIN, OPT_RANK_SORT_NT, OPT_RANK_SORT_SMALL,
   OPT_COUNT
 };
 int64_t opt(Opt id, int64_t dflt);

@@ -42,7 +42,7 @@ static const char* const kOptNames[OPT_COUNT] = {
     "refine_global", "refine_expt", "seg_prepare_flat", "select_2stage", "level_scores_v1", "scan_split3", "scan_occ", "scanov_split3", "sample_hi",
     "precomp_ws", "precomp_leaf_rot", "precomp_order", "scanov_v1", "ov_pf", "precomp_g2reg",
     "refine_coop", "precomp_compact", "prep_coop", "pool_sort_mem", "refine_small", "final_rounds",
-    "rank_ct", "rank_win", "rank_sort_nt"};
+    "rank_ct", "rank_win", "rank_sort_nt", "rank_sort_small"};
 static int64_t g_opt_val[OPT_COUNT];
 static bool g_opt_set[OPT_COUNT];
 

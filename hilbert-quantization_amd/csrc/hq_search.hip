@@ -4571,23 +4571,25 @@ struct FinalOut {
 // (round 6: a register-resident form — two entries per thread, in-wave partners by lane shuffles, LDS only
 // across waves, NT = n2 / 2 — measured slower, 97.5 -> 121 us at M = 1000 and 20.8 -> 28.2 us at M = 100:
 // profiles/r06_ab_scan_occ.txt; not kept)
-template <int NT>
+// CAP: list entries the workgroup holds (a power of two >= kp): kMaxTopKBig, or 128 for the M = 100 lists
+// (4 KB of LDS per workgroup instead of 33: many queries per CU)
+template <int NT, int CAP = kMaxTopKBig>
 __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __restrict__ cs, double eps,
                                                    double* __restrict__ os, int64_t* __restrict__ oid,
                                                    int* __restrict__ ocnt, int* __restrict__ ores, int count_empty,
                                                    int* __restrict__ oredo, double* __restrict__ odet,
                                                    int* __restrict__ onext, FinalOut fin) {
   if (onext && blockIdx.x == 0 && threadIdx.x == 0) *onext = 0;  // the next batch's redo counter
-  __shared__ double se[kMaxTopKBig];
-  __shared__ int64_t sid[kMaxTopKBig];
-  __shared__ int pos[kMaxTopKBig];
-  __shared__ int fpos[kMaxTopKBig];
+  __shared__ double se[CAP];
+  __shared__ int64_t sid[CAP];
+  __shared__ int pos[CAP];
+  __shared__ int fpos[CAP];
   __shared__ double rv[2][NT / 64];
   __shared__ int ri[2][NT / 64];
   __shared__ int red[NT / 64];
-  __shared__ double csl[kMaxTopKBig];  // window ranking: the list's approximate scores (-inf: empty slot)
-  __shared__ unsigned long long vmask[kMaxTopKBig / 64];  // valid entries, 64 list positions per word
-  __shared__ int vpre[kMaxTopKBig / 64];
+  __shared__ double csl[CAP];  // window ranking: the list's approximate scores (-inf: empty slot)
+  __shared__ unsigned long long vmask[CAP / 64];  // valid entries, 64 list positions per word
+  __shared__ int vpre[CAP / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kp = a.kp, k = a.k, W = 1 + a.cs.nseg;
   const int n2 = pow2_at_least(kp);
@@ -4608,7 +4610,7 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
     };
     for (int x = tid; x < n2; x += NT) {
       nv += load(x);
-      if (a.win && n2 <= (kMaxTopKBig / NT) * NT) {
+      if (a.win && n2 <= (CAP / NT) * NT) {
         csl[x] = x < kp && a.cid[base + x] >= 0 ? cs[base + x] : -__builtin_huge_val();
         fpos[x] = -1;
       }
@@ -4628,7 +4630,7 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
     // the check fails or a window passes kRankWin entries (runs of near-equal scores), so the ranking is the
     // sort's whatever the input.  Replaces the sort's 10 x 11 / 2 barrier stages by a few LDS reads per entry.
     bool sorted = false;
-    constexpr int WE = kMaxTopKBig / NT;  // list entries per thread
+    constexpr int WE = CAP / NT;  // list entries per thread
     if (a.win && n2 <= WE * NT) {
       constexpr int kRankWin = 32;
       for (int c = wave; c < n2 / 64; c += NT / 64) {
@@ -4775,7 +4777,7 @@ __global__ __launch_bounds__(NT) void k_rank_sort(RankArgs a, const double* __re
       auto first = [](double x, int ix, double y, int iy) { return ix >= 0 && (iy < 0 || x > y || (x == y && ix < iy)); };
       if (fin.rounds && fin.K <= kFinalRounds && 3 * outn < lg * (lg + 1) / 2) {
         // outn rounds of the workgroup's first (overall desc, position asc) among the entries not yet taken
-        constexpr int E = kMaxTopKBig / NT;
+        constexpr int E = CAP / NT;
         double v[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) v[e] = tid + NT * e < cnt ? se[tid + NT * e] : 0.0;
@@ -5804,7 +5806,10 @@ static int refine_launch(const double* Rq, const double* Zq, const double* Sq, i
       const int ce = count_empty ? 1 : 0;
       // lists > 512: 256 threads, four entries each (4 queries per CU at 118 VGPRs: M = 1000 1.70 -> 1.76M QPS,
       // profiles/r06_ab_rank_win.txt); option rank_sort_nt 512: one compare-exchange per thread and stage
-      if (kp > 512 && opt(OPT_RANK_SORT_NT, 256) == 512)
+      if (pow2_at_least(kp) <= 128 && opt(OPT_RANK_SORT_SMALL, 1) != 0)
+        hipLaunchKernelGGL((k_rank_sort<128, 128>), dim3(grid), dim3(128), 0, s, ra, cand_score, eps, out_score,
+                           out_id, out_count, out_resolved, ce, out_redo, od, next_redo, fo);
+      else if (kp > 512 && opt(OPT_RANK_SORT_NT, 256) == 512)
         hipLaunchKernelGGL(k_rank_sort<512>, dim3(grid), dim3(512), 0, s, ra, cand_score, eps, out_score, out_id,
                            out_count, out_resolved, ce, out_redo, od, next_redo, fo);
       else

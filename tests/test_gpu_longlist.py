@@ -361,7 +361,7 @@ def test_sort_select_equals_reference_order(hq_lib, hq_option, k):
             assert got[3][r] == int(np.argmax(sc[r])) + 7 and got[2][r] == sc[r].max()
 
 
-@pytest.mark.parametrize("nt", [512, 256])
+@pytest.mark.parametrize("nt", [512, 256, "no-small"])
 @pytest.mark.parametrize("dups", [0, 40])
 @pytest.mark.parametrize("kind", ["f64", "f32"])
 def test_window_ranking_equals_sort(hq_lib, hq_option, kind, dups, nt):
@@ -371,9 +371,12 @@ def test_window_ranking_equals_sort(hq_lib, hq_option, kind, dups, nt):
     (refine_coop 0): progressive M = 100 / 1000 with K = 10 and 150, brute force k > 64, frame scan.
     dups 40: runs of 40 identical rows (windows past the 32-entry cap: the sort fallback on every list
     holding a run) beside distinct rows.  nt: workgroup size of the lists > 512 (option rank_sort_nt: two or four
-    entries per thread)."""
+    entries per thread; lists <= 128 take a 128-entry workgroup unless option rank_sort_small is 0)."""
     from hq_mi355x.core.search_engine import IndexCorpus
-    hq_option("rank_sort_nt", nt)
+    if nt == "no-small":
+        hq_option("rank_sort_small", 0)
+    else:
+        hq_option("rank_sort_nt", nt)
     C = _corpus(20000, 64, 91)
     if dups:
         C[1000:1000 + 50 * dups] = np.repeat(C[1000:1050], dups, axis=0)
