@@ -55,12 +55,16 @@ const char* hq_last_error(void);
  * "chunk_wpb", "chunk_cpw", "precomp_grid", "precomp_tree_lds", "cos_kernel" (1 register-staged,
  * 2 lockstep), "refine_global", "select_2stage", "level_scores_v1" (the one-thread-per-pair dense scorer),
  * "scan_split3" (the level-0 scan's pre-filter on the three-MFMA split contraction instead of hi.hi),
- * "scan_occ" (4 / 5 / 6: the level-0 scan's register target in waves per SIMD), "scanov_split3" (the
+ * "scan_occ" (3 (default) / 4 / 5 / 6: the level-0 scan's register target in waves per SIMD), "scanov_split3" (the
  * overall scan's pre-filter on the split contraction), "ov_occ" (2 / 3 / 4: the overall scan's target),
  * "sample_hi" (1: the sample passes' step loops on hi.hi with a split-G epilogue),
  * "sample_kth" (0 = provable bound), "scan_v1" (the
  * LDS-tiled level-0 scan), "scan_variant", "scan_wpb" (4 = four waves per level-0 scan block), "scan_pf" (prefetch
- * distance 2, 3, 4 (default), 6 or 8), "sample_variant" (1 = the full-filter sample pass).  Options are process-wide: set them before launching, not
+ * distance 2, 3, 4, 6 or 8; default 6 at scan_occ 3, else 4), "sample_variant" (1 = the full-filter sample pass),
+ * "rank_ct" (0: the long-list re-rank's runtime level structure; 2: the compile-time one in the short-list kernel too),
+ * "rank_win" (0: the long-list ranking by the bitonic sort alone, no window ranking), "rank_sort_nt" (512: lists
+ * > 512 in 512-thread workgroups), "rank_sort_small" (0: lists <= 128 in the 1024-entry workgroup).  Options are
+ * process-wide: set them before launching, not
  * while other host threads launch.  hq_reset_option restores the default; hq_get_option returns 1 when
  * the option is set (value in *value), 0 when it is at its default, HQ_E_INVALID for an unknown name.
  * hq_diag_build() = 1 for a `make DIAG=1` library (diagnostics kernels; HQ_<NAME> environment variables
